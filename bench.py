@@ -1,0 +1,247 @@
+#!/usr/bin/env python
+"""bench.py -- V-cycle iterations/s and SpMV HBM GB/s, 3D 7-pt Poisson (BASELINE.json:2).
+
+Workload (BASELINE.json configs[1], weak-scaled for --gpus N):
+  N=1: 256^3   N=2: 256x256x512   N=4: 256x512x512   N=8: 512^3   (16.8M rows per GPU)
+  PMIS coarsening + classical interpolation, 1 pre / 1 post Jacobi sweep (omega 2/3),
+  dense solve at <= 256 rows; b = A x*, x* ~ U(-1,1) (splitmix64, seed 42), x0 = 0.
+One "step" = one ParMultilevel::solve iteration (V-cycle + residual norm) of the global
+problem.  Timed: K steps of amg_solver_solve (no host sync inside), barrier + device sync on
+both sides, max over ranks.  value = V-cycles/s x (global rows / 256^3): 256^3-equivalent
+V-cycles per second, the whole-job aggregate (equals plain iterations/s at N=1).
+
+roofline: the level-0 ParCSRMatrix::mult kernel (csr_stream<SPMV>), timed live with HIP
+events on the context stream; algorithmic bytes = 12 nnz + 4 (n+1) + 16 n.
+cpu_baseline (rank 0, N=1): the oracle's V-cycle (C, OpenMP) on the same hierarchy and
+inputs, timed for --cpu-seconds; "port" = this repo's CPU restatement (the reference
+has no AMG code).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GRIDS = {1: (256, 256, 256), 2: (256, 256, 512), 4: (256, 512, 512), 8: (512, 512, 512)}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(rank, *a):
+    if rank == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--grid", type=str, default=None, help="override nx,ny,nz")
+    ap.add_argument("--spmv-reps", type=int, default=50)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import raptor_amd as ra
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(local_rank)
+        ctx = ra.Context.distributed(local_rank)
+    else:
+        torch.cuda.set_device(0)
+        ctx = ra.Context(0)
+
+    if args.grid:
+        grid = tuple(int(v) for v in args.grid.split(","))
+    else:
+        grid = GRIDS.get(world, (256, 256, 256 * world))
+    n_global = grid[0] * grid[1] * grid[2]
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    t0 = time.perf_counter()
+    A = ra.par_stencil_grid(ctx, "7pt", grid)
+    log(rank, f"matrix {grid} built in {time.perf_counter() - t0:.1f}s; local rows {A.local_rows}")
+    t1 = time.perf_counter()
+    ml = ra.ParRugeStubenSolver(coarsen="pmis",
+                                use_graph=False if args.no_graph else None).setup(A)
+    setup_s = time.perf_counter() - t1
+    nlev = ml.num_levels
+    infos = [ml.level_info(l) for l in range(nlev)]
+    log(rank, f"setup {setup_s:.1f}s, levels {nlev}: " +
+        " ".join(f"{i['n_global']}/{i['nnz_global']}" for i in infos))
+
+    n = A.local_rows
+    with torch.cuda.stream(ctx.stream):
+        xs = ra.vector_uniform(ctx, n, A.first_row, 42)
+        b = ctx.empty(n)
+        A.mult(xs, b)
+        x = ctx.zeros(n)
+        y = ctx.empty(n)
+    ctx.synchronize()
+
+    # warmup (captures the hipGraph on 1 rank)
+    if args.warmup > 0:
+        ml.solve(x, b, max_iter=args.warmup)
+    x.zero_()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+
+    barrier()
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    _, hist = ml.solve(x, b, max_iter=args.steps)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - ts
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    iters_per_s = args.steps / dt
+    value = iters_per_s * n_global / float(256 ** 3)
+    conv = float((hist[-1] / hist[0]) ** (1.0 / max(1, len(hist) - 1))) if hist[0] > 0 else None
+    log(rank, f"{args.steps} V-cycles in {dt * 1e3:.2f} ms -> {iters_per_s:.1f} it/s, conv {conv}")
+
+    # bytes of one V-cycle (algorithmic, all ranks) + the residual norm each iteration
+    cyc_bytes_local = ml.bytes_per_cycle() + (12 * A.nnz + 4 * (n + 1) + 24 * n)
+    if world > 1:
+        t = torch.tensor([cyc_bytes_local], dtype=torch.float64)
+        dist.all_reduce(t)
+        cyc_bytes = float(t.item())
+    else:
+        cyc_bytes = float(cyc_bytes_local)
+
+    # roofline: level-0 SpMV, HIP events on the context stream
+    spmv_bytes = 12 * A.nnz + 4 * (n + 1) + 16 * n
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    for _ in range(5):
+        A.mult(x, y)
+    barrier()
+    with torch.cuda.stream(ctx.stream):
+        e0.record(ctx.stream)
+        for _ in range(args.spmv_reps):
+            A.mult(x, y)
+        e1.record(ctx.stream)
+    e1.synchronize()
+    spmv_ms = e0.elapsed_time(e1) / args.spmv_reps
+    achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
+    barrier()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(ml, b, args.cpu_seconds, n_global)
+
+    if rank == 0:
+        out = {
+            "metric": "V-cycle iters/sec + SpMV HBM GB/s, 3D 7-pt Poisson 256^3, 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "V-cycles/s (256^3-equivalent: rows*cycles/s / 256^3)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (7-pt Poisson, b = A x*, x* splitmix64 U(-1,1) seed 42, x0 = 0)",
+            "config": {
+                "workload": f"3D 7-pt Poisson {grid[0]}x{grid[1]}x{grid[2]}, PMIS + classical interp, "
+                            "Jacobi(2/3) 1+1 V-cycle, z-slab row partition",
+                "grid": list(grid),
+                "global_rows": n_global,
+                "levels": nlev,
+                "level_rows": [i["n_global"] for i in infos],
+                "level_nnz": [i["nnz_global"] for i in infos],
+                "operator_complexity": round(sum(i["nnz_global"] for i in infos) / infos[0]["nnz_global"], 3),
+                "parallelism": f"row-partition x{world}, RCCL halo",
+                "setup_s": round(setup_s, 2),
+                "hipgraph": world == 1 and not args.no_graph,
+            },
+            "iters_per_s": round(iters_per_s, 3),
+            "convergence_factor": conv,
+            "vcycle_bytes": cyc_bytes,
+            "vcycle_effective_GBps": round(cyc_bytes * iters_per_s / 1e9, 1),
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "csr_stream_kernel<SPMV> (level-0 ParCSRMatrix::mult, rank 0)",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "bytes_per_launch": spmv_bytes,
+                "avg_launch_ms": round(spmv_ms, 5),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(ml, b, seconds, n_global):
+    """Oracle V-cycle (C, OpenMP) on the product's own level operators, rank 0, N=1."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    levels = []
+    for l in range(ml.num_levels):
+        mats = []
+        for w in "APR":
+            if w != "A" and l == ml.num_levels - 1:
+                mats.append(None)
+                continue
+            rp, col, val = ml.level_matrix(l, w).export()
+            ncols = ml.level_matrix(l, w).info["n_global_cols"]
+            mats.append(O.Csr.from_arrays(rp.size - 1, ncols, rp, col, val))
+            del rp, col, val
+        levels.append(tuple(mats))
+    H = O.Hierarchy(levels[0][0], levels=levels)
+    bh = b.cpu().numpy()
+    x = np.zeros(bh.size)
+    x = H.cycle(x, bh)  # untimed first touch
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        x = H.cycle(x, bh)
+        k += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    rate = k / el * n_global / float(256 ** 3)
+    return {
+        "value": round(rate, 4),
+        "unit": "V-cycles/s (256^3-equivalent)",
+        "cores": int(O.lib().orc_num_threads()),
+        "kind": "port",
+        "sample": f"{k} oracle V-cycles (C/OpenMP, same hierarchy and b) in {el:.1f}s; "
+                  "reference has no AMG CPU path (SURVEY.md 0)",
+    }
+
+
+if __name__ == "__main__":
+    main()

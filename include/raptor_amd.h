@@ -1,0 +1,188 @@
+/*
+ * raptor_amd.h -- C-ABI drop-in boundary for the MI355X AMG V-cycle hot path.
+ *
+ * Spec: BASELINE.json:5 (north_star) asks for an AMG V-cycle that "keeps the
+ * ParMultilevel/ParCSRMatrix API surface so it drops in as the level solver: C++ host code
+ * calls HIP through a thin extern-"C" layer".  The mounted reference (Siddarthareddy1/raptor)
+ * holds no such interface -- it is three RAPTOR flowchart files, SURVEY.md section 0 -- so
+ * there is no reference file:line to replace; each entry point below cites the SURVEY.md
+ * section 8 row and the RAPtor-style method it stands for.  Names follow SURVEY.md 8(b).
+ *
+ * Rules of the boundary:
+ *   - plain C types only; host arrays are borrowed for the duration of a call;
+ *   - vectors passed to compute calls are DEVICE pointers of the rank-local length,
+ *     fp64, owned by the caller; all work is enqueued on the context's HIP stream;
+ *   - every call returns AMG_OK (0) or an error code; amg_last_error() gives the message
+ *     for the calling thread.  No exception crosses the boundary.
+ *   - one context per GPU per process (rank); a context is not re-entrant.
+ */
+#ifndef RAPTOR_AMD_H
+#define RAPTOR_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AMG_OK 0
+#define AMG_ERR_INVALID 1   /* bad argument / state                          */
+#define AMG_ERR_HIP 2       /* HIP runtime error                              */
+#define AMG_ERR_RCCL 3      /* RCCL error                                      */
+#define AMG_ERR_COMM 4      /* host exchange callback failed                  */
+#define AMG_ERR_INTERNAL 5  /* invariant violated (bug)                        */
+#define AMG_ERR_NOMEM 6     /* host or device allocation failed                */
+
+typedef struct amg_context_s* amg_context;
+typedef struct amg_matrix_s* amg_matrix;
+typedef struct amg_solver_s* amg_solver;
+
+/* Host-side all-to-all-v of bytes among the ranks of the context.  Used only during
+ * setup (halo plans, ghost rows, coarse numbering).  send_bytes[r] bytes starting at
+ * sendbuf + sum(send_bytes[0..r)) go to rank r; recv_bytes[r] bytes arrive from rank r,
+ * packed the same way.  Must return 0 on success.  The data path never calls it: the
+ * solve-time halo exchange is RCCL over xGMI. */
+typedef int (*amg_alltoallv_fn)(void* user, const void* sendbuf, const int64_t* send_bytes,
+                                void* recvbuf, const int64_t* recv_bytes);
+
+/* ---- error / version ----------------------------------------------------------- */
+const char* amg_last_error(void);
+int amg_version(void); /* 100 * major + minor */
+
+/* ---- context (one per GPU / rank) ----------------------------------------------- */
+/* hip_stream: a hipStream_t owned by the caller (NULL: the context creates one).      */
+int amg_context_create(int device, void* hip_stream, amg_context* out);
+/* Multi-GPU: rank/nranks of a row partition, the 128-byte RCCL unique id produced by
+ * rank 0's amg_rccl_unique_id(), and the host exchange used during setup.              */
+int amg_context_set_comm(amg_context ctx, int rank, int nranks, const void* rccl_unique_id,
+                         amg_alltoallv_fn exchange, void* user);
+int amg_rccl_unique_id(void* out128);
+int amg_context_stream(amg_context ctx, void** hip_stream);
+int amg_context_synchronize(amg_context ctx);
+int amg_context_destroy(amg_context ctx);
+
+/* ---- ParCSRMatrix ------------------------------------------ */
+/* Rank-local rows [first_row, first_row + n_local) of an n_global x n_global matrix;
+ * row_ptr[n_local+1], col_global[nnz] (global column ids; sorted per row on entry or
+ * sorted by the call), val[nnz].  Collective over the ranks of the context.             */
+int amg_par_csr_create(amg_context ctx, int64_t n_global, int64_t first_row, int64_t n_local,
+                       const int64_t* row_ptr, const int64_t* col_global, const double* val,
+                       amg_matrix* out);
+
+#define AMG_STENCIL_5PT 0    /* 2D Poisson, nz must be 1            (BASELINE.json:7)  */
+#define AMG_STENCIL_7PT 1    /* 3D Poisson                           (BASELINE.json:8)  */
+#define AMG_STENCIL_27PT 2   /* 3D Q1 anisotropic diffusion eps[3]   (BASELINE.json:9)  */
+/* Generates this rank's z-slab (2D: y-slab) of the model problem directly on the host of
+ * the rank and uploads it: par_stencil_grid analogue.  Collective.                       */
+int amg_par_stencil_create(amg_context ctx, int kind, int64_t nx, int64_t ny, int64_t nz,
+                           const double* eps3, amg_matrix* out);
+
+typedef struct amg_matrix_info {
+    int64_t n_global_rows, n_global_cols;
+    int64_t first_row, n_local_rows;
+    int64_t first_col, n_local_cols;
+    int64_t nnz_local;
+    int64_t n_halo;        /* off-process columns received per mult                     */
+    int64_t n_send;        /* entries sent per mult                                      */
+    int32_t n_neighbors;   /* ranks exchanged with                                       */
+    int32_t n_blocks;      /* CSR-stream row blocks                                      */
+} amg_matrix_info;
+int amg_par_csr_info(amg_matrix A, amg_matrix_info* info);
+/* Host copy of the local rows (global column ids). */
+int amg_par_csr_export(amg_matrix A, int64_t* row_ptr, int64_t* col_global, double* val);
+
+/* ParCSRMatrix::mult and the level kernels (rows a2-a5).  Device pointers, local length.
+ * Each call performs the RCCL halo exchange of x it needs, overlapped with the interior
+ * rows.                                                                                  */
+int amg_par_csr_mult(amg_matrix A, const double* x, double* y);            /* y = A x       */
+int amg_par_csr_mult_add(amg_matrix A, const double* x, double* y);        /* y = y + A x   */
+int amg_par_csr_residual(amg_matrix A, const double* x, const double* b, double* r);
+int amg_par_csr_jacobi(amg_matrix A, const double* x, const double* b, double* x_out,
+                       double omega);
+int amg_par_csr_hybrid_gs(amg_matrix A, const double* x, const double* b, double* x_out,
+                          int64_t block);
+/* ||b - A x||_2 over all ranks (deterministic reduction order). */
+int amg_par_csr_residual_norm(amg_matrix A, const double* x, const double* b, double* out);
+int amg_par_csr_destroy(amg_matrix A);
+
+/* ---- ParMultilevel (rows a6-a10) -------------------------------------------------- */
+#define AMG_COARSEN_RS 0     /* Ruge-Stueben first pass (serial only)                    */
+#define AMG_COARSEN_PMIS 1   /* PMIS, partition independent                              */
+#define AMG_COARSEN_SA 2     /* smoothed aggregation over MIS(2) aggregates              */
+#define AMG_SMOOTH_JACOBI 0
+#define AMG_SMOOTH_HYBRID_GS 1
+
+typedef struct amg_options {
+    int32_t coarsen;
+    int32_t smoother;
+    double strong_threshold;  /* 0.25 classical, 0.08 SA (halved per level)              */
+    double jacobi_omega;      /* 2/3                                                     */
+    int32_t pre_sweeps, post_sweeps;
+    int32_t max_levels;
+    int64_t max_coarse;       /* stop when the global size is <= this; dense solve there */
+    int64_t gs_block;         /* hybrid GS block (global row multiples)                 */
+    uint64_t seed;            /* PMIS / MIS(2) hash seed                                 */
+} amg_options;
+
+#define AMG_PRESET_PMIS_JACOBI 0  /* config 2/4: 7-pt Poisson, Jacobi V-cycle            */
+#define AMG_PRESET_RS_JACOBI 1    /* config 1: 2D 5-pt, Ruge-Stueben                      */
+#define AMG_PRESET_SA_HYBRID_GS 2 /* config 3/5: smoothed aggregation + hybrid GS         */
+int amg_options_default(int preset, amg_options* opt);
+
+int amg_solver_setup(amg_matrix A, const amg_options* opt, amg_solver* out);
+int amg_solver_num_levels(amg_solver S, int32_t* out);
+
+typedef struct amg_level_info {
+    int64_t n_global, nnz_global;          /* A_l                                        */
+    int64_t n_local, nnz_local;
+    int64_t p_nnz_local, r_nnz_local;      /* P_l, R_l (0 on the coarsest level)         */
+    int64_t bytes_per_cycle_local;         /* algorithmic HBM bytes this level moves     */
+} amg_level_info;
+int amg_solver_level_info(amg_solver S, int32_t level, amg_level_info* info);
+/* which: 0 = A_l, 1 = P_l, 2 = R_l.  Borrowed handle, valid while S lives. */
+int amg_solver_level_matrix(amg_solver S, int32_t level, int32_t which, amg_matrix* out);
+/* Integer setup result of level l for the local rows: C/F marker (1 = C, 0 = F) for
+ * RS/PMIS, global aggregate id for SA.  Bit-exact against the oracle. */
+int amg_solver_level_split(amg_solver S, int32_t level, int32_t* out_local);
+/* One V-cycle x <- cycle(x, b) (ParMultilevel::cycle). */
+int amg_solver_cycle(amg_solver S, double* x, const double* b);
+/* ParMultilevel::solve: r0 = ||b-Ax||; up to max_iter cycles until ||r||/r0 < tol.
+ * hist (host, max_iter+1 doubles) receives the residual history; *iters the count.
+ * Norms stay on the device until the end: no host sync inside the loop. */
+int amg_solver_solve(amg_solver S, double* x, const double* b, int32_t max_iter, double tol,
+                     double* hist, int32_t* iters);
+/* Capture each V-cycle in a hipGraph and replay it (1 = on, default on for 1 rank). */
+int amg_solver_set_graph(amg_solver S, int32_t enable);
+int amg_solver_destroy(amg_solver S);
+
+/* ---- host-only hierarchy (no GPU needed) ------------------------------------------ */
+/* The setup half of ParMultilevel (rows a8-a10) run on the CPU of each rank: exactly the
+ * code amg_solver_setup() runs before uploading.  Exposed for inspection and for CPU
+ * parity tests (multi-rank through `exchange`; NULL allowed when nranks == 1).           */
+typedef struct amg_host_hierarchy_s* amg_host_hierarchy;
+int amg_host_hierarchy_build(int rank, int nranks, amg_alltoallv_fn exchange, void* user,
+                             int64_t n_global, int64_t first_row, int64_t n_local,
+                             const int64_t* row_ptr, const int64_t* col_global,
+                             const double* val, const amg_options* opt,
+                             amg_host_hierarchy* out);
+int amg_host_hierarchy_num_levels(amg_host_hierarchy H, int32_t* out);
+/* which: 0 = A_l, 1 = P_l, 2 = R_l.  sizes[5] = {n_global_rows, n_global_cols, first_row,
+ * n_local_rows, nnz_local}. */
+int amg_host_hierarchy_level_size(amg_host_hierarchy H, int32_t level, int32_t which,
+                                  int64_t* sizes5);
+int amg_host_hierarchy_level_export(amg_host_hierarchy H, int32_t level, int32_t which,
+                                    int64_t* row_ptr, int64_t* col_global, double* val);
+int amg_host_hierarchy_level_split(amg_host_hierarchy H, int32_t level, int32_t* out_local);
+/* row-major n_c x n_c inverse of the coarsest operator (identical on every rank) */
+int amg_host_hierarchy_coarse_inverse(amg_host_hierarchy H, double* out);
+int amg_host_hierarchy_destroy(amg_host_hierarchy H);
+
+/* ---- vectors ---------------------------------------------------------------------- */
+/* out[i] = uniform(-1,1) from splitmix64(seed, first_gid + i) on the device. */
+int amg_vector_uniform(amg_context ctx, int64_t n, int64_t first_gid, uint64_t seed,
+                       double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,374 @@
+"""raptor_amd -- MI355X-native AMG V-cycle hot path behind a ParCSRMatrix / ParMultilevel API.
+
+The compute path is ``libraptor_amd.so`` (hand-written gfx950 HIP kernels + C++ host setup +
+RCCL halo exchange) reached through the C-ABI in ``include/raptor_amd.h``.  This module is
+the Python host mirror of that API (BASELINE.json:5: "keeps the ParMultilevel/ParCSRMatrix
+API surface"); it holds no numerics of its own and never falls back to a CPU path: if the
+shared library or a GPU is missing, it raises.
+
+    import raptor_amd as ra
+    ctx = ra.Context()                               # one per GPU / rank
+    A = ra.par_stencil_grid(ctx, "7pt", (256, 256, 256))
+    ml = ra.ParRugeStubenSolver(coarsen="pmis")       # PMIS + classical interp, Jacobi
+    ml.setup(A)
+    x, hist = ml.solve(x, b, max_iter=20)
+
+Vectors are rank-local float64 torch tensors on the context's device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from ._lib import (  # noqa: F401  (re-exported constants)
+    AMG_COARSEN_PMIS,
+    AMG_COARSEN_RS,
+    AMG_COARSEN_SA,
+    AMG_SMOOTH_HYBRID_GS,
+    AMG_SMOOTH_JACOBI,
+    AMG_STENCIL_5PT,
+    AMG_STENCIL_7PT,
+    AMG_STENCIL_27PT,
+    AmgError,
+    LevelInfo,
+    MatrixInfo,
+    Options,
+    check,
+    lib,
+    lib_path,
+)
+
+__all__ = [
+    "Context",
+    "ParCSRMatrix",
+    "ParMultilevel",
+    "ParRugeStubenSolver",
+    "ParSmoothedAggregationSolver",
+    "par_stencil_grid",
+    "vector_uniform",
+    "AmgError",
+]
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _ptr(t):
+    """Device pointer of a float64 torch tensor (checked)."""
+    torch = _torch()
+    if t is None:
+        return None
+    if not isinstance(t, torch.Tensor) or t.dtype != torch.float64 or not t.is_cuda:
+        raise TypeError("vectors must be float64 CUDA(HIP) torch tensors")
+    if not t.is_contiguous():
+        raise ValueError("vectors must be contiguous")
+    return C.c_void_p(t.data_ptr())
+
+
+class Context:
+    """One GPU / rank.  ``Context(device, stream)``; multi-rank via ``Context.distributed``.
+
+    The context's HIP stream is a torch stream, so torch events and the C-ABI kernels share
+    one queue (``ctx.stream``)."""
+
+    def __init__(self, device: int | None = None, stream=None):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise RuntimeError("raptor_amd needs an AMD GPU (torch.cuda.is_available() is False)")
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = int(device)
+        self.torch_device = torch.device("cuda", self.device)
+        self.stream = stream if stream is not None else torch.cuda.Stream(device=self.torch_device)
+        self.h = C.c_void_p()
+        check(lib().amg_context_create(self.device, C.c_void_p(self.stream.cuda_stream),
+                                       C.byref(self.h)))
+        self.rank, self.nranks = 0, 1
+        self._keep = []
+
+    @classmethod
+    def distributed(cls, device: int | None = None, group=None, stream=None):
+        """Collective: every rank of ``torch.distributed`` calls this.  Setup-time metadata
+        moves over a gloo group; the solve-time halo exchange is RCCL (created here)."""
+        import torch.distributed as dist
+
+        from ._comm import make_exchange
+
+        ctx = cls(device, stream)
+        rank, nranks = dist.get_rank(group), dist.get_world_size(group)
+        gloo = dist.new_group(backend="gloo") if group is None else group
+        uid = (C.c_char * 128)()
+        if rank == 0:
+            check(lib().amg_rccl_unique_id(uid))
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0, group=gloo)
+        uid = (C.c_char * 128).from_buffer_copy(obj[0])
+        cb = make_exchange(gloo, nranks)
+        ctx._keep.append(cb)
+        check(lib().amg_context_set_comm(ctx.h, rank, nranks, uid, cb, None))
+        ctx.rank, ctx.nranks, ctx.group = rank, nranks, gloo
+        return ctx
+
+    def synchronize(self):
+        check(lib().amg_context_synchronize(self.h))
+
+    def empty(self, n: int):
+        """Allocate on the context's stream (torch's caching allocator is stream-aware)."""
+        torch = _torch()
+        with torch.cuda.stream(self.stream):
+            return torch.empty(int(n), dtype=torch.float64, device=self.torch_device)
+
+    def zeros(self, n: int):
+        torch = _torch()
+        with torch.cuda.stream(self.stream):
+            return torch.zeros(int(n), dtype=torch.float64, device=self.torch_device)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            try:
+                lib().amg_context_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+
+class ParCSRMatrix:
+    """Row-partitioned CSR on the GPU (RAPtor ParCSRMatrix analogue).
+
+    Rank-local rows ``[first_row, first_row + local_rows)``; ``mult`` performs the RCCL halo
+    exchange it needs, overlapped with the interior rows."""
+
+    def __init__(self, ctx: Context, handle, owner=None):
+        self.ctx = ctx
+        self.h = handle
+        self._owner = owner  # solver that owns a borrowed level matrix
+        self.info = self._info()
+
+    # ---- construction -------------------------------------------------------------
+    @classmethod
+    def from_csr(cls, ctx: Context, n_global: int, first_row: int, row_ptr, col, val):
+        rp = np.ascontiguousarray(row_ptr, np.int64)
+        cg = np.ascontiguousarray(col, np.int64)
+        v = np.ascontiguousarray(val, np.float64)
+        if rp.ndim != 1 or rp.size < 1 or cg.size != rp[-1] or v.size != rp[-1]:
+            raise ValueError("row_ptr / col / val sizes are inconsistent")
+        h = C.c_void_p()
+        i64 = C.POINTER(C.c_int64)
+        check(lib().amg_par_csr_create(ctx.h, int(n_global), int(first_row), rp.size - 1,
+                                       rp.ctypes.data_as(i64), cg.ctypes.data_as(i64),
+                                       v.ctypes.data_as(C.POINTER(C.c_double)), C.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_scipy_local(cls, ctx: Context, M, n_global: int, first_row: int):
+        M = M.tocsr()
+        return cls.from_csr(ctx, n_global, first_row, M.indptr, M.indices, M.data)
+
+    def _info(self):
+        inf = MatrixInfo()
+        check(lib().amg_par_csr_info(self.h, C.byref(inf)))
+        return {k: getattr(inf, k) for k, _ in MatrixInfo._fields_}
+
+    @property
+    def global_rows(self):
+        return self.info["n_global_rows"]
+
+    @property
+    def local_rows(self):
+        return self.info["n_local_rows"]
+
+    @property
+    def first_row(self):
+        return self.info["first_row"]
+
+    @property
+    def local_cols(self):
+        return self.info["n_local_cols"]
+
+    @property
+    def nnz(self):
+        return self.info["nnz_local"]
+
+    def export(self):
+        """Host copy of the local rows: (row_ptr, global cols, vals) as numpy arrays."""
+        n, nnz = self.local_rows, self.nnz
+        rp = np.empty(n + 1, np.int64)
+        col = np.empty(nnz, np.int64)
+        val = np.empty(nnz, np.float64)
+        i64 = C.POINTER(C.c_int64)
+        check(lib().amg_par_csr_export(self.h, rp.ctypes.data_as(i64), col.ctypes.data_as(i64),
+                                       val.ctypes.data_as(C.POINTER(C.c_double))))
+        return rp, col, val
+
+    def to_scipy_local(self):
+        import scipy.sparse as sp
+
+        rp, col, val = self.export()
+        return sp.csr_matrix((val, col, rp), shape=(self.local_rows, self.info["n_global_cols"]))
+
+    # ---- level kernels (ParCSRMatrix::mult & friends) -------------------------------
+    def mult(self, x, y):
+        check(lib().amg_par_csr_mult(self.h, _ptr(x), _ptr(y)))
+        return y
+
+    def mult_add(self, x, y):
+        check(lib().amg_par_csr_mult_add(self.h, _ptr(x), _ptr(y)))
+        return y
+
+    def residual(self, x, b, r):
+        check(lib().amg_par_csr_residual(self.h, _ptr(x), _ptr(b), _ptr(r)))
+        return r
+
+    def jacobi(self, x, b, x_out, omega=2.0 / 3.0):
+        check(lib().amg_par_csr_jacobi(self.h, _ptr(x), _ptr(b), _ptr(x_out), float(omega)))
+        return x_out
+
+    def hybrid_gs(self, x, b, x_out, block=64):
+        check(lib().amg_par_csr_hybrid_gs(self.h, _ptr(x), _ptr(b), _ptr(x_out), int(block)))
+        return x_out
+
+    def residual_norm(self, x, b) -> float:
+        out = C.c_double()
+        check(lib().amg_par_csr_residual_norm(self.h, _ptr(x), _ptr(b), C.byref(out)))
+        return out.value
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h and self._owner is None:
+            try:
+                lib().amg_par_csr_destroy(h)
+            except Exception:
+                pass
+        self.h = None
+
+
+_STENCILS = {"5pt": AMG_STENCIL_5PT, "7pt": AMG_STENCIL_7PT, "27pt": AMG_STENCIL_27PT}
+
+
+def par_stencil_grid(ctx: Context, kind: str, dims, eps=(1.0, 1.0, 1e-3)) -> ParCSRMatrix:
+    """Model problem of SURVEY.md 8d; this rank's z-slab (2D: y-slab).  Collective."""
+    dims = tuple(int(d) for d in dims)
+    if kind == "5pt":
+        if len(dims) != 2:
+            raise ValueError("5pt takes (nx, ny)")
+        nx, ny, nz = dims[0], dims[1], 1
+    else:
+        if len(dims) != 3:
+            raise ValueError(f"{kind} takes (nx, ny, nz)")
+        nx, ny, nz = dims
+    e = (C.c_double * 3)(*eps)
+    h = C.c_void_p()
+    check(lib().amg_par_stencil_create(ctx.h, _STENCILS[kind], nx, ny, nz, e, C.byref(h)))
+    return ParCSRMatrix(ctx, h)
+
+
+def vector_uniform(ctx: Context, n: int, first_gid: int = 0, seed: int = 42):
+    """Device vector u_i = uniform(-1, 1) of splitmix64(seed, first_gid + i)."""
+    out = ctx.empty(n)
+    check(lib().amg_vector_uniform(ctx.h, int(n), int(first_gid), C.c_uint64(seed), _ptr(out)))
+    return out
+
+
+class ParMultilevel:
+    """AMG hierarchy + V-cycle (RAPtor ParMultilevel analogue).
+
+    ``coarsen``: "rs" (serial Ruge-Stueben), "pmis", or "sa" (smoothed aggregation over MIS(2)
+    aggregates).  ``smoother``: "jacobi" or "hybrid_gs"."""
+
+    _COARSEN = {"rs": AMG_COARSEN_RS, "pmis": AMG_COARSEN_PMIS, "sa": AMG_COARSEN_SA}
+    _SMOOTH = {"jacobi": AMG_SMOOTH_JACOBI, "hybrid_gs": AMG_SMOOTH_HYBRID_GS}
+
+    def __init__(self, coarsen="pmis", smoother="jacobi", strong_threshold=None,
+                 jacobi_omega=2.0 / 3.0, pre_sweeps=1, post_sweeps=1, max_levels=25,
+                 max_coarse=256, gs_block=64, seed=0x5EED, use_graph=None):
+        if strong_threshold is None:
+            strong_threshold = 0.08 if coarsen == "sa" else 0.25
+        self.options = Options(self._COARSEN[coarsen], self._SMOOTH[smoother],
+                               float(strong_threshold), float(jacobi_omega), int(pre_sweeps),
+                               int(post_sweeps), int(max_levels), int(max_coarse), int(gs_block),
+                               int(seed))
+        self.use_graph = use_graph
+        self.h = None
+        self.A = None
+
+    def setup(self, A: ParCSRMatrix):
+        if self.h:
+            lib().amg_solver_destroy(self.h)
+        self.A = A
+        self.h = C.c_void_p()
+        check(lib().amg_solver_setup(A.h, C.byref(self.options), C.byref(self.h)))
+        if self.use_graph is not None:
+            check(lib().amg_solver_set_graph(self.h, 1 if self.use_graph else 0))
+        return self
+
+    @property
+    def num_levels(self) -> int:
+        n = C.c_int32()
+        check(lib().amg_solver_num_levels(self.h, C.byref(n)))
+        return n.value
+
+    def level_info(self, level: int) -> dict:
+        inf = LevelInfo()
+        check(lib().amg_solver_level_info(self.h, int(level), C.byref(inf)))
+        return {k: getattr(inf, k) for k, _ in LevelInfo._fields_}
+
+    def level_matrix(self, level: int, which: str = "A") -> ParCSRMatrix:
+        h = C.c_void_p()
+        check(lib().amg_solver_level_matrix(self.h, int(level), {"A": 0, "P": 1, "R": 2}[which],
+                                            C.byref(h)))
+        return ParCSRMatrix(self.A.ctx, h, owner=self)
+
+    def level_split(self, level: int):
+        n = self.level_info(level)["n_local"]
+        out = np.empty(n, np.int32)
+        check(lib().amg_solver_level_split(self.h, int(level),
+                                           out.ctypes.data_as(C.POINTER(C.c_int32))))
+        return out
+
+    def bytes_per_cycle(self) -> int:
+        """Algorithmic HBM bytes of one V-cycle on this rank."""
+        return sum(self.level_info(l)["bytes_per_cycle_local"] for l in range(self.num_levels))
+
+    def cycle(self, x, b):
+        check(lib().amg_solver_cycle(self.h, _ptr(x), _ptr(b)))
+        return x
+
+    def solve(self, x, b, max_iter=20, tol=0.0):
+        hist = np.zeros(int(max_iter) + 1)
+        it = C.c_int32()
+        check(lib().amg_solver_solve(self.h, _ptr(x), _ptr(b), int(max_iter), float(tol),
+                                     hist.ctypes.data_as(C.POINTER(C.c_double)), C.byref(it)))
+        return x, hist[: it.value + 1]
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            try:
+                lib().amg_solver_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+
+class ParRugeStubenSolver(ParMultilevel):
+    """Classical AMG: strength theta = 0.25, RS (serial) or PMIS coarsening, classical
+    interpolation, Jacobi smoothing."""
+
+    def __init__(self, coarsen="pmis", **kw):
+        if coarsen not in ("rs", "pmis"):
+            raise ValueError("ParRugeStubenSolver coarsen must be 'rs' or 'pmis'")
+        super().__init__(coarsen=coarsen, **kw)
+
+
+class ParSmoothedAggregationSolver(ParMultilevel):
+    """Smoothed aggregation: symmetric strength 0.08 (halved per level), MIS(2) aggregates,
+    Jacobi-smoothed prolongator, hybrid Gauss-Seidel smoothing."""
+
+    def __init__(self, smoother="hybrid_gs", **kw):
+        super().__init__(coarsen="sa", smoother=smoother, **kw)

@@ -1,0 +1,530 @@
+// capi.hip -- extern "C" boundary (include/raptor_amd.h).  Every entry point catches
+// exceptions and turns them into an error code + thread-local message.
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+
+#include "device.hpp"
+
+using namespace amg;
+
+struct amg_context_s {
+    Context c;
+};
+struct amg_matrix_s {
+    std::unique_ptr<DevMatrix> own;  // null for borrowed level views
+    DevMatrix* m = nullptr;
+};
+struct amg_solver_s {
+    Solver s;
+    std::vector<std::unique_ptr<amg_matrix_s>> views;  // borrowed level handles
+};
+
+static thread_local std::string g_err;
+
+template <class F>
+static int guard(F&& f) {
+    try {
+        f();
+        return AMG_OK;
+    } catch (const Error& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_err = "out of host memory";
+        return AMG_ERR_NOMEM;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return AMG_ERR_INTERNAL;
+    }
+}
+
+static void set_device(Context& c) { HIP_CHECK(hipSetDevice(c.device)); }
+
+static HostCSR make_host_csr(const HostComm& comm, int64_t n_global, int64_t first_row,
+                             int64_t n_local, const int64_t* row_ptr, const int64_t* col_global,
+                             const double* val) {
+    AMG_CHECK(row_ptr, "null row_ptr");
+    AMG_CHECK(n_local >= 0 && first_row >= 0 && first_row + n_local <= n_global, "bad row range");
+    HostCSR h;
+    h.n_global_rows = h.n_global_cols = n_global;
+    std::vector<int64_t> counts = comm.allgather(n_local);
+    h.row_starts.assign(comm.nranks + 1, 0);
+    for (int r = 0; r < comm.nranks; ++r) h.row_starts[r + 1] = h.row_starts[r] + counts[r];
+    AMG_CHECK(h.row_starts[comm.rank] == first_row, "first_row inconsistent with rank order");
+    AMG_CHECK(h.row_starts[comm.nranks] == n_global, "local row counts do not sum to n_global");
+    h.col_starts = h.row_starts;
+    AMG_CHECK(row_ptr[0] == 0, "row_ptr[0] must be 0");
+    const int64_t nnz = row_ptr[n_local];
+    h.rp.assign(row_ptr, row_ptr + n_local + 1);
+    h.col.assign(col_global, col_global + nnz);
+    h.val.assign(val, val + nnz);
+    for (int64_t i = 0; i < n_local; ++i) {
+        AMG_CHECK(row_ptr[i + 1] >= row_ptr[i], "row_ptr not monotone");
+        const int64_t b = row_ptr[i], e = row_ptr[i + 1];
+        bool sorted = true;
+        for (int64_t k = b; k < e; ++k) {
+            AMG_CHECK(col_global[k] >= 0 && col_global[k] < n_global, "column id out of range");
+            if (k > b && col_global[k] <= col_global[k - 1]) sorted = false;
+        }
+        if (!sorted) {
+            std::vector<int64_t> idx(e - b);
+            std::iota(idx.begin(), idx.end(), b);
+            std::sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return col_global[x] < col_global[y]; });
+            for (int64_t t = 0; t < e - b; ++t) {
+                h.col[b + t] = col_global[idx[t]];
+                h.val[b + t] = val[idx[t]];
+                AMG_CHECK(t == 0 || h.col[b + t] != h.col[b + t - 1], "duplicate column in a row");
+            }
+        }
+    }
+    return h;
+}
+
+extern "C" {
+
+const char* amg_last_error(void) { return g_err.c_str(); }
+int amg_version(void) { return 100; }
+
+int amg_context_create(int device, void* hip_stream, amg_context* out) {
+    return guard([&] {
+        AMG_CHECK(out, "null output");
+        int ndev = 0;
+        HIP_CHECK(hipGetDeviceCount(&ndev));
+        AMG_CHECK(device >= 0 && device < ndev, "device index out of range");
+        auto* h = new amg_context_s();
+        h->c.device = device;
+        try {
+            set_device(h->c);
+            if (hip_stream) {
+                h->c.stream = (hipStream_t)hip_stream;
+            } else {
+                HIP_CHECK(hipStreamCreateWithFlags(&h->c.stream, hipStreamNonBlocking));
+                h->c.own_stream = true;
+            }
+            HIP_CHECK(hipStreamCreateWithFlags(&h->c.comm_stream, hipStreamNonBlocking));
+            HIP_CHECK(hipEventCreateWithFlags(&h->c.ev_pack, hipEventDisableTiming));
+            HIP_CHECK(hipEventCreateWithFlags(&h->c.ev_halo, hipEventDisableTiming));
+        } catch (...) {
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
+int amg_rccl_unique_id(void* out128) {
+    return guard([&] {
+        AMG_CHECK(out128, "null output");
+        static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+        ncclUniqueId id;
+        NCCL_CHECK(ncclGetUniqueId(&id));
+        std::memcpy(out128, &id, sizeof(id));
+    });
+}
+
+int amg_context_set_comm(amg_context ctx, int rank, int nranks, const void* uid,
+                         amg_alltoallv_fn exchange, void* user) {
+    return guard([&] {
+        AMG_CHECK(ctx, "null context");
+        AMG_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
+        Context& c = ctx->c;
+        set_device(c);
+        AMG_CHECK(!c.nccl, "communicator already set");
+        c.host.rank = rank;
+        c.host.nranks = nranks;
+        c.host.fn = exchange;
+        c.host.user = user;
+        if (nranks > 1) {
+            AMG_CHECK(uid && exchange, "multi-rank needs an RCCL unique id and a host exchange");
+            ncclUniqueId id;
+            std::memcpy(&id, uid, sizeof(id));
+            NCCL_CHECK(ncclCommInitRank(&c.nccl, nranks, id, rank));
+        }
+    });
+}
+
+int amg_context_stream(amg_context ctx, void** s) {
+    return guard([&] {
+        AMG_CHECK(ctx && s, "null argument");
+        *s = (void*)ctx->c.stream;
+    });
+}
+
+int amg_context_synchronize(amg_context ctx) {
+    return guard([&] {
+        AMG_CHECK(ctx, "null context");
+        set_device(ctx->c);
+        HIP_CHECK(hipStreamSynchronize(ctx->c.stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->c.comm_stream));
+    });
+}
+
+int amg_context_destroy(amg_context ctx) {
+    return guard([&] {
+        if (!ctx) return;
+        (void)hipSetDevice(ctx->c.device);
+        (void)hipStreamSynchronize(ctx->c.stream);
+        delete ctx;
+    });
+}
+
+int amg_par_csr_create(amg_context ctx, int64_t n_global, int64_t first_row, int64_t n_local,
+                       const int64_t* row_ptr, const int64_t* col_global, const double* val,
+                       amg_matrix* out) {
+    return guard([&] {
+        AMG_CHECK(ctx && out && row_ptr, "null argument");
+        AMG_CHECK(n_local >= 0 && first_row >= 0 && first_row + n_local <= n_global, "bad row range");
+        Context& c = ctx->c;
+        set_device(c);
+        HostCSR h = make_host_csr(c.host, n_global, first_row, n_local, row_ptr, col_global, val);
+        std::unique_ptr<amg_matrix_s> m(new amg_matrix_s());
+        m->own.reset(new DevMatrix());
+        m->m = m->own.get();
+        m->m->build(&c, std::move(h));
+        *out = m.release();
+    });
+}
+
+int amg_par_stencil_create(amg_context ctx, int kind, int64_t nx, int64_t ny, int64_t nz,
+                           const double* eps3, amg_matrix* out) {
+    return guard([&] {
+        AMG_CHECK(ctx && out, "null argument");
+        AMG_CHECK(kind == AMG_STENCIL_5PT || kind == AMG_STENCIL_7PT || kind == AMG_STENCIL_27PT,
+                  "unknown stencil");
+        Context& c = ctx->c;
+        set_device(c);
+        HostCSR h = stencil_slab(c.host, kind, nx, ny, nz, eps3);
+        std::unique_ptr<amg_matrix_s> m(new amg_matrix_s());
+        m->own.reset(new DevMatrix());
+        m->m = m->own.get();
+        m->m->build(&c, std::move(h));
+        *out = m.release();
+    });
+}
+
+int amg_par_csr_info(amg_matrix A, amg_matrix_info* info) {
+    return guard([&] {
+        AMG_CHECK(A && info, "null argument");
+        const DevMatrix& m = *A->m;
+        info->n_global_rows = m.host.n_global_rows;
+        info->n_global_cols = m.host.n_global_cols;
+        info->first_row = m.first_row;
+        info->n_local_rows = m.n_rows;
+        info->first_col = m.first_col;
+        info->n_local_cols = m.n_cols_local;
+        info->nnz_local = m.nnz;
+        info->n_halo = m.plan.n_halo();
+        info->n_send = (int64_t)m.plan.send_idx.size();
+        info->n_neighbors = (int32_t)std::max(m.plan.send_procs.size(), m.plan.recv_procs.size());
+        info->n_blocks = m.nb_int + m.nb_bnd;
+    });
+}
+
+int amg_par_csr_export(amg_matrix A, int64_t* rp, int64_t* col, double* val) {
+    return guard([&] {
+        AMG_CHECK(A && rp && col && val, "null argument");
+        const HostCSR& h = A->m->host;
+        std::copy(h.rp.begin(), h.rp.end(), rp);
+        std::copy(h.col.begin(), h.col.end(), col);
+        std::copy(h.val.begin(), h.val.end(), val);
+    });
+}
+
+static int apply(amg_matrix A, int mode, const double* x, const double* b, double* y, double w) {
+    return guard([&] {
+        AMG_CHECK(A, "null matrix");
+        AMG_CHECK((x || A->m->n_cols_local == 0) && (y || A->m->n_rows == 0), "null vector");
+        set_device(*A->m->ctx);
+        par_apply(*A->m, mode, x, b, y, w, nullptr);
+    });
+}
+
+int amg_par_csr_mult(amg_matrix A, const double* x, double* y) { return apply(A, KM_SPMV, x, nullptr, y, 0.0); }
+int amg_par_csr_mult_add(amg_matrix A, const double* x, double* y) {
+    return apply(A, KM_SPMV_ADD, x, nullptr, y, 0.0);
+}
+int amg_par_csr_residual(amg_matrix A, const double* x, const double* b, double* r) {
+    return apply(A, KM_RESID, x, b, r, 0.0);
+}
+int amg_par_csr_jacobi(amg_matrix A, const double* x, const double* b, double* xo, double omega) {
+    return apply(A, KM_JACOBI, x, b, xo, omega);
+}
+
+int amg_par_csr_hybrid_gs(amg_matrix A, const double* x, const double* b, double* xo, int64_t block) {
+    return guard([&] {
+        AMG_CHECK(A, "null matrix");
+        AMG_CHECK(x != xo, "hybrid GS is out of place: x and x_out must differ");
+        set_device(*A->m->ctx);
+        par_hybrid_gs(*A->m, x, b, xo, block);
+    });
+}
+
+int amg_par_csr_residual_norm(amg_matrix A, const double* x, const double* b, double* out) {
+    return guard([&] {
+        AMG_CHECK(A && out, "null argument");
+        Context& c = *A->m->ctx;
+        set_device(c);
+        DevBuf<double> r, o;
+        r.alloc((size_t)std::max<int64_t>(A->m->n_rows, 1));
+        o.alloc(1);
+        par_residual_norm(*A->m, x, b, r.p, o.p);
+        HIP_CHECK(hipMemcpyAsync(out, o.p, sizeof(double), hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+    });
+}
+
+int amg_par_csr_destroy(amg_matrix A) {
+    return guard([&] {
+        if (!A) return;
+        AMG_CHECK(A->own != nullptr, "cannot destroy a borrowed level matrix");
+        (void)hipSetDevice(A->m->ctx->device);
+        (void)hipStreamSynchronize(A->m->ctx->stream);
+        delete A;
+    });
+}
+
+int amg_options_default(int preset, amg_options* o) {
+    return guard([&] {
+        AMG_CHECK(o, "null argument");
+        o->coarsen = AMG_COARSEN_PMIS;
+        o->smoother = AMG_SMOOTH_JACOBI;
+        o->strong_threshold = 0.25;
+        o->jacobi_omega = 2.0 / 3.0;
+        o->pre_sweeps = 1;
+        o->post_sweeps = 1;
+        o->max_levels = 25;
+        o->max_coarse = 256;
+        o->gs_block = 64;
+        o->seed = 0x5EED;
+        if (preset == AMG_PRESET_RS_JACOBI) {
+            o->coarsen = AMG_COARSEN_RS;
+        } else if (preset == AMG_PRESET_SA_HYBRID_GS) {
+            o->coarsen = AMG_COARSEN_SA;
+            o->smoother = AMG_SMOOTH_HYBRID_GS;
+            o->strong_threshold = 0.08;
+        } else {
+            AMG_CHECK(preset == AMG_PRESET_PMIS_JACOBI, "unknown preset");
+        }
+    });
+}
+
+int amg_solver_setup(amg_matrix A, const amg_options* opt, amg_solver* out) {
+    return guard([&] {
+        AMG_CHECK(A && opt && out, "null argument");
+        set_device(*A->m->ctx);
+        auto* s = new amg_solver_s();
+        try {
+            s->s.setup(*A->m, *opt);
+        } catch (...) {
+            delete s;
+            throw;
+        }
+        *out = s;
+    });
+}
+
+int amg_solver_num_levels(amg_solver S, int32_t* out) {
+    return guard([&] {
+        AMG_CHECK(S && out, "null argument");
+        *out = (int32_t)S->s.levels.size();
+    });
+}
+
+int amg_solver_level_info(amg_solver S, int32_t l, amg_level_info* info) {
+    return guard([&] {
+        AMG_CHECK(S && info, "null argument");
+        AMG_CHECK(l >= 0 && l < (int32_t)S->s.levels.size(), "level out of range");
+        DevMatrix& A = S->s.Amat(l);
+        const HostComm& comm = S->s.ctx->host;
+        info->n_global = A.host.n_global_rows;
+        info->n_local = A.n_rows;
+        info->nnz_local = A.nnz;
+        info->nnz_global = comm.allreduce_sum(A.nnz);
+        const Level& L = S->s.levels[l];
+        info->p_nnz_local = L.P ? L.P->nnz : 0;
+        info->r_nnz_local = L.R ? L.R->nnz : 0;
+        info->bytes_per_cycle_local = S->s.bytes_per_cycle(l);
+    });
+}
+
+int amg_solver_level_matrix(amg_solver S, int32_t l, int32_t which, amg_matrix* out) {
+    return guard([&] {
+        AMG_CHECK(S && out, "null argument");
+        AMG_CHECK(l >= 0 && l < (int32_t)S->s.levels.size(), "level out of range");
+        AMG_CHECK(which >= 0 && which <= 2, "which must be 0 (A), 1 (P) or 2 (R)");
+        DevMatrix* m = which == 0 ? &S->s.Amat(l)
+                                  : which == 1 ? S->s.levels[l].P.get() : S->s.levels[l].R.get();
+        AMG_CHECK(m, "no such matrix on this level (the coarsest level has no P/R)");
+        std::unique_ptr<amg_matrix_s> v(new amg_matrix_s());
+        v->m = m;
+        S->views.push_back(std::move(v));
+        *out = S->views.back().get();
+    });
+}
+
+int amg_solver_level_split(amg_solver S, int32_t l, int32_t* out) {
+    return guard([&] {
+        AMG_CHECK(S && out, "null argument");
+        AMG_CHECK(l >= 0 && l + 1 < (int32_t)S->s.levels.size(), "level has no splitting");
+        const auto& sp = S->s.levels[l].split;
+        std::copy(sp.begin(), sp.end(), out);
+    });
+}
+
+int amg_solver_cycle(amg_solver S, double* x, const double* b) {
+    return guard([&] {
+        AMG_CHECK(S, "null solver");
+        set_device(*S->s.ctx);
+        S->s.cycle(x, b);
+    });
+}
+
+int amg_solver_solve(amg_solver S, double* x, const double* b, int32_t max_iter, double tol,
+                     double* hist, int32_t* iters) {
+    return guard([&] {
+        AMG_CHECK(S && hist && iters, "null argument");
+        AMG_CHECK(max_iter >= 0, "max_iter must be >= 0");
+        Solver& s = S->s;
+        Context& c = *s.ctx;
+        set_device(c);
+        DevMatrix& A = *s.A0;
+        if (s.hist.n < (size_t)max_iter + 1) s.hist.alloc((size_t)max_iter + 1);
+        double* r = s.levels[0].r.p;
+        par_residual_norm(A, x, b, r, s.hist.p);
+        int32_t it = 0;
+        double r0 = -1.0;
+        if (tol > 0.0) {
+            HIP_CHECK(hipMemcpyAsync(&r0, s.hist.p, sizeof(double), hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+        }
+        while (it < max_iter) {
+            s.cycle(x, b);
+            par_residual_norm(A, x, b, r, s.hist.p + it + 1);
+            ++it;
+            if (tol > 0.0) {
+                double rn;
+                HIP_CHECK(hipMemcpyAsync(&rn, s.hist.p + it, sizeof(double), hipMemcpyDeviceToHost, c.stream));
+                HIP_CHECK(hipStreamSynchronize(c.stream));
+                if (r0 > 0.0 && rn / r0 < tol) break;
+            }
+        }
+        HIP_CHECK(hipMemcpyAsync(hist, s.hist.p, sizeof(double) * (size_t)(it + 1), hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        *iters = it;
+    });
+}
+
+int amg_solver_set_graph(amg_solver S, int32_t enable) {
+    return guard([&] {
+        AMG_CHECK(S, "null solver");
+        AMG_CHECK(!enable || S->s.ctx->host.nranks == 1, "hipGraph capture is single-rank only");
+        S->s.use_graph = enable != 0;
+        if (S->s.graph) {
+            HIP_CHECK(hipGraphExecDestroy(S->s.graph));
+            S->s.graph = nullptr;
+        }
+    });
+}
+
+int amg_solver_destroy(amg_solver S) {
+    return guard([&] {
+        if (!S) return;
+        (void)hipSetDevice(S->s.ctx->device);
+        (void)hipStreamSynchronize(S->s.ctx->stream);
+        delete S;
+    });
+}
+
+struct amg_host_hierarchy_s {
+    HostComm comm;
+    HostCSR A0;
+    HostHierarchy H;
+};
+
+int amg_host_hierarchy_build(int rank, int nranks, amg_alltoallv_fn exchange, void* user,
+                             int64_t n_global, int64_t first_row, int64_t n_local,
+                             const int64_t* row_ptr, const int64_t* col_global, const double* val,
+                             const amg_options* opt, amg_host_hierarchy* out) {
+    return guard([&] {
+        AMG_CHECK(opt && out, "null argument");
+        AMG_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
+        AMG_CHECK(nranks == 1 || exchange, "multi-rank needs a host exchange");
+        std::unique_ptr<amg_host_hierarchy_s> h(new amg_host_hierarchy_s());
+        h->comm.rank = rank;
+        h->comm.nranks = nranks;
+        h->comm.fn = exchange;
+        h->comm.user = user;
+        h->A0 = make_host_csr(h->comm, n_global, first_row, n_local, row_ptr, col_global, val);
+        build_hierarchy(h->comm, h->A0, *opt, h->H);
+        *out = h.release();
+    });
+}
+
+static const HostCSR& host_level(amg_host_hierarchy H, int32_t l, int32_t which) {
+    AMG_CHECK(H, "null hierarchy");
+    AMG_CHECK(l >= 0 && l < (int32_t)H->H.levels.size(), "level out of range");
+    AMG_CHECK(which >= 0 && which <= 2, "which must be 0 (A), 1 (P) or 2 (R)");
+    AMG_CHECK(which == 0 || l + 1 < (int32_t)H->H.levels.size(), "coarsest level has no P/R");
+    return which == 0 ? H->H.A(l) : which == 1 ? H->H.levels[l].P : H->H.levels[l].R;
+}
+
+int amg_host_hierarchy_num_levels(amg_host_hierarchy H, int32_t* out) {
+    return guard([&] {
+        AMG_CHECK(H && out, "null argument");
+        *out = (int32_t)H->H.levels.size();
+    });
+}
+
+int amg_host_hierarchy_level_size(amg_host_hierarchy H, int32_t l, int32_t which, int64_t* s) {
+    return guard([&] {
+        AMG_CHECK(s, "null argument");
+        const HostCSR& M = host_level(H, l, which);
+        s[0] = M.n_global_rows;
+        s[1] = M.n_global_cols;
+        s[2] = M.row_starts[H->comm.rank];
+        s[3] = M.nrows();
+        s[4] = M.nnz();
+    });
+}
+
+int amg_host_hierarchy_level_export(amg_host_hierarchy H, int32_t l, int32_t which, int64_t* rp,
+                                    int64_t* col, double* val) {
+    return guard([&] {
+        AMG_CHECK(rp && col && val, "null argument");
+        const HostCSR& M = host_level(H, l, which);
+        std::copy(M.rp.begin(), M.rp.end(), rp);
+        std::copy(M.col.begin(), M.col.end(), col);
+        std::copy(M.val.begin(), M.val.end(), val);
+    });
+}
+
+int amg_host_hierarchy_level_split(amg_host_hierarchy H, int32_t l, int32_t* out) {
+    return guard([&] {
+        AMG_CHECK(H && out, "null argument");
+        AMG_CHECK(l >= 0 && l + 1 < (int32_t)H->H.levels.size(), "level has no splitting");
+        const auto& sp = H->H.levels[l].split;
+        std::copy(sp.begin(), sp.end(), out);
+    });
+}
+
+int amg_host_hierarchy_coarse_inverse(amg_host_hierarchy H, double* out) {
+    return guard([&] {
+        AMG_CHECK(H && out, "null argument");
+        std::copy(H->H.coarse_inv.begin(), H->H.coarse_inv.end(), out);
+    });
+}
+
+int amg_host_hierarchy_destroy(amg_host_hierarchy H) {
+    return guard([&] { delete H; });
+}
+
+int amg_vector_uniform(amg_context ctx, int64_t n, int64_t first_gid, uint64_t seed, double* out) {
+    return guard([&] {
+        AMG_CHECK(ctx && (out || n == 0), "null argument");
+        set_device(ctx->c);
+        launch_uniform(ctx->c.stream, n, first_gid, seed, out);
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,163 @@
+// device.hpp -- device (gfx950) side of the product: context, ParCSRMatrix on the GPU,
+// the CSR-stream level kernels and the V-cycle.  SURVEY.md 8a rows a1-a7, a11.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "host.hpp"
+
+namespace amg {
+
+#define HIP_CHECK(expr)                                                                   \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            throw ::amg::Error(AMG_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+#define NCCL_CHECK(expr)                                                                  \
+    do {                                                                                  \
+        ncclResult_t r_ = (expr);                                                         \
+        if (r_ != ncclSuccess)                                                            \
+            throw ::amg::Error(AMG_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+// kernel geometry shared by host-side block building and the kernels
+constexpr int kTPB = 256;   // threads per workgroup (4 waves of 64)
+constexpr int kCAP = 2048;  // nonzeros staged in LDS per workgroup (16 KiB of products)
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr, o.n = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) {
+            reset();
+            p = o.p, n = o.n;
+            o.p = nullptr, o.n = 0;
+        }
+        return *this;
+    }
+    ~DevBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void alloc(size_t count) {
+        reset();
+        if (count) HIP_CHECK(hipMalloc(&p, count * sizeof(T)));
+        n = count;
+    }
+    void upload(const T* h, size_t count) {
+        alloc(count);
+        if (count) HIP_CHECK(hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice));
+    }
+};
+
+struct Context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
+    HostComm host;
+    ncclComm_t nccl = nullptr;
+    DevBuf<double> scratch;  // norm partials + gathered sums
+    ~Context();
+};
+
+// ParCSRMatrix on the device: rank-local rows, columns renumbered [local | halo].
+struct DevMatrix {
+    Context* ctx = nullptr;
+    HostCSR host;              // host image (global column ids), kept for export / setup
+    int64_t first_row = 0, n_rows = 0, first_col = 0, n_cols_local = 0, nnz = 0;
+    bool square = false;
+    DevBuf<int> rp, col;
+    DevBuf<double> val, dinv;
+    // CSR-stream row blocks: [0, nb_int) interior rows, [nb_int, nb_int+nb_bnd) rows that
+    // touch halo columns.  Each block is {row begin, row end}.
+    DevBuf<int2> blocks;
+    int nb_int = 0, nb_bnd = 0;
+    // hybrid-GS blocks (built on first use for a given block size)
+    DevBuf<int2> gs_blocks;
+    int n_gs_blocks = 0;
+    int64_t gs_block = 0;
+    // halo (ParComm): RCCL neighbour exchange
+    HaloPlan plan;
+    DevBuf<int> send_idx;
+    DevBuf<double> send_buf, halo;
+
+    void build(Context* c, HostCSR&& h);
+    void ensure_gs_blocks(int64_t block);
+    // start the halo exchange of x (pack on the compute stream, RCCL on the comm stream);
+    // returns true when a boundary phase is needed
+    bool halo_begin(const double* x);
+    void halo_wait();
+    int64_t n_halo() const { return plan.n_halo(); }
+};
+
+enum KernelMode { KM_SPMV = 0, KM_SPMV_ADD = 1, KM_RESID = 2, KM_JACOBI = 3 };
+
+// launchers (kernels.hip); all enqueue on s
+void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, int first_block,
+                       int n_blocks, const double* x, const double* b, double* y, double omega,
+                       double* partial);
+void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
+                      double* y);
+void launch_jacobi_zero(hipStream_t s, int64_t n, const double* b, const double* dinv, double* y,
+                        double omega);
+void launch_pack(hipStream_t s, int64_t n, const int* idx, const double* x, double* out);
+void launch_sum_partials(hipStream_t s, int n, const double* partial, double* out);
+void launch_sum_ranks(hipStream_t s, int n, const double* in, double* out, bool take_sqrt);
+void launch_dense_gemv(hipStream_t s, int64_t n_local, int64_t n, const double* invT,
+                       const double* bfull, double* x);
+void launch_uniform(hipStream_t s, int64_t n, int64_t first_gid, uint64_t seed, double* out);
+void launch_zero(hipStream_t s, int64_t n, double* y);
+
+// ParCSRMatrix operations with halo exchange + interior/boundary overlap
+void par_apply(DevMatrix& A, int mode, const double* x, const double* b, double* y, double omega,
+               double* partial_or_null);
+void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block);
+// ||b - A x|| into dev_out[0] (device), deterministic; uses ctx scratch
+void par_residual_norm(DevMatrix& A, const double* x, const double* b, double* r, double* dev_out);
+
+struct Level {
+    std::unique_ptr<DevMatrix> A, P, R;
+    std::vector<int32_t> split;  // C/F or aggregate id (local rows)
+    DevBuf<double> x, b, r, t;
+};
+
+struct Solver {
+    Context* ctx = nullptr;
+    amg_options opt{};
+    std::vector<Level> levels;
+    DevMatrix* A0 = nullptr;  // borrowed fine matrix (levels[0].A is null)
+    // coarsest level: dense inverse rows of this rank, transposed: invT[j * n_local + i]
+    DevBuf<double> invT, bfull;
+    int64_t coarse_n = 0;
+    std::vector<int> coarse_counts, coarse_displs;
+    // solve state
+    DevBuf<double> hist;
+    bool use_graph = true;
+    hipGraphExec_t graph = nullptr;
+    const double* graph_x = nullptr;
+    const double* graph_b = nullptr;
+
+    DevMatrix& Amat(size_t l) { return l == 0 ? *A0 : *levels[l].A; }
+    void setup(DevMatrix& A, const amg_options& o);
+    void cycle(double* x, const double* b);
+    void cycle_rec(size_t l, double* x, const double* b, bool x_zero);
+    void smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_zero);
+    int64_t bytes_per_cycle(size_t l) const;
+    ~Solver();
+};
+
+}  // namespace amg

@@ -1,0 +1,155 @@
+// host.hpp -- host-side (CPU) part of the product: row-partitioned CSR, the setup-time
+// exchange layer and the AMG setup algorithms.
+//
+// Everything here works on the rank-local rows of a row-partitioned matrix with GLOBAL
+// column ids (int64), sorted ascending per row.  Keeping global column order everywhere
+// makes every row sum partition-independent: 1, 2, 4 or 8 ranks produce bit-identical
+// hierarchies (integer AND fp64), and the same bits as the serial oracle.
+//
+// The setup exchange goes through HostComm::alltoallv (a C callback supplied over the
+// C-ABI, torch.distributed/gloo in the Python host layer); the solve-time data path never
+// touches it (RCCL, see device.hpp).
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/raptor_amd.h"
+
+namespace amg {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+#define AMG_CHECK(cond, msg)                                                              \
+    do {                                                                                  \
+        if (!(cond)) throw ::amg::Error(AMG_ERR_INVALID, std::string(msg));               \
+    } while (0)
+#define AMG_ASSERT(cond)                                                                  \
+    do {                                                                                  \
+        if (!(cond))                                                                      \
+            throw ::amg::Error(AMG_ERR_INTERNAL, std::string("invariant failed: ") + #cond \
+                                                     + " at " + __FILE__ + ":" +           \
+                                                     std::to_string(__LINE__));           \
+    } while (0)
+
+// ---------------------------------------------------------------------------------
+// Setup-time communicator: rank/nranks + an all-to-all-v byte callback.
+// ---------------------------------------------------------------------------------
+struct HostComm {
+    int rank = 0, nranks = 1;
+    amg_alltoallv_fn fn = nullptr;
+    void* user = nullptr;
+
+    void alltoallv(const void* send, const std::vector<int64_t>& sbytes, void* recv,
+                   const std::vector<int64_t>& rbytes) const;
+    // every rank sends counts[r] to rank r; returns what each rank sent to us
+    std::vector<int64_t> alltoall_counts(const std::vector<int64_t>& counts) const;
+    // typed variable all-to-all: send[r] goes to rank r
+    template <class T>
+    std::vector<std::vector<T>> exchange(const std::vector<std::vector<T>>& send) const;
+    std::vector<int64_t> allgather(int64_t v) const;
+    std::vector<double> allgather(double v) const;
+    int64_t allreduce_sum(int64_t v) const;
+    double allreduce_max(double v) const;
+};
+
+// ---------------------------------------------------------------------------------
+// Rank-local rows of a row-partitioned CSR matrix (ParCSRMatrix host image, row a1).
+// ---------------------------------------------------------------------------------
+struct HostCSR {
+    int64_t n_global_rows = 0, n_global_cols = 0;
+    std::vector<int64_t> row_starts;  // nranks+1: global row partition
+    std::vector<int64_t> col_starts;  // nranks+1: partition of the column space (x owners)
+    std::vector<int64_t> rp;          // n_local+1
+    std::vector<int64_t> col;         // global column ids, ascending per row
+    std::vector<double> val;
+
+    int64_t first_row(int rank) const { return row_starts[rank]; }
+    int64_t n_local(int rank) const { return row_starts[rank + 1] - row_starts[rank]; }
+    int64_t nrows() const { return (int64_t)rp.size() - 1; }
+    int64_t nnz() const { return rp.empty() ? 0 : rp.back(); }
+};
+
+// owner of global id g under a contiguous partition
+int owner_of(const std::vector<int64_t>& starts, int64_t g);
+
+// ---------------------------------------------------------------------------------
+// Halo plan (ParComm): which off-process ids this rank receives and which local ids it
+// sends.  Built collectively from the set of needed global ids (row a11).
+// ---------------------------------------------------------------------------------
+struct HaloPlan {
+    std::vector<int64_t> halo_gid;     // sorted ascending (=> grouped by owner)
+    std::vector<int> recv_procs;       // owners, ascending
+    std::vector<int64_t> recv_ptr;     // recv_procs.size()+1 into halo_gid
+    std::vector<int> send_procs;       // destinations, ascending
+    std::vector<int64_t> send_ptr;     // send_procs.size()+1 into send_idx
+    std::vector<int64_t> send_idx;     // local indices (gid - owner start)
+
+    int64_t n_halo() const { return (int64_t)halo_gid.size(); }
+    // index of gid in halo_gid (binary search), -1 if absent
+    int64_t find(int64_t gid) const;
+
+    template <class T>
+    void forward(const HostComm& comm, const T* local, T* halo) const;
+};
+
+HaloPlan build_halo_plan(const HostComm& comm, const std::vector<int64_t>& starts,
+                         std::vector<int64_t> needed_gids);
+// halo plan for the off-process columns of A (columns partitioned by A.col_starts)
+HaloPlan halo_plan_for_cols(const HostComm& comm, const HostCSR& A);
+
+// ghost rows of B for plan.halo_gid (B rows partitioned like plan's partition)
+struct GhostRows {
+    std::vector<int64_t> rp, col;
+    std::vector<double> val;
+};
+GhostRows fetch_rows(const HostComm& comm, const HaloPlan& plan, const HostCSR& B);
+
+// ---------------------------------------------------------------------------------
+// Setup algorithms (identical definitions to the oracle).
+// ---------------------------------------------------------------------------------
+HostCSR transpose(const HostComm& comm, const HostCSR& P);
+HostCSR spgemm(const HostComm& comm, const HostCSR& A, const HostCSR& B);
+std::vector<double> diagonal(const HostComm& comm, const HostCSR& A);  // local rows
+HostCSR strength_classical(const HostComm& comm, const HostCSR& A, double theta);
+HostCSR strength_symmetric(const HostComm& comm, const HostCSR& A, double theta);
+std::vector<int32_t> rs_split(const HostComm& comm, const HostCSR& S);
+std::vector<int32_t> pmis_split(const HostComm& comm, const HostCSR& S, uint64_t seed);
+HostCSR interp_classical(const HostComm& comm, const HostCSR& A, const HostCSR& S,
+                         const std::vector<int32_t>& cf);
+// returns global aggregate id per local row; *n_agg_global receives the count
+std::vector<int64_t> mis2_aggregate(const HostComm& comm, const HostCSR& S, uint64_t seed,
+                                    int64_t* n_agg_global, std::vector<int64_t>* agg_starts);
+HostCSR sa_prolongator(const HostComm& comm, const HostCSR& A, const std::vector<int64_t>& agg,
+                       int64_t n_agg, const std::vector<int64_t>& agg_starts);
+// Gauss-Jordan inverse of the whole (gathered) coarsest matrix, row-major n*n
+std::vector<double> dense_inverse_gathered(const HostComm& comm, const HostCSR& A);
+
+// model problems: this rank's slab (rows split evenly by planes)
+HostCSR stencil_slab(const HostComm& comm, int kind, int64_t nx, int64_t ny, int64_t nz,
+                     const double* eps3);
+
+// Whole hierarchy on the host (rows a7-a10): level l holds A_l (l >= 1), P_l, R_l and the
+// integer splitting; the coarsest level's gathered dense inverse.  Same stopping rule and
+// per-level seeds/thresholds as the oracle.
+struct HostLevel {
+    HostCSR A;  // empty for level 0 (the caller's matrix)
+    HostCSR P, R;
+    std::vector<int32_t> split;
+};
+struct HostHierarchy {
+    std::vector<HostLevel> levels;
+    std::vector<double> coarse_inv;  // row-major n_c x n_c
+    const HostCSR* A0 = nullptr;
+    const HostCSR& A(size_t l) const { return l == 0 ? *A0 : levels[l].A; }
+};
+void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options& opt,
+                     HostHierarchy& H);
+
+uint64_t mix64(uint64_t z);
+uint32_t hash32(int64_t gid, uint64_t seed);
+
+}  // namespace amg

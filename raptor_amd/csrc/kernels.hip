@@ -1,0 +1,368 @@
+// kernels.hip -- hand-written gfx950 kernels for the AMG level operations.
+// SURVEY.md 8a rows a2-a6; DESIGN.md section 4 (layout, rooflines).
+//
+// CSR-stream SpMV family (HBM-bound, AI ~0.13 flop/B; no MFMA):
+//   one 256-thread workgroup per row block of <= kCAP nonzeros and <= 256 rows;
+//   phase 1: the workgroup streams the block's col/val ranges with consecutive lanes on
+//            consecutive nonzeros (fully coalesced, nontemporal: each byte is read once),
+//            gathers x (L2 / Infinity-Cache resident) and stages products in LDS;
+//   phase 2: one lane per row sums its products sequentially in CSR order and applies the
+//            fused epilogue (SpMV, y += Ax, residual, Jacobi).
+// Products are rounded and summed exactly as the oracle does (-ffp-contract=off), so the
+// kernels are bit-identical to oracle/amg_oracle.c.
+#include <hip/hip_runtime.h>
+
+#include "device.hpp"
+
+namespace amg {
+
+namespace {
+
+struct CsrArgs {
+    const int2* blocks;
+    const int* rp;
+    const int* col;
+    const double* val;
+    const double* x;   // local part of x
+    const double* xh;  // halo part of x
+    int ncl;           // number of local columns
+    const double* b;
+    const double* dinv;
+    double* y;
+    double omega;
+    double* partial;
+};
+
+__device__ __forceinline__ double xload(const CsrArgs& a, int c) {
+    const double* p = c < a.ncl ? a.x + c : a.xh + (c - a.ncl);
+    return *p;
+}
+
+template <int MODE>
+__device__ __forceinline__ double epilogue(const CsrArgs& a, int r, double s) {
+    if (MODE == KM_SPMV) return s;
+    if (MODE == KM_SPMV_ADD) return a.y[r] + s;
+    if (MODE == KM_RESID) return a.b[r] - s;
+    // Jacobi: x + omega * (dinv * (b - s))
+    return a.x[r] + a.omega * (a.dinv[r] * (a.b[r] - s));
+}
+
+template <int MODE, bool NORM>
+__global__ __launch_bounds__(kTPB) void csr_stream_kernel(CsrArgs a, int first_block) {
+    __shared__ double prod[kCAP];
+    __shared__ double red[kTPB / 64];
+    const int bid = first_block + blockIdx.x;
+    const int2 br = a.blocks[bid];
+    const int r0 = br.x, r1 = br.y;
+    const int k0 = a.rp[r0];
+    const int nnz = a.rp[r1] - k0;
+    const int tid = threadIdx.x;
+    double sq = 0.0;
+    if (nnz <= kCAP) {
+        constexpr int U = kCAP / kTPB;  // 8 nonzeros per lane
+        int c[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int k = tid + u * kTPB;
+            if (k < nnz) {
+                c[u] = __builtin_nontemporal_load(a.col + k0 + k);
+                v[u] = __builtin_nontemporal_load(a.val + k0 + k);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int k = tid + u * kTPB;
+            if (k < nnz) prod[k] = v[u] * xload(a, c[u]);
+        }
+        __syncthreads();
+        for (int r = r0 + tid; r < r1; r += kTPB) {
+            const int e0 = a.rp[r] - k0, e1 = a.rp[r + 1] - k0;
+            double s = 0.0;
+            for (int k = e0; k < e1; ++k) s += prod[k];
+            double out = epilogue<MODE>(a, r, s);
+            a.y[r] = out;
+            if (NORM) sq += out * out;
+        }
+    } else {
+        // one row longer than the LDS stage: chunked, summed by lane 0 in CSR order
+        double s = 0.0;
+        for (int base = 0; base < nnz; base += kCAP) {
+            const int cnt = min(kCAP, nnz - base);
+            for (int k = tid; k < cnt; k += kTPB)
+                prod[k] = a.val[k0 + base + k] * xload(a, a.col[k0 + base + k]);
+            __syncthreads();
+            if (tid == 0)
+                for (int k = 0; k < cnt; ++k) s += prod[k];
+            __syncthreads();
+        }
+        if (tid == 0) {
+            double out = epilogue<MODE>(a, r0, s);
+            a.y[r0] = out;
+            if (NORM) sq = out * out;
+        }
+    }
+    if (NORM) {
+        // fixed-shape reduction: wave butterfly then 4 wave sums in order
+        for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
+        if ((tid & 63) == 0) red[tid >> 6] = sq;
+        __syncthreads();
+        if (tid == 0) a.partial[bid] = (red[0] + red[1]) + (red[2] + red[3]);
+    }
+}
+
+// Hybrid Gauss-Seidel (row a5).  Workgroup = whole GS chunks (global row multiples of B)
+// with <= kCAP nonzeros, <= 256 rows.  Phase 1 stages a_ij * x_old_j; phase 2 (lane per
+// row) subtracts the "old" terms in CSR order and marks the in-chunk lower entries
+// (contiguous just before the diagonal because columns are sorted); phase 3 (lane per
+// chunk) runs the short dependency chain in LDS.  Oversized chunks: lane 0 of the
+// workgroup walks them exactly like the oracle.
+struct GsArgs {
+    const int2* blocks;
+    const int* rp;
+    const int* col;
+    const double* val;
+    const double* x;
+    const double* xh;
+    int ncl;
+    const double* b;
+    const double* dinv;
+    double* y;
+    long long first_row;
+    long long B;
+};
+
+__device__ __forceinline__ int chunk_start(const GsArgs& a, int r) {
+    long long g = a.first_row + r;
+    long long cs = (g / a.B) * a.B - a.first_row;
+    return cs < 0 ? 0 : (int)cs;
+}
+
+__global__ __launch_bounds__(kTPB) void hybrid_gs_kernel(GsArgs a) {
+    __shared__ double prod[kCAP];
+    __shared__ int lcl[kCAP];
+    __shared__ double sacc[kTPB];
+    __shared__ double xnew[kTPB];
+    __shared__ int lob[kTPB], loe[kTPB];
+    const int2 br = a.blocks[blockIdx.x];
+    const int r0 = br.x, r1 = br.y;
+    const int k0 = a.rp[r0];
+    const int nnz = a.rp[r1] - k0;
+    const int tid = threadIdx.x;
+    if (nnz > kCAP || r1 - r0 > kTPB) {
+        if (tid != 0) return;
+        for (int r = r0; r < r1; ++r) {
+            const int cs = chunk_start(a, r);
+            double acc = a.b[r];
+            for (int k = a.rp[r]; k < a.rp[r + 1]; ++k) {
+                int c = a.col[k];
+                if (c == r || (c >= cs && c < r)) continue;
+                acc -= a.val[k] * (c < a.ncl ? a.x[c] : a.xh[c - a.ncl]);
+            }
+            for (int k = a.rp[r]; k < a.rp[r + 1]; ++k) {
+                int c = a.col[k];
+                if (c >= cs && c < r) acc -= a.val[k] * a.y[c];
+            }
+            a.y[r] = acc * a.dinv[r];
+        }
+        return;
+    }
+    for (int k = tid; k < nnz; k += kTPB) {
+        int c = __builtin_nontemporal_load(a.col + k0 + k);
+        double v = __builtin_nontemporal_load(a.val + k0 + k);
+        const double* p = c < a.ncl ? a.x + c : a.xh + (c - a.ncl);
+        prod[k] = v * *p;
+        lcl[k] = c;
+    }
+    __syncthreads();
+    for (int r = r0 + tid; r < r1; r += kTPB) {
+        const int cs = chunk_start(a, r);
+        const int e0 = a.rp[r] - k0, e1 = a.rp[r + 1] - k0;
+        double acc = a.b[r];
+        int lb = -1, le = -1;
+        for (int k = e0; k < e1; ++k) {
+            int c = lcl[k];
+            if (c == r) continue;
+            if (c >= cs && c < r) {
+                if (lb < 0) lb = k;
+                le = k + 1;
+                prod[k] = a.val[k0 + k];  // keep a_ij for the chain
+                continue;
+            }
+            acc -= prod[k];
+        }
+        sacc[r - r0] = acc;
+        lob[r - r0] = lb;
+        loe[r - r0] = le;
+    }
+    __syncthreads();
+    // chains: lane t walks chunk t of this block
+    const long long g0 = (a.first_row + r0) / a.B;
+    const long long gl = (a.first_row + r1 - 1) / a.B;
+    if (tid <= gl - g0) {
+        const long long g = g0 + tid;
+        long long cb = g * a.B - a.first_row, ce = cb + a.B;
+        const int rb = (int)(cb < r0 ? r0 : cb), re = (int)(ce > r1 ? r1 : ce);
+        for (int r = rb; r < re; ++r) {
+            double acc = sacc[r - r0];
+            const int lb = lob[r - r0], le = loe[r - r0];
+            for (int k = lb; k < le && lb >= 0; ++k) acc -= prod[k] * xnew[lcl[k] - r0];
+            const double xn = acc * a.dinv[r];
+            xnew[r - r0] = xn;
+            a.y[r] = xn;
+        }
+    }
+}
+
+__global__ void jacobi_zero_kernel(long long n, const double* b, const double* dinv, double* y,
+                                   double omega) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long stride = (long long)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) y[i] = omega * (dinv[i] * b[i]);
+}
+
+__global__ void pack_kernel(long long n, const int* idx, const double* x, double* out) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = x[idx[i]];
+}
+
+__global__ void zero_kernel(long long n, double* y) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long stride = (long long)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) y[i] = 0.0;
+}
+
+// deterministic sum of n partials: each lane sums a fixed strided subset, then a fixed
+// shuffle tree and 4 wave sums in order
+__global__ __launch_bounds__(kTPB) void sum_partials_kernel(int n, const double* p, double* out) {
+    __shared__ double red[kTPB / 64];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < n; i += kTPB) s += p[i];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) *out = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// sum of per-rank sums in rank order (identical on every rank); optional sqrt
+__global__ void sum_ranks_kernel(int n, const double* in, double* out, int take_sqrt) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        double s = 0.0;
+        for (int i = 0; i < n; ++i) s += in[i];
+        *out = take_sqrt ? sqrt(s) : s;
+    }
+}
+
+// coarsest level: x_i = sum_j inv_ij * b_j, sequential j per lane (bit-identical to the
+// oracle); invT is stored column-major for coalesced lanes
+__global__ void dense_gemv_kernel(long long nl, long long n, const double* invT,
+                                  const double* bfull, double* x) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    double s = 0.0;
+    for (long long j = 0; j < n; ++j) s += invT[j * nl + i] * bfull[j];
+    x[i] = s;
+}
+
+__device__ __forceinline__ unsigned long long dmix64(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void uniform_kernel(long long n, long long first, unsigned long long seed, double* out) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long stride = (long long)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) {
+        unsigned long long u = dmix64(seed * 0xD1B54A32D192ED03ull + (unsigned long long)(first + i));
+        out[i] = (double)(u >> 11) * 0x1.0p-52 - 1.0;
+    }
+}
+
+inline int grid_for(long long n, int tpb = kTPB) {
+    long long g = (n + tpb - 1) / tpb;
+    if (g > 256 * 16) g = 256 * 16;
+    return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+
+void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, int first_block,
+                       int n_blocks, const double* x, const double* b, double* y, double omega,
+                       double* partial) {
+    if (n_blocks <= 0) return;
+    CsrArgs a{A.blocks.p, A.rp.p, A.col.p, A.val.p, x, A.halo.p, (int)A.n_cols_local,
+              b, A.dinv.p, y, omega, partial};
+    dim3 g(n_blocks), t(kTPB);
+#define AMG_L(M, N) hipLaunchKernelGGL((csr_stream_kernel<M, N>), g, t, 0, s, a, first_block)
+    switch (mode) {
+        case KM_SPMV: AMG_L(KM_SPMV, false); break;
+        case KM_SPMV_ADD: AMG_L(KM_SPMV_ADD, false); break;
+        case KM_RESID:
+            if (norm) AMG_L(KM_RESID, true);
+            else AMG_L(KM_RESID, false);
+            break;
+        case KM_JACOBI: AMG_L(KM_JACOBI, false); break;
+        default: throw Error(AMG_ERR_INTERNAL, "bad kernel mode");
+    }
+#undef AMG_L
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
+                      double* y) {
+    if (A.n_gs_blocks <= 0) return;
+    GsArgs a{A.gs_blocks.p, A.rp.p, A.col.p, A.val.p, x, A.halo.p, (int)A.n_cols_local,
+             b, A.dinv.p, y, (long long)A.first_row, (long long)A.gs_block};
+    hipLaunchKernelGGL(hybrid_gs_kernel, dim3(A.n_gs_blocks), dim3(kTPB), 0, s, a);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_jacobi_zero(hipStream_t s, int64_t n, const double* b, const double* dinv, double* y,
+                        double omega) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(jacobi_zero_kernel, dim3(grid_for(n)), dim3(kTPB), 0, s, (long long)n, b,
+                       dinv, y, omega);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_pack(hipStream_t s, int64_t n, const int* idx, const double* x, double* out) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((n + kTPB - 1) / kTPB)), dim3(kTPB), 0, s,
+                       (long long)n, idx, x, out);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_zero(hipStream_t s, int64_t n, double* y) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(zero_kernel, dim3(grid_for(n)), dim3(kTPB), 0, s, (long long)n, y);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_sum_partials(hipStream_t s, int n, const double* partial, double* out) {
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(kTPB), 0, s, n, partial, out);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_sum_ranks(hipStream_t s, int n, const double* in, double* out, bool take_sqrt) {
+    hipLaunchKernelGGL(sum_ranks_kernel, dim3(1), dim3(64), 0, s, n, in, out, take_sqrt ? 1 : 0);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_dense_gemv(hipStream_t s, int64_t n_local, int64_t n, const double* invT,
+                       const double* bfull, double* x) {
+    if (n_local <= 0) return;
+    hipLaunchKernelGGL(dense_gemv_kernel, dim3((unsigned)((n_local + 63) / 64)), dim3(64), 0, s,
+                       (long long)n_local, (long long)n, invT, bfull, x);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_uniform(hipStream_t s, int64_t n, int64_t first_gid, uint64_t seed, double* out) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(uniform_kernel, dim3(grid_for(n)), dim3(kTPB), 0, s, (long long)n,
+                       (long long)first_gid, (unsigned long long)seed, out);
+    HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace amg

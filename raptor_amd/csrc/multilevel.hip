@@ -1,0 +1,190 @@
+// multilevel.hip -- ParMultilevel: hierarchy setup (host, distributed) and the GPU V-cycle.
+// SURVEY.md 8a rows a6-a10.  The cycle mirrors oracle/amg_oracle.c cycle_rec() operation
+// for operation, so the iterates are bit-identical to the oracle's.
+#include <cmath>
+
+#include "device.hpp"
+
+namespace amg {
+
+Solver::~Solver() {
+    if (graph) (void)hipGraphExecDestroy(graph);
+}
+
+void Solver::setup(DevMatrix& A, const amg_options& o) {
+    AMG_CHECK(A.square, "AMG setup needs a square matrix");
+    AMG_CHECK(o.pre_sweeps >= 0 && o.post_sweeps >= 0, "negative sweep count");
+    AMG_CHECK(o.max_levels >= 1, "max_levels must be >= 1");
+    AMG_CHECK(o.smoother == AMG_SMOOTH_JACOBI || o.smoother == AMG_SMOOTH_HYBRID_GS, "bad smoother");
+    ctx = A.ctx;
+    opt = o;
+    A0 = &A;
+    const HostComm& comm = ctx->host;
+    HostHierarchy H;
+    build_hierarchy(comm, A.host, opt, H);
+    levels.clear();
+    levels.resize(H.levels.size());
+    for (size_t l = 0; l < H.levels.size(); ++l) {
+        HostLevel& hl = H.levels[l];
+        if (l > 0) {
+            levels[l].A.reset(new DevMatrix());
+            levels[l].A->build(ctx, std::move(hl.A));
+        }
+        if (l + 1 < H.levels.size()) {
+            levels[l].split = std::move(hl.split);
+            levels[l].P.reset(new DevMatrix());
+            levels[l].P->build(ctx, std::move(hl.P));
+            levels[l].R.reset(new DevMatrix());
+            levels[l].R->build(ctx, std::move(hl.R));
+        }
+    }
+    // per-level work vectors
+    size_t max_blocks = 0;
+    for (size_t l = 0; l < levels.size(); ++l) {
+        DevMatrix& Al = Amat(l);
+        const size_t n = (size_t)Al.n_rows;
+        if (l > 0) {
+            levels[l].x.alloc(n);
+            levels[l].b.alloc(n);
+        }
+        levels[l].r.alloc(n);
+        levels[l].t.alloc(n);
+        max_blocks = std::max(max_blocks, (size_t)(Al.nb_int + Al.nb_bnd));
+        if (opt.smoother == AMG_SMOOTH_HYBRID_GS) Al.ensure_gs_blocks(opt.gs_block);
+    }
+    const size_t need = max_blocks + 2 * (size_t)comm.nranks + 8;
+    if (ctx->scratch.n < need) ctx->scratch.alloc(need + 1024);
+    // coarsest level: gathered dense inverse, this rank's rows, column-major.  With several
+    // ranks b is allgathered into a padded [nranks x cmax] layout; invT has zero rows at the
+    // padding so the sum order over real entries is the global order j = 0..n-1.
+    DevMatrix& Ac = Amat(levels.size() - 1);
+    coarse_n = Ac.host.n_global_rows;
+    const std::vector<double>& inv = H.coarse_inv;
+    const int64_t nl = Ac.n_rows, f = Ac.first_row;
+    int64_t cmax = 0;
+    for (int r = 0; r < comm.nranks; ++r)
+        cmax = std::max(cmax, Ac.host.row_starts[r + 1] - Ac.host.row_starts[r]);
+    const int64_t npad = comm.nranks == 1 ? coarse_n : cmax * comm.nranks;
+    std::vector<double> invT((size_t)std::max<int64_t>(npad * nl, 1), 0.0);
+    for (int r = 0; r < comm.nranks; ++r)
+        for (int64_t j = Ac.host.row_starts[r]; j < Ac.host.row_starts[r + 1]; ++j) {
+            const int64_t jp = comm.nranks == 1 ? j : r * cmax + (j - Ac.host.row_starts[r]);
+            for (int64_t i = 0; i < nl; ++i) invT[jp * nl + i] = inv[(f + i) * coarse_n + j];
+        }
+    this->invT.upload(invT.data(), invT.size());
+    coarse_counts.assign(1, (int)cmax);
+    if (comm.nranks > 1) {
+        bfull.alloc((size_t)npad + (size_t)cmax);  // gathered + local padded send slot
+        HIP_CHECK(hipMemset(bfull.p, 0, bfull.n * sizeof(double)));
+    }
+    hist.alloc(1);
+    use_graph = comm.nranks == 1;
+}
+
+void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_zero) {
+    DevMatrix& A = Amat(l);
+    if (opt.smoother == AMG_SMOOTH_HYBRID_GS) {
+        if (x_zero) launch_zero(ctx->stream, A.n_rows, x);
+        par_hybrid_gs(A, x, b, tmp, opt.gs_block);
+    } else if (x_zero) {
+        launch_jacobi_zero(ctx->stream, A.n_rows, b, A.dinv.p, tmp, opt.jacobi_omega);
+    } else {
+        par_apply(A, KM_JACOBI, x, b, tmp, opt.jacobi_omega, nullptr);
+    }
+    std::swap(x, tmp);
+}
+
+void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero) {
+    DevMatrix& A = Amat(l);
+    hipStream_t s = ctx->stream;
+    const HostComm& comm = ctx->host;
+    if (l + 1 == levels.size()) {
+        const double* bf = b;
+        if (comm.nranks > 1) {
+            const int64_t cmax = coarse_counts[0];
+            double* slot = bfull.p + cmax * comm.nranks;
+            if (A.n_rows > 0)
+                HIP_CHECK(hipMemcpyAsync(slot, b, A.n_rows * sizeof(double), hipMemcpyDeviceToDevice, s));
+            NCCL_CHECK(ncclAllGather(slot, bfull.p, (size_t)cmax, ncclDouble, ctx->nccl, s));
+            bf = bfull.p;
+            launch_dense_gemv(s, A.n_rows, cmax * comm.nranks, invT.p, bf, x);
+        } else {
+            launch_dense_gemv(s, A.n_rows, coarse_n, invT.p, bf, x);
+        }
+        return;
+    }
+    Level& L = levels[l];
+    double* cur = x;
+    double* tmp = L.t.p;
+    bool zero = x_zero;
+    for (int k = 0; k < opt.pre_sweeps; ++k) {
+        smooth(l, cur, b, tmp, zero);
+        zero = false;
+    }
+    if (zero) launch_zero(s, A.n_rows, cur);
+    par_apply(A, KM_RESID, cur, b, L.r.p, 0.0, nullptr);
+    Level& C = levels[l + 1];
+    par_apply(*L.R, KM_SPMV, L.r.p, nullptr, C.b.p, 0.0, nullptr);
+    cycle_rec(l + 1, C.x.p, C.b.p, true);
+    par_apply(*L.P, KM_SPMV_ADD, C.x.p, nullptr, cur, 0.0, nullptr);
+    for (int k = 0; k < opt.post_sweeps; ++k) smooth(l, cur, b, tmp, false);
+    if (cur != x)
+        HIP_CHECK(hipMemcpyAsync(x, cur, A.n_rows * sizeof(double), hipMemcpyDeviceToDevice, s));
+}
+
+void Solver::cycle(double* x, const double* b) {
+    if (!use_graph) {
+        cycle_rec(0, x, b, false);
+        return;
+    }
+    hipStream_t s = ctx->stream;
+    if (!graph || graph_x != x || graph_b != b) {
+        if (graph) HIP_CHECK(hipGraphExecDestroy(graph));
+        graph = nullptr;
+        hipGraph_t g = nullptr;
+        HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        try {
+            cycle_rec(0, x, b, false);
+        } catch (...) {
+            (void)hipStreamEndCapture(s, &g);
+            if (g) (void)hipGraphDestroy(g);
+            throw;
+        }
+        HIP_CHECK(hipStreamEndCapture(s, &g));
+        HIP_CHECK(hipGraphInstantiate(&graph, g, nullptr, nullptr, 0));
+        HIP_CHECK(hipGraphDestroy(g));
+        graph_x = x;
+        graph_b = b;
+    }
+    HIP_CHECK(hipGraphLaunch(graph, s));
+}
+
+static int64_t spmv_bytes(const DevMatrix& M) {
+    return 12 * M.nnz + 4 * (M.n_rows + 1) + 8 * M.n_cols_local + 8 * M.n_rows;
+}
+
+int64_t Solver::bytes_per_cycle(size_t l) const {
+    const DevMatrix& A = const_cast<Solver*>(this)->Amat(l);
+    const int64_t n = A.n_rows;
+    if (l + 1 == levels.size()) return 8 * coarse_n * n + 8 * coarse_n + 8 * n;
+    const int64_t base = 12 * A.nnz + 4 * (n + 1);
+    const int64_t jac = base + 32 * n;
+    int64_t b = 0;
+    bool zero = l > 0;
+    int64_t sweeps = 0;
+    for (int k = 0; k < opt.pre_sweeps; ++k, ++sweeps) {
+        if (zero && opt.smoother == AMG_SMOOTH_JACOBI) b += 24 * n;
+        else b += jac + (zero ? 8 * n : 0);
+        zero = false;
+    }
+    if (zero) b += 8 * n;
+    b += base + 24 * n;                                   // residual
+    b += spmv_bytes(*levels[l].R);                        // restriction
+    b += spmv_bytes(*levels[l].P) + 8 * n;                // interpolation (reads x)
+    b += opt.post_sweeps * jac;
+    sweeps += opt.post_sweeps;
+    if (sweeps % 2 == 1) b += 16 * n;                     // copy back
+    return b;
+}
+
+}  // namespace amg

@@ -1,0 +1,186 @@
+// par_matrix.hip -- ParCSRMatrix on the GPU.
+//
+// Layout in HBM: rank-local rows, int32 row_ptr, int32 column ids
+// renumbered [0, n_cols_local) local | [n_cols_local, +n_halo) halo, fp64 values, fp64
+// 1/a_ii.  Columns stay in ascending GLOBAL order inside a row, so row sums are identical
+// for any partition.  Row blocks are split into "interior" (no halo column) and
+// "boundary" lists: the interior kernel runs while RCCL moves the halo on a second
+// stream; the boundary kernel runs after the halo event.
+#include <algorithm>
+#include <climits>
+
+#include "device.hpp"
+
+namespace amg {
+
+Context::~Context() {
+    if (nccl) (void)ncclCommDestroy(nccl);
+    if (ev_pack) (void)hipEventDestroy(ev_pack);
+    if (ev_halo) (void)hipEventDestroy(ev_halo);
+    if (comm_stream) (void)hipStreamDestroy(comm_stream);
+    if (own_stream && stream) (void)hipStreamDestroy(stream);
+}
+
+static void build_row_blocks(const std::vector<int>& rp, const std::vector<uint8_t>& cls,
+                             std::vector<int2>& inter, std::vector<int2>& bnd) {
+    const int n = (int)rp.size() - 1;
+    int r0 = 0;
+    long long acc = 0;
+    auto emit = [&](int a, int b) {
+        if (b <= a) return;
+        (cls[a] ? bnd : inter).push_back(make_int2(a, b));
+    };
+    for (int r = 0; r < n; ++r) {
+        const long long len = rp[r + 1] - rp[r];
+        if (r > r0 && (cls[r] != cls[r0] || acc + len > kCAP || r - r0 >= kTPB)) {
+            emit(r0, r);
+            r0 = r;
+            acc = 0;
+        }
+        acc += len;
+    }
+    emit(r0, n);
+}
+
+void DevMatrix::build(Context* c, HostCSR&& h) {
+    ctx = c;
+    host = std::move(h);
+    const HostComm& comm = ctx->host;
+    AMG_CHECK((int)host.row_starts.size() == comm.nranks + 1, "matrix row partition size");
+    AMG_CHECK((int)host.col_starts.size() == comm.nranks + 1, "matrix column partition size");
+    first_row = host.row_starts[comm.rank];
+    n_rows = host.nrows();
+    AMG_CHECK(n_rows == host.row_starts[comm.rank + 1] - first_row, "local row count mismatch");
+    first_col = host.col_starts[comm.rank];
+    n_cols_local = host.col_starts[comm.rank + 1] - first_col;
+    nnz = host.nnz();
+    AMG_CHECK(nnz < INT_MAX && n_rows < INT_MAX, "local matrix exceeds int32 indexing");
+    square = host.n_global_rows == host.n_global_cols && host.row_starts == host.col_starts;
+    plan = halo_plan_for_cols(comm, host);
+    AMG_CHECK(n_cols_local + plan.n_halo() < INT_MAX, "too many columns for int32");
+
+    std::vector<int> hrp(n_rows + 1), hcol(nnz);
+    std::vector<uint8_t> cls(n_rows, 0);
+    for (int64_t i = 0; i <= n_rows; ++i) hrp[i] = (int)host.rp[i];
+    const int64_t clo = first_col, chi = first_col + n_cols_local;
+    for (int64_t i = 0; i < n_rows; ++i) {
+        uint8_t b = 0;
+        for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) {
+            const int64_t g = host.col[k];
+            if (g >= clo && g < chi) {
+                hcol[k] = (int)(g - clo);
+            } else {
+                hcol[k] = (int)(n_cols_local + plan.find(g));
+                b = 1;
+            }
+        }
+        cls[i] = b;
+    }
+    rp.upload(hrp.data(), hrp.size());
+    col.upload(hcol.data(), hcol.size());
+    val.upload(host.val.data(), host.val.size());
+    if (square) {
+        std::vector<double> d = diagonal(comm, host), di(n_rows);
+        for (int64_t i = 0; i < n_rows; ++i) di[i] = 1.0 / d[i];
+        dinv.upload(di.data(), di.size());
+    }
+    std::vector<int2> bi, bb;
+    build_row_blocks(hrp, cls, bi, bb);
+    nb_int = (int)bi.size();
+    nb_bnd = (int)bb.size();
+    bi.insert(bi.end(), bb.begin(), bb.end());
+    blocks.upload(bi.data(), bi.size());
+    std::vector<int> sidx(plan.send_idx.begin(), plan.send_idx.end());
+    send_idx.upload(sidx.data(), sidx.size());
+    send_buf.alloc(sidx.size());
+    halo.alloc(plan.n_halo());
+}
+
+void DevMatrix::ensure_gs_blocks(int64_t B) {
+    AMG_CHECK(square, "hybrid GS needs a square matrix");
+    AMG_CHECK(B >= 1 && B <= kTPB, "hybrid GS block must be in [1, 256]");
+    if (gs_block == B && (n_gs_blocks > 0 || n_rows == 0)) return;
+    std::vector<int2> out;
+    const std::vector<int64_t>& hrp = host.rp;
+    if (n_rows > 0) {
+        int64_t q0 = first_row / B, q1 = (first_row + n_rows - 1) / B;
+        int64_t br = -1, be = -1, acc = 0;
+        for (int64_t q = q0; q <= q1; ++q) {
+            int64_t cb = std::max<int64_t>(0, q * B - first_row);
+            int64_t ce = std::min<int64_t>(n_rows, (q + 1) * B - first_row);
+            int64_t cn = hrp[ce] - hrp[cb];
+            if (br >= 0 && (acc + cn > kCAP || ce - br > kTPB)) {
+                out.push_back(make_int2((int)br, (int)be));
+                br = -1;
+            }
+            if (br < 0) br = cb, acc = 0;
+            be = ce;
+            acc += cn;
+        }
+        if (br >= 0) out.push_back(make_int2((int)br, (int)be));
+    }
+    gs_blocks.upload(out.data(), out.size());
+    n_gs_blocks = (int)out.size();
+    gs_block = B;
+}
+
+bool DevMatrix::halo_begin(const double* x) {
+    const HostComm& comm = ctx->host;
+    if (comm.nranks == 1) return false;
+    if (plan.send_idx.empty() && plan.halo_gid.empty()) return false;
+    hipStream_t s = ctx->stream, cs = ctx->comm_stream;
+    launch_pack(s, (int64_t)plan.send_idx.size(), send_idx.p, x, send_buf.p);
+    HIP_CHECK(hipEventRecord(ctx->ev_pack, s));
+    HIP_CHECK(hipStreamWaitEvent(cs, ctx->ev_pack, 0));
+    NCCL_CHECK(ncclGroupStart());
+    for (size_t p = 0; p < plan.send_procs.size(); ++p)
+        NCCL_CHECK(ncclSend(send_buf.p + plan.send_ptr[p], (size_t)(plan.send_ptr[p + 1] - plan.send_ptr[p]),
+                            ncclDouble, plan.send_procs[p], ctx->nccl, cs));
+    for (size_t p = 0; p < plan.recv_procs.size(); ++p)
+        NCCL_CHECK(ncclRecv(halo.p + plan.recv_ptr[p], (size_t)(plan.recv_ptr[p + 1] - plan.recv_ptr[p]),
+                            ncclDouble, plan.recv_procs[p], ctx->nccl, cs));
+    NCCL_CHECK(ncclGroupEnd());
+    HIP_CHECK(hipEventRecord(ctx->ev_halo, cs));
+    return true;
+}
+
+void DevMatrix::halo_wait() { HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_halo, 0)); }
+
+void par_apply(DevMatrix& A, int mode, const double* x, const double* b, double* y, double omega,
+               double* partial) {
+    if (mode == KM_JACOBI || mode == KM_RESID) AMG_CHECK(A.square, "Jacobi/residual need a square matrix");
+    const bool comm = A.halo_begin(x);
+    hipStream_t s = A.ctx->stream;
+    launch_csr_stream(s, mode, partial != nullptr, A, 0, A.nb_int, x, b, y, omega, partial);
+    if (comm) A.halo_wait();
+    launch_csr_stream(s, mode, partial != nullptr, A, A.nb_int, A.nb_bnd, x, b, y, omega, partial);
+}
+
+void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block) {
+    A.ensure_gs_blocks(block);
+    const bool comm = A.halo_begin(x);
+    if (comm) A.halo_wait();
+    launch_hybrid_gs(A.ctx->stream, A, x, b, y);
+}
+
+void par_residual_norm(DevMatrix& A, const double* x, const double* b, double* r, double* dev_out) {
+    Context* c = A.ctx;
+    const int nb = A.nb_int + A.nb_bnd;
+    const int nr = c->host.nranks;
+    size_t need = (size_t)nb + 2 * (size_t)nr + 8;
+    if (c->scratch.n < need) c->scratch.alloc(need + 1024);
+    double* partial = c->scratch.p;
+    double* local = partial + nb;
+    double* gathered = local + 1;
+    par_apply(A, KM_RESID, x, b, r, 0.0, partial);
+    if (nb > 0) launch_sum_partials(c->stream, nb, partial, local);
+    else launch_zero(c->stream, 1, local);
+    if (nr > 1) {
+        NCCL_CHECK(ncclAllGather(local, gathered, 1, ncclDouble, c->nccl, c->stream));
+        launch_sum_ranks(c->stream, nr, gathered, dev_out, true);
+    } else {
+        launch_sum_ranks(c->stream, 1, local, dev_out, true);
+    }
+}
+
+}  // namespace amg

@@ -1,0 +1,98 @@
+"""Host-only (CPU) view of the product's AMG setup: ``amg_host_hierarchy_*`` of the C-ABI.
+
+This is the exact setup code ``ParMultilevel.setup`` runs before uploading the hierarchy to
+the GPU, callable without a GPU so the CPU test suite can check
+it -- serial and multi-rank over gloo -- bit for bit against the oracle."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import ALLTOALLV_FN, Options, check, lib
+
+_WHICH = {"A": 0, "P": 1, "R": 2}
+_NULL_FN = ALLTOALLV_FN()
+
+
+class HostHierarchy:
+    def __init__(self, n_global, first_row, row_ptr, col, val, options: Options, rank=0,
+                 nranks=1, group=None):
+        rp = np.ascontiguousarray(row_ptr, np.int64)
+        cg = np.ascontiguousarray(col, np.int64)
+        v = np.ascontiguousarray(val, np.float64)
+        fn = _NULL_FN
+        if nranks > 1:
+            from ._comm import make_exchange
+
+            fn = make_exchange(group, nranks)
+        self._fn = fn
+        self.rank = rank
+        self.h = C.c_void_p()
+        i64 = C.POINTER(C.c_int64)
+        check(lib().amg_host_hierarchy_build(rank, nranks, fn, None, int(n_global), int(first_row),
+                                             rp.size - 1, rp.ctypes.data_as(i64),
+                                             cg.ctypes.data_as(i64),
+                                             v.ctypes.data_as(C.POINTER(C.c_double)),
+                                             C.byref(options), C.byref(self.h)))
+
+    @property
+    def num_levels(self):
+        n = C.c_int32()
+        check(lib().amg_host_hierarchy_num_levels(self.h, C.byref(n)))
+        return n.value
+
+    def sizes(self, level, which="A"):
+        s = np.zeros(5, np.int64)
+        check(lib().amg_host_hierarchy_level_size(self.h, level, _WHICH[which],
+                                                  s.ctypes.data_as(C.POINTER(C.c_int64))))
+        return dict(zip(("n_global_rows", "n_global_cols", "first_row", "n_local_rows",
+                         "nnz_local"), s.tolist()))
+
+    def export(self, level, which="A"):
+        sz = self.sizes(level, which)
+        rp = np.empty(sz["n_local_rows"] + 1, np.int64)
+        col = np.empty(sz["nnz_local"], np.int64)
+        val = np.empty(sz["nnz_local"], np.float64)
+        i64 = C.POINTER(C.c_int64)
+        check(lib().amg_host_hierarchy_level_export(self.h, level, _WHICH[which],
+                                                    rp.ctypes.data_as(i64), col.ctypes.data_as(i64),
+                                                    val.ctypes.data_as(C.POINTER(C.c_double))))
+        return rp, col, val, sz
+
+    def to_scipy(self, level, which="A"):
+        import scipy.sparse as sp
+
+        rp, col, val, sz = self.export(level, which)
+        return sp.csr_matrix((val, col, rp), shape=(sz["n_local_rows"], sz["n_global_cols"]))
+
+    def split(self, level):
+        n = self.sizes(level, "A")["n_local_rows"]
+        out = np.empty(n, np.int32)
+        check(lib().amg_host_hierarchy_level_split(self.h, level,
+                                                   out.ctypes.data_as(C.POINTER(C.c_int32))))
+        return out
+
+    def coarse_inverse(self):
+        n = self.sizes(self.num_levels - 1, "A")["n_global_rows"]
+        out = np.empty((n, n))
+        check(lib().amg_host_hierarchy_coarse_inverse(self.h,
+                                                      out.ctypes.data_as(C.POINTER(C.c_double))))
+        return out
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            try:
+                lib().amg_host_hierarchy_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+
+def options(coarsen="pmis", smoother="jacobi", strong_threshold=None, jacobi_omega=2.0 / 3.0,
+            pre_sweeps=1, post_sweeps=1, max_levels=25, max_coarse=256, gs_block=64, seed=0x5EED):
+    from . import ParMultilevel
+
+    return ParMultilevel(coarsen, smoother, strong_threshold, jacobi_omega, pre_sweeps,
+                         post_sweeps, max_levels, max_coarse, gs_block, seed).options

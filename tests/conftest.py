@@ -1,0 +1,32 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through the C-ABI)")
+    config.addinivalue_line("markers", "slow: full-size (BASELINE.json) property checks")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import oracle as O
+
+    O.lib()
+    return O
+
+
+@pytest.fixture(scope="session")
+def ctx():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import raptor_amd as ra
+
+    return ra.Context(0)

@@ -1,0 +1,212 @@
+"""GPU parity: the HIP level kernels and the V-cycle through the C-ABI against the CPU oracle.
+
+Bar: bit-identical for every kernel and every V-cycle iterate (both sides
+round each product and sum as written, same order); residual norms (different reduction
+order) within 1e-12 relative; solve histories within 1e-10 relative (BASELINE.json:5).
+Parity against Siddarthareddy1/raptor itself is unpinned (no AMG code in the reference)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from tests.util import oracle_levels, same_csr, to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+
+def _problems(O):
+    rng = np.random.default_rng(7)
+    # ragged random matrix: empty rows, variable row length, a dense-ish row > LDS stage
+    n = 3000
+    M = sp.random(n, n, density=0.002, random_state=11, format="lil")
+    M[5, :] = 0
+    M[17, :] = 0
+    M[100, :] = rng.standard_normal(n)  # 3000 nnz in one row: long-row path (kCAP = 2048)
+    M = (M + sp.eye(n) * 10.0).tocsr()
+    M.sort_indices()
+    return {
+        "7pt_20": O.gen_7pt(20, 20, 20),
+        "5pt_37x29": O.gen_5pt(37, 29),
+        "27pt_13": O.gen_27pt(13, 13, 13),
+        "ragged": O.Csr.from_scipy(M),
+    }
+
+
+@pytest.fixture(scope="module")
+def problems(oracle):
+    return _problems(oracle)
+
+
+def _dev_matrix(ra, ctx, Ao):
+    rp, col, val = Ao.arrays()
+    return ra.ParCSRMatrix.from_csr(ctx, Ao.shape[0], 0, rp, col, val)
+
+
+@pytest.mark.parametrize("name", ["7pt_20", "5pt_37x29", "27pt_13", "ragged"])
+def test_level_kernels_bit_exact(ctx, oracle, problems, name):
+    import raptor_amd as ra
+
+    O = oracle
+    Ao = problems[name]
+    A = _dev_matrix(ra, ctx, Ao)
+    n = Ao.shape[0]
+    x = O.vec_uniform(n, 3)
+    b = O.vec_uniform(n, 4)
+    y0 = O.vec_uniform(n, 5)
+    dx, db = to_dev(ctx, x), to_dev(ctx, b)
+    out = ctx.empty(n)
+    A.mult(dx, out)
+    assert np.array_equal(to_host(ctx, out), Ao.spmv(x))
+    dy = to_dev(ctx, y0)
+    A.mult_add(dx, dy)
+    assert np.array_equal(to_host(ctx, dy), Ao.spmv_add(x, y0))
+    A.residual(dx, db, out)
+    assert np.array_equal(to_host(ctx, out), Ao.residual(x, b))
+    A.jacobi(dx, db, out, 2.0 / 3.0)
+    assert np.array_equal(to_host(ctx, out), Ao.jacobi(x, b, 2.0 / 3.0))
+    for blk in (64, 17, 1, 256):
+        A.hybrid_gs(dx, db, out, blk)
+        assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs(x, b, blk)), blk
+    rn = A.residual_norm(dx, db)
+    ro = O.norm2(Ao.residual(x, b))
+    assert abs(rn - ro) <= 1e-12 * ro
+
+
+def test_empty_and_tiny(ctx, oracle):
+    import raptor_amd as ra
+
+    O = oracle
+    # 1x1 and a matrix whose rows are all empty except the diagonal
+    for n in (1, 2, 65):
+        M = sp.eye(n, format="csr") * 3.0
+        Ao = O.Csr.from_scipy(M)
+        A = _dev_matrix(ra, ctx, Ao)
+        x = O.vec_uniform(n, 9)
+        out = ctx.empty(n)
+        A.mult(to_dev(ctx, x), out)
+        assert np.array_equal(to_host(ctx, out), Ao.spmv(x))
+
+
+def test_bad_arguments_fail_loudly(ctx):
+    import raptor_amd as ra
+
+    with pytest.raises(ra.AmgError):
+        ra.ParCSRMatrix.from_csr(ctx, 3, 0, [0, 1, 2, 3], [0, 1, 5], [1.0, 1.0, 1.0])
+    with pytest.raises(ra.AmgError):
+        ra.ParCSRMatrix.from_csr(ctx, 3, 0, [0, 2, 2, 3], [1, 1, 2], [1.0, 1.0, 1.0])
+    A = ra.par_stencil_grid(ctx, "5pt", (4, 4))
+    x = ctx.zeros(16)
+    with pytest.raises(ra.AmgError):
+        A.hybrid_gs(x, x, x, 64)  # in-place GS refused
+    with pytest.raises(ra.AmgError):
+        A.hybrid_gs(x, x, ctx.zeros(16), 1000)  # block > 256
+
+
+CASES = [
+    ("7pt", (24, 24, 24), "pmis", "jacobi"),
+    ("5pt", (48, 40), "rs", "jacobi"),
+    ("27pt", (14, 14, 14), "sa", "hybrid_gs"),
+    ("7pt", (20, 18, 22), "sa", "hybrid_gs"),
+    ("5pt", (64, 64), "pmis", "hybrid_gs"),
+]
+
+
+@pytest.mark.parametrize("kind,dims,coarsen,smoother", CASES)
+def test_vcycle_bit_exact(ctx, oracle, kind, dims, coarsen, smoother):
+    """Product hierarchy == oracle hierarchy (bit-exact, integer + fp64) and GPU V-cycle
+    iterates == oracle iterates (bit-exact); residual history within 1e-10."""
+    import raptor_amd as ra
+
+    O = oracle
+    gen = {"7pt": O.gen_7pt, "5pt": O.gen_5pt, "27pt": O.gen_27pt}[kind]
+    Ao = gen(*dims)
+    A = ra.par_stencil_grid(ctx, kind, dims)
+    assert same_csr(A.to_scipy_local(), Ao.to_scipy())  # generators agree bit for bit
+    ml = ra.ParMultilevel(coarsen=coarsen, smoother=smoother).setup(A)
+    Ho = O.Hierarchy(Ao, coarsen={"rs": O.COARSEN_RS, "pmis": O.COARSEN_PMIS, "sa": O.COARSEN_SA}[coarsen],
+                     smoother={"jacobi": O.SMOOTH_JACOBI, "hybrid_gs": O.SMOOTH_HYBRID_GS}[smoother],
+                     strong_threshold=0.08 if coarsen == "sa" else 0.25)
+    assert ml.num_levels == Ho.num_levels >= 2
+    for l in range(ml.num_levels):
+        assert same_csr(ml.level_matrix(l, "A").to_scipy_local(), Ho.matrix(l, "A"))
+        if l + 1 < ml.num_levels:
+            assert same_csr(ml.level_matrix(l, "P").to_scipy_local(), Ho.matrix(l, "P"))
+            assert same_csr(ml.level_matrix(l, "R").to_scipy_local(), Ho.matrix(l, "R"))
+            assert np.array_equal(ml.level_split(l), Ho.split(l))
+    n = Ao.shape[0]
+    b = Ao.spmv(O.vec_uniform(n, 42))
+    db = to_dev(ctx, b)
+    dx = ctx.zeros(n)
+    xo = np.zeros(n)
+    for _ in range(3):
+        ml.cycle(dx, db)
+        xo = Ho.cycle(xo, b)
+        assert np.array_equal(to_host(ctx, dx), xo)
+    dx = ctx.zeros(n)
+    _, hist = ml.solve(dx, db, max_iter=8)
+    _, hist_o = Ho.solve(np.zeros(n), b, max_iter=8)
+    assert hist.shape == hist_o.shape
+    assert np.all(np.abs(hist - hist_o) <= 1e-10 * hist_o)
+    assert hist[-1] < hist[0]
+
+
+def test_graph_and_eager_agree(ctx, oracle):
+    import raptor_amd as ra
+
+    A = ra.par_stencil_grid(ctx, "7pt", (30, 30, 30))
+    n = A.local_rows
+    b = ra.vector_uniform(ctx, n, 0, 1)
+    res = []
+    for g in (True, False):
+        ml = ra.ParRugeStubenSolver(use_graph=g).setup(A)
+        x = ctx.zeros(n)
+        _, h = ml.solve(x, b, max_iter=5)
+        res.append((to_host(ctx, x), h))
+    assert np.array_equal(res[0][0], res[1][0])
+    assert np.array_equal(res[0][1], res[1][1])
+
+
+def test_solve_tolerance_stops(ctx):
+    import raptor_amd as ra
+
+    A = ra.par_stencil_grid(ctx, "5pt", (64, 64))
+    ml = ra.ParRugeStubenSolver(coarsen="rs").setup(A)
+    n = A.local_rows
+    b = ra.vector_uniform(ctx, n, 0, 2)
+    x = ctx.zeros(n)
+    _, h = ml.solve(x, b, max_iter=100, tol=1e-8)
+    assert h[-1] / h[0] < 1e-8 and len(h) < 101
+    assert np.all(h[1:-1] / h[0] >= 1e-8)
+
+
+@pytest.mark.slow
+def test_full_size_spmv_and_cycle_256(ctx, oracle):
+    """BASELINE.json configs[1] size: 7-pt 256^3 (117M nnz).  GPU SpMV bit-exact vs the
+    oracle at full size; A*1 equals the exact integer row sums; one full V-cycle iterate
+    bit-exact vs the oracle on the same hierarchy."""
+    import raptor_amd as ra
+
+    O = oracle
+    N = 256
+    A = ra.par_stencil_grid(ctx, "7pt", (N, N, N))
+    n = A.local_rows
+    ones = to_dev(ctx, np.ones(n))
+    y = ctx.empty(n)
+    A.mult(ones, y)
+    yh = to_host(ctx, y)
+    g = np.arange(n)
+    i, j, k = g % N, (g // N) % N, g // (N * N)
+    expect = ((i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (k == 0) + (k == N - 1)).astype(float)
+    assert np.array_equal(yh, expect)
+    x = O.vec_uniform(n, 77)
+    dx = to_dev(ctx, x)
+    A.mult(dx, y)
+    Ao = O.gen_7pt(N, N, N)
+    assert np.array_equal(to_host(ctx, y), Ao.spmv(x))
+    del Ao
+    ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
+    H = O.Hierarchy(None, levels=oracle_levels(O, ml))
+    b = to_host(ctx, y)
+    dx = ctx.zeros(n)
+    ml.cycle(dx, y)
+    xo = H.cycle(np.zeros(n), b)
+    assert np.array_equal(to_host(ctx, dx), xo)
