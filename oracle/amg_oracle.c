@@ -515,9 +515,10 @@ void orc_pmis_split(const orc_csr* S, uint64_t seed, int32_t* cf) {
 /* ------------------------------------------------------------------------------ */
 /* Classical (modified) interpolation, distance 1 (row a8).                          */
 /* F row i: C_i = strong C neighbours; d = a_ii + sum of weak a_ij (CSR order); for  */
-/* each strong F neighbour k (CSR order): s_k = sum_{m in C_i} a_km (row k order);  */
-/* s_k == 0 -> d += a_ik, else num_m += (a_ik * a_km) / s_k for m in C_i (row k     */
-/* order); num_j starts at a_ij.  w_ij = -num_j / d.  C row: 1 at its coarse index. */
+/* each strong F neighbour k (CSR order): s_k = sum of a_km over m in C_i whose sign */
+/* is opposite to a_kk (row k order); s_k == 0 -> d += a_ik, else num_m +=           */
+/* (a_ik * a_km) / s_k over the same m (row k order); num_j starts at a_ij.          */
+/* w_ij = -num_j / d.  C row: 1 at its coarse index.                                 */
 /* ------------------------------------------------------------------------------ */
 orc_csr* orc_interp_classical(const orc_csr* A, const orc_csr* S, const int32_t* cf) {
     int64_t n = A->n_rows;
@@ -561,14 +562,18 @@ orc_csr* orc_interp_classical(const orc_csr* A, const orc_csr* S, const int32_t*
             for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
                 int64_t kk = A->col[k];
                 if (kk == i || strong[kk] != i || cf[kk] == ST_C) continue;
+                /* only couplings of sign opposite to a_kk distribute (no cancellation) */
+                int pos = diag_of(A, kk) > 0.0;
                 double s = 0.0;
                 for (int64_t u = A->rp[kk]; u < A->rp[kk + 1]; ++u)
-                    if (cpos[A->col[u]] >= 0) s += A->val[u];
+                    if (cpos[A->col[u]] >= 0 && (pos ? A->val[u] < 0.0 : A->val[u] > 0.0))
+                        s += A->val[u];
                 if (s == 0.0) {
                     d += A->val[k];
                 } else {
                     for (int64_t u = A->rp[kk]; u < A->rp[kk + 1]; ++u)
-                        if (cpos[A->col[u]] >= 0) num[A->col[u]] += (A->val[k] * A->val[u]) / s;
+                        if (cpos[A->col[u]] >= 0 && (pos ? A->val[u] < 0.0 : A->val[u] > 0.0))
+                            num[A->col[u]] += (A->val[k] * A->val[u]) / s;
                 }
             }
         }

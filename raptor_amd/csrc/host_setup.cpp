@@ -346,13 +346,23 @@ HostCSR interp_classical(const HostComm& comm, const HostCSR& A, const HostCSR& 
                         int64_t h = plan.find(kk);
                         rc = &G.col[G.rp[h]], rv = &G.val[G.rp[h]], rl = G.rp[h + 1] - G.rp[h];
                     }
+                    // only couplings of sign opposite to a_kk distribute (no cancellation)
+                    double akk = 0.0;
+                    for (int64_t u = 0; u < rl; ++u)
+                        if (rc[u] == kk) {
+                            akk = rv[u];
+                            break;
+                        }
+                    const bool pos = akk > 0.0;
+                    auto opp = [pos](double v) { return pos ? v < 0.0 : v > 0.0; };
                     double s = 0.0;
                     for (int64_t u = 0; u < rl; ++u)
-                        if (std::binary_search(ci.begin(), ci.end(), rc[u])) s += rv[u];
+                        if (opp(rv[u]) && std::binary_search(ci.begin(), ci.end(), rc[u])) s += rv[u];
                     if (s == 0.0) {
                         d += A.val[k];
                     } else {
                         for (int64_t u = 0; u < rl; ++u) {
+                            if (!opp(rv[u])) continue;
                             auto it = std::lower_bound(ci.begin(), ci.end(), rc[u]);
                             if (it != ci.end() && *it == rc[u])
                                 num[it - ci.begin()] += (A.val[k] * rv[u]) / s;

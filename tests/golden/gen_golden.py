@@ -1,0 +1,281 @@
+"""Generate tests/golden/*.npz: independent fixtures that pin the oracle.
+
+The reference (Siddarthareddy1/raptor) holds no AMG code or vectors, so the
+oracle is pinned here by implementations that share no code with it:
+  * scipy.sparse 1.15.3 -- model-problem matrices built from Kronecker products, SpMV,
+    residual, Jacobi, transposes and Galerkin products R (A P);
+  * numpy uint64 arithmetic -- the splitmix64 vector generator and hashes;
+  * small pure-Python loop restatements -- RS first pass, PMIS, MIS(2) aggregation, hybrid GS
+    (small sizes only), written from DESIGN.md section 3, not from the C code.
+Run: python tests/golden/gen_golden.py   (writes the .npz files next to this script)
+"""
+from __future__ import annotations
+
+import heapq
+import os
+
+import numpy as np
+import scipy.sparse as sp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+M64 = (1 << 64) - 1
+
+
+# --------------------------------------------------------------------------------------
+# model problems by Kronecker products (independent of the C generators)
+# --------------------------------------------------------------------------------------
+def lap1d(n):
+    return sp.diags([-np.ones(n - 1), 2 * np.ones(n), -np.ones(n - 1)], [-1, 0, 1], format="csr")
+
+
+def eye(n):
+    return sp.identity(n, format="csr")
+
+
+def poisson5(nx, ny):
+    # row id = i + nx*j: x fastest => kron(Iy, Tx) + kron(Ty, Ix)
+    return (sp.kron(eye(ny), lap1d(nx)) + sp.kron(lap1d(ny), eye(nx))).tocsr()
+
+
+def poisson7(nx, ny, nz):
+    return (sp.kron(eye(nz), sp.kron(eye(ny), lap1d(nx)))
+            + sp.kron(eye(nz), sp.kron(lap1d(ny), eye(nx)))
+            + sp.kron(lap1d(nz), sp.kron(eye(ny), eye(nx)))).tocsr()
+
+
+def fe27(nx, ny, nz, ex=1.0, ey=1.0, ez=1e-3):
+    """36 x Q1 stiffness of -div(diag(ex,ey,ez) grad u): K1 = tridiag(-1,2,-1),
+    m1 = tridiag(1,4,1); A = ex Kx.my.mz + ey mx.Ky.mz + ez mx.my.Kz (x fastest)."""
+    def m1(n):
+        return sp.diags([np.ones(n - 1), 4 * np.ones(n), np.ones(n - 1)], [-1, 0, 1], format="csr")
+
+    t1 = ex * sp.kron(m1(nz), sp.kron(m1(ny), lap1d(nx)))
+    t2 = ey * sp.kron(m1(nz), sp.kron(lap1d(ny), m1(nx)))
+    t3 = ez * sp.kron(lap1d(nz), sp.kron(m1(ny), m1(nx)))
+    return ((t1 + t2) + t3).tocsr()
+
+
+# --------------------------------------------------------------------------------------
+# splitmix64 in numpy uint64
+# --------------------------------------------------------------------------------------
+def mix64(z):
+    z = np.asarray(z, np.uint64)
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def uniform(n, seed, first=0):
+    with np.errstate(over="ignore"):
+        base = np.uint64((seed * 0xD1B54A32D192ED03) & M64)
+        u = mix64(base + np.arange(first, first + n, dtype=np.uint64))
+    return (u >> np.uint64(11)).astype(np.float64) * 2.0 ** -52 - 1.0
+
+
+def hash32(ids, seed):
+    with np.errstate(over="ignore"):
+        s = np.uint64((seed * 0x9E3779B97F4A7C15) & M64)
+        return (mix64(np.asarray(ids, np.uint64) ^ s) >> np.uint64(32)).astype(np.uint64)
+
+
+# --------------------------------------------------------------------------------------
+# pure-Python restatements
+# --------------------------------------------------------------------------------------
+def rows(M):
+    M = M.tocsr()
+    M.sort_indices()
+    return [(M.indices[M.indptr[i]:M.indptr[i + 1]].tolist(),
+             M.data[M.indptr[i]:M.indptr[i + 1]].tolist()) for i in range(M.shape[0])]
+
+
+def strength_classical(A, theta):
+    R = rows(A)
+    out = []
+    for i, (cols, vals) in enumerate(R):
+        off = [-v for c, v in zip(cols, vals) if c != i]
+        keep = []
+        if off and max(off) > 0.0:
+            thr = theta * max(off)
+            keep = [c for c, v in zip(cols, vals) if c != i and -v >= thr]
+        out.append(keep)
+    return out
+
+
+def strength_symmetric(A, theta):
+    R = rows(A)
+    d = A.diagonal()
+    return [[(c, v) for c, v in zip(cols, vals)
+             if c != i and abs(v) >= theta * np.sqrt(abs(d[i] * d[c]))] for i, (cols, vals) in enumerate(R)]
+
+
+def transpose_lists(S, n):
+    T = [[] for _ in range(n)]
+    for i, cols in enumerate(S):
+        for c in cols:
+            T[c].append(i)
+    return T
+
+
+def rs_split(S):
+    n = len(S)
+    ST = transpose_lists(S, n)
+    U, F, Cc = -1, 0, 1
+    cf = [F if (not S[i] and not ST[i]) else U for i in range(n)]
+    lam = [len(ST[i]) for i in range(n)]
+    heap = [(-lam[i], i) for i in range(n) if cf[i] == U]
+    heapq.heapify(heap)
+    while heap:
+        nl, i = heapq.heappop(heap)
+        if cf[i] != U or -nl != lam[i]:
+            continue
+        cf[i] = Cc
+        for j in ST[i]:
+            if cf[j] == U:
+                cf[j] = F
+                for k in S[j]:
+                    if cf[k] == U:
+                        lam[k] += 1
+                        heapq.heappush(heap, (-lam[k], k))
+        for j in S[i]:
+            if cf[j] == U:
+                lam[j] -= 1
+                heapq.heappush(heap, (-lam[j], j))
+    return np.array(cf, np.int32)
+
+
+def pmis_split(S, seed):
+    n = len(S)
+    ST = transpose_lists(S, n)
+    h = hash32(np.arange(n), seed)
+    key = [(len(ST[i]) << 32) | int(h[i]) for i in range(n)]
+    U, F, Cc = -1, 0, 1
+    cf = [F if not ST[i] else U for i in range(n)]
+    while any(c == U for c in cf):
+        newc = []
+        for i in range(n):
+            if cf[i] != U:
+                continue
+            if all(not (cf[j] == U and (key[j], j) > (key[i], i)) for j in S[i] + ST[i]):
+                newc.append(i)
+        for i in newc:
+            cf[i] = Cc
+        for i in range(n):
+            if cf[i] == U and any(cf[j] == Cc for j in S[i]):
+                cf[i] = F
+    return np.array(cf, np.int32)
+
+
+def mis2_aggregate(Sv, seed):
+    n = len(Sv)
+    S = [[c for c, _ in r] for r in Sv]
+    h = [int(v) for v in hash32(np.arange(n), seed)]
+    OUT, UND, IN = 0, 1, 2
+    st = [UND] * n
+    while UND in st:
+        t = [(st[i], h[i], i) for i in range(n)]
+        for _ in range(2):
+            t = [max([t[i]] + [t[j] for j in S[i]]) for i in range(n)]
+        for i in range(n):
+            if st[i] == UND:
+                if t[i][2] == i:
+                    st[i] = IN
+                elif t[i][0] == IN:
+                    st[i] = OUT
+    roots = [i for i in range(n) if st[i] == IN]
+    agg = [-1] * n
+    for a, r in enumerate(roots):
+        agg[r] = a
+    a1 = list(agg)
+    for i in range(n):
+        if a1[i] < 0:
+            for j in S[i]:
+                if st[j] == IN:
+                    a1[i] = agg[j]
+                    break
+    out = list(a1)
+    for i in range(n):
+        if a1[i] < 0:
+            best, ba = -1.0, -1
+            for j, v in Sv[i]:
+                if a1[j] < 0:
+                    continue
+                w = abs(v)
+                if w > best or (w == best and a1[j] < ba):
+                    best, ba = w, a1[j]
+            out[i] = ba
+    return np.array(out, np.int32), len(roots)
+
+
+def hybrid_gs(A, x, b, block):
+    R = rows(A)
+    n = len(R)
+    out = np.zeros(n)
+    d = A.diagonal()
+    for s in range(0, n, block):
+        e = min(n, s + block)
+        for i in range(s, e):
+            acc = b[i]
+            cols, vals = R[i]
+            for c, v in zip(cols, vals):
+                if c == i or s <= c < i:
+                    continue
+                acc -= v * x[c]
+            for c, v in zip(cols, vals):
+                if s <= c < i:
+                    acc -= v * out[c]
+            out[i] = acc * (1.0 / d[i])
+    return out
+
+
+def save(name, **arrays):
+    np.savez_compressed(os.path.join(HERE, name), **arrays)
+
+
+def csr_arrays(prefix, M):
+    M = M.tocsr()
+    M.sort_indices()
+    return {f"{prefix}_indptr": M.indptr.astype(np.int64), f"{prefix}_indices": M.indices.astype(np.int64),
+            f"{prefix}_data": M.data, f"{prefix}_shape": np.array(M.shape, np.int64)}
+
+
+def main():
+    problems = {
+        "p5_16x12": poisson5(16, 12),
+        "p5_32x32": poisson5(32, 32),
+        "p7_10x9x8": poisson7(10, 9, 8),
+        "fe27_8x7x6": fe27(8, 7, 6),
+    }
+    for name, A in problems.items():
+        n = A.shape[0]
+        x = uniform(n, 3)
+        b = uniform(n, 4)
+        d = A.diagonal()
+        out = dict(csr_arrays("A", A))
+        out["x"] = x
+        out["b"] = b
+        out["y"] = A @ x
+        out["r"] = b - A @ x
+        out["jac"] = x + (2.0 / 3.0) * ((1.0 / d) * (b - A @ x))
+        out["gs64"] = hybrid_gs(A, x, b, 64)
+        out["gs7"] = hybrid_gs(A, x, b, 7)
+        S = strength_classical(A, 0.25)
+        out["S_classical_nnz"] = np.array([len(s) for s in S], np.int64)
+        out["cf_rs"] = rs_split(S)
+        out["cf_pmis"] = pmis_split(S, 0x5EED)
+        Ss = strength_symmetric(A, 0.08)
+        agg, na = mis2_aggregate(Ss, 0x5EED)
+        out["agg_mis2"] = agg
+        out["n_agg"] = np.array(na, np.int64)
+        out["hash32_seed5eed"] = hash32(np.arange(n), 0x5EED).astype(np.int64)
+        save(f"{name}.npz", **out)
+        print(name, n, A.nnz, "C(rs)", int(out["cf_rs"].sum()), "C(pmis)", int(out["cf_pmis"].sum()),
+              "aggs", na)
+    # vector generator at an offset (partition independence of the generator)
+    save("uniform.npz", u0=uniform(1000, 42), u_off=uniform(1000, 42, first=123456789),
+         u_seed7=uniform(17, 7))
+
+
+if __name__ == "__main__":
+    main()
