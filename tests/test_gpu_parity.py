@@ -195,7 +195,7 @@ def test_full_size_spmv_and_cycle_256(ctx, oracle):
     yh = to_host(ctx, y)
     g = np.arange(n)
     i, j, k = g % N, (g // N) % N, g // (N * N)
-    expect = ((i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (k == 0) + (k == N - 1)).astype(float)
+    expect = sum((c == 0).astype(float) + (c == N - 1).astype(float) for c in (i, j, k))
     assert np.array_equal(yh, expect)
     x = O.vec_uniform(n, 77)
     dx = to_dev(ctx, x)
