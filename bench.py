@@ -123,8 +123,9 @@ def main():
     conv = float((hist[-1] / hist[0]) ** (1.0 / max(1, len(hist) - 1))) if hist[0] > 0 else None
     log(rank, f"{args.steps} V-cycles in {dt * 1e3:.2f} ms -> {iters_per_s:.1f} it/s, conv {conv}")
 
-    # bytes of one V-cycle (algorithmic, all ranks) + the residual norm each iteration
-    cyc_bytes_local = ml.bytes_per_cycle() + (12 * A.nnz + 4 * (n + 1) + 24 * n)
+    # algorithmic bytes of one V-cycle, all ranks (the per-iteration residual norm is fused
+    # into the next cycle's first Jacobi sweep: no extra bytes except the last one)
+    cyc_bytes_local = ml.bytes_per_cycle()
     if world > 1:
         t = torch.tensor([cyc_bytes_local], dtype=torch.float64)
         dist.all_reduce(t)

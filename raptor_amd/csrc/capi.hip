@@ -265,11 +265,21 @@ int amg_par_csr_residual_norm(amg_matrix A, const double* x, const double* b, do
         AMG_CHECK(A && out, "null argument");
         Context& c = *A->m->ctx;
         set_device(c);
-        DevBuf<double> r, o;
+        const size_t nb = (size_t)(A->m->nb_int + A->m->nb_bnd), tmpn = nb / 4096 + 64;
+        DevBuf<double> r, buf;
+        DevBuf<int> cnt;
         r.alloc((size_t)std::max<int64_t>(A->m->n_rows, 1));
-        o.alloc(1);
-        par_residual_norm(*A->m, x, b, r.p, o.p);
-        HIP_CHECK(hipMemcpyAsync(out, o.p, sizeof(double), hipMemcpyDeviceToHost, c.stream));
+        buf.alloc(nb + tmpn + (size_t)c.host.nranks + 8);
+        cnt.alloc(1);
+        HIP_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int), c.stream));
+        NormSink ns;
+        ns.partial = buf.p;
+        ns.tmp = buf.p + nb;
+        ns.gathered = ns.tmp + tmpn;
+        ns.hist = ns.gathered + c.host.nranks + 2;
+        ns.counter = cnt.p;
+        par_residual_norm(*A->m, x, b, r.p, ns);
+        HIP_CHECK(hipMemcpyAsync(out, ns.hist, sizeof(double), hipMemcpyDeviceToHost, c.stream));
         HIP_CHECK(hipStreamSynchronize(c.stream));
     });
 }
@@ -385,32 +395,8 @@ int amg_solver_solve(amg_solver S, double* x, const double* b, int32_t max_iter,
     return guard([&] {
         AMG_CHECK(S && hist && iters, "null argument");
         AMG_CHECK(max_iter >= 0, "max_iter must be >= 0");
-        Solver& s = S->s;
-        Context& c = *s.ctx;
-        set_device(c);
-        DevMatrix& A = *s.A0;
-        if (s.hist.n < (size_t)max_iter + 1) s.hist.alloc((size_t)max_iter + 1);
-        double* r = s.levels[0].r.p;
-        par_residual_norm(A, x, b, r, s.hist.p);
-        int32_t it = 0;
-        double r0 = -1.0;
-        if (tol > 0.0) {
-            HIP_CHECK(hipMemcpyAsync(&r0, s.hist.p, sizeof(double), hipMemcpyDeviceToHost, c.stream));
-            HIP_CHECK(hipStreamSynchronize(c.stream));
-        }
-        while (it < max_iter) {
-            s.cycle(x, b);
-            par_residual_norm(A, x, b, r, s.hist.p + it + 1);
-            ++it;
-            if (tol > 0.0) {
-                double rn;
-                HIP_CHECK(hipMemcpyAsync(&rn, s.hist.p + it, sizeof(double), hipMemcpyDeviceToHost, c.stream));
-                HIP_CHECK(hipStreamSynchronize(c.stream));
-                if (r0 > 0.0 && rn / r0 < tol) break;
-            }
-        }
-        HIP_CHECK(hipMemcpyAsync(hist, s.hist.p, sizeof(double) * (size_t)(it + 1), hipMemcpyDeviceToHost, c.stream));
-        HIP_CHECK(hipStreamSynchronize(c.stream));
+        set_device(*S->s.ctx);
+        const int32_t it = S->s.solve(x, b, max_iter, tol, hist);
         *iters = it;
     });
 }
@@ -420,10 +406,11 @@ int amg_solver_set_graph(amg_solver S, int32_t enable) {
         AMG_CHECK(S, "null solver");
         AMG_CHECK(!enable || S->s.ctx->host.nranks == 1, "hipGraph capture is single-rank only");
         S->s.use_graph = enable != 0;
-        if (S->s.graph) {
-            HIP_CHECK(hipGraphExecDestroy(S->s.graph));
-            S->s.graph = nullptr;
-        }
+        for (auto& g : S->s.graphs)
+            if (g.exec) {
+                HIP_CHECK(hipGraphExecDestroy(g.exec));
+                g.exec = nullptr;
+            }
     });
 }
 

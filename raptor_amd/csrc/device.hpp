@@ -70,7 +70,6 @@ struct Context {
     hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
     HostComm host;
     ncclComm_t nccl = nullptr;
-    DevBuf<double> scratch;  // norm partials + gathered sums
     ~Context();
 };
 
@@ -115,8 +114,10 @@ void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const 
 void launch_jacobi_zero(hipStream_t s, int64_t n, const double* b, const double* dinv, double* y,
                         double omega);
 void launch_pack(hipStream_t s, int64_t n, const int* idx, const double* x, double* out);
-void launch_sum_partials(hipStream_t s, int n, const double* partial, double* out);
-void launch_sum_ranks(hipStream_t s, int n, const double* in, double* out, bool take_sqrt);
+// deterministic sum of n per-block partials into *out (tmp: >= n/4096 + 16 doubles)
+void launch_reduce_partials(hipStream_t s, int n, const double* partial, double* tmp, double* out);
+// hist[*counter] = sqrt(sum_{i<n} in[i]) (rank order); ++*counter
+void launch_finish_norm(hipStream_t s, int n, const double* in, double* hist, int* counter);
 void launch_dense_gemv(hipStream_t s, int64_t n_local, int64_t n, const double* invT,
                        const double* bfull, double* x);
 void launch_uniform(hipStream_t s, int64_t n, int64_t first_gid, uint64_t seed, double* out);
@@ -126,8 +127,20 @@ void launch_zero(hipStream_t s, int64_t n, double* y);
 void par_apply(DevMatrix& A, int mode, const double* x, const double* b, double* y, double omega,
                double* partial_or_null);
 void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block);
-// ||b - A x|| into dev_out[0] (device), deterministic; uses ctx scratch
-void par_residual_norm(DevMatrix& A, const double* x, const double* b, double* r, double* dev_out);
+// Norm plumbing: a mode-NORM level kernel leaves per-block partial sums of (b - Ax)^2 in
+// NormSink::partial; norm_finish() reduces them (fixed order), combines ranks (RCCL
+// allgather, rank order) and appends sqrt to hist[*counter] -- all on the device.
+struct NormSink {
+    double* partial = nullptr;  // >= number of blocks of the matrix
+    double* tmp = nullptr;      // reduction scratch
+    double* gathered = nullptr; // nranks + 1
+    double* hist = nullptr;
+    int* counter = nullptr;
+};
+void norm_finish(DevMatrix& A, const NormSink& ns);
+// r = b - A x and append ||r|| (device-side) through ns
+void par_residual_norm(DevMatrix& A, const double* x, const double* b, double* r,
+                       const NormSink& ns);
 
 struct Level {
     std::unique_ptr<DevMatrix> A, P, R;
@@ -144,18 +157,28 @@ struct Solver {
     DevBuf<double> invT, bfull;
     int64_t coarse_n = 0;
     std::vector<int> coarse_counts, coarse_displs;
-    // solve state
-    DevBuf<double> hist;
+    // solve state: residual history kept on the device, appended by finish_norm_kernel
+    DevBuf<double> hist, norm_scratch;
+    DevBuf<int> hist_counter;
+    NormSink sink;
     bool use_graph = true;
-    hipGraphExec_t graph = nullptr;
-    const double* graph_x = nullptr;
-    const double* graph_b = nullptr;
+    struct Graph {
+        hipGraphExec_t exec = nullptr;
+        const double* x = nullptr;
+        const double* b = nullptr;
+    } graphs[2];  // [0] plain cycle, [1] cycle that also appends ||b - A x_in||
 
     DevMatrix& Amat(size_t l) { return l == 0 ? *A0 : *levels[l].A; }
     void setup(DevMatrix& A, const amg_options& o);
-    void cycle(double* x, const double* b);
-    void cycle_rec(size_t l, double* x, const double* b, bool x_zero);
-    void smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_zero);
+    // one V-cycle; with_norm: the first level-0 Jacobi sweep also appends ||b - A x_in||
+    // to the device history (falls back to a separate residual when it cannot)
+    void cycle(double* x, const double* b, bool with_norm = false);
+    void cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool with_norm);
+    void smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_zero, bool with_norm);
+    void ensure_hist(int32_t n);
+    bool can_fuse_norm() const;
+    // ParMultilevel::solve; hist_host gets it+1 norms
+    int32_t solve(double* x, const double* b, int32_t max_iter, double tol, double* hist_host);
     int64_t bytes_per_cycle(size_t l) const;
     ~Solver();
 };

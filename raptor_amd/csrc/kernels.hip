@@ -38,13 +38,16 @@ __device__ __forceinline__ double xload(const CsrArgs& a, int c) {
     return *p;
 }
 
+// fused epilogue; *res receives b - s for the residual and Jacobi modes (for the norm)
 template <int MODE>
-__device__ __forceinline__ double epilogue(const CsrArgs& a, int r, double s) {
+__device__ __forceinline__ double epilogue(const CsrArgs& a, int r, double s, double* res) {
     if (MODE == KM_SPMV) return s;
     if (MODE == KM_SPMV_ADD) return a.y[r] + s;
-    if (MODE == KM_RESID) return a.b[r] - s;
+    const double t = a.b[r] - s;
+    *res = t;
+    if (MODE == KM_RESID) return t;
     // Jacobi: x + omega * (dinv * (b - s))
-    return a.x[r] + a.omega * (a.dinv[r] * (a.b[r] - s));
+    return a.x[r] + a.omega * (a.dinv[r] * t);
 }
 
 template <int MODE, bool NORM>
@@ -80,9 +83,9 @@ __global__ __launch_bounds__(kTPB) void csr_stream_kernel(CsrArgs a, int first_b
             const int e0 = a.rp[r] - k0, e1 = a.rp[r + 1] - k0;
             double s = 0.0;
             for (int k = e0; k < e1; ++k) s += prod[k];
-            double out = epilogue<MODE>(a, r, s);
-            a.y[r] = out;
-            if (NORM) sq += out * out;
+            double res = 0.0;
+            a.y[r] = epilogue<MODE>(a, r, s, &res);
+            if (NORM) sq += res * res;
         }
     } else {
         // one row longer than the LDS stage: chunked, summed by lane 0 in CSR order
@@ -97,9 +100,9 @@ __global__ __launch_bounds__(kTPB) void csr_stream_kernel(CsrArgs a, int first_b
             __syncthreads();
         }
         if (tid == 0) {
-            double out = epilogue<MODE>(a, r0, s);
-            a.y[r0] = out;
-            if (NORM) sq = out * out;
+            double res = 0.0;
+            a.y[r0] = epilogue<MODE>(a, r0, s, &res);
+            if (NORM) sq = res * res;
         }
     }
     if (NORM) {
@@ -232,24 +235,34 @@ __global__ void zero_kernel(long long n, double* y) {
     for (; i < n; i += stride) y[i] = 0.0;
 }
 
-// deterministic sum of n partials: each lane sums a fixed strided subset, then a fixed
-// shuffle tree and 4 wave sums in order
+// deterministic two-stage sum of n partials: block g sums [g*4096, (g+1)*4096) with 16
+// fixed loads per lane, a fixed shuffle tree and 4 wave sums in order
+constexpr int kRedSpan = kTPB * 16;
 __global__ __launch_bounds__(kTPB) void sum_partials_kernel(int n, const double* p, double* out) {
     __shared__ double red[kTPB / 64];
+    const int base = blockIdx.x * kRedSpan + threadIdx.x;
+    double v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int i = base + j * kTPB;
+        v[j] = i < n ? p[i] : 0.0;
+    }
     double s = 0.0;
-    for (int i = threadIdx.x; i < n; i += kTPB) s += p[i];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += v[j];
     for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (threadIdx.x == 0) *out = (red[0] + red[1]) + (red[2] + red[3]);
+    if (threadIdx.x == 0) out[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-// sum of per-rank sums in rank order (identical on every rank); optional sqrt
-__global__ void sum_ranks_kernel(int n, const double* in, double* out, int take_sqrt) {
+// sum of per-rank sums in rank order (identical on every rank), sqrt, append to hist
+__global__ void finish_norm_kernel(int n, const double* in, double* hist, int* counter) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         double s = 0.0;
         for (int i = 0; i < n; ++i) s += in[i];
-        *out = take_sqrt ? sqrt(s) : s;
+        hist[*counter] = sqrt(s);
+        *counter += 1;
     }
 }
 
@@ -303,7 +316,10 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
             if (norm) AMG_L(KM_RESID, true);
             else AMG_L(KM_RESID, false);
             break;
-        case KM_JACOBI: AMG_L(KM_JACOBI, false); break;
+        case KM_JACOBI:
+            if (norm) AMG_L(KM_JACOBI, true);
+            else AMG_L(KM_JACOBI, false);
+            break;
         default: throw Error(AMG_ERR_INTERNAL, "bad kernel mode");
     }
 #undef AMG_L
@@ -340,13 +356,19 @@ void launch_zero(hipStream_t s, int64_t n, double* y) {
     HIP_CHECK(hipGetLastError());
 }
 
-void launch_sum_partials(hipStream_t s, int n, const double* partial, double* out) {
-    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(kTPB), 0, s, n, partial, out);
+void launch_reduce_partials(hipStream_t s, int n, const double* partial, double* tmp, double* out) {
+    if (n <= kRedSpan) {
+        hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(kTPB), 0, s, n, partial, out);
+    } else {
+        const int g = (n + kRedSpan - 1) / kRedSpan;
+        hipLaunchKernelGGL(sum_partials_kernel, dim3(g), dim3(kTPB), 0, s, n, partial, tmp);
+        launch_reduce_partials(s, g, tmp, tmp + g, out);
+    }
     HIP_CHECK(hipGetLastError());
 }
 
-void launch_sum_ranks(hipStream_t s, int n, const double* in, double* out, bool take_sqrt) {
-    hipLaunchKernelGGL(sum_ranks_kernel, dim3(1), dim3(64), 0, s, n, in, out, take_sqrt ? 1 : 0);
+void launch_finish_norm(hipStream_t s, int n, const double* in, double* hist, int* counter) {
+    hipLaunchKernelGGL(finish_norm_kernel, dim3(1), dim3(64), 0, s, n, in, hist, counter);
     HIP_CHECK(hipGetLastError());
 }
 

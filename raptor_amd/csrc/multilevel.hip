@@ -8,7 +8,8 @@
 namespace amg {
 
 Solver::~Solver() {
-    if (graph) (void)hipGraphExecDestroy(graph);
+    for (auto& g : graphs)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
 }
 
 void Solver::setup(DevMatrix& A, const amg_options& o) {
@@ -52,8 +53,15 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         max_blocks = std::max(max_blocks, (size_t)(Al.nb_int + Al.nb_bnd));
         if (opt.smoother == AMG_SMOOTH_HYBRID_GS) Al.ensure_gs_blocks(opt.gs_block);
     }
-    const size_t need = max_blocks + 2 * (size_t)comm.nranks + 8;
-    if (ctx->scratch.n < need) ctx->scratch.alloc(need + 1024);
+    // norm plumbing: partials | reduction scratch | gathered rank sums
+    const size_t tmpn = max_blocks / 4096 + 64;
+    norm_scratch.alloc(max_blocks + tmpn + (size_t)comm.nranks + 8);
+    sink.partial = norm_scratch.p;
+    sink.tmp = sink.partial + max_blocks;
+    sink.gathered = sink.tmp + tmpn;
+    hist_counter.alloc(1);
+    sink.counter = hist_counter.p;
+    ensure_hist(1024);
     // coarsest level: gathered dense inverse, this rank's rows, column-major.  With several
     // ranks b is allgathered into a padded [nranks x cmax] layout; invT has zero rows at the
     // padding so the sum order over real entries is the global order j = 0..n-1.
@@ -77,13 +85,28 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         bfull.alloc((size_t)npad + (size_t)cmax);  // gathered + local padded send slot
         HIP_CHECK(hipMemset(bfull.p, 0, bfull.n * sizeof(double)));
     }
-    hist.alloc(1);
     use_graph = comm.nranks == 1;
 }
 
-void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_zero) {
+void Solver::ensure_hist(int32_t n) {
+    if (hist.n >= (size_t)n) return;
+    hist.alloc((size_t)n);
+    sink.hist = hist.p;
+    for (auto& g : graphs)  // captured graphs baked the old pointer
+        if (g.exec) {
+            HIP_CHECK(hipGraphExecDestroy(g.exec));
+            g.exec = nullptr;
+        }
+}
+
+void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_zero,
+                    bool with_norm) {
     DevMatrix& A = Amat(l);
-    if (opt.smoother == AMG_SMOOTH_HYBRID_GS) {
+    if (with_norm) {  // Jacobi sweep that also leaves the partials of ||b - A x||
+        AMG_ASSERT(opt.smoother == AMG_SMOOTH_JACOBI && !x_zero);
+        par_apply(A, KM_JACOBI, x, b, tmp, opt.jacobi_omega, sink.partial);
+        norm_finish(A, sink);
+    } else if (opt.smoother == AMG_SMOOTH_HYBRID_GS) {
         if (x_zero) launch_zero(ctx->stream, A.n_rows, x);
         par_hybrid_gs(A, x, b, tmp, opt.gs_block);
     } else if (x_zero) {
@@ -94,7 +117,7 @@ void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_
     std::swap(x, tmp);
 }
 
-void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero) {
+void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool with_norm) {
     DevMatrix& A = Amat(l);
     hipStream_t s = ctx->stream;
     const HostComm& comm = ctx->host;
@@ -118,45 +141,89 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero) {
     double* tmp = L.t.p;
     bool zero = x_zero;
     for (int k = 0; k < opt.pre_sweeps; ++k) {
-        smooth(l, cur, b, tmp, zero);
+        smooth(l, cur, b, tmp, zero, with_norm && k == 0);
         zero = false;
     }
     if (zero) launch_zero(s, A.n_rows, cur);
     par_apply(A, KM_RESID, cur, b, L.r.p, 0.0, nullptr);
     Level& C = levels[l + 1];
     par_apply(*L.R, KM_SPMV, L.r.p, nullptr, C.b.p, 0.0, nullptr);
-    cycle_rec(l + 1, C.x.p, C.b.p, true);
+    cycle_rec(l + 1, C.x.p, C.b.p, true, false);
     par_apply(*L.P, KM_SPMV_ADD, C.x.p, nullptr, cur, 0.0, nullptr);
-    for (int k = 0; k < opt.post_sweeps; ++k) smooth(l, cur, b, tmp, false);
+    for (int k = 0; k < opt.post_sweeps; ++k) smooth(l, cur, b, tmp, false, false);
     if (cur != x)
         HIP_CHECK(hipMemcpyAsync(x, cur, A.n_rows * sizeof(double), hipMemcpyDeviceToDevice, s));
 }
 
-void Solver::cycle(double* x, const double* b) {
+bool Solver::can_fuse_norm() const {
+    return opt.smoother == AMG_SMOOTH_JACOBI && opt.pre_sweeps >= 1 && levels.size() >= 2;
+}
+
+void Solver::cycle(double* x, const double* b, bool with_norm) {
+    AMG_ASSERT(!with_norm || can_fuse_norm());
     if (!use_graph) {
-        cycle_rec(0, x, b, false);
+        cycle_rec(0, x, b, false, with_norm);
         return;
     }
     hipStream_t s = ctx->stream;
-    if (!graph || graph_x != x || graph_b != b) {
-        if (graph) HIP_CHECK(hipGraphExecDestroy(graph));
-        graph = nullptr;
+    Graph& G = graphs[with_norm ? 1 : 0];
+    if (!G.exec || G.x != x || G.b != b) {
+        if (G.exec) HIP_CHECK(hipGraphExecDestroy(G.exec));
+        G.exec = nullptr;
         hipGraph_t g = nullptr;
         HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         try {
-            cycle_rec(0, x, b, false);
+            cycle_rec(0, x, b, false, with_norm);
         } catch (...) {
             (void)hipStreamEndCapture(s, &g);
             if (g) (void)hipGraphDestroy(g);
             throw;
         }
         HIP_CHECK(hipStreamEndCapture(s, &g));
-        HIP_CHECK(hipGraphInstantiate(&graph, g, nullptr, nullptr, 0));
+        HIP_CHECK(hipGraphInstantiate(&G.exec, g, nullptr, nullptr, 0));
         HIP_CHECK(hipGraphDestroy(g));
-        graph_x = x;
-        graph_b = b;
+        G.x = x;
+        G.b = b;
     }
-    HIP_CHECK(hipGraphLaunch(graph, s));
+    HIP_CHECK(hipGraphLaunch(G.exec, s));
+}
+
+int32_t Solver::solve(double* x, const double* b, int32_t max_iter, double tol, double* hist_host) {
+    AMG_CHECK(max_iter >= 0, "max_iter must be >= 0");
+    hipStream_t s = ctx->stream;
+    ensure_hist(max_iter + 1);
+    HIP_CHECK(hipMemsetAsync(hist_counter.p, 0, sizeof(int), s));
+    DevMatrix& A = *A0;
+    double* r = levels[0].r.p;
+    int32_t it = 0;
+    if (tol <= 0.0 && can_fuse_norm()) {
+        // ||b - A x_k|| comes out of cycle k+1's first Jacobi sweep (same b - Ax values);
+        // only the last norm needs its own residual pass.  No host sync in the loop.
+        for (; it < max_iter; ++it) cycle(x, b, true);
+        par_residual_norm(A, x, b, r, sink);
+    } else {
+        par_residual_norm(A, x, b, r, sink);
+        double r0 = 0.0;
+        if (tol > 0.0) {
+            HIP_CHECK(hipMemcpyAsync(&r0, hist.p, sizeof(double), hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+        }
+        while (it < max_iter) {
+            cycle(x, b, false);
+            par_residual_norm(A, x, b, r, sink);
+            ++it;
+            if (tol > 0.0) {
+                double rn = 0.0;
+                HIP_CHECK(hipMemcpyAsync(&rn, hist.p + it, sizeof(double), hipMemcpyDeviceToHost, s));
+                HIP_CHECK(hipStreamSynchronize(s));
+                if (r0 > 0.0 && rn / r0 < tol) break;
+            }
+        }
+    }
+    HIP_CHECK(hipMemcpyAsync(hist_host, hist.p, sizeof(double) * (size_t)(it + 1),
+                             hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    return it;
 }
 
 static int64_t spmv_bytes(const DevMatrix& M) {

@@ -163,24 +163,25 @@ void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, in
     launch_hybrid_gs(A.ctx->stream, A, x, b, y);
 }
 
-void par_residual_norm(DevMatrix& A, const double* x, const double* b, double* r, double* dev_out) {
+void norm_finish(DevMatrix& A, const NormSink& ns) {
     Context* c = A.ctx;
     const int nb = A.nb_int + A.nb_bnd;
     const int nr = c->host.nranks;
-    size_t need = (size_t)nb + 2 * (size_t)nr + 8;
-    if (c->scratch.n < need) c->scratch.alloc(need + 1024);
-    double* partial = c->scratch.p;
-    double* local = partial + nb;
-    double* gathered = local + 1;
-    par_apply(A, KM_RESID, x, b, r, 0.0, partial);
-    if (nb > 0) launch_sum_partials(c->stream, nb, partial, local);
+    double* local = ns.gathered + nr;
+    if (nb > 0) launch_reduce_partials(c->stream, nb, ns.partial, ns.tmp, local);
     else launch_zero(c->stream, 1, local);
     if (nr > 1) {
-        NCCL_CHECK(ncclAllGather(local, gathered, 1, ncclDouble, c->nccl, c->stream));
-        launch_sum_ranks(c->stream, nr, gathered, dev_out, true);
+        NCCL_CHECK(ncclAllGather(local, ns.gathered, 1, ncclDouble, c->nccl, c->stream));
+        launch_finish_norm(c->stream, nr, ns.gathered, ns.hist, ns.counter);
     } else {
-        launch_sum_ranks(c->stream, 1, local, dev_out, true);
+        launch_finish_norm(c->stream, 1, local, ns.hist, ns.counter);
     }
+}
+
+void par_residual_norm(DevMatrix& A, const double* x, const double* b, double* r,
+                       const NormSink& ns) {
+    par_apply(A, KM_RESID, x, b, r, 0.0, ns.partial);
+    norm_finish(A, ns);
 }
 
 }  // namespace amg
