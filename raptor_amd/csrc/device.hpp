@@ -28,6 +28,9 @@ namespace amg {
 // kernel geometry shared by host-side block building and the kernels
 constexpr int kTPB = 256;   // threads per workgroup (4 waves of 64)
 constexpr int kCAP = 2048;  // nonzeros staged in LDS per workgroup (16 KiB of products)
+constexpr int kPad = 4;     // col/val padding (entries) for the 16-byte vector-load tail
+constexpr int kDefaultVariant = 0;  // csr-stream variant (kernels.hip kernel_variant())
+int kernel_variant();
 
 template <class T>
 struct DevBuf {

@@ -77,8 +77,14 @@ void DevMatrix::build(Context* c, HostCSR&& h) {
         cls[i] = b;
     }
     rp.upload(hrp.data(), hrp.size());
+    // padded by kPad zero entries: the vector-load tail of the last block stays in bounds
+    hcol.resize(nnz + kPad, 0);
     col.upload(hcol.data(), hcol.size());
-    val.upload(host.val.data(), host.val.size());
+    {
+        std::vector<double> hv(host.val);
+        hv.resize(nnz + kPad, 0.0);
+        val.upload(hv.data(), hv.size());
+    }
     if (square) {
         std::vector<double> d = diagonal(comm, host), di(n_rows);
         for (int64_t i = 0; i < n_rows; ++i) di[i] = 1.0 / d[i];
