@@ -57,6 +57,12 @@ int amg_context_create(int device, void* hip_stream, amg_context* out);
 int amg_context_set_comm(amg_context ctx, int rank, int nranks, const void* rccl_unique_id,
                          amg_alltoallv_fn exchange, void* user);
 int amg_rccl_unique_id(void* out128);
+/* In-process virtual ranks: `nranks` contexts of ONE process (one thread each, any devices)
+ * join the world named `world`; halo exchange and allgathers become device-to-device copies
+ * ordered by events and host barriers, the setup exchange an in-process all-to-all-v.  For
+ * running and testing the multi-rank path on a single GPU (RCCL refuses two ranks per GPU).
+ * Every collective call must be made by all ranks, from their own threads. */
+int amg_context_set_loopback(amg_context ctx, int rank, int nranks, const char* world);
 int amg_context_stream(amg_context ctx, void** hip_stream);
 int amg_context_synchronize(amg_context ctx);
 int amg_context_destroy(amg_context ctx);

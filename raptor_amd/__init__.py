@@ -114,6 +114,15 @@ class Context:
         ctx.rank, ctx.nranks, ctx.group = rank, nranks, gloo
         return ctx
 
+    @classmethod
+    def loopback(cls, rank: int, nranks: int, world: str, device: int = 0, stream=None):
+        """In-process virtual rank ``rank`` of ``nranks`` (one thread per rank, shared GPU):
+        the multi-rank path with device-to-device copies in place of RCCL."""
+        ctx = cls(device, stream)
+        check(lib().amg_context_set_loopback(ctx.h, int(rank), int(nranks), world.encode()))
+        ctx.rank, ctx.nranks = int(rank), int(nranks)
+        return ctx
+
     def synchronize(self):
         check(lib().amg_context_synchronize(self.h))
 

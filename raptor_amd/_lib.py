@@ -83,6 +83,7 @@ SIGNATURES = {
     "amg_context_create": (C.c_int, [C.c_int, _vp, C.POINTER(_vp)]),
     "amg_context_set_comm": (C.c_int, [_vp, C.c_int, C.c_int, _vp, ALLTOALLV_FN, _vp]),
     "amg_rccl_unique_id": (C.c_int, [_vp]),
+    "amg_context_set_loopback": (C.c_int, [_vp, C.c_int, C.c_int, C.c_char_p]),
     "amg_context_stream": (C.c_int, [_vp, C.POINTER(_vp)]),
     "amg_context_synchronize": (C.c_int, [_vp]),
     "amg_context_destroy": (C.c_int, [_vp]),

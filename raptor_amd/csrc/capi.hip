@@ -130,7 +130,7 @@ int amg_context_set_comm(amg_context ctx, int rank, int nranks, const void* uid,
         AMG_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
         Context& c = ctx->c;
         set_device(c);
-        AMG_CHECK(!c.nccl, "communicator already set");
+        AMG_CHECK(!c.nccl && !c.lb, "communicator already set");
         c.host.rank = rank;
         c.host.nranks = nranks;
         c.host.fn = exchange;
@@ -140,7 +140,19 @@ int amg_context_set_comm(amg_context ctx, int rank, int nranks, const void* uid,
             ncclUniqueId id;
             std::memcpy(&id, uid, sizeof(id));
             NCCL_CHECK(ncclCommInitRank(&c.nccl, nranks, id, rank));
+            c.transport = TR_RCCL;
         }
+    });
+}
+
+int amg_context_set_loopback(amg_context ctx, int rank, int nranks, const char* world) {
+    return guard([&] {
+        AMG_CHECK(ctx && world, "null argument");
+        AMG_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
+        Context& c = ctx->c;
+        AMG_CHECK(!c.nccl && !c.lb, "communicator already set");
+        set_device(c);
+        loopback_join(c, rank, nranks, world);
     });
 }
 

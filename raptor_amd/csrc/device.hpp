@@ -65,6 +65,15 @@ struct DevBuf {
     }
 };
 
+struct LoopbackWorld;
+
+// Solve-time data path between ranks.  RCCL over xGMI (one process per GPU) is the product
+// transport; LOOPBACK joins N contexts of ONE process (threads) that share a device: the
+// same plans, pack kernels and interior/boundary overlap, with D2D copies + events + host
+// barriers as the wire.  It exists so the multi-rank device path can be tested on a
+// 1-GPU machine (RCCL refuses two ranks on one GPU).
+enum Transport { TR_NONE = 0, TR_RCCL = 1, TR_LOOPBACK = 2 };
+
 struct Context {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -72,9 +81,24 @@ struct Context {
     hipStream_t comm_stream = nullptr;
     hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
     HostComm host;
+    int transport = TR_NONE;
     ncclComm_t nccl = nullptr;
+    std::shared_ptr<LoopbackWorld> lb;
+    void* lb_user = nullptr;  // host-exchange callback state for the loopback world
+    int64_t mat_seq = 0;      // collective creation counter: matches matrices across ranks
     ~Context();
+    // recv[q*count ..] = rank q's send[0..count) for every q (device pointers, on `stream`)
+    void allgather(const double* send, double* recv, size_t count);
 };
+
+void loopback_join(Context& c, int rank, int nranks, const std::string& world);
+void loopback_leave(Context& c);
+void loopback_before_pack(Context& c, const std::vector<int>& send_procs);
+void loopback_register(Context& c, int64_t seq, const double* send_buf,
+                       const std::vector<int>& send_procs, const std::vector<int64_t>& send_ptr);
+void loopback_halo(Context& c, int64_t seq, const double* x_send_buf, double* halo,
+                   const std::vector<int>& send_procs, const std::vector<int>& recv_procs,
+                   const std::vector<int64_t>& recv_ptr, bool packed);
 
 // ParCSRMatrix on the device: rank-local rows, columns renumbered [local | halo].
 struct DevMatrix {
@@ -96,6 +120,7 @@ struct DevMatrix {
     HaloPlan plan;
     DevBuf<int> send_idx;
     DevBuf<double> send_buf, halo;
+    int64_t seq = -1;  // collective id (loopback transport)
 
     void build(Context* c, HostCSR&& h);
     void ensure_gs_blocks(int64_t block);

@@ -128,7 +128,7 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
             double* slot = bfull.p + cmax * comm.nranks;
             if (A.n_rows > 0)
                 HIP_CHECK(hipMemcpyAsync(slot, b, A.n_rows * sizeof(double), hipMemcpyDeviceToDevice, s));
-            NCCL_CHECK(ncclAllGather(slot, bfull.p, (size_t)cmax, ncclDouble, ctx->nccl, s));
+            ctx->allgather(slot, bfull.p, (size_t)cmax);
             bf = bfull.p;
             launch_dense_gemv(s, A.n_rows, cmax * comm.nranks, invT.p, bf, x);
         } else {

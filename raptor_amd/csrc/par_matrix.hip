@@ -14,6 +14,7 @@
 namespace amg {
 
 Context::~Context() {
+    loopback_leave(*this);
     if (nccl) (void)ncclCommDestroy(nccl);
     if (ev_pack) (void)hipEventDestroy(ev_pack);
     if (ev_halo) (void)hipEventDestroy(ev_halo);
@@ -100,6 +101,9 @@ void DevMatrix::build(Context* c, HostCSR&& h) {
     send_idx.upload(sidx.data(), sidx.size());
     send_buf.alloc(sidx.size());
     halo.alloc(plan.n_halo());
+    seq = ctx->mat_seq++;  // collective order: the same id on every rank
+    if (ctx->transport == TR_LOOPBACK)
+        loopback_register(*ctx, seq, send_buf.p, plan.send_procs, plan.send_ptr);
 }
 
 void DevMatrix::ensure_gs_blocks(int64_t B) {
@@ -133,8 +137,15 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
 bool DevMatrix::halo_begin(const double* x) {
     const HostComm& comm = ctx->host;
     if (comm.nranks == 1) return false;
-    if (plan.send_idx.empty() && plan.halo_gid.empty()) return false;
     hipStream_t s = ctx->stream, cs = ctx->comm_stream;
+    if (ctx->transport == TR_LOOPBACK) {  // collective on every rank, even with no neighbours
+        loopback_before_pack(*ctx, plan.send_procs);
+        launch_pack(s, (int64_t)plan.send_idx.size(), send_idx.p, x, send_buf.p);
+        loopback_halo(*ctx, seq, send_buf.p, halo.p, plan.send_procs, plan.recv_procs,
+                      plan.recv_ptr, true);
+        return true;
+    }
+    if (plan.send_idx.empty() && plan.halo_gid.empty()) return false;
     launch_pack(s, (int64_t)plan.send_idx.size(), send_idx.p, x, send_buf.p);
     HIP_CHECK(hipEventRecord(ctx->ev_pack, s));
     HIP_CHECK(hipStreamWaitEvent(cs, ctx->ev_pack, 0));
@@ -177,7 +188,7 @@ void norm_finish(DevMatrix& A, const NormSink& ns) {
     if (nb > 0) launch_reduce_partials(c->stream, nb, ns.partial, ns.tmp, local);
     else launch_zero(c->stream, 1, local);
     if (nr > 1) {
-        NCCL_CHECK(ncclAllGather(local, ns.gathered, 1, ncclDouble, c->nccl, c->stream));
+        c->allgather(local, ns.gathered, 1);
         launch_finish_norm(c->stream, nr, ns.gathered, ns.hist, ns.counter);
     } else {
         launch_finish_norm(c->stream, 1, local, ns.hist, ns.counter);

@@ -1,0 +1,8 @@
+#!/bin/bash
+# GPU box: the full gpu-marked test suite (one process), then stop.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+TAG=${TAG:-t}
+timeout -k 10 1100 python -m pytest tests -q -m gpu ${PYTEST_ARGS} > gpurun_out/tests_$TAG.log 2>&1; rc=$?
+tail -30 gpurun_out/tests_$TAG.log
+exit $rc

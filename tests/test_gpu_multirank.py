@@ -1,0 +1,161 @@
+"""Multi-rank device path on ONE GPU: N virtual ranks (threads, loopback transport) run the
+same halo plans, pack kernels, interior/boundary overlap, distributed setup and coarse/norm
+allgathers as the RCCL path.  Every rank's slice of every kernel output, level operator and
+V-cycle iterate must be bit-identical to the serial oracle."""
+import threading
+import uuid
+
+import numpy as np
+import pytest
+
+from tests.util import to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+
+def run_ranks(n, fn):
+    """fn(rank, nranks, world) in n threads; re-raise the first failure."""
+    world = "w-" + uuid.uuid4().hex
+    errs = [None] * n
+    out = [None] * n
+
+    def body(r):
+        try:
+            out[r] = fn(r, n, world)
+        except BaseException as e:  # noqa: BLE001
+            errs[r] = e
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    for e in errs:
+        if e is not None:
+            raise e
+    return out
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_slab_kernels_bit_exact(oracle, nranks):
+    import raptor_amd as ra
+
+    O = oracle
+    dims = (14, 13, 17)
+    Ao = O.gen_7pt(*dims)
+    n = Ao.shape[0]
+    x = O.vec_uniform(n, 3)
+    b = O.vec_uniform(n, 4)
+    ref = {"y": Ao.spmv(x), "r": Ao.residual(x, b), "j": Ao.jacobi(x, b, 2.0 / 3.0)}
+    rn_ref = O.norm2(Ao.residual(x, b))
+
+    def rank(r, nr, world):
+        ctx = ra.Context.loopback(r, nr, world)
+        A = ra.par_stencil_grid(ctx, "7pt", dims)
+        f, m = A.first_row, A.local_rows
+        dx, db = to_dev(ctx, x[f:f + m]), to_dev(ctx, b[f:f + m])
+        out = ctx.empty(m)
+        A.mult(dx, out)
+        got = {"y": to_host(ctx, out)}
+        A.residual(dx, db, out)
+        got["r"] = to_host(ctx, out)
+        A.jacobi(dx, db, out)
+        got["j"] = to_host(ctx, out)
+        got["rn"] = A.residual_norm(dx, db)
+        got["halo"] = A.info["n_halo"]
+        return f, m, got
+
+    res = run_ranks(nranks, rank)
+    assert sum(m for _, m, _ in res) == n
+    for f, m, got in res:
+        for k in ("y", "r", "j"):
+            assert np.array_equal(got[k], ref[k][f:f + m]), k
+        assert abs(got["rn"] - rn_ref) <= 1e-12 * rn_ref
+        assert got["halo"] > 0
+
+
+CASES = [(2, "7pt", (16, 15, 18), "pmis", "jacobi"),
+         (3, "7pt", (14, 14, 21), "pmis", "jacobi"),
+         (4, "27pt", (10, 11, 16), "sa", "hybrid_gs"),
+         (2, "5pt", (40, 34), "pmis", "jacobi")]
+
+
+@pytest.mark.parametrize("nranks,kind,dims,coarsen,smoother", CASES)
+def test_multirank_vcycle_bit_exact(oracle, nranks, kind, dims, coarsen, smoother):
+    import raptor_amd as ra
+
+    O = oracle
+    Ao = {"7pt": O.gen_7pt, "5pt": O.gen_5pt, "27pt": O.gen_27pt}[kind](*dims)
+    Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS[coarsen], smoother=O.SMOOTH_JACOBI if smoother == "jacobi"
+                                else O.SMOOTH_HYBRID_GS))
+    n = Ao.shape[0]
+    b = Ao.spmv(O.vec_uniform(n, 42))
+    xs = []
+    xo = np.zeros(n)
+    for _ in range(3):
+        xo = Ho.cycle(xo, b)
+        xs.append(xo.copy())
+    _, hist_o = Ho.solve(np.zeros(n), b, max_iter=6)
+    levels = [(Ho.matrix(l, "A"), Ho.matrix(l, "P") if l + 1 < Ho.num_levels else None)
+              for l in range(Ho.num_levels)]
+
+    def rank(r, nr, world):
+        ctx = ra.Context.loopback(r, nr, world)
+        A = ra.par_stencil_grid(ctx, kind, dims)
+        ml = ra.ParMultilevel(coarsen=coarsen, smoother=smoother).setup(A)
+        f, m = A.first_row, A.local_rows
+        bad = []
+        if ml.num_levels != Ho.num_levels:
+            bad.append(("levels", ml.num_levels, Ho.num_levels))
+        for l in range(min(ml.num_levels, Ho.num_levels)):
+            M = ml.level_matrix(l, "A")
+            loc = M.to_scipy_local()
+            G = levels[l][0][M.first_row:M.first_row + M.local_rows]
+            if not (np.array_equal(loc.indptr, G.indptr) and np.array_equal(loc.indices, G.indices)
+                    and np.array_equal(loc.data, G.data)):
+                bad.append(("A", l))
+        db = to_dev(ctx, b[f:f + m])
+        dx = ctx.zeros(m)
+        for k in range(3):
+            ml.cycle(dx, db)
+            if not np.array_equal(to_host(ctx, dx), xs[k][f:f + m]):
+                bad.append(("cycle", k))
+        dx = ctx.zeros(m)
+        _, hist = ml.solve(dx, db, max_iter=6)
+        return bad, hist
+
+    res = run_ranks(nranks, rank)
+    for bad, hist in res:
+        assert bad == []
+        assert np.all(np.abs(hist - hist_o) <= 1e-10 * hist_o)
+    assert all(np.array_equal(res[0][1], h) for _, h in res)  # every rank reports the same
+
+
+def test_uneven_partition_from_csr(oracle):
+    """ParCSRMatrix.from_csr with a ragged, non-plane-aligned row partition."""
+    import raptor_amd as ra
+
+    O = oracle
+    Ao = O.gen_27pt(9, 8, 7)
+    M = Ao.to_scipy()
+    n = M.shape[0]
+    cuts = [0, 37, 300, n]
+    x = O.vec_uniform(n, 5)
+    y_ref = Ao.spmv(x)
+    xo = O.Hierarchy(Ao, **O.DEFAULTS["pmis"]).cycle(np.zeros(n), y_ref)
+
+    def rank(r, nr, world):
+        ctx = ra.Context.loopback(r, nr, world)
+        lo, hi = cuts[r], cuts[r + 1]
+        A = ra.ParCSRMatrix.from_scipy_local(ctx, M[lo:hi], n, lo)
+        out = ctx.empty(hi - lo)
+        A.mult(to_dev(ctx, x[lo:hi]), out)
+        ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
+        dx = ctx.zeros(hi - lo)
+        ml.cycle(dx, to_dev(ctx, y_ref[lo:hi]))
+        return to_host(ctx, out), to_host(ctx, dx)
+
+    res = run_ranks(3, rank)
+    for r, (y, xc) in enumerate(res):
+        assert np.array_equal(y, y_ref[cuts[r]:cuts[r + 1]])
+        assert np.array_equal(xc, xo[cuts[r]:cuts[r + 1]])
