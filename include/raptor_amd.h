@@ -107,6 +107,10 @@ int amg_par_csr_jacobi(amg_matrix A, const double* x, const double* b, double* x
                        double omega);
 int amg_par_csr_hybrid_gs(amg_matrix A, const double* x, const double* b, double* x_out,
                           int64_t block);
+/* C = A * B (ParCSRMatrix * ParCSRMatrix, row a10): the Galerkin SpGEMM kernel (one
+ * wavefront per output row, LDS hash, canonical accumulation order => bit-identical to the
+ * oracle).  A's column partition must equal B's row partition.  Collective.              */
+int amg_par_csr_matmat(amg_matrix A, amg_matrix B, amg_matrix* C);
 /* ||b - A x||_2 over all ranks (deterministic reduction order). */
 int amg_par_csr_residual_norm(amg_matrix A, const double* x, const double* b, double* out);
 int amg_par_csr_destroy(amg_matrix A);
@@ -128,6 +132,7 @@ typedef struct amg_options {
     int64_t max_coarse;       /* stop when the global size is <= this; dense solve there */
     int64_t gs_block;         /* hybrid GS block (global row multiples)                 */
     uint64_t seed;            /* PMIS / MIS(2) hash seed                                 */
+    int32_t setup_device;     /* 1: Galerkin SpGEMM R(AP) on the GPU (default), 0: host  */
 } amg_options;
 
 #define AMG_PRESET_PMIS_JACOBI 0  /* config 2/4: 7-pt Poisson, Jacobi V-cycle            */

@@ -242,6 +242,12 @@ class ParCSRMatrix:
         check(lib().amg_par_csr_hybrid_gs(self.h, _ptr(x), _ptr(b), _ptr(x_out), int(block)))
         return x_out
 
+    def matmat(self, B: "ParCSRMatrix") -> "ParCSRMatrix":
+        """C = self * B on the GPU (Galerkin SpGEMM kernel; collective)."""
+        h = C.c_void_p()
+        check(lib().amg_par_csr_matmat(self.h, B.h, C.byref(h)))
+        return ParCSRMatrix(self.ctx, h)
+
     def residual_norm(self, x, b) -> float:
         out = C.c_double()
         check(lib().amg_par_csr_residual_norm(self.h, _ptr(x), _ptr(b), C.byref(out)))
@@ -295,13 +301,13 @@ class ParMultilevel:
 
     def __init__(self, coarsen="pmis", smoother="jacobi", strong_threshold=None,
                  jacobi_omega=2.0 / 3.0, pre_sweeps=1, post_sweeps=1, max_levels=25,
-                 max_coarse=256, gs_block=64, seed=0x5EED, use_graph=None):
+                 max_coarse=256, gs_block=64, seed=0x5EED, use_graph=None, setup_device=True):
         if strong_threshold is None:
             strong_threshold = 0.08 if coarsen == "sa" else 0.25
         self.options = Options(self._COARSEN[coarsen], self._SMOOTH[smoother],
                                float(strong_threshold), float(jacobi_omega), int(pre_sweeps),
                                int(post_sweeps), int(max_levels), int(max_coarse), int(gs_block),
-                               int(seed))
+                               int(seed), 1 if setup_device else 0)
         self.use_graph = use_graph
         self.h = None
         self.A = None

@@ -37,6 +37,7 @@ class Options(C.Structure):
         ("max_coarse", C.c_int64),
         ("gs_block", C.c_int64),
         ("seed", C.c_uint64),
+        ("setup_device", C.c_int32),
     ]
 
 
@@ -97,6 +98,7 @@ SIGNATURES = {
     "amg_par_csr_jacobi": (C.c_int, [_vp, _vp, _vp, _vp, _f64]),
     "amg_par_csr_hybrid_gs": (C.c_int, [_vp, _vp, _vp, _vp, _i64]),
     "amg_par_csr_residual_norm": (C.c_int, [_vp, _vp, _vp, _pf64]),
+    "amg_par_csr_matmat": (C.c_int, [_vp, _vp, C.POINTER(_vp)]),
     "amg_par_csr_destroy": (C.c_int, [_vp]),
     "amg_options_default": (C.c_int, [C.c_int, C.POINTER(Options)]),
     "amg_solver_setup": (C.c_int, [_vp, C.POINTER(Options), C.POINTER(_vp)]),

@@ -272,6 +272,21 @@ int amg_par_csr_hybrid_gs(amg_matrix A, const double* x, const double* b, double
     });
 }
 
+int amg_par_csr_matmat(amg_matrix A, amg_matrix B, amg_matrix* out) {
+    return guard([&] {
+        AMG_CHECK(A && B && out, "null argument");
+        AMG_CHECK(A->m->ctx == B->m->ctx, "matrices belong to different contexts");
+        Context& c = *A->m->ctx;
+        set_device(c);
+        HostCSR h = spgemm_device(c, c.host, A->m->host, B->m->host);
+        std::unique_ptr<amg_matrix_s> m(new amg_matrix_s());
+        m->own.reset(new DevMatrix());
+        m->m = m->own.get();
+        m->m->build(&c, std::move(h));
+        *out = m.release();
+    });
+}
+
 int amg_par_csr_residual_norm(amg_matrix A, const double* x, const double* b, double* out) {
     return guard([&] {
         AMG_CHECK(A && out, "null argument");
@@ -319,6 +334,7 @@ int amg_options_default(int preset, amg_options* o) {
         o->max_coarse = 256;
         o->gs_block = 64;
         o->seed = 0x5EED;
+        o->setup_device = 1;
         if (preset == AMG_PRESET_RS_JACOBI) {
             o->coarsen = AMG_COARSEN_RS;
         } else if (preset == AMG_PRESET_SA_HYBRID_GS) {

@@ -91,6 +91,9 @@ struct Context {
     void allgather(const double* send, double* recv, size_t count);
 };
 
+// Galerkin SpGEMM on the device (spgemm.hip); result downloaded as a host image
+HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, const HostCSR& B);
+
 void loopback_join(Context& c, int rank, int nranks, const std::string& world);
 void loopback_leave(Context& c);
 void loopback_before_pack(Context& c, const std::vector<int>& send_procs);

@@ -11,6 +11,7 @@
 // touches it (RCCL, see device.hpp).
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -146,8 +147,11 @@ struct HostHierarchy {
     const HostCSR* A0 = nullptr;
     const HostCSR& A(size_t l) const { return l == 0 ? *A0 : levels[l].A; }
 };
+// Galerkin SpGEMM hook: C = A * B for the local rows (the device SpGEMM of spgemm.hip when
+// the hierarchy is built for a GPU solver; the host spgemm() otherwise).  Same results.
+using SpgemmFn = std::function<HostCSR(const HostCSR&, const HostCSR&)>;
 void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options& opt,
-                     HostHierarchy& H);
+                     HostHierarchy& H, const SpgemmFn& galerkin = nullptr);
 
 uint64_t mix64(uint64_t z);
 uint32_t hash32(int64_t gid, uint64_t seed);

@@ -598,8 +598,11 @@ std::vector<double> dense_inverse_gathered(const HostComm& comm, const HostCSR& 
 }
 
 void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options& opt,
-                     HostHierarchy& H) {
+                     HostHierarchy& H, const SpgemmFn& galerkin) {
     AMG_CHECK(opt.max_levels >= 1, "max_levels must be >= 1");
+    auto mm = [&](const HostCSR& X, const HostCSR& Y) {
+        return galerkin ? galerkin(X, Y) : spgemm(comm, X, Y);
+    };
     H.levels.clear();
     H.A0 = &A0;
     H.levels.emplace_back();
@@ -627,8 +630,8 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
         const int64_t nc = P.n_global_cols;
         if (nc == 0 || nc >= n) break;  // coarsening stalled (same rule as the oracle)
         HostCSR R = transpose(comm, P);
-        HostCSR AP = spgemm(comm, A, P);
-        HostCSR Ac = spgemm(comm, R, AP);
+        HostCSR AP = mm(A, P);
+        HostCSR Ac = mm(R, AP);
         H.levels[l].split = std::move(split);
         H.levels[l].P = std::move(P);
         H.levels[l].R = std::move(R);

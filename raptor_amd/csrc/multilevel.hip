@@ -22,7 +22,12 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     A0 = &A;
     const HostComm& comm = ctx->host;
     HostHierarchy H;
-    build_hierarchy(comm, A.host, opt, H);
+    SpgemmFn galerkin = nullptr;
+    if (opt.setup_device)
+        galerkin = [this, &comm](const HostCSR& X, const HostCSR& Y) {
+            return spgemm_device(*ctx, comm, X, Y);
+        };
+    build_hierarchy(comm, A.host, opt, H, galerkin);
     levels.clear();
     levels.resize(H.levels.size());
     for (size_t l = 0; l < H.levels.size(); ++l) {
