@@ -29,6 +29,7 @@ namespace amg {
 constexpr int kTPB = 256;   // threads per workgroup (4 waves of 64)
 constexpr int kCAP = 2048;  // nonzeros staged in LDS per workgroup (16 KiB of products)
 constexpr int kPad = 4;     // col/val padding (entries) for the 16-byte vector-load tail
+constexpr int kTileLines = 256;  // x tile per workgroup: 256 lines x 64 B = 16 KiB of LDS
 constexpr int kDefaultVariant = 0;  // csr-stream variant (kernels.hip kernel_variant())
 int kernel_variant();
 
@@ -115,6 +116,15 @@ struct DevMatrix {
     // touch halo columns.  Each block is {row begin, row end}.
     DevBuf<int2> blocks;
     int nb_int = 0, nb_bnd = 0;
+    // x tiles: per block the sorted distinct 64-byte lines of x it reads (tile_ptr[nb+1],
+    // tile_lines) and per nonzero a 16-bit index into that tile (lcol)
+    DevBuf<int> tile_ptr, tile_lines;
+    DevBuf<uint16_t> lcol;
+    int64_t tile_bytes = 0;  // bytes the tiled kernel streams per launch (format, not CSR)
+    // csr-stream variant bits (kernels.hip): 2 = XCD block order, 4 = gather (no x tile).
+    // Set at build: x tile when blocks average >= kCAP/2 nonzeros (the lane-major index
+    // tile is padded to kCAP), gather otherwise; XCD order for rectangular operators.
+    int default_variant = 0;
     // hybrid-GS blocks (built on first use for a given block size)
     DevBuf<int2> gs_blocks;
     int n_gs_blocks = 0;

@@ -31,6 +31,11 @@ struct CsrArgs {
     double* y;
     double omega;
     double* partial;
+    const int* tile_ptr;     // x tiles (par_matrix.hip build_row_blocks)
+    const int* tile_lines;
+    const uint16_t* lcol;
+    int hl0;                 // first halo line id = ceil(ncl / 8)
+    int nhalo;
 };
 
 __device__ __forceinline__ double xload(const CsrArgs& a, int c) {
@@ -50,9 +55,6 @@ __device__ __forceinline__ double epilogue(const CsrArgs& a, int r, double s, do
     return a.x[r] + a.omega * (a.dinv[r] * t);
 }
 
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef double v2d __attribute__((ext_vector_type(2)));
-
 // XCD-aware bijection: consecutive row blocks land on the same XCD (blocks b and b+8 share
 // one under round-robin dispatch), so a row block's x neighbours (+-nx*ny rows) are in the
 // same L2.  Placement only changes speed, never results (MI355X_MICROARCH.md).
@@ -61,77 +63,132 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
     return x * q + min(x, rem) + (b >> 3);
 }
 
-template <int MODE, bool NORM, bool VEC, bool XCD>
+// Blocks hold <= kTPB rows, so lane t owns at most row r0 + t.  Its row bounds and
+// epilogue operands are loaded at entry, in flight together with the phase-1 stream, so
+// the epilogue costs no extra memory round trip after the barrier.
+//
+// TILE: instead of gathering x from global memory per nonzero, the workgroup first loads its
+// x tile (the block's distinct 64-byte lines, coalesced: 8 lanes per line) into LDS while the
+// val / 16-bit tile-index streams are in flight; products then read x from LDS.  Same
+// products, same order: bit-identical to the gather path and the oracle.
+template <int MODE, bool NORM, bool XCD, bool TILE>
 __global__ __launch_bounds__(kTPB) void csr_stream_kernel(CsrArgs a, int first_block) {
+    // one 16 KiB stage: first the x tile, then (after the products are in registers) the
+    // products -- the same LDS footprint as the gather path, so the same occupancy
+    static_assert(kTileLines * 8 <= kCAP, "x tile must fit the product stage");
     __shared__ double prod[kCAP];
+    double* const xt = prod;
     __shared__ double red[kTPB / 64];
     const int bid = first_block + (XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x);
     const int2 br = a.blocks[bid];
     const int r0 = br.x, r1 = br.y;
+    const int tid = threadIdx.x;
+    const int r = r0 + tid;
+    const bool own = r < r1;
     const int k0 = a.rp[r0];
     const int nnz = a.rp[r1] - k0;
-    const int tid = threadIdx.x;
+    int e0 = 0, e1 = 0;
+    double pb = 0.0, pd = 0.0, px = 0.0;
+    if (own) {
+        e0 = a.rp[r] - k0;
+        e1 = a.rp[r + 1] - k0;
+        if (MODE == KM_SPMV_ADD) px = a.y[r];
+        if (MODE == KM_RESID || MODE == KM_JACOBI) pb = a.b[r];
+        if (MODE == KM_JACOBI) {
+            pd = a.dinv[r];
+            px = a.x[r];
+        }
+    }
     double sq = 0.0;
-    if (VEC && nnz <= kCAP) {
-        // 16-byte loads: lane t owns entries kb + p*1024 + 4t .. +3 (kb = k0 rounded down to 4;
-        // col/val are padded by 4 entries so the tail never leaves the allocation)
-        constexpr int P = 3;  // ceil((kCAP + 3) / 1024)
-        const int kb = k0 & ~3, k1 = k0 + nnz;
-        v4i c[P];
-        v2d va[P], vb[P];
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-            const int k = kb + p * 4 * kTPB + 4 * tid;
-            if (k < k1) {
-                c[p] = __builtin_nontemporal_load((const v4i*)(a.col + k));
-                va[p] = __builtin_nontemporal_load((const v2d*)(a.val + k));
-                vb[p] = __builtin_nontemporal_load((const v2d*)(a.val + k + 2));
-            }
-        }
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-            const int k = kb + p * 4 * kTPB + 4 * tid;
-            if (k < k1) {
-                if (k >= k0) prod[k - k0] = va[p].x * xload(a, c[p].x);
-                if (k + 1 >= k0 && k + 1 < k1) prod[k + 1 - k0] = va[p].y * xload(a, c[p].y);
-                if (k + 2 >= k0 && k + 2 < k1) prod[k + 2 - k0] = vb[p].x * xload(a, c[p].z);
-                if (k + 3 >= k0 && k + 3 < k1) prod[k + 3 - k0] = vb[p].y * xload(a, c[p].w);
-            }
-        }
-        __syncthreads();
-        for (int r = r0 + tid; r < r1; r += kTPB) {
-            const int e0 = a.rp[r] - k0, e1 = a.rp[r + 1] - k0;
-            double s = 0.0;
-            for (int k = e0; k < e1; ++k) s += prod[k];
-            double res = 0.0;
-            a.y[r] = epilogue<MODE>(a, r, s, &res);
-            if (NORM) sq += res * res;
-        }
-    } else if (nnz <= kCAP) {
+    const int t0 = TILE ? a.tile_ptr[bid] : 0;
+    const int ntl = TILE ? a.tile_ptr[bid + 1] - t0 : 0;
+    if (nnz <= kCAP && (!TILE || ntl <= kTileLines)) {
         constexpr int U = kCAP / kTPB;  // 8 nonzeros per lane
-        int c[U];
         double v[U];
+        if (TILE) {
+            static_assert(U == 8, "lane-major tile indices assume 8 entries per lane");
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            const v4u q = __builtin_nontemporal_load(
+                (const v4u*)(a.lcol + (size_t)bid * kCAP + (size_t)tid * U));
+            const unsigned li[U] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16,
+                                    q.z & 0xffffu, q.z >> 16, q.w & 0xffffu, q.w >> 16};
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            int k = tid + u * kTPB;
-            if (k < nnz) {
-                c[u] = __builtin_nontemporal_load(a.col + k0 + k);
-                v[u] = __builtin_nontemporal_load(a.val + k0 + k);
+            for (int u = 0; u < U; ++u) {
+                const int k = tid + u * kTPB;
+                if (k < nnz) v[u] = __builtin_nontemporal_load(a.val + k0 + k);
+            }
+            // x tile: element e of line L is column 8L + e (local) or halo entry 8(L - hl0) + e
+            // fixed 8 slots per lane, fully unrolled: all line ids, then all x loads in flight
+            constexpr int TU = kTileLines * 8 / kTPB;
+            const int nt = ntl * 8;
+            int Ls[TU];
+#pragma unroll
+            for (int j = 0; j < TU; ++j) {
+                const int idx = tid + j * kTPB;
+                Ls[j] = idx < nt ? a.tile_lines[t0 + (idx >> 3)] : 0;
+            }
+            double xs[TU];
+#pragma unroll
+            for (int j = 0; j < TU; ++j) {
+                const int idx = tid + j * kTPB, e = idx & 7, L = Ls[j];
+                const double* p = nullptr;
+                if (idx < nt) {
+                    if (L < a.hl0) {
+                        const int c = L * 8 + e;
+                        if (c < a.ncl) p = a.x + c;
+                    } else {
+                        const int h = (L - a.hl0) * 8 + e;
+                        if (h < a.nhalo) p = a.xh + h;
+                    }
+                }
+                xs[j] = p ? *p : 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < TU; ++j) {
+                const int idx = tid + j * kTPB;
+                if (idx < nt) xt[idx] = xs[j];
+            }
+            __syncthreads();
+            double pr[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) pr[u] = v[u] * xt[li[u]];
+            __syncthreads();  // every lane has read the tile; reuse it for the products
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = tid + u * kTPB;
+                if (k < nnz) prod[k] = pr[u];
+            }
+        } else {
+            int c[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = tid + u * kTPB;
+                if (k < nnz) {
+                    c[u] = __builtin_nontemporal_load(a.col + k0 + k);
+                    v[u] = __builtin_nontemporal_load(a.val + k0 + k);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = tid + u * kTPB;
+                if (k < nnz) prod[k] = v[u] * xload(a, c[u]);
             }
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            int k = tid + u * kTPB;
-            if (k < nnz) prod[k] = v[u] * xload(a, c[u]);
-        }
         __syncthreads();
-        for (int r = r0 + tid; r < r1; r += kTPB) {
-            const int e0 = a.rp[r] - k0, e1 = a.rp[r + 1] - k0;
+        if (own) {
             double s = 0.0;
             for (int k = e0; k < e1; ++k) s += prod[k];
-            double res = 0.0;
-            a.y[r] = epilogue<MODE>(a, r, s, &res);
-            if (NORM) sq += res * res;
+            double out;
+            if (MODE == KM_SPMV) {
+                out = s;
+            } else if (MODE == KM_SPMV_ADD) {
+                out = px + s;
+            } else {
+                const double t = pb - s;
+                if (NORM) sq = t * t;
+                out = MODE == KM_RESID ? t : px + a.omega * (pd * t);
+            }
+            a.y[r] = out;
         }
     } else {
         // one row longer than the LDS stage: chunked, summed by lane 0 in CSR order
@@ -359,21 +416,23 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
                        double* partial) {
     if (n_blocks <= 0) return;
     CsrArgs a{A.blocks.p, A.rp.p, A.col.p, A.val.p, x, A.halo.p, (int)A.n_cols_local,
-              b, A.dinv.p, y, omega, partial};
+              b, A.dinv.p, y, omega, partial, A.tile_ptr.p, A.tile_lines.p, A.lcol.p,
+              (int)((A.n_cols_local + 7) / 8), (int)A.n_halo()};
     dim3 g(n_blocks), t(kTPB);
-    // default: XCD-ordered blocks for rectangular operators (P, R: +5..17% measured), plain
-    // order for square ones (neutral); scalar loads (the 16-B variant measured slower)
+    // variant bits: 2 = XCD-ordered blocks, 4 = gather path (no x tile).  Default: x tile;
+    // XCD order for rectangular operators (P, R: +5..17% measured), plain order for square
+    // ones (neutral).  (A 16-byte vector-load variant measured 15-20% slower on every level,
+    // profiles/r1b_spmv_variants.txt, and was removed.)
     const char* ev = getenv("AMG_KERNEL_VARIANT");
-    const int var = ev ? (atoi(ev) & 3) : (A.square ? 0 : 2);
-#define AMG_L1(M, N, V, X) hipLaunchKernelGGL((csr_stream_kernel<M, N, V, X>), g, t, 0, s, a, first_block)
-#define AMG_L(M, N)                                          \
-    do {                                                     \
-        switch (var) {                                       \
-            case 1: AMG_L1(M, N, true, false); break;        \
-            case 2: AMG_L1(M, N, false, true); break;        \
-            case 3: AMG_L1(M, N, true, true); break;         \
-            default: AMG_L1(M, N, false, false); break;      \
-        }                                                    \
+    const int var = ev ? atoi(ev) : A.default_variant;
+#define AMG_L1(M, N, X, T) hipLaunchKernelGGL((csr_stream_kernel<M, N, X, T>), g, t, 0, s, a, first_block)
+#define AMG_L(M, N)                                                   \
+    do {                                                              \
+        const bool xo = var & 2, tl = !(var & 4);                     \
+        if (xo && tl) AMG_L1(M, N, true, true);                       \
+        else if (xo) AMG_L1(M, N, true, false);                       \
+        else if (tl) AMG_L1(M, N, false, true);                       \
+        else AMG_L1(M, N, false, false);                              \
     } while (0)
     switch (mode) {
         case KM_SPMV: AMG_L(KM_SPMV, false); break;

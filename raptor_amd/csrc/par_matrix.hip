@@ -22,25 +22,93 @@ Context::~Context() {
     if (own_stream && stream) (void)hipStreamDestroy(stream);
 }
 
-static void build_row_blocks(const std::vector<int>& rp, const std::vector<uint8_t>& cls,
-                             std::vector<int2>& inter, std::vector<int2>& bnd) {
+// Row blocks of the CSR-stream kernel: <= kCAP nonzeros, <= kTPB rows, one class (interior /
+// boundary), and <= kTileLines distinct 64-byte lines of x (8 doubles; local lines first,
+// then halo lines).  Each block gets its sorted line list ("x tile") and every nonzero a
+// 16-bit index into the tile: slot * 8 + (column & 7).  A single row touching more lines
+// than a tile holds becomes a block of its own and takes the untiled path.
+struct BlockBuild {
+    std::vector<int2> blocks;     // interior blocks, then boundary blocks
+    std::vector<int> tile_ptr;    // nb + 1
+    std::vector<int> tile_lines;  // global line ids per block
+    std::vector<uint16_t> lcol;   // per nonzero (nnz + kPad)
+    int nb_int = 0, nb_bnd = 0;
+};
+
+static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector<int>& col,
+                                   const std::vector<uint8_t>& cls, int64_t ncl, int64_t nhalo) {
     const int n = (int)rp.size() - 1;
-    int r0 = 0;
+    const int64_t hl0 = (ncl + 7) / 8;
+    auto line_of = [&](int c) -> int64_t { return c < ncl ? c >> 3 : hl0 + ((c - ncl) >> 3); };
+    std::vector<int> stamp((size_t)(hl0 + (nhalo + 7) / 8) + 1, -1), slot(stamp.size(), 0);
+    struct Rec {
+        int r0, r1;
+        std::vector<int> lines;
+        bool bnd;
+    };
+    std::vector<Rec> recs;
+    BlockBuild out;
+    out.lcol.assign(col.size() + kPad, 0);
+    int r0 = 0, nl = 0, blk = 0;
     long long acc = 0;
+    std::vector<int> lines;
     auto emit = [&](int a, int b) {
         if (b <= a) return;
-        (cls[a] ? bnd : inter).push_back(make_int2(a, b));
+        std::sort(lines.begin(), lines.end());
+        for (size_t s = 0; s < lines.size(); ++s) slot[lines[s]] = (int)s;
+        const bool tiled = (int)lines.size() <= kTileLines;
+        for (int k = rp[a]; k < rp[b]; ++k) {
+            const int c = col[k];
+            const int e = c < ncl ? (c & 7) : (int)((c - ncl) & 7);  // element within its line
+            out.lcol[k] = tiled ? (uint16_t)(slot[line_of(c)] * 8 + e) : (uint16_t)0;
+        }
+        recs.push_back({a, b, tiled ? lines : std::vector<int>(), cls[a] != 0});
+        if (!tiled) recs.back().lines.assign(kTileLines + 1, 0);  // marker: untiled
+        lines.clear();
+        ++blk;
+    };
+    std::vector<int64_t> tstamp(stamp.size(), -1);
+    std::vector<int> cand;
+    // distinct lines of row r not yet in the open block (marker keeps them distinct per call)
+    auto collect = [&](int r, int64_t marker) {
+        cand.clear();
+        for (int k = rp[r]; k < rp[r + 1]; ++k) {
+            const int64_t L = line_of(col[k]);
+            if (stamp[L] != blk && tstamp[L] != marker) {
+                tstamp[L] = marker;
+                cand.push_back((int)L);
+            }
+        }
     };
     for (int r = 0; r < n; ++r) {
         const long long len = rp[r + 1] - rp[r];
-        if (r > r0 && (cls[r] != cls[r0] || acc + len > kCAP || r - r0 >= kTPB)) {
-            emit(r0, r);
+        collect(r, 2 * (int64_t)r);
+        if (r > r0 && (cls[r] != cls[r0] || acc + len > kCAP || r - r0 >= kTPB ||
+                       nl + (int)cand.size() > kTileLines)) {
+            emit(r0, r);  // closes [r0, r); blk advances
             r0 = r;
             acc = 0;
+            nl = 0;
+            collect(r, 2 * (int64_t)r + 1);  // all of row r's lines are new to the new block
         }
+        for (int L : cand) {
+            stamp[L] = blk;
+            lines.push_back(L);
+        }
+        nl += (int)cand.size();
         acc += len;
     }
     emit(r0, n);
+    for (int pass = 0; pass < 2; ++pass)
+        for (const Rec& R : recs) {
+            if (R.bnd != (pass == 1)) continue;
+            out.blocks.push_back(make_int2(R.r0, R.r1));
+            out.tile_ptr.push_back((int)out.tile_lines.size());
+            out.tile_lines.insert(out.tile_lines.end(), R.lines.begin(), R.lines.end());
+            (pass ? out.nb_bnd : out.nb_int)++;
+        }
+    out.tile_ptr.push_back((int)out.tile_lines.size());
+    return out;
 }
 
 void DevMatrix::build(Context* c, HostCSR&& h) {
@@ -91,12 +159,30 @@ void DevMatrix::build(Context* c, HostCSR&& h) {
         for (int64_t i = 0; i < n_rows; ++i) di[i] = 1.0 / d[i];
         dinv.upload(di.data(), di.size());
     }
-    std::vector<int2> bi, bb;
-    build_row_blocks(hrp, cls, bi, bb);
-    nb_int = (int)bi.size();
-    nb_bnd = (int)bb.size();
-    bi.insert(bi.end(), bb.begin(), bb.end());
-    blocks.upload(bi.data(), bi.size());
+    {
+        BlockBuild bb = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo());
+        nb_int = bb.nb_int;
+        nb_bnd = bb.nb_bnd;
+        blocks.upload(bb.blocks.data(), bb.blocks.size());
+        tile_ptr.upload(bb.tile_ptr.data(), bb.tile_ptr.size());
+        if (bb.tile_lines.empty()) bb.tile_lines.push_back(0);
+        tile_lines.upload(bb.tile_lines.data(), bb.tile_lines.size());
+        // lane-major per block: lane t's indices for entries t + 256u (u = 0..7) are 16
+        // contiguous bytes, so the kernel reads them with one 16-byte load per lane
+        const size_t nbk = bb.blocks.size();
+        std::vector<uint16_t> perm(std::max<size_t>(nbk, 1) * kCAP, 0);
+        for (size_t q = 0; q < nbk; ++q) {
+            const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
+            if (nz > kCAP) continue;
+            for (int j = 0; j < nz; ++j)
+                perm[q * kCAP + (size_t)(j % kTPB) * (kCAP / kTPB) + j / kTPB] = bb.lcol[kb + j];
+        }
+        lcol.upload(perm.data(), perm.size());
+        tile_bytes = 8 * nnz + 2 * kCAP * (int64_t)nbk + 4 * (n_rows + 1) +
+                     8 * (int64_t)nbk + 4 * (int64_t)bb.tile_lines.size();
+        const bool dense_blocks = nbk > 0 && nnz >= (int64_t)nbk * (kCAP / 2);
+        default_variant = (dense_blocks ? 0 : 4) | (square ? 0 : 2);
+    }
     std::vector<int> sidx(plan.send_idx.begin(), plan.send_idx.end());
     send_idx.upload(sidx.data(), sidx.size());
     send_buf.alloc(sidx.size());
