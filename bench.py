@@ -46,6 +46,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--traffic-json", type=str,
+                    default=os.path.join(ROOT, "profiles", "pmc_level0_spmv.json"),
+                    help="PMC-measured per-launch HBM traffic of the level-0 SpMV "
+                         "(scripts/gpu_round_profile.sh); reported as roofline.traffic")
     args = ap.parse_args()
 
     import numpy as np
@@ -150,6 +154,18 @@ def main():
     achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
     barrier()
 
+    traffic = None
+    traffic_src = None
+    if grid == (256, 256, 256) and args.traffic_json and os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            traffic = float(tj["traffic_bytes"]) / (spmv_ms * 1e-3) / 1e9
+            traffic_src = (f"{os.path.relpath(args.traffic_json, ROOT)}: "
+                           f"{tj['traffic_bytes'] / 1e9:.3f} GB/launch (2xFETCH_SIZE+WRITE_SIZE) "
+                           "over this run's avg launch time")
+        except (OSError, KeyError, ValueError):
+            traffic = None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(ml, b, args.cpu_seconds, n_global)
@@ -192,7 +208,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": None if traffic is None else round(traffic, 1),
+                "traffic_source": traffic_src,
                 "bytes_per_launch": spmv_bytes,
                 "avg_launch_ms": round(spmv_ms, 5),
             },

@@ -122,8 +122,7 @@ struct DevMatrix {
     DevBuf<uint16_t> lcol;
     int64_t tile_bytes = 0;  // bytes the tiled kernel streams per launch (format, not CSR)
     // csr-stream variant bits (kernels.hip): 2 = XCD block order, 4 = gather (no x tile).
-    // Set at build: x tile when blocks average >= kCAP/2 nonzeros (the lane-major index
-    // tile is padded to kCAP), gather otherwise; XCD order for rectangular operators.
+    // Set at build: x tile for square operators; gather + XCD order for rectangular ones.
     int default_variant = 0;
     // hybrid-GS blocks (built on first use for a given block size)
     DevBuf<int2> gs_blocks;

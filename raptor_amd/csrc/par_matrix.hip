@@ -180,8 +180,10 @@ void DevMatrix::build(Context* c, HostCSR&& h) {
         lcol.upload(perm.data(), perm.size());
         tile_bytes = 8 * nnz + 2 * kCAP * (int64_t)nbk + 4 * (n_rows + 1) +
                      8 * (int64_t)nbk + 4 * (int64_t)bb.tile_lines.size();
-        const bool dense_blocks = nbk > 0 && nnz >= (int64_t)nbk * (kCAP / 2);
-        default_variant = (dense_blocks ? 0 : 4) | (square ? 0 : 2);
+        // measured (profiles/r1c_spmv_variants_tiled.txt, r1d): x tiles win on every square
+        // level operator (A0 -17%, A1/A2 -40%); the rectangular transfer operators are faster
+        // with gathers in XCD order (P0: ~2 nnz/row, R0: lines spread over +-nx*ny)
+        default_variant = square ? 0 : (4 | 2);
     }
     std::vector<int> sidx(plan.send_idx.begin(), plan.send_idx.end());
     send_idx.upload(sidx.data(), sidx.size());

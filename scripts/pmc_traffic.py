@@ -1,0 +1,39 @@
+"""Per-launch HBM traffic of the level-0 SpMV from the PMC passes of scripts/gpu_pmc.sh.
+
+traffic = 2 x FETCH_SIZE + WRITE_SIZE (bytes; FETCH_SIZE reads half the bytes of wide
+streaming loads on gfx950, MI355X_MICROARCH.md "HBM"), averaged over the SpMV launches of
+the 7-pt 256^3 level-0 operator (grid 65536 workgroups, SPMV instantiation).  Writes a JSON
+that bench.py reports as roofline.traffic."""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def per_dispatch(path):
+    vals = defaultdict(dict)
+    meta = {}
+    for r in csv.DictReader(open(path)):
+        d = int(r["Dispatch_Id"])
+        vals[d][r["Counter_Name"]] = float(r["Counter_Value"])
+        meta[d] = (r["Kernel_Name"], int(r["Grid_Size"]) // int(r["Workgroup_Size"]))
+    return vals, meta
+
+
+def main(prefix, out):
+    f, meta = per_dispatch(f"{prefix}_FETCH_SIZE/run_counter_collection.csv")
+    w, _ = per_dispatch(f"{prefix}_WRITE_SIZE/run_counter_collection.csv")
+    # level-0 operator = first matrix in pmc_levels.py: its first 3 csr_stream launches are SpMV
+    ds = [d for d in sorted(meta) if "csr_stream_kernel<0" in meta[d][0]][:3]
+    fetch = sum(f[d]["FETCH_SIZE"] for d in ds) / len(ds) * 1024
+    write = sum(w[d]["WRITE_SIZE"] for d in ds) / len(ds) * 1024
+    res = {"kernel": meta[ds[0]][0].split("(amg::")[0], "grid": meta[ds[0]][1], "launches": len(ds),
+           "fetch_size_bytes": fetch, "write_size_bytes": write,
+           "traffic_bytes": 2 * fetch + write,
+           "note": "2 x FETCH_SIZE + WRITE_SIZE per launch, separate rocprofv3 --pmc passes"}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
