@@ -133,6 +133,9 @@ typedef struct amg_options {
     int64_t gs_block;         /* hybrid GS block (global row multiples)                 */
     uint64_t seed;            /* PMIS / MIS(2) hash seed                                 */
     int32_t setup_device;     /* 1: Galerkin SpGEMM R(AP) on the GPU (default), 0: host  */
+    int64_t replicate_below;  /* multi-rank: levels with <= this many global rows are held
+                                 whole by every rank and cycled without communication (one
+                                 allgather of b per cycle); 0 = never.  Default 65536.      */
 } amg_options;
 
 #define AMG_PRESET_PMIS_JACOBI 0  /* config 2/4: 7-pt Poisson, Jacobi V-cycle            */

@@ -301,13 +301,14 @@ class ParMultilevel:
 
     def __init__(self, coarsen="pmis", smoother="jacobi", strong_threshold=None,
                  jacobi_omega=2.0 / 3.0, pre_sweeps=1, post_sweeps=1, max_levels=25,
-                 max_coarse=256, gs_block=64, seed=0x5EED, use_graph=None, setup_device=True):
+                 max_coarse=256, gs_block=64, seed=0x5EED, use_graph=None, setup_device=True,
+                 replicate_below=65536):
         if strong_threshold is None:
             strong_threshold = 0.08 if coarsen == "sa" else 0.25
         self.options = Options(self._COARSEN[coarsen], self._SMOOTH[smoother],
                                float(strong_threshold), float(jacobi_omega), int(pre_sweeps),
                                int(post_sweeps), int(max_levels), int(max_coarse), int(gs_block),
-                               int(seed), 1 if setup_device else 0)
+                               int(seed), 1 if setup_device else 0, int(replicate_below))
         self.use_graph = use_graph
         self.h = None
         self.A = None

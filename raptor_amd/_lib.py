@@ -38,6 +38,7 @@ class Options(C.Structure):
         ("gs_block", C.c_int64),
         ("seed", C.c_uint64),
         ("setup_device", C.c_int32),
+        ("replicate_below", C.c_int64),
     ]
 
 

@@ -335,6 +335,7 @@ int amg_options_default(int preset, amg_options* o) {
         o->gs_block = 64;
         o->seed = 0x5EED;
         o->setup_device = 1;
+        o->replicate_below = 65536;
         if (preset == AMG_PRESET_RS_JACOBI) {
             o->coarsen = AMG_COARSEN_RS;
         } else if (preset == AMG_PRESET_SA_HYBRID_GS) {

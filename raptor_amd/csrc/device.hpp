@@ -134,7 +134,9 @@ struct DevMatrix {
     DevBuf<double> send_buf, halo;
     int64_t seq = -1;  // collective id (loopback transport)
 
-    void build(Context* c, HostCSR&& h);
+    // replicated: a whole matrix held by every rank (one-rank view, no halo, no exchange)
+    bool replicated = false;
+    void build(Context* c, HostCSR&& h, bool replicated_view = false);
     void ensure_gs_blocks(int64_t block);
     // start the halo exchange of x (pack on the compute stream, RCCL on the comm stream);
     // returns true when a boundary phase is needed
@@ -197,6 +199,11 @@ struct Solver {
     DevBuf<double> invT, bfull;
     int64_t coarse_n = 0;
     std::vector<int> coarse_counts, coarse_displs;
+    // replicated coarse levels: levels >= rep_level are whole on every rank (-1: none)
+    int rep_level = -1;
+    std::vector<int64_t> rep_starts;
+    int64_t rep_cmax = 0;
+    DevBuf<double> rep_pad;
     // solve state: residual history kept on the device, appended by finish_norm_kernel
     DevBuf<double> hist, norm_scratch;
     DevBuf<int> hist_counter;

@@ -126,6 +126,9 @@ std::vector<int64_t> mis2_aggregate(const HostComm& comm, const HostCSR& S, uint
                                     int64_t* n_agg_global, std::vector<int64_t>* agg_starts);
 HostCSR sa_prolongator(const HostComm& comm, const HostCSR& A, const std::vector<int64_t>& agg,
                        int64_t n_agg, const std::vector<int64_t>& agg_starts);
+// every rank receives the whole matrix (rows in global order); the result is a one-rank
+// matrix (row_starts {0, n}, col_starts {0, n_cols}) for replicated coarse levels
+HostCSR gather_global(const HostComm& comm, const HostCSR& M);
 // Gauss-Jordan inverse of the whole (gathered) coarsest matrix, row-major n*n
 std::vector<double> dense_inverse_gathered(const HostComm& comm, const HostCSR& A);
 

@@ -427,4 +427,34 @@ HostCSR stencil_slab(const HostComm& comm, int kind, int64_t nx, int64_t ny, int
     return A;
 }
 
+// ----------------------------------------------------------------------------------
+// Replicated coarse levels: every rank gets all rows (rank order = global row order).
+// ----------------------------------------------------------------------------------
+HostCSR gather_global(const HostComm& comm, const HostCSR& M) {
+    const int64_t n = M.nrows();
+    std::vector<std::vector<int64_t>> sl(comm.nranks), sc(comm.nranks);
+    std::vector<std::vector<double>> sv(comm.nranks);
+    for (int r = 0; r < comm.nranks; ++r) {
+        for (int64_t i = 0; i < n; ++i) sl[r].push_back(M.rp[i + 1] - M.rp[i]);
+        sc[r] = M.col;
+        sv[r] = M.val;
+    }
+    auto gl = comm.exchange(sl);
+    auto gc = comm.exchange(sc);
+    auto gv = comm.exchange(sv);
+    HostCSR G;
+    G.n_global_rows = M.n_global_rows;
+    G.n_global_cols = M.n_global_cols;
+    G.row_starts = {0, M.n_global_rows};
+    G.col_starts = {0, M.n_global_cols};
+    G.rp.assign(1, 0);
+    for (int r = 0; r < comm.nranks; ++r) {
+        for (int64_t l : gl[r]) G.rp.push_back(G.rp.back() + l);
+        G.col.insert(G.col.end(), gc[r].begin(), gc[r].end());
+        G.val.insert(G.val.end(), gv[r].begin(), gv[r].end());
+    }
+    AMG_ASSERT(G.nrows() == M.n_global_rows);
+    return G;
+}
+
 }  // namespace amg

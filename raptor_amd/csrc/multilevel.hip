@@ -28,21 +28,41 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
             return spgemm_device(*ctx, comm, X, Y);
         };
     build_hierarchy(comm, A.host, opt, H, galerkin);
+    // replicated coarse levels (multi-rank): from the first level with <= replicate_below
+    // global rows on, every rank holds the whole operators and cycles them locally
+    rep_level = -1;
+    if (comm.nranks > 1 && opt.replicate_below > 0)
+        for (size_t l = 1; l < H.levels.size(); ++l)
+            if (H.A(l).n_global_rows <= opt.replicate_below) {
+                rep_level = (int)l;
+                break;
+            }
     levels.clear();
     levels.resize(H.levels.size());
     for (size_t l = 0; l < H.levels.size(); ++l) {
         HostLevel& hl = H.levels[l];
-        if (l > 0) {
-            levels[l].A.reset(new DevMatrix());
-            levels[l].A->build(ctx, std::move(hl.A));
-        }
+        const bool rep = rep_level >= 0 && (int)l >= rep_level;
+        auto make = [&](HostCSR& M) {
+            std::unique_ptr<DevMatrix> d(new DevMatrix());
+            if (rep) d->build(ctx, gather_global(comm, M), true);
+            else d->build(ctx, std::move(M));
+            return d;
+        };
+        if (l > 0) levels[l].A = make(hl.A);
         if (l + 1 < H.levels.size()) {
             levels[l].split = std::move(hl.split);
-            levels[l].P.reset(new DevMatrix());
-            levels[l].P->build(ctx, std::move(hl.P));
-            levels[l].R.reset(new DevMatrix());
-            levels[l].R->build(ctx, std::move(hl.R));
+            levels[l].P = make(hl.P);
+            levels[l].R = make(hl.R);
         }
+    }
+    if (rep_level > 0) {  // transition: distributed R output -> whole vector on every rank
+        const HostCSR& Rh = levels[rep_level - 1].R->host;
+        rep_starts = Rh.row_starts;
+        rep_cmax = 0;
+        for (int r = 0; r < comm.nranks; ++r)
+            rep_cmax = std::max(rep_cmax, rep_starts[r + 1] - rep_starts[r]);
+        rep_pad.alloc((size_t)rep_cmax * (comm.nranks + 1));
+        HIP_CHECK(hipMemset(rep_pad.p, 0, rep_pad.n * sizeof(double)));
     }
     // per-level work vectors
     size_t max_blocks = 0;
@@ -74,19 +94,21 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     coarse_n = Ac.host.n_global_rows;
     const std::vector<double>& inv = H.coarse_inv;
     const int64_t nl = Ac.n_rows, f = Ac.first_row;
+    const bool serial_coarse = comm.nranks == 1 || Ac.replicated;
+    const int nparts = serial_coarse ? 1 : comm.nranks;
     int64_t cmax = 0;
-    for (int r = 0; r < comm.nranks; ++r)
+    for (int r = 0; r < nparts; ++r)
         cmax = std::max(cmax, Ac.host.row_starts[r + 1] - Ac.host.row_starts[r]);
-    const int64_t npad = comm.nranks == 1 ? coarse_n : cmax * comm.nranks;
+    const int64_t npad = serial_coarse ? coarse_n : cmax * comm.nranks;
     std::vector<double> invT((size_t)std::max<int64_t>(npad * nl, 1), 0.0);
-    for (int r = 0; r < comm.nranks; ++r)
+    for (int r = 0; r < nparts; ++r)
         for (int64_t j = Ac.host.row_starts[r]; j < Ac.host.row_starts[r + 1]; ++j) {
-            const int64_t jp = comm.nranks == 1 ? j : r * cmax + (j - Ac.host.row_starts[r]);
+            const int64_t jp = serial_coarse ? j : r * cmax + (j - Ac.host.row_starts[r]);
             for (int64_t i = 0; i < nl; ++i) invT[jp * nl + i] = inv[(f + i) * coarse_n + j];
         }
     this->invT.upload(invT.data(), invT.size());
     coarse_counts.assign(1, (int)cmax);
-    if (comm.nranks > 1) {
+    if (!serial_coarse) {
         bfull.alloc((size_t)npad + (size_t)cmax);  // gathered + local padded send slot
         HIP_CHECK(hipMemset(bfull.p, 0, bfull.n * sizeof(double)));
     }
@@ -128,7 +150,7 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
     const HostComm& comm = ctx->host;
     if (l + 1 == levels.size()) {
         const double* bf = b;
-        if (comm.nranks > 1) {
+        if (comm.nranks > 1 && !A.replicated) {
             const int64_t cmax = coarse_counts[0];
             double* slot = bfull.p + cmax * comm.nranks;
             if (A.n_rows > 0)
@@ -152,9 +174,27 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
     if (zero) launch_zero(s, A.n_rows, cur);
     par_apply(A, KM_RESID, cur, b, L.r.p, 0.0, nullptr);
     Level& C = levels[l + 1];
-    par_apply(*L.R, KM_SPMV, L.r.p, nullptr, C.b.p, 0.0, nullptr);
-    cycle_rec(l + 1, C.x.p, C.b.p, true, false);
-    par_apply(*L.P, KM_SPMV_ADD, C.x.p, nullptr, cur, 0.0, nullptr);
+    if ((int)l + 1 == rep_level) {
+        // distributed R output -> whole b_{l+1} on every rank (padded allgather + unpad)
+        const int64_t cmax = rep_cmax, me = comm.rank;
+        double* slot = rep_pad.p + cmax * comm.nranks;
+        par_apply(*L.R, KM_SPMV, L.r.p, nullptr, slot, 0.0, nullptr);
+        ctx->allgather(slot, rep_pad.p, (size_t)cmax);
+        for (int q = 0; q < comm.nranks; ++q) {
+            const int64_t cnt = rep_starts[q + 1] - rep_starts[q];
+            if (cnt)
+                HIP_CHECK(hipMemcpyAsync(C.b.p + rep_starts[q], rep_pad.p + q * cmax,
+                                         cnt * sizeof(double), hipMemcpyDeviceToDevice, s));
+        }
+        (void)me;
+        cycle_rec(l + 1, C.x.p, C.b.p, true, false);
+        // this rank's slice of the whole correction feeds the distributed interpolation
+        par_apply(*L.P, KM_SPMV_ADD, C.x.p + L.P->first_col, nullptr, cur, 0.0, nullptr);
+    } else {
+        par_apply(*L.R, KM_SPMV, L.r.p, nullptr, C.b.p, 0.0, nullptr);
+        cycle_rec(l + 1, C.x.p, C.b.p, true, false);
+        par_apply(*L.P, KM_SPMV_ADD, C.x.p, nullptr, cur, 0.0, nullptr);
+    }
     for (int k = 0; k < opt.post_sweeps; ++k) smooth(l, cur, b, tmp, false, false);
     if (cur != x)
         HIP_CHECK(hipMemcpyAsync(x, cur, A.n_rows * sizeof(double), hipMemcpyDeviceToDevice, s));

@@ -111,10 +111,12 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
     return out;
 }
 
-void DevMatrix::build(Context* c, HostCSR&& h) {
+void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
     ctx = c;
     host = std::move(h);
-    const HostComm& comm = ctx->host;
+    replicated = replicated_view;
+    static const HostComm serial;  // rank 0 of 1: replicated matrices have no halo
+    const HostComm& comm = replicated ? serial : ctx->host;
     AMG_CHECK((int)host.row_starts.size() == comm.nranks + 1, "matrix row partition size");
     AMG_CHECK((int)host.col_starts.size() == comm.nranks + 1, "matrix column partition size");
     first_row = host.row_starts[comm.rank];
@@ -190,7 +192,7 @@ void DevMatrix::build(Context* c, HostCSR&& h) {
     send_buf.alloc(sidx.size());
     halo.alloc(plan.n_halo());
     seq = ctx->mat_seq++;  // collective order: the same id on every rank
-    if (ctx->transport == TR_LOOPBACK)
+    if (ctx->transport == TR_LOOPBACK && !replicated)
         loopback_register(*ctx, seq, send_buf.p, plan.send_procs, plan.send_ptr);
 }
 
@@ -224,7 +226,7 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
 
 bool DevMatrix::halo_begin(const double* x) {
     const HostComm& comm = ctx->host;
-    if (comm.nranks == 1) return false;
+    if (comm.nranks == 1 || replicated) return false;
     hipStream_t s = ctx->stream, cs = ctx->comm_stream;
     if (ctx->transport == TR_LOOPBACK) {  // collective on every rank, even with no neighbours
         loopback_before_pack(*ctx, plan.send_procs);

@@ -80,8 +80,11 @@ CASES = [(2, "7pt", (16, 15, 18), "pmis", "jacobi"),
          (2, "5pt", (40, 34), "pmis", "jacobi")]
 
 
+@pytest.mark.parametrize("rep", [0, 800, 10 ** 9], ids=["distributed", "rep-deep", "rep-all"])
 @pytest.mark.parametrize("nranks,kind,dims,coarsen,smoother", CASES)
-def test_multirank_vcycle_bit_exact(oracle, nranks, kind, dims, coarsen, smoother):
+def test_multirank_vcycle_bit_exact(oracle, nranks, kind, dims, coarsen, smoother, rep):
+    """rep = replicate_below: 0 keeps every level distributed; 800 replicates the coarse
+    tail; 1e9 replicates everything below the fine level."""
     import raptor_amd as ra
 
     O = oracle
@@ -102,7 +105,7 @@ def test_multirank_vcycle_bit_exact(oracle, nranks, kind, dims, coarsen, smoothe
     def rank(r, nr, world):
         ctx = ra.Context.loopback(r, nr, world)
         A = ra.par_stencil_grid(ctx, kind, dims)
-        ml = ra.ParMultilevel(coarsen=coarsen, smoother=smoother).setup(A)
+        ml = ra.ParMultilevel(coarsen=coarsen, smoother=smoother, replicate_below=rep).setup(A)
         f, m = A.first_row, A.local_rows
         bad = []
         if ml.num_levels != Ho.num_levels:
