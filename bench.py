@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--config", choices=["7pt", "sa27"], default="7pt",
+                    help="7pt: the metric workload (default); sa27: BASELINE.json configs[2], "
+                         "27-pt anisotropic Q1 diffusion, smoothed aggregation + hybrid GS")
     ap.add_argument("--traffic-json", type=str,
                     default=os.path.join(ROOT, "profiles", "pmc_level0_spmv.json"),
                     help="PMC-measured per-launch HBM traffic of the level-0 SpMV "
@@ -83,11 +86,15 @@ def main():
             dist.barrier()
 
     t0 = time.perf_counter()
-    A = ra.par_stencil_grid(ctx, "7pt", grid)
+    sa27 = args.config == "sa27"
+    A = ra.par_stencil_grid(ctx, "27pt" if sa27 else "7pt", grid)
     log(rank, f"matrix {grid} built in {time.perf_counter() - t0:.1f}s; local rows {A.local_rows}")
     t1 = time.perf_counter()
-    ml = ra.ParRugeStubenSolver(coarsen="pmis",
-                                use_graph=False if args.no_graph else None).setup(A)
+    graph = False if args.no_graph else None
+    if sa27:  # BASELINE.json configs[2]: smoothed aggregation + hybrid Gauss-Seidel
+        ml = ra.ParSmoothedAggregationSolver(use_graph=graph).setup(A)
+    else:     # BASELINE.json configs[1]/[3]: PMIS + classical interpolation, Jacobi
+        ml = ra.ParRugeStubenSolver(coarsen="pmis", use_graph=graph).setup(A)
     setup_s = time.perf_counter() - t1
     nlev = ml.num_levels
     infos = [ml.level_info(l) for l in range(nlev)]
@@ -156,7 +163,8 @@ def main():
 
     traffic = None
     traffic_src = None
-    if grid == (256, 256, 256) and args.traffic_json and os.path.exists(args.traffic_json):
+    if (not sa27 and grid == (256, 256, 256) and args.traffic_json
+            and os.path.exists(args.traffic_json)):
         try:
             tj = json.load(open(args.traffic_json))
             traffic = float(tj["traffic_bytes"]) / (spmv_ms * 1e-3) / 1e9
@@ -183,10 +191,13 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (7-pt Poisson, b = A x*, x* splitmix64 U(-1,1) seed 42, x0 = 0)",
+            "data": "synthetic (b = A x*, x* splitmix64 U(-1,1) seed 42, x0 = 0)",
             "config": {
-                "workload": f"3D 7-pt Poisson {grid[0]}x{grid[1]}x{grid[2]}, PMIS + classical interp, "
-                            "Jacobi(2/3) 1+1 V-cycle, z-slab row partition",
+                "workload": (f"3D 27-pt Q1 anisotropic diffusion (1,1,1e-3) {grid[0]}x{grid[1]}x{grid[2]}, "
+                             "smoothed aggregation (MIS(2)), hybrid GS(64) 1+1 V-cycle, z-slab row partition")
+                if sa27 else
+                (f"3D 7-pt Poisson {grid[0]}x{grid[1]}x{grid[2]}, PMIS + classical interp, "
+                 "Jacobi(2/3) 1+1 V-cycle, z-slab row partition"),
                 "grid": list(grid),
                 "global_rows": n_global,
                 "levels": nlev,
