@@ -165,6 +165,10 @@ int amg_solver_cycle(amg_solver S, double* x, const double* b);
  * Norms stay on the device until the end: no host sync inside the loop. */
 int amg_solver_solve(amg_solver S, double* x, const double* b, int32_t max_iter, double tol,
                      double* hist, int32_t* iters);
+/* Conjugate gradients preconditioned by one V-cycle per iteration (row f3: the natural
+ * caller of the cycle).  Same contract as amg_solver_solve; hist receives ||r_k||. */
+int amg_solver_pcg(amg_solver S, double* x, const double* b, int32_t max_iter, double tol,
+                   double* hist, int32_t* iters);
 /* Capture each V-cycle in a hipGraph and replay it (1 = on, default on for 1 rank). */
 int amg_solver_set_graph(amg_solver S, int32_t enable);
 int amg_solver_destroy(amg_solver S);

@@ -928,6 +928,55 @@ int32_t orc_hier_solve(orc_hier* H, double* x, const double* b, int32_t max_iter
     return it;
 }
 
+static double dotp(int64_t n, const double* a, const double* b) {
+    double s = 0.0;
+    for (int64_t i = 0; i < n; ++i) s += a[i] * b[i];
+    return s;
+}
+
+/* PCG (row f3): r = b - Ax; z = M r; p = z; loop { q = Ap; alpha = (r,z)/(p,q);
+ * x += alpha p; r -= alpha q; record ||r||; z = M r; beta = (r,z_new)/(r,z); p = z + beta p } */
+int32_t orc_hier_pcg(orc_hier* H, double* x, const double* b, int32_t max_iter, double tol,
+                     double* hist) {
+    const orc_csr* A = H->A[0];
+    int64_t n = A->n_rows;
+    double* r = XMALLOC(double, n);
+    double* z = XMALLOC(double, n);
+    double* p = XMALLOC(double, n);
+    double* q = XMALLOC(double, n);
+    orc_residual(A, x, b, r);
+    double r0 = sqrt(dotp(n, r, r));
+    hist[0] = r0;
+    memset(z, 0, sizeof(double) * (size_t)n);
+    orc_hier_cycle(H, z, r);
+    memcpy(p, z, sizeof(double) * (size_t)n);
+    double rz = dotp(n, r, z);
+    int32_t it = 0;
+    while (it < max_iter) {
+        orc_spmv(A, p, q);
+        double alpha = rz / dotp(n, p, q);
+        for (int64_t i = 0; i < n; ++i) {
+            x[i] = x[i] + alpha * p[i];
+            r[i] = r[i] - alpha * q[i];
+        }
+        double rn = sqrt(dotp(n, r, r));
+        hist[++it] = rn;
+        if (tol > 0.0 && r0 > 0.0 && rn / r0 < tol) break;
+        if (it == max_iter) break;
+        memset(z, 0, sizeof(double) * (size_t)n);
+        orc_hier_cycle(H, z, r);
+        double rzn = dotp(n, r, z);
+        double beta = rzn / rz;
+        for (int64_t i = 0; i < n; ++i) p[i] = z[i] + beta * p[i];
+        rz = rzn;
+    }
+    free(r);
+    free(z);
+    free(p);
+    free(q);
+    return it;
+}
+
 #ifdef _OPENMP
 #include <omp.h>
 #endif

@@ -101,6 +101,9 @@ void orc_hier_cycle(orc_hier* H, double* x, const double* b);
 int32_t orc_num_threads(void); /* OpenMP threads the level kernels use */
 int32_t orc_hier_solve(orc_hier* H, double* x, const double* b, int32_t max_iter, double tol,
                        double* hist);
+/* CG preconditioned by one V-cycle (z = 0; cycle(z, r)) per iteration (row f3). */
+int32_t orc_hier_pcg(orc_hier* H, double* x, const double* b, int32_t max_iter, double tol,
+                     double* hist);
 
 #ifdef __cplusplus
 }

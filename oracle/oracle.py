@@ -87,6 +87,7 @@ def lib():
                                           C.POINTER(vp), C.POINTER(_Opt)]),
             "orc_hier_levels": (C.c_int32, [vp]),
             "orc_num_threads": (C.c_int32, []),
+            "orc_hier_pcg": (C.c_int32, [vp, _f64p, _f64p, C.c_int32, C.c_double, _f64p]),
             "orc_hier_matrix": (vp, [vp, C.c_int32, C.c_int32]),
             "orc_hier_split": (None, [vp, C.c_int32, _i32p]),
             "orc_hier_cycle": (None, [vp, _f64p, _f64p]),
@@ -327,4 +328,12 @@ class Hierarchy:
         hist = np.zeros(max_iter + 1)
         it = lib().orc_hier_solve(self.h, _p(x, _f64p), _p(b, _f64p), max_iter, tol,
                                   _p(hist, _f64p))
+        return x, hist[: it + 1]
+
+    def pcg(self, x, b, max_iter=10, tol=0.0):
+        x = np.array(x, np.float64, copy=True)
+        b = np.ascontiguousarray(b, np.float64)
+        hist = np.zeros(max_iter + 1)
+        it = lib().orc_hier_pcg(self.h, _p(x, _f64p), _p(b, _f64p), max_iter, tol,
+                                _p(hist, _f64p))
         return x, hist[: it + 1]

@@ -362,6 +362,14 @@ class ParMultilevel:
                                      hist.ctypes.data_as(C.POINTER(C.c_double)), C.byref(it)))
         return x, hist[: it.value + 1]
 
+    def pcg(self, x, b, max_iter=20, tol=0.0):
+        """Conjugate gradients with one V-cycle as the preconditioner."""
+        hist = np.zeros(int(max_iter) + 1)
+        it = C.c_int32()
+        check(lib().amg_solver_pcg(self.h, _ptr(x), _ptr(b), int(max_iter), float(tol),
+                                   hist.ctypes.data_as(C.POINTER(C.c_double)), C.byref(it)))
+        return x, hist[: it.value + 1]
+
     def __del__(self):
         h = getattr(self, "h", None)
         if h:

@@ -430,6 +430,15 @@ int amg_solver_solve(amg_solver S, double* x, const double* b, int32_t max_iter,
     });
 }
 
+int amg_solver_pcg(amg_solver S, double* x, const double* b, int32_t max_iter, double tol,
+                   double* hist, int32_t* iters) {
+    return guard([&] {
+        AMG_CHECK(S && hist && iters, "null argument");
+        set_device(*S->s.ctx);
+        *iters = S->s.pcg(x, b, max_iter, tol, hist);
+    });
+}
+
 int amg_solver_set_graph(amg_solver S, int32_t enable) {
     return guard([&] {
         AMG_CHECK(S, "null solver");

@@ -160,6 +160,15 @@ void launch_pack(hipStream_t s, int64_t n, const int* idx, const double* x, doub
 void launch_reduce_partials(hipStream_t s, int n, const double* partial, double* tmp, double* out);
 // hist[*counter] = sqrt(sum_{i<n} in[i]) (rank order); ++*counter
 void launch_finish_norm(hipStream_t s, int n, const double* in, double* hist, int* counter);
+// PCG helpers: deterministic dot partials (fixed block span), scalar finish, fused updates
+int dot_partial_count(int64_t n);
+void launch_dot_partials(hipStream_t s, int64_t n, const double* a, const double* b, double* partial);
+void launch_finish_sum(hipStream_t s, int n, const double* in, double* out, bool take_sqrt);
+void launch_pcg_xr(hipStream_t s, int64_t n, const double* rz, const double* pq, const double* p,
+                   const double* q, double* x, double* r);
+void launch_pcg_p(hipStream_t s, int64_t n, const double* rz_new, const double* rz_old,
+                  const double* z, double* p);
+void launch_append(hipStream_t s, const double* v, double* hist, int* counter);
 void launch_dense_gemv(hipStream_t s, int64_t n_local, int64_t n, const double* invT,
                        const double* bfull, double* x);
 void launch_uniform(hipStream_t s, int64_t n, int64_t first_gid, uint64_t seed, double* out);
@@ -226,6 +235,10 @@ struct Solver {
     bool can_fuse_norm() const;
     // ParMultilevel::solve; hist_host gets it+1 norms
     int32_t solve(double* x, const double* b, int32_t max_iter, double tol, double* hist_host);
+    // AMG-preconditioned conjugate gradients (one V-cycle per iteration as M^-1)
+    int32_t pcg(double* x, const double* b, int32_t max_iter, double tol, double* hist_host);
+    DevBuf<double> pcg_vec, pcg_scratch;  // r | z | p | q ; dot partials | tmp | gathered | scalars
+    void dot(const double* a, const double* b, double* dst, bool take_sqrt);
     int64_t bytes_per_cycle(size_t l) const;
     ~Solver();
 };

@@ -402,7 +402,96 @@ inline int grid_for(long long n, int tpb = kTPB) {
     return (int)(g < 1 ? 1 : g);
 }
 
+// ---- PCG vector kernels (row f3) ---------------------------------------------------
+// dot partials: block g covers [g*kDotSpan, (g+1)*kDotSpan) with 8 fixed loads per lane,
+// fixed shuffle tree, 4 wave sums in order => deterministic for a given n
+constexpr int kDotSpan = kTPB * 8;
+__global__ __launch_bounds__(kTPB) void dot_partials_kernel(long long n, const double* a,
+                                                            const double* b, double* partial) {
+    __shared__ double red[kTPB / 64];
+    const long long base = (long long)blockIdx.x * kDotSpan + threadIdx.x;
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const long long i = base + (long long)j * kTPB;
+        if (i < n) s += a[i] * b[i];
+    }
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// out = sum_{i<n} in[i] (rank order), optional sqrt
+__global__ void finish_sum_kernel(int n, const double* in, double* out, int take_sqrt) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        double s = 0.0;
+        for (int i = 0; i < n; ++i) s += in[i];
+        *out = take_sqrt ? sqrt(s) : s;
+    }
+}
+
+// x += (rz/pq) p ; r -= (rz/pq) q
+__global__ void pcg_xr_kernel(long long n, const double* rz, const double* pq, const double* p,
+                              const double* q, double* x, double* r) {
+    const double alpha = *rz / *pq;
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) {
+        x[i] = x[i] + alpha * p[i];
+        r[i] = r[i] - alpha * q[i];
+    }
+}
+
+// p = z + (rz_new/rz_old) p
+__global__ void pcg_p_kernel(long long n, const double* rz_new, const double* rz_old,
+                             const double* z, double* p) {
+    const double beta = *rz_new / *rz_old;
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) p[i] = z[i] + beta * p[i];
+}
+
+__global__ void append_kernel(const double* v, double* hist, int* counter) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        hist[*counter] = *v;
+        *counter += 1;
+    }
+}
+
 }  // namespace
+
+int dot_partial_count(int64_t n) { return (int)std::max<int64_t>(1, (n + kDotSpan - 1) / kDotSpan); }
+
+void launch_dot_partials(hipStream_t s, int64_t n, const double* a, const double* b, double* partial) {
+    const int g = dot_partial_count(n);
+    hipLaunchKernelGGL(dot_partials_kernel, dim3(g), dim3(kTPB), 0, s, (long long)n, a, b, partial);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_finish_sum(hipStream_t s, int n, const double* in, double* out, bool take_sqrt) {
+    hipLaunchKernelGGL(finish_sum_kernel, dim3(1), dim3(64), 0, s, n, in, out, take_sqrt ? 1 : 0);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_pcg_xr(hipStream_t s, int64_t n, const double* rz, const double* pq, const double* p,
+                   const double* q, double* x, double* r) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(pcg_xr_kernel, dim3(grid_for(n)), dim3(kTPB), 0, s, (long long)n, rz, pq, p, q, x, r);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_pcg_p(hipStream_t s, int64_t n, const double* rz_new, const double* rz_old,
+                  const double* z, double* p) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(pcg_p_kernel, dim3(grid_for(n)), dim3(kTPB), 0, s, (long long)n, rz_new, rz_old, z, p);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_append(hipStream_t s, const double* v, double* hist, int* counter) {
+    hipLaunchKernelGGL(append_kernel, dim3(1), dim3(64), 0, s, v, hist, counter);
+    HIP_CHECK(hipGetLastError());
+}
 
 // CSR-stream variant: bit 0 = 16-byte vector loads, bit 1 = XCD-aware block order.
 // AMG_KERNEL_VARIANT overrides the default (A/B timing; results are identical).

@@ -271,6 +271,88 @@ int32_t Solver::solve(double* x, const double* b, int32_t max_iter, double tol, 
     return it;
 }
 
+// ---- AMG-preconditioned CG ------------------------------------
+// Scalars never leave the device (alpha/beta are formed inside the update kernels), so an
+// iteration has no host synchronisation unless a tolerance is requested.  Dot products use
+// a fixed block span + fixed trees + rank-ordered sums: deterministic for a given partition.
+enum { SC_RZ = 0, SC_RZN, SC_PQ, SC_RN, SC_N };
+
+void Solver::dot(const double* a, const double* b, double* dst, bool take_sqrt) {
+    DevMatrix& A = *A0;
+    const int g = dot_partial_count(A.n_rows);
+    double* partial = pcg_scratch.p;
+    double* tmp = partial + g;
+    double* gathered = tmp + g / 4096 + 64;
+    double* local = gathered + ctx->host.nranks;
+    launch_dot_partials(ctx->stream, A.n_rows, a, b, partial);
+    launch_reduce_partials(ctx->stream, g, partial, tmp, local);
+    if (ctx->host.nranks > 1) {
+        ctx->allgather(local, gathered, 1);
+        launch_finish_sum(ctx->stream, ctx->host.nranks, gathered, dst, take_sqrt);
+    } else {
+        launch_finish_sum(ctx->stream, 1, local, dst, take_sqrt);
+    }
+}
+
+int32_t Solver::pcg(double* x, const double* b, int32_t max_iter, double tol, double* hist_host) {
+    AMG_CHECK(max_iter >= 0, "max_iter must be >= 0");
+    DevMatrix& A = *A0;
+    const int64_t n = A.n_rows;
+    hipStream_t s = ctx->stream;
+    if (pcg_vec.n < (size_t)(4 * n + 4)) pcg_vec.alloc((size_t)(4 * n + 4));
+    const int g = dot_partial_count(n);
+    const size_t need = (size_t)g + g / 4096 + 64 + ctx->host.nranks + 2 + SC_N;
+    if (pcg_scratch.n < need) pcg_scratch.alloc(need);
+    double* r = pcg_vec.p;
+    double* z = r + n;
+    double* p = z + n;
+    double* q = p + n;
+    double* sc = pcg_scratch.p + (need - SC_N);
+    ensure_hist(max_iter + 1);
+    HIP_CHECK(hipMemsetAsync(hist_counter.p, 0, sizeof(int), s));
+    auto record_norm = [&] {
+        dot(r, r, sc + SC_RN, true);
+        launch_append(s, sc + SC_RN, hist.p, hist_counter.p);
+    };
+    auto precondition = [&] {  // z = M^-1 r: one V-cycle from z = 0
+        launch_zero(s, n, z);
+        cycle(z, r, false);
+    };
+    par_apply(A, KM_RESID, x, b, r, 0.0, nullptr);
+    record_norm();
+    double r0 = 0.0;
+    if (tol > 0.0) {
+        HIP_CHECK(hipMemcpyAsync(&r0, hist.p, sizeof(double), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+    }
+    precondition();
+    if (n) HIP_CHECK(hipMemcpyAsync(p, z, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+    dot(r, z, sc + SC_RZ, false);
+    int32_t it = 0;
+    while (it < max_iter) {
+        par_apply(A, KM_SPMV, p, nullptr, q, 0.0, nullptr);
+        dot(p, q, sc + SC_PQ, false);
+        launch_pcg_xr(s, n, sc + SC_RZ, sc + SC_PQ, p, q, x, r);
+        record_norm();
+        ++it;
+        if (tol > 0.0) {
+            double rn = 0.0;
+            HIP_CHECK(hipMemcpyAsync(&rn, hist.p + it, sizeof(double), hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            if (r0 > 0.0 && rn / r0 < tol) break;
+        }
+        if (it == max_iter) break;
+        precondition();
+        dot(r, z, sc + SC_RZN, false);
+        launch_pcg_p(s, n, sc + SC_RZN, sc + SC_RZ, z, p);
+        HIP_CHECK(hipMemcpyAsync(sc + SC_RZ, sc + SC_RZN, sizeof(double), hipMemcpyDeviceToDevice, s));
+    }
+    HIP_CHECK(hipMemcpyAsync(hist_host, hist.p, sizeof(double) * (size_t)(it + 1),
+                             hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    return it;
+}
+
 static int64_t spmv_bytes(const DevMatrix& M) {
     return 12 * M.nnz + 4 * (M.n_rows + 1) + 8 * M.n_cols_local + 8 * M.n_rows;
 }

@@ -162,3 +162,26 @@ def test_uneven_partition_from_csr(oracle):
     for r, (y, xc) in enumerate(res):
         assert np.array_equal(y, y_ref[cuts[r]:cuts[r + 1]])
         assert np.array_equal(xc, xo[cuts[r]:cuts[r + 1]])
+
+
+def test_multirank_pcg(oracle):
+    import raptor_amd as ra
+
+    O = oracle
+    dims = (18, 16, 21)
+    Ao = O.gen_7pt(*dims)
+    n = Ao.shape[0]
+    b = O.vec_uniform(n, 5)
+    Ho = O.Hierarchy(Ao, **O.DEFAULTS["pmis"])
+    _, hist_o = Ho.pcg(np.zeros(n), b, max_iter=10)
+
+    def rank(r, nr, world):
+        ctx = ra.Context.loopback(r, nr, world)
+        A = ra.par_stencil_grid(ctx, "7pt", dims)
+        ml = ra.ParRugeStubenSolver(coarsen="pmis", replicate_below=500).setup(A)
+        f, m = A.first_row, A.local_rows
+        _, hist = ml.pcg(ctx.zeros(m), to_dev(ctx, b[f:f + m]), max_iter=10)
+        return hist
+
+    for hist in run_ranks(3, rank):
+        assert np.all(np.abs(hist - hist_o) <= 1e-9 * hist_o[0])

@@ -148,3 +148,16 @@ def test_vcycle_converges(oracle, coarsen):
     b = A.spmv(O.vec_uniform(A.shape[0], 42))
     _, hist = H.solve(np.zeros(A.shape[0]), b, max_iter=10)
     assert hist[-1] / hist[0] < 0.05
+
+
+def test_oracle_pcg_beats_stationary_iteration(oracle):
+    O = oracle
+    A = O.gen_7pt(20, 20, 20)
+    n = A.shape[0]
+    H = O.Hierarchy(A, **O.DEFAULTS["pmis"])
+    b = A.spmv(O.vec_uniform(n, 42))
+    _, hv = H.solve(np.zeros(n), b, max_iter=10)
+    x, hp = H.pcg(np.zeros(n), b, max_iter=10)
+    assert hp[-1] < 0.1 * hv[-1]
+    r = b - A.spmv(x)
+    assert abs(np.linalg.norm(r) - hp[-1]) <= 1e-6 * hp[0]  # recursive residual ~ true residual
