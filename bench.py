@@ -46,9 +46,14 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--config", choices=["7pt", "sa27"], default="7pt",
+    ap.add_argument("--config", choices=["7pt", "sa27", "g3sub"], default="7pt",
                     help="7pt: the metric workload (default); sa27: BASELINE.json configs[2], "
-                         "27-pt anisotropic Q1 diffusion, smoothed aggregation + hybrid GS")
+                         "27-pt anisotropic Q1 diffusion, smoothed aggregation + hybrid GS; "
+                         "g3sub: BASELINE.json configs[4] with the offline substitute for "
+                         "G3_circuit (seeded unstructured graph Laplacian, RCM-reordered), SA")
+    ap.add_argument("--lattice", type=int, default=1225,
+                    help="g3sub: lattice side (1225^2 = 1.5M rows, G3_circuit size)")
+    ap.add_argument("--no-reorder", action="store_true", help="g3sub: keep the random numbering")
     ap.add_argument("--traffic-json", type=str,
                     default=os.path.join(ROOT, "profiles", "pmc_level0_spmv.json"),
                     help="PMC-measured per-launch HBM traffic of the level-0 SpMV "
@@ -75,11 +80,17 @@ def main():
         torch.cuda.set_device(0)
         ctx = ra.Context(0)
 
-    if args.grid:
+    g3 = args.config == "g3sub"
+    if g3:
+        grid = (args.lattice, args.lattice, 1)
+    elif args.grid:
         grid = tuple(int(v) for v in args.grid.split(","))
     else:
         grid = GRIDS.get(world, (256, 256, 256 * world))
     n_global = grid[0] * grid[1] * grid[2]
+    # 7pt/sa27 are weak-scaled and reported in 256^3-equivalent cycles; g3sub is one fixed
+    # matrix (strong scaling), reported in plain cycles/s
+    scale = 1.0 if g3 else n_global / float(256 ** 3)
 
     def barrier():
         if world > 1:
@@ -87,11 +98,19 @@ def main():
 
     t0 = time.perf_counter()
     sa27 = args.config == "sa27"
-    A = ra.par_stencil_grid(ctx, "27pt" if sa27 else "7pt", grid)
+    reorder_s = None
+    if g3:
+        A = ra.par_graph_laplacian(ctx, grid[0], grid[1], seed=1)
+        if not args.no_reorder:
+            tr = time.perf_counter()
+            A, _ = A.reorder("rcm")
+            reorder_s = time.perf_counter() - tr
+    else:
+        A = ra.par_stencil_grid(ctx, "27pt" if sa27 else "7pt", grid)
     log(rank, f"matrix {grid} built in {time.perf_counter() - t0:.1f}s; local rows {A.local_rows}")
     t1 = time.perf_counter()
     graph = False if args.no_graph else None
-    if sa27:  # BASELINE.json configs[2]: smoothed aggregation + hybrid Gauss-Seidel
+    if sa27 or g3:  # BASELINE.json configs[2]/[4]: smoothed aggregation + hybrid Gauss-Seidel
         ml = ra.ParSmoothedAggregationSolver(use_graph=graph).setup(A)
     else:     # BASELINE.json configs[1]/[3]: PMIS + classical interpolation, Jacobi
         ml = ra.ParRugeStubenSolver(coarsen="pmis", use_graph=graph).setup(A)
@@ -130,7 +149,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     iters_per_s = args.steps / dt
-    value = iters_per_s * n_global / float(256 ** 3)
+    value = iters_per_s * scale
     conv = float((hist[-1] / hist[0]) ** (1.0 / max(1, len(hist) - 1))) if hist[0] > 0 else None
     log(rank, f"{args.steps} V-cycles in {dt * 1e3:.2f} ms -> {iters_per_s:.1f} it/s, conv {conv}")
 
@@ -163,7 +182,7 @@ def main():
 
     traffic = None
     traffic_src = None
-    if (not sa27 and grid == (256, 256, 256) and args.traffic_json
+    if (args.config == "7pt" and grid == (256, 256, 256) and args.traffic_json
             and os.path.exists(args.traffic_json)):
         try:
             tj = json.load(open(args.traffic_json))
@@ -176,24 +195,32 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(ml, b, args.cpu_seconds, n_global)
+        cpu = cpu_baseline(ml, b, args.cpu_seconds, scale, hybrid_gs=sa27 or g3)
 
     if rank == 0:
         out = {
             "metric": "V-cycle iters/sec + SpMV HBM GB/s, 3D 7-pt Poisson 256^3, 1/2/4/8 MI355X",
             "value": round(value, 3),
-            "unit": "V-cycles/s (256^3-equivalent: rows*cycles/s / 256^3)",
+            "unit": ("V-cycles/s (fixed 1.5M-row graph)" if g3 else
+                     "V-cycles/s (256^3-equivalent: rows*cycles/s / 256^3)"),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt * 1e3 / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if g3 else "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (b = A x*, x* splitmix64 U(-1,1) seed 42, x0 = 0)",
+            "data": ("synthetic (b = A x*, x* splitmix64 U(-1,1) seed 42, x0 = 0)" +
+                     ("; matrix: seeded graph-Laplacian SUBSTITUTE for SuiteSparse G3_circuit "
+                      "(not available offline)" if g3 else "")),
             "config": {
-                "workload": (f"3D 27-pt Q1 anisotropic diffusion (1,1,1e-3) {grid[0]}x{grid[1]}x{grid[2]}, "
+                "workload": (f"G3_circuit substitute: graph Laplacian on a {grid[0]}x{grid[1]} lattice "
+                             f"({n_global} rows, {infos[0]['nnz_global']} nnz, seed 1), "
+                             f"{'random numbering' if args.no_reorder else 'RCM-reordered'}, smoothed "
+                             "aggregation (MIS(2)), hybrid GS(64) 1+1 V-cycle, even row partition")
+                if g3 else
+                (f"3D 27-pt Q1 anisotropic diffusion (1,1,1e-3) {grid[0]}x{grid[1]}x{grid[2]}, "
                              "smoothed aggregation (MIS(2)), hybrid GS(64) 1+1 V-cycle, z-slab row partition")
                 if sa27 else
                 (f"3D 7-pt Poisson {grid[0]}x{grid[1]}x{grid[2]}, PMIS + classical interp, "
@@ -206,6 +233,7 @@ def main():
                 "operator_complexity": round(sum(i["nnz_global"] for i in infos) / infos[0]["nnz_global"], 3),
                 "parallelism": f"row-partition x{world}, RCCL halo",
                 "setup_s": round(setup_s, 2),
+                "reorder_s": None if reorder_s is None else round(reorder_s, 2),
                 "hipgraph": world == 1 and not args.no_graph,
             },
             "iters_per_s": round(iters_per_s, 3),
@@ -231,7 +259,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(ml, b, seconds, n_global):
+def cpu_baseline(ml, b, seconds, scale, hybrid_gs=False):
     """Oracle V-cycle (C, OpenMP) on the product's own level operators, rank 0, N=1."""
     import numpy as np
 
@@ -249,7 +277,8 @@ def cpu_baseline(ml, b, seconds, n_global):
             mats.append(O.Csr.from_arrays(rp.size - 1, ncols, rp, col, val))
             del rp, col, val
         levels.append(tuple(mats))
-    H = O.Hierarchy(levels[0][0], levels=levels)
+    H = O.Hierarchy(levels[0][0], levels=levels,
+                    smoother=O.SMOOTH_HYBRID_GS if hybrid_gs else O.SMOOTH_JACOBI)
     bh = b.cpu().numpy()
     x = np.zeros(bh.size)
     x = H.cycle(x, bh)  # untimed first touch
@@ -261,10 +290,10 @@ def cpu_baseline(ml, b, seconds, n_global):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    rate = k / el * n_global / float(256 ** 3)
+    rate = k / el * scale
     return {
         "value": round(rate, 4),
-        "unit": "V-cycles/s (256^3-equivalent)",
+        "unit": "V-cycles/s" if scale == 1.0 else "V-cycles/s (256^3-equivalent)",
         "cores": int(O.lib().orc_num_threads()),
         "kind": "port",
         "sample": f"{k} oracle V-cycles (C/OpenMP, same hierarchy and b) in {el:.1f}s; "

@@ -83,6 +83,27 @@ int amg_par_csr_create(amg_context ctx, int64_t n_global, int64_t first_row, int
 int amg_par_stencil_create(amg_context ctx, int kind, int64_t nx, int64_t ny, int64_t nz,
                            const double* eps3, amg_matrix* out);
 
+/* ---- unstructured inputs ------------------------------------ */
+/* All of these use the even row partition: rank r holds rows [n r / P, n (r+1) / P).
+ * Seeded, randomly numbered graph Laplacian on an nx x ny lattice with long-range edges
+ * (the offline substitute for SuiteSparse G3_circuit, BASELINE.json:11).  Collective.   */
+int amg_par_graph_laplacian_create(amg_context ctx, int64_t nx, int64_t ny, uint64_t seed,
+                                   amg_matrix* out);
+/* readParMatrix analogue: Matrix Market (coordinate real/integer/pattern, general/
+ * symmetric/skew-symmetric; duplicates summed in file order) or binary CSR ("RAMGCSR1"
+ * header, then int64 n_rows, n_cols, nnz, int64 row_ptr[n+1], int64 col[nnz], double
+ * val[nnz]), detected from the first bytes.  Every rank reads only what it keeps of a
+ * binary file.  Collective.                                                              */
+int amg_par_csr_read(amg_context ctx, const char* path, amg_matrix* out);
+/* Binary CSR writer; every rank writes its rows at their global offsets.  Collective.  */
+int amg_par_csr_write(amg_matrix A, const char* path);
+#define AMG_REORDER_RCM 1
+/* B = P A P^T for a bandwidth-reducing symmetric permutation (reverse Cuthill-McKee on
+ * the pattern of A + A^T).  new_to_old_local[n_local of B] receives the old global id of
+ * each new local row (x_new[i] = x_old[new_to_old_local[i]]).  Gathers the whole graph
+ * on every rank.  Collective.                                                            */
+int amg_par_csr_reorder(amg_matrix A, int method, amg_matrix* out, int64_t* new_to_old_local);
+
 typedef struct amg_matrix_info {
     int64_t n_global_rows, n_global_cols;
     int64_t first_row, n_local_rows;
@@ -194,6 +215,20 @@ int amg_host_hierarchy_level_split(amg_host_hierarchy H, int32_t level, int32_t*
 /* row-major n_c x n_c inverse of the coarsest operator (identical on every rank) */
 int amg_host_hierarchy_coarse_inverse(amg_host_hierarchy H, double* out);
 int amg_host_hierarchy_destroy(amg_host_hierarchy H);
+
+/* Host-only halves of the unstructured-input calls above (no GPU needed): the exact code
+ * the amg_par_* versions run before uploading.  sizes5 as for the hierarchy levels.      */
+typedef struct amg_host_csr_s* amg_host_csr;
+int amg_host_csr_graph_laplacian(int rank, int nranks, int64_t nx, int64_t ny, uint64_t seed,
+                                 amg_host_csr* out);
+int amg_host_csr_read(int rank, int nranks, const char* path, amg_host_csr* out);
+int amg_host_csr_write(int rank, int nranks, amg_alltoallv_fn exchange, void* user,
+                       amg_host_csr A, const char* path);
+int amg_host_csr_reorder(int rank, int nranks, amg_alltoallv_fn exchange, void* user,
+                         amg_host_csr A, int method, amg_host_csr* out, int64_t* new_to_old_local);
+int amg_host_csr_size(amg_host_csr A, int64_t* sizes5);
+int amg_host_csr_export(amg_host_csr A, int64_t* row_ptr, int64_t* col_global, double* val);
+int amg_host_csr_destroy(amg_host_csr A);
 
 /* ---- vectors ---------------------------------------------------------------------- */
 /* out[i] = uniform(-1,1) from splitmix64(seed, first_gid + i) on the device. */

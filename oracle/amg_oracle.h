@@ -69,6 +69,11 @@ int64_t orc_mis2_aggregate(const orc_csr* S, uint64_t seed, int32_t* agg);
 orc_csr* orc_sa_prolongator(const orc_csr* A, const int32_t* agg, int64_t n_agg);
 void orc_dense_inverse(int64_t n, const orc_csr* A, double* inv); /* row-major n*n */
 
+/* unstructured inputs (io_oracle.c, row f2; specs in DESIGN.md 8) */
+orc_csr* orc_gen_graph_laplacian(int64_t nx, int64_t ny, uint64_t seed);
+void orc_rcm(const orc_csr* A, int64_t* new_to_old);
+orc_csr* orc_permute(const orc_csr* A, const int64_t* new_to_old);  /* P A P^T */
+
 /* ---- hierarchy (ParMultilevel analogue) --------------------- */
 enum { ORC_COARSEN_RS = 0, ORC_COARSEN_PMIS = 1, ORC_COARSEN_SA = 2 };
 enum { ORC_SMOOTH_JACOBI = 0, ORC_SMOOTH_HYBRID_GS = 1 };

@@ -64,6 +64,9 @@ def lib():
             "orc_gen_5pt": (vp, [C.c_int64, C.c_int64]),
             "orc_gen_7pt": (vp, [C.c_int64, C.c_int64, C.c_int64]),
             "orc_gen_27pt": (vp, [C.c_int64] * 3 + [C.c_double] * 3),
+            "orc_gen_graph_laplacian": (vp, [C.c_int64, C.c_int64, C.c_uint64]),
+            "orc_rcm": (None, [vp, _i64p]),
+            "orc_permute": (vp, [vp, _i64p]),
             "orc_vec_uniform": (None, [C.c_int64, C.c_int64, C.c_uint64, _f64p]),
             "orc_spmv": (None, [vp, _f64p, _f64p]),
             "orc_spmv_add": (None, [vp, _f64p, _f64p]),
@@ -204,6 +207,24 @@ def gen_7pt(nx, ny, nz):
 
 def gen_27pt(nx, ny, nz, ex=1.0, ey=1.0, ez=1e-3):
     return Csr(lib().orc_gen_27pt(nx, ny, nz, ex, ey, ez))
+
+
+def gen_graph_laplacian(nx, ny, seed=1):
+    """G3_circuit substitute (io_oracle.c; spec DESIGN.md 8)."""
+    return Csr(lib().orc_gen_graph_laplacian(nx, ny, seed))
+
+
+def rcm(A):
+    """Reverse Cuthill-McKee order: new_to_old (io_oracle.c orc_rcm)."""
+    out = np.empty(A.shape[0], np.int64)
+    lib().orc_rcm(A.h, _p(out, _i64p))
+    return out
+
+
+def permute(A, new_to_old):
+    """P A P^T with B[k, :] = A[new_to_old[k], :] renumbered."""
+    p = np.ascontiguousarray(new_to_old, np.int64)
+    return Csr(lib().orc_permute(A.h, _p(p, _i64p)))
 
 
 def vec_uniform(n, seed, first_gid=0):

@@ -24,6 +24,7 @@ import numpy as np
 
 from ._lib import (  # noqa: F401  (re-exported constants)
     AMG_COARSEN_PMIS,
+    AMG_REORDER_RCM,
     AMG_COARSEN_RS,
     AMG_COARSEN_SA,
     AMG_SMOOTH_HYBRID_GS,
@@ -47,6 +48,8 @@ __all__ = [
     "ParRugeStubenSolver",
     "ParSmoothedAggregationSolver",
     "par_stencil_grid",
+    "par_graph_laplacian",
+    "read_par_matrix",
     "vector_uniform",
     "AmgError",
 ]
@@ -221,6 +224,24 @@ class ParCSRMatrix:
         rp, col, val = self.export()
         return sp.csr_matrix((val, col, rp), shape=(self.local_rows, self.info["n_global_cols"]))
 
+    # ---- files and orderings (row f2) ------------------------------------------------
+    def write(self, path):
+        """Binary CSR file ("RAMGCSR1", read back by read_par_matrix).  Collective."""
+        check(lib().amg_par_csr_write(self.h, os.fsencode(path)))
+
+    def reorder(self, method="rcm"):
+        """(P A P^T, new_to_old_local): reverse Cuthill-McKee renumbering, even row
+        partition; x_new = x_old[new_to_old_local] (gathered).  Collective."""
+        if method != "rcm":
+            raise ValueError("only 'rcm' is supported")
+        n = self.global_rows
+        r, p = self.ctx.rank, self.ctx.nranks
+        perm = np.empty(n * (r + 1) // p - n * r // p, np.int64)
+        h = C.c_void_p()
+        check(lib().amg_par_csr_reorder(self.h, AMG_REORDER_RCM, C.byref(h),
+                                        perm.ctypes.data_as(C.POINTER(C.c_int64))))
+        return ParCSRMatrix(self.ctx, h), perm
+
     # ---- level kernels (ParCSRMatrix::mult & friends) -------------------------------
     def mult(self, x, y):
         check(lib().amg_par_csr_mult(self.h, _ptr(x), _ptr(y)))
@@ -280,6 +301,21 @@ def par_stencil_grid(ctx: Context, kind: str, dims, eps=(1.0, 1.0, 1e-3)) -> Par
     e = (C.c_double * 3)(*eps)
     h = C.c_void_p()
     check(lib().amg_par_stencil_create(ctx.h, _STENCILS[kind], nx, ny, nz, e, C.byref(h)))
+    return ParCSRMatrix(ctx, h)
+
+
+def par_graph_laplacian(ctx: Context, nx: int, ny: int, seed: int = 1) -> ParCSRMatrix:
+    """Seeded, randomly numbered unstructured graph Laplacian on an nx x ny lattice (the
+    offline G3_circuit substitute).  Even row partition.  Collective."""
+    h = C.c_void_p()
+    check(lib().amg_par_graph_laplacian_create(ctx.h, int(nx), int(ny), C.c_uint64(seed), C.byref(h)))
+    return ParCSRMatrix(ctx, h)
+
+
+def read_par_matrix(ctx: Context, path) -> ParCSRMatrix:
+    """readParMatrix analogue: Matrix Market or binary CSR, even row partition.  Collective."""
+    h = C.c_void_p()
+    check(lib().amg_par_csr_read(ctx.h, os.fsencode(path), C.byref(h)))
     return ParCSRMatrix(ctx, h)
 
 

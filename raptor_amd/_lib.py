@@ -15,6 +15,7 @@ AMG_STENCIL_5PT, AMG_STENCIL_7PT, AMG_STENCIL_27PT = 0, 1, 2
 AMG_COARSEN_RS, AMG_COARSEN_PMIS, AMG_COARSEN_SA = 0, 1, 2
 AMG_SMOOTH_JACOBI, AMG_SMOOTH_HYBRID_GS = 0, 1
 AMG_PRESET_PMIS_JACOBI, AMG_PRESET_RS_JACOBI, AMG_PRESET_SA_HYBRID_GS = 0, 1, 2
+AMG_REORDER_RCM = 1
 
 ERROR_NAMES = {1: "INVALID", 2: "HIP", 3: "RCCL", 4: "COMM", 5: "INTERNAL", 6: "NOMEM"}
 
@@ -93,6 +94,10 @@ SIGNATURES = {
     "amg_par_stencil_create": (C.c_int, [_vp, C.c_int, _i64, _i64, _i64, _pf64, C.POINTER(_vp)]),
     "amg_par_csr_info": (C.c_int, [_vp, C.POINTER(MatrixInfo)]),
     "amg_par_csr_export": (C.c_int, [_vp, _pi64, _pi64, _pf64]),
+    "amg_par_graph_laplacian_create": (C.c_int, [_vp, _i64, _i64, C.c_uint64, C.POINTER(_vp)]),
+    "amg_par_csr_read": (C.c_int, [_vp, C.c_char_p, C.POINTER(_vp)]),
+    "amg_par_csr_write": (C.c_int, [_vp, C.c_char_p]),
+    "amg_par_csr_reorder": (C.c_int, [_vp, C.c_int, C.POINTER(_vp), _pi64]),
     "amg_par_csr_mult": (C.c_int, [_vp, _vp, _vp]),
     "amg_par_csr_mult_add": (C.c_int, [_vp, _vp, _vp]),
     "amg_par_csr_residual": (C.c_int, [_vp, _vp, _vp, _vp]),
@@ -122,6 +127,14 @@ SIGNATURES = {
     "amg_host_hierarchy_level_split": (C.c_int, [_vp, _i32, C.POINTER(_i32)]),
     "amg_host_hierarchy_coarse_inverse": (C.c_int, [_vp, _pf64]),
     "amg_host_hierarchy_destroy": (C.c_int, [_vp]),
+    "amg_host_csr_graph_laplacian": (C.c_int, [C.c_int, C.c_int, _i64, _i64, C.c_uint64, C.POINTER(_vp)]),
+    "amg_host_csr_read": (C.c_int, [C.c_int, C.c_int, C.c_char_p, C.POINTER(_vp)]),
+    "amg_host_csr_write": (C.c_int, [C.c_int, C.c_int, ALLTOALLV_FN, _vp, _vp, C.c_char_p]),
+    "amg_host_csr_reorder": (C.c_int, [C.c_int, C.c_int, ALLTOALLV_FN, _vp, _vp, C.c_int, C.POINTER(_vp),
+                                       _pi64]),
+    "amg_host_csr_size": (C.c_int, [_vp, _pi64]),
+    "amg_host_csr_export": (C.c_int, [_vp, _pi64, _pi64, _pf64]),
+    "amg_host_csr_destroy": (C.c_int, [_vp]),
 }
 
 _lib = None

@@ -215,6 +215,53 @@ int amg_par_stencil_create(amg_context ctx, int kind, int64_t nx, int64_t ny, in
     });
 }
 
+static void upload(Context& c, HostCSR&& h, amg_matrix* out) {
+    std::unique_ptr<amg_matrix_s> m(new amg_matrix_s());
+    m->own.reset(new DevMatrix());
+    m->m = m->own.get();
+    m->m->build(&c, std::move(h));
+    *out = m.release();
+}
+
+int amg_par_graph_laplacian_create(amg_context ctx, int64_t nx, int64_t ny, uint64_t seed,
+                                   amg_matrix* out) {
+    return guard([&] {
+        AMG_CHECK(ctx && out, "null argument");
+        set_device(ctx->c);
+        upload(ctx->c, graph_laplacian_slab(ctx->c.host, nx, ny, seed), out);
+    });
+}
+
+int amg_par_csr_read(amg_context ctx, const char* path, amg_matrix* out) {
+    return guard([&] {
+        AMG_CHECK(ctx && path && out, "null argument");
+        set_device(ctx->c);
+        HostCSR h = read_par_matrix(ctx->c.host, path);
+        AMG_CHECK(h.n_global_rows == h.n_global_cols, "ParCSRMatrix needs a square matrix");
+        upload(ctx->c, std::move(h), out);
+    });
+}
+
+int amg_par_csr_write(amg_matrix A, const char* path) {
+    return guard([&] {
+        AMG_CHECK(A && path, "null argument");
+        write_par_matrix(A->m->ctx->host, A->m->host, path);
+    });
+}
+
+int amg_par_csr_reorder(amg_matrix A, int method, amg_matrix* out, int64_t* new_to_old_local) {
+    return guard([&] {
+        AMG_CHECK(A && out && new_to_old_local, "null argument");
+        AMG_CHECK(method == AMG_REORDER_RCM, "unknown reorder method");
+        Context& c = *A->m->ctx;
+        set_device(c);
+        std::vector<int64_t> n2o;
+        HostCSR h = reorder_rcm(c.host, A->m->host, n2o);
+        std::copy(n2o.begin(), n2o.end(), new_to_old_local);
+        upload(c, std::move(h), out);
+    });
+}
+
 int amg_par_csr_info(amg_matrix A, amg_matrix_info* info) {
     return guard([&] {
         AMG_CHECK(A && info, "null argument");
@@ -542,6 +589,86 @@ int amg_host_hierarchy_coarse_inverse(amg_host_hierarchy H, double* out) {
 
 int amg_host_hierarchy_destroy(amg_host_hierarchy H) {
     return guard([&] { delete H; });
+}
+
+struct amg_host_csr_s {
+    HostCSR A;
+    int rank = 0;
+};
+
+static HostComm host_comm(int rank, int nranks, amg_alltoallv_fn exchange, void* user,
+                          bool communicates = true) {
+    AMG_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
+    AMG_CHECK(nranks == 1 || exchange || !communicates, "multi-rank needs a host exchange");
+    HostComm c;
+    c.rank = rank, c.nranks = nranks, c.fn = exchange, c.user = user;
+    return c;
+}
+
+static void host_out(HostCSR&& h, int rank, amg_host_csr* out) {
+    std::unique_ptr<amg_host_csr_s> o(new amg_host_csr_s());
+    o->A = std::move(h);
+    o->rank = rank;
+    *out = o.release();
+}
+
+int amg_host_csr_graph_laplacian(int rank, int nranks, int64_t nx, int64_t ny, uint64_t seed,
+                                 amg_host_csr* out) {
+    return guard([&] {
+        AMG_CHECK(out, "null argument");
+        host_out(graph_laplacian_slab(host_comm(rank, nranks, nullptr, nullptr, false), nx, ny, seed), rank, out);
+    });
+}
+
+// the reader needs no communication (even partition from the file header)
+int amg_host_csr_read(int rank, int nranks, const char* path, amg_host_csr* out) {
+    return guard([&] {
+        AMG_CHECK(path && out, "null argument");
+        host_out(read_par_matrix(host_comm(rank, nranks, nullptr, nullptr, false), path), rank, out);
+    });
+}
+
+int amg_host_csr_write(int rank, int nranks, amg_alltoallv_fn exchange, void* user, amg_host_csr A,
+                       const char* path) {
+    return guard([&] {
+        AMG_CHECK(A && path, "null argument");
+        write_par_matrix(host_comm(rank, nranks, exchange, user), A->A, path);
+    });
+}
+
+int amg_host_csr_reorder(int rank, int nranks, amg_alltoallv_fn exchange, void* user, amg_host_csr A,
+                         int method, amg_host_csr* out, int64_t* new_to_old_local) {
+    return guard([&] {
+        AMG_CHECK(A && out && new_to_old_local, "null argument");
+        AMG_CHECK(method == AMG_REORDER_RCM, "unknown reorder method");
+        std::vector<int64_t> n2o;
+        HostCSR h = reorder_rcm(host_comm(rank, nranks, exchange, user), A->A, n2o);
+        std::copy(n2o.begin(), n2o.end(), new_to_old_local);
+        host_out(std::move(h), rank, out);
+    });
+}
+
+int amg_host_csr_size(amg_host_csr A, int64_t* s) {
+    return guard([&] {
+        AMG_CHECK(A && s, "null argument");
+        const HostCSR& h = A->A;
+        s[0] = h.n_global_rows, s[1] = h.n_global_cols;
+        s[2] = h.row_starts[A->rank];
+        s[3] = h.nrows(), s[4] = h.nnz();
+    });
+}
+
+int amg_host_csr_export(amg_host_csr A, int64_t* row_ptr, int64_t* col_global, double* val) {
+    return guard([&] {
+        AMG_CHECK(A && row_ptr && col_global && val, "null argument");
+        std::copy(A->A.rp.begin(), A->A.rp.end(), row_ptr);
+        std::copy(A->A.col.begin(), A->A.col.end(), col_global);
+        std::copy(A->A.val.begin(), A->A.val.end(), val);
+    });
+}
+
+int amg_host_csr_destroy(amg_host_csr A) {
+    return guard([&] { delete A; });
 }
 
 int amg_vector_uniform(amg_context ctx, int64_t n, int64_t first_gid, uint64_t seed, double* out) {

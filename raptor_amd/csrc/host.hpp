@@ -159,4 +159,18 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
 uint64_t mix64(uint64_t z);
 uint32_t hash32(int64_t gid, uint64_t seed);
 
+// ---- inputs beyond the stencils (host_io.cpp, row f2) ----------------------------
+// seeded unstructured graph Laplacian (G3_circuit substitute), even row partition
+HostCSR graph_laplacian_slab(const HostComm& comm, int64_t nx, int64_t ny, uint64_t seed);
+// Matrix Market (coordinate real/integer/pattern; general/symmetric/skew) or binary CSR
+// (magic "RAMGCSR1"), detected from the first bytes; this rank's rows of an even partition
+HostCSR read_par_matrix(const HostComm& comm, const std::string& path);
+// collective binary CSR writer (every rank writes its rows at their global offsets)
+void write_par_matrix(const HostComm& comm, const HostCSR& A, const std::string& path);
+// reverse Cuthill-McKee order (new_to_old) of a whole square matrix
+std::vector<int64_t> rcm_order(const HostCSR& full);
+// P A P^T by RCM; the result uses the even row partition; new_to_old_local[i] is the
+// old global id of the new local row i
+HostCSR reorder_rcm(const HostComm& comm, const HostCSR& A, std::vector<int64_t>& new_to_old_local);
+
 }  // namespace amg

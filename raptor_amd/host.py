@@ -6,10 +6,11 @@ it -- serial and multi-rank over gloo -- bit for bit against the oracle."""
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
-from ._lib import ALLTOALLV_FN, Options, check, lib
+from ._lib import ALLTOALLV_FN, AMG_REORDER_RCM, Options, check, lib
 
 _WHICH = {"A": 0, "P": 1, "R": 2}
 _NULL_FN = ALLTOALLV_FN()
@@ -85,6 +86,86 @@ class HostHierarchy:
         if h:
             try:
                 lib().amg_host_hierarchy_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+
+class HostCSR:
+    """This rank's rows (even row partition) of a host-side matrix: ``amg_host_csr_*``.
+    The unstructured-input code run without a GPU."""
+
+    def __init__(self, handle, rank=0, nranks=1, group=None):
+        self.h = handle
+        self.rank, self.nranks, self.group = rank, nranks, group
+
+    def _fn(self):
+        if self.nranks == 1:
+            return _NULL_FN
+        from ._comm import make_exchange
+
+        self._keep = make_exchange(self.group, self.nranks)
+        return self._keep
+
+    @classmethod
+    def graph_laplacian(cls, nx, ny, seed=1, rank=0, nranks=1, group=None):
+        h = C.c_void_p()
+        check(lib().amg_host_csr_graph_laplacian(rank, nranks, int(nx), int(ny), C.c_uint64(seed),
+                                                 C.byref(h)))
+        return cls(h, rank, nranks, group)
+
+    @classmethod
+    def read(cls, path, rank=0, nranks=1, group=None):
+        h = C.c_void_p()
+        check(lib().amg_host_csr_read(rank, nranks, os.fsencode(path), C.byref(h)))
+        return cls(h, rank, nranks, group)
+
+    def write(self, path):
+        check(lib().amg_host_csr_write(self.rank, self.nranks, self._fn(), None, self.h,
+                                       os.fsencode(path)))
+
+    def reorder(self, method="rcm"):
+        """(P A P^T, new_to_old_local) for the RCM permutation (collective)."""
+        if method != "rcm":
+            raise ValueError("only 'rcm' is supported")
+        n = self.sizes()
+        lo = n["n_global_rows"] * self.rank // self.nranks
+        hi = n["n_global_rows"] * (self.rank + 1) // self.nranks
+        perm = np.empty(hi - lo, np.int64)
+        h = C.c_void_p()
+        check(lib().amg_host_csr_reorder(self.rank, self.nranks, self._fn(), None, self.h,
+                                         AMG_REORDER_RCM, C.byref(h),
+                                         perm.ctypes.data_as(C.POINTER(C.c_int64))))
+        return HostCSR(h, self.rank, self.nranks, self.group), perm
+
+    def sizes(self):
+        s = np.empty(5, np.int64)
+        check(lib().amg_host_csr_size(self.h, s.ctypes.data_as(C.POINTER(C.c_int64))))
+        return dict(zip(("n_global_rows", "n_global_cols", "first_row", "n_local_rows", "nnz_local"),
+                        (int(v) for v in s)))
+
+    def export(self):
+        s = self.sizes()
+        rp = np.empty(s["n_local_rows"] + 1, np.int64)
+        col = np.empty(s["nnz_local"], np.int64)
+        val = np.empty(s["nnz_local"])
+        i64 = C.POINTER(C.c_int64)
+        check(lib().amg_host_csr_export(self.h, rp.ctypes.data_as(i64), col.ctypes.data_as(i64),
+                                        val.ctypes.data_as(C.POINTER(C.c_double))))
+        return rp, col, val
+
+    def to_scipy_local(self):
+        import scipy.sparse as sp
+
+        s = self.sizes()
+        rp, col, val = self.export()
+        return sp.csr_matrix((val, col, rp), shape=(s["n_local_rows"], s["n_global_cols"]))
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            try:
+                lib().amg_host_csr_destroy(h)
             except Exception:
                 pass
             self.h = None

@@ -89,3 +89,62 @@ def test_distributed_setup_matches_serial_oracle(oracle, ws):
         p.join(timeout=60)
     for rank, fails in res:
         assert fails == [], (rank, fails)
+
+
+def _io_worker(rank, ws, port, path, q):
+    """Reorder (gathers the graph over gloo) and the collective binary writer, ws ranks."""
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from oracle import oracle as O
+        from raptor_amd import host
+
+        fails = []
+        nx, ny = 53, 47
+        A = O.gen_graph_laplacian(nx, ny, 9)
+        p = O.rcm(A)
+        B = O.permute(A, p).to_scipy()
+        n = nx * ny
+        lo, hi = n * rank // ws, n * (rank + 1) // ws
+        H = host.HostCSR.graph_laplacian(nx, ny, 9, rank=rank, nranks=ws, group=dist.group.WORLD)
+        Hb, perm = H.reorder("rcm")
+        if not np.array_equal(perm, p[lo:hi]):
+            fails.append("perm")
+        L = Hb.to_scipy_local()
+        G = B[lo:hi]
+        if not (np.array_equal(L.indptr, G.indptr) and np.array_equal(L.indices, G.indices)
+                and np.array_equal(L.data, G.data)):
+            fails.append("reordered rows")
+        Hb.write(path)
+        dist.barrier()
+        R = host.HostCSR.read(path).to_scipy_local()  # every rank reads the whole file
+        if not (np.array_equal(R.indptr, B.indptr) and np.array_equal(R.indices, B.indices)
+                and np.array_equal(R.data, B.data)):
+            fails.append("written file")
+        q.put((rank, fails))
+    except Exception as e:
+        q.put((rank, [repr(e)]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_distributed_reorder_and_write(oracle, tmp_path, ws):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    path = str(tmp_path / "rcm.bin")
+    procs = [ctx.Process(target=_io_worker, args=(r, ws, port, path, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in range(ws)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, fails in res:
+        assert fails == [], (rank, fails)

@@ -1,0 +1,103 @@
+"""Unstructured inputs on the GPU (SURVEY.md 8f row f2 / BASELINE.json:11 substitute):
+generator, reader, writer and RCM through the device C-ABI, and the SA / PMIS V-cycle on
+the randomly numbered and the RCM-reordered graph Laplacian, bit-exact against the oracle
+(1 rank and 2-3 loopback ranks)."""
+import numpy as np
+import pytest
+import scipy.io
+
+from tests.test_gpu_multirank import run_ranks
+from tests.util import same_csr, to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+
+def test_graph_laplacian_and_rcm_on_device(ctx, oracle, tmp_path):
+    import raptor_amd as ra
+
+    O = oracle
+    A = ra.par_graph_laplacian(ctx, 61, 58, seed=4)
+    Ao = O.gen_graph_laplacian(61, 58, 4)
+    assert same_csr(A.to_scipy_local(), Ao.to_scipy())
+    n = A.local_rows
+    x = O.vec_uniform(n, 1)
+    y = ctx.empty(n)
+    A.mult(to_dev(ctx, x), y)
+    assert np.array_equal(to_host(ctx, y), Ao.spmv(x))
+    B, perm = A.reorder("rcm")
+    p = O.rcm(Ao)
+    assert np.array_equal(perm, p)
+    Bo = O.permute(Ao, p)
+    assert same_csr(B.to_scipy_local(), Bo.to_scipy())
+    B.mult(to_dev(ctx, x[perm]), y)
+    assert np.array_equal(to_host(ctx, y), Ao.spmv(x)[perm])  # same products, renumbered
+    path = str(tmp_path / "b.bin")
+    B.write(path)
+    C = ra.read_par_matrix(ctx, path)
+    assert same_csr(C.to_scipy_local(), Bo.to_scipy())
+    mm = str(tmp_path / "b.mtx")
+    scipy.io.mmwrite(mm, Bo.to_scipy(), precision=17)
+    D = ra.read_par_matrix(ctx, mm)
+    assert same_csr(D.to_scipy_local(), Bo.to_scipy())
+
+
+@pytest.mark.parametrize("coarsen,smoother,reorder", [("sa", "hybrid_gs", False), ("sa", "hybrid_gs", True),
+                                                      ("sa", "jacobi", True), ("pmis", "jacobi", False)])
+def test_vcycle_on_graph_laplacian(ctx, oracle, coarsen, smoother, reorder):
+    import raptor_amd as ra
+
+    O = oracle
+    A = ra.par_graph_laplacian(ctx, 90, 77, seed=2)
+    Ao = O.gen_graph_laplacian(90, 77, 2)
+    if reorder:
+        A, perm = A.reorder("rcm")
+        Ao = O.permute(Ao, perm)
+    ml = ra.ParMultilevel(coarsen=coarsen, smoother=smoother).setup(A)
+    Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS[coarsen], smoother=O.SMOOTH_JACOBI if smoother == "jacobi"
+                                else O.SMOOTH_HYBRID_GS))
+    assert ml.num_levels == Ho.num_levels
+    for l in range(ml.num_levels):
+        assert same_csr(ml.level_matrix(l, "A").to_scipy_local(), Ho.matrix(l, "A"))
+    n = Ao.shape[0]
+    b = O.vec_uniform(n, 42)
+    db = to_dev(ctx, b)
+    dx = ctx.zeros(n)
+    xo = np.zeros(n)
+    for _ in range(3):
+        ml.cycle(dx, db)
+        xo = Ho.cycle(xo, b)
+        assert np.array_equal(to_host(ctx, dx), xo)
+    _, hist = ml.pcg(ctx.zeros(n), db, max_iter=10)
+    _, hist_o = Ho.pcg(np.zeros(n), b, max_iter=10)
+    assert np.all(np.abs(hist - hist_o) <= 1e-9 * hist_o[0])
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_multirank_graph_laplacian(oracle, nranks):
+    import raptor_amd as ra
+
+    O = oracle
+    Ao = O.gen_graph_laplacian(70, 66, 5)
+    p = O.rcm(Ao)
+    Bo = O.permute(Ao, p)
+    Ho = O.Hierarchy(Bo, **O.DEFAULTS["sa"])
+    n = Bo.shape[0]
+    b = O.vec_uniform(n, 8)
+    xo = Ho.cycle(Ho.cycle(np.zeros(n), b), b)
+
+    def rank(r, nr, world):
+        ctx = ra.Context.loopback(r, nr, world)
+        A = ra.par_graph_laplacian(ctx, 70, 66, seed=5)
+        B, perm = A.reorder("rcm")
+        ml = ra.ParSmoothedAggregationSolver(replicate_below=400).setup(B)
+        f, m = B.first_row, B.local_rows
+        dx = ctx.zeros(m)
+        db = to_dev(ctx, b[f:f + m])
+        ml.cycle(dx, db)
+        ml.cycle(dx, db)
+        return f, m, perm, to_host(ctx, dx), B.info["n_halo"]
+
+    for f, m, perm, x, halo in run_ranks(nranks, rank):
+        assert np.array_equal(perm, p[f:f + m])
+        assert np.array_equal(x, xo[f:f + m])
+        assert halo > 0
