@@ -128,6 +128,9 @@ int amg_par_csr_jacobi(amg_matrix A, const double* x, const double* b, double* x
                        double omega);
 int amg_par_csr_hybrid_gs(amg_matrix A, const double* x, const double* b, double* x_out,
                           int64_t block);
+/* the backward sweep (rows of each block in descending order; the V-cycle's post-smoother) */
+int amg_par_csr_hybrid_gs_backward(amg_matrix A, const double* x, const double* b, double* x_out,
+                                   int64_t block);
 /* C = A * B (ParCSRMatrix * ParCSRMatrix, row a10): the Galerkin SpGEMM kernel (one
  * wavefront per output row, LDS hash, canonical accumulation order => bit-identical to the
  * oracle).  A's column partition must equal B's row partition.  Collective.              */

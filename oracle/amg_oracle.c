@@ -211,26 +211,57 @@ void orc_jacobi(const orc_csr* A, const double* x, const double* b, double* xout
  * blocks Jacobi.  acc = b_i; acc -= a_ij*x_j over "old" entries (j != i, j outside
  * [block_start, i)) in CSR order; then acc -= a_ij*xnew_j over in-block lower entries in
  * CSR order; xnew_i = acc * dinv_i. */
-void orc_hybrid_gs(const orc_csr* A, const double* x, const double* b, double* xout,
-                   int64_t block) {
-    int64_t nb = (A->n_rows + block - 1) / block;
+/* one GS block [s, e): Jacobi for couplings outside it, Gauss-Seidel inside.  Forward:
+ * rows s..e-1, new values for in-block j < i.  Backward: rows e-1..s, new values for
+ * in-block j > i.  Old-value couplings first, then new-value couplings, each in CSR order. */
+static void gs_block_rows(const orc_csr* A, const double* x, const double* b, double* xout,
+                          int64_t s, int64_t e, int backward) {
+    for (int64_t t = 0; t < e - s; ++t) {
+        int64_t i = backward ? e - 1 - t : s + t;
+        int64_t lo = backward ? i + 1 : s, hi = backward ? e : i; /* new-value range [lo, hi) */
+        double acc = b[i], dinv = 1.0 / diag_of(A, i);
+        for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
+            int64_t j = A->col[k];
+            if (j == i || (j >= lo && j < hi)) continue;
+            acc -= A->val[k] * x[j];
+        }
+        for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
+            int64_t j = A->col[k];
+            if (j >= lo && j < hi) acc -= A->val[k] * xout[j];
+        }
+        xout[i] = acc * dinv;
+    }
+}
+
+/* Blocks = global multiples of `block` clipped to the rank segments [cuts[t], cuts[t+1])
+ * (cuts[0] = 0, the last segment ends at n): GS never reaches across a rank boundary,
+ * exactly like the product's per-rank blocks. */
+void orc_hybrid_gs_cut(const orc_csr* A, const double* x, const double* b, double* xout,
+                       int64_t block, int32_t backward, int32_t ncuts, const int64_t* cuts) {
+    int64_t n = A->n_rows;
+    for (int32_t t = 0; t < ncuts; ++t) {
+        int64_t lo = cuts[t], hi = t + 1 < ncuts ? cuts[t + 1] : n;
+        if (hi <= lo) continue;
+        int64_t q0 = lo / block, q1 = (hi - 1) / block;
 #pragma omp parallel for schedule(static)
-    for (int64_t q = 0; q < nb; ++q) {
-        int64_t s = q * block, e = s + block < A->n_rows ? s + block : A->n_rows;
-        for (int64_t i = s; i < e; ++i) {
-            double acc = b[i], dinv = 1.0 / diag_of(A, i);
-            for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
-                int64_t j = A->col[k];
-                if (j == i || (j >= s && j < i)) continue;
-                acc -= A->val[k] * x[j];
-            }
-            for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
-                int64_t j = A->col[k];
-                if (j >= s && j < i) acc -= A->val[k] * xout[j];
-            }
-            xout[i] = acc * dinv;
+        for (int64_t q = q0; q <= q1; ++q) {
+            int64_t s = q * block > lo ? q * block : lo;
+            int64_t e = (q + 1) * block < hi ? (q + 1) * block : hi;
+            gs_block_rows(A, x, b, xout, s, e, backward);
         }
     }
+}
+
+void orc_hybrid_gs(const orc_csr* A, const double* x, const double* b, double* xout,
+                   int64_t block) {
+    const int64_t zero = 0;
+    orc_hybrid_gs_cut(A, x, b, xout, block, 0, 1, &zero);
+}
+
+void orc_hybrid_gs_backward(const orc_csr* A, const double* x, const double* b, double* xout,
+                            int64_t block) {
+    const int64_t zero = 0;
+    orc_hybrid_gs_cut(A, x, b, xout, block, 1, 1, &zero);
 }
 
 double orc_norm2(int64_t n, const double* v) {
@@ -769,7 +800,17 @@ struct orc_hier {
     double* r[ORC_MAX_LEVELS];
     double* t[ORC_MAX_LEVELS];
     double* inv; /* coarsest level dense inverse, row-major */
+    int32_t ncuts[ORC_MAX_LEVELS]; /* 0: one segment (serial) */
+    int64_t* cuts[ORC_MAX_LEVELS];
 };
+
+void orc_hier_set_cuts(orc_hier* H, int32_t level, int32_t ncuts, const int64_t* cuts) {
+    if (level < 0 || level >= H->nlev) return;
+    free(H->cuts[level]);
+    H->cuts[level] = (int64_t*)malloc(sizeof(int64_t) * (size_t)(ncuts > 0 ? ncuts : 1));
+    memcpy(H->cuts[level], cuts, sizeof(int64_t) * (size_t)ncuts);
+    H->ncuts[level] = ncuts;
+}
 
 orc_hier* orc_hier_setup(const orc_csr* A0, const orc_options* opt) {
     orc_hier* H = (orc_hier*)calloc(1, sizeof(orc_hier));
@@ -862,6 +903,7 @@ void orc_hier_free(orc_hier* H) {
         free(H->b[k]);
         free(H->r[k]);
         free(H->t[k]);
+        free(H->cuts[k]);
     }
     free(H->inv);
     free(H);
@@ -878,9 +920,14 @@ void orc_hier_split(const orc_hier* H, int32_t level, int32_t* out) {
     memcpy(out, H->split[level], sizeof(int32_t) * (size_t)H->A[level]->n_rows);
 }
 
-static void smooth(orc_hier* H, int32_t l, double* x, const double* b, double* tmp) {
+/* post = 1: post-smoothing.  Hybrid GS sweeps forward before the coarse correction and
+ * backward after it, so the V-cycle is a symmetric operator (usable inside CG). */
+static void smooth(orc_hier* H, int32_t l, double* x, const double* b, double* tmp, int post) {
     const orc_csr* A = H->A[l];
-    if (H->opt.smoother == ORC_SMOOTH_HYBRID_GS) orc_hybrid_gs(A, x, b, tmp, H->opt.gs_block);
+    const int64_t zero = 0;
+    if (H->opt.smoother == ORC_SMOOTH_HYBRID_GS)
+        orc_hybrid_gs_cut(A, x, b, tmp, H->opt.gs_block, post, H->ncuts[l] > 0 ? H->ncuts[l] : 1,
+                          H->ncuts[l] > 0 ? H->cuts[l] : &zero);
     else orc_jacobi(A, x, b, tmp, H->opt.jacobi_omega);
     memcpy(x, tmp, sizeof(double) * (size_t)A->n_rows);
 }
@@ -898,14 +945,14 @@ static void cycle_rec(orc_hier* H, int32_t l, double* x, const double* b) {
         }
         return;
     }
-    for (int32_t s = 0; s < H->opt.pre_sweeps; ++s) smooth(H, l, x, b, H->t[l]);
+    for (int32_t s = 0; s < H->opt.pre_sweeps; ++s) smooth(H, l, x, b, H->t[l], 0);
     orc_residual(A, x, b, H->r[l]);
     orc_spmv(H->R[l], H->r[l], H->b[l + 1]);
     int64_t nc = H->A[l + 1]->n_rows;
     memset(H->x[l + 1], 0, sizeof(double) * (size_t)nc);
     cycle_rec(H, l + 1, H->x[l + 1], H->b[l + 1]);
     orc_spmv_add(H->P[l], H->x[l + 1], x);
-    for (int32_t s = 0; s < H->opt.post_sweeps; ++s) smooth(H, l, x, b, H->t[l]);
+    for (int32_t s = 0; s < H->opt.post_sweeps; ++s) smooth(H, l, x, b, H->t[l], 1);
 }
 
 void orc_hier_cycle(orc_hier* H, double* x, const double* b) { cycle_rec(H, 0, x, b); }

@@ -55,6 +55,12 @@ void orc_residual(const orc_csr* A, const double* x, const double* b, double* r)
 void orc_jacobi(const orc_csr* A, const double* x, const double* b, double* xout, double omega);
 void orc_hybrid_gs(const orc_csr* A, const double* x, const double* b, double* xout,
                    int64_t block);
+/* backward sweep: rows of each block in descending order, new values for in-block j > i */
+void orc_hybrid_gs_backward(const orc_csr* A, const double* x, const double* b, double* xout,
+                            int64_t block);
+/* blocks clipped to rank segments starting at cuts[0..ncuts) (cuts[0] = 0) */
+void orc_hybrid_gs_cut(const orc_csr* A, const double* x, const double* b, double* xout,
+                       int64_t block, int32_t backward, int32_t ncuts, const int64_t* cuts);
 double orc_norm2(int64_t n, const double* v);
 
 /* ---- setup building blocks ---------------------------- */
@@ -96,6 +102,8 @@ orc_hier* orc_hier_setup(const orc_csr* A, const orc_options* opt);
  * computes the coarsest inverse.  Lets the CPU baseline run on the product's hierarchy. */
 orc_hier* orc_hier_from_levels(int32_t nlev, const orc_csr* const* A, const orc_csr* const* P,
                                const orc_csr* const* R, const orc_options* opt);
+/* rank partition of level `level` (start rows); hybrid GS blocks are clipped to it */
+void orc_hier_set_cuts(orc_hier* H, int32_t level, int32_t ncuts, const int64_t* cuts);
 void orc_hier_free(orc_hier* H);
 int32_t orc_hier_levels(const orc_hier* H);
 /* which: 0 = A_l, 1 = P_l, 2 = R_l (borrowed pointer, do not free) */

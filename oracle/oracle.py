@@ -66,6 +66,7 @@ def lib():
             "orc_gen_27pt": (vp, [C.c_int64] * 3 + [C.c_double] * 3),
             "orc_gen_graph_laplacian": (vp, [C.c_int64, C.c_int64, C.c_uint64]),
             "orc_rcm": (None, [vp, _i64p]),
+            "orc_hier_set_cuts": (None, [vp, C.c_int32, C.c_int32, _i64p]),
             "orc_permute": (vp, [vp, _i64p]),
             "orc_vec_uniform": (None, [C.c_int64, C.c_int64, C.c_uint64, _f64p]),
             "orc_spmv": (None, [vp, _f64p, _f64p]),
@@ -73,6 +74,7 @@ def lib():
             "orc_residual": (None, [vp, _f64p, _f64p, _f64p]),
             "orc_jacobi": (None, [vp, _f64p, _f64p, _f64p, C.c_double]),
             "orc_hybrid_gs": (None, [vp, _f64p, _f64p, _f64p, C.c_int64]),
+            "orc_hybrid_gs_backward": (None, [vp, _f64p, _f64p, _f64p, C.c_int64]),
             "orc_norm2": (C.c_double, [C.c_int64, _f64p]),
             "orc_transpose": (vp, [vp]),
             "orc_spgemm": (vp, [vp, vp]),
@@ -188,6 +190,13 @@ class Csr:
         b = np.ascontiguousarray(b, np.float64)
         out = np.empty(self.shape[0])
         lib().orc_hybrid_gs(self.h, _p(x, _f64p), _p(b, _f64p), _p(out, _f64p), block)
+        return out
+
+    def hybrid_gs_backward(self, x, b, block):
+        x = np.ascontiguousarray(x, np.float64)
+        b = np.ascontiguousarray(b, np.float64)
+        out = np.empty(self.shape[0])
+        lib().orc_hybrid_gs_backward(self.h, _p(x, _f64p), _p(b, _f64p), _p(out, _f64p), block)
         return out
 
     def transpose(self):
@@ -350,6 +359,12 @@ class Hierarchy:
         it = lib().orc_hier_solve(self.h, _p(x, _f64p), _p(b, _f64p), max_iter, tol,
                                   _p(hist, _f64p))
         return x, hist[: it + 1]
+
+    def set_cuts(self, level, cuts):
+        """Rank partition (start rows, cuts[0] = 0) of level ``level``: hybrid-GS blocks are
+        clipped to it, as on the product's ranks."""
+        c = np.ascontiguousarray(cuts, np.int64)
+        lib().orc_hier_set_cuts(self.h, int(level), int(c.size), _p(c, _i64p))
 
     def pcg(self, x, b, max_iter=10, tol=0.0):
         x = np.array(x, np.float64, copy=True)

@@ -259,8 +259,11 @@ class ParCSRMatrix:
         check(lib().amg_par_csr_jacobi(self.h, _ptr(x), _ptr(b), _ptr(x_out), float(omega)))
         return x_out
 
-    def hybrid_gs(self, x, b, x_out, block=64):
-        check(lib().amg_par_csr_hybrid_gs(self.h, _ptr(x), _ptr(b), _ptr(x_out), int(block)))
+    def hybrid_gs(self, x, b, x_out, block=64, backward=False):
+        """One hybrid GS sweep (GS inside blocks of `block` rows, Jacobi across blocks and
+        ranks); backward=True walks each block's rows in descending order."""
+        fn = lib().amg_par_csr_hybrid_gs_backward if backward else lib().amg_par_csr_hybrid_gs
+        check(fn(self.h, _ptr(x), _ptr(b), _ptr(x_out), int(block)))
         return x_out
 
     def matmat(self, B: "ParCSRMatrix") -> "ParCSRMatrix":

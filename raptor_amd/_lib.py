@@ -103,6 +103,7 @@ SIGNATURES = {
     "amg_par_csr_residual": (C.c_int, [_vp, _vp, _vp, _vp]),
     "amg_par_csr_jacobi": (C.c_int, [_vp, _vp, _vp, _vp, _f64]),
     "amg_par_csr_hybrid_gs": (C.c_int, [_vp, _vp, _vp, _vp, _i64]),
+    "amg_par_csr_hybrid_gs_backward": (C.c_int, [_vp, _vp, _vp, _vp, _i64]),
     "amg_par_csr_residual_norm": (C.c_int, [_vp, _vp, _vp, _pf64]),
     "amg_par_csr_matmat": (C.c_int, [_vp, _vp, C.POINTER(_vp)]),
     "amg_par_csr_destroy": (C.c_int, [_vp]),

@@ -319,6 +319,16 @@ int amg_par_csr_hybrid_gs(amg_matrix A, const double* x, const double* b, double
     });
 }
 
+int amg_par_csr_hybrid_gs_backward(amg_matrix A, const double* x, const double* b, double* xo,
+                                   int64_t block) {
+    return guard([&] {
+        AMG_CHECK(A, "null matrix");
+        AMG_CHECK(x != xo, "hybrid GS is out of place: x and x_out must differ");
+        set_device(*A->m->ctx);
+        par_hybrid_gs(*A->m, x, b, xo, block, true);
+    });
+}
+
 int amg_par_csr_matmat(amg_matrix A, amg_matrix B, amg_matrix* out) {
     return guard([&] {
         AMG_CHECK(A && B && out, "null argument");

@@ -152,7 +152,7 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
                        int n_blocks, const double* x, const double* b, double* y, double omega,
                        double* partial);
 void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
-                      double* y);
+                      double* y, bool backward = false);
 void launch_jacobi_zero(hipStream_t s, int64_t n, const double* b, const double* dinv, double* y,
                         double omega);
 void launch_pack(hipStream_t s, int64_t n, const int* idx, const double* x, double* out);
@@ -177,7 +177,8 @@ void launch_zero(hipStream_t s, int64_t n, double* y);
 // ParCSRMatrix operations with halo exchange + interior/boundary overlap
 void par_apply(DevMatrix& A, int mode, const double* x, const double* b, double* y, double omega,
                double* partial_or_null);
-void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block);
+void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block,
+                   bool backward = false);
 // Norm plumbing: a mode-NORM level kernel leaves per-block partial sums of (b - Ax)^2 in
 // NormSink::partial; norm_finish() reduces them (fixed order), combines ranks (RCCL
 // allgather, rank order) and appends sqrt to hist[*counter] -- all on the device.
@@ -230,7 +231,8 @@ struct Solver {
     // to the device history (falls back to a separate residual when it cannot)
     void cycle(double* x, const double* b, bool with_norm = false);
     void cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool with_norm);
-    void smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_zero, bool with_norm);
+    void smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_zero, bool with_norm,
+                bool post = false);
     void ensure_hist(int32_t n);
     bool can_fuse_norm() const;
     // ParMultilevel::solve; hist_host gets it+1 norms

@@ -236,6 +236,7 @@ struct GsArgs {
     double* y;
     long long first_row;
     long long B;
+    int n;  // local rows (chunks are clipped to the rank)
 };
 
 __device__ __forceinline__ int chunk_start(const GsArgs& a, int r) {
@@ -243,7 +244,18 @@ __device__ __forceinline__ int chunk_start(const GsArgs& a, int r) {
     long long cs = (g / a.B) * a.B - a.first_row;
     return cs < 0 ? 0 : (int)cs;
 }
+__device__ __forceinline__ int chunk_end(const GsArgs& a, int r) {
+    long long g = a.first_row + r;
+    long long ce = (g / a.B + 1) * a.B - a.first_row;
+    return ce > a.n ? a.n : (int)ce;
+}
+// in-chunk couplings that take the NEW value: j < i (forward) or j > i (backward)
+template <bool BACK>
+__device__ __forceinline__ bool chained(const GsArgs& a, int r, int c) {
+    return BACK ? (c > r && c < chunk_end(a, r)) : (c >= chunk_start(a, r) && c < r);
+}
 
+template <bool BACK>
 __global__ __launch_bounds__(kTPB) void hybrid_gs_kernel(GsArgs a) {
     __shared__ double prod[kCAP];
     __shared__ int lcl[kCAP];
@@ -257,17 +269,17 @@ __global__ __launch_bounds__(kTPB) void hybrid_gs_kernel(GsArgs a) {
     const int tid = threadIdx.x;
     if (nnz > kCAP || r1 - r0 > kTPB) {
         if (tid != 0) return;
-        for (int r = r0; r < r1; ++r) {
-            const int cs = chunk_start(a, r);
+        for (int t = 0; t < r1 - r0; ++t) {
+            const int r = BACK ? r1 - 1 - t : r0 + t;
             double acc = a.b[r];
             for (int k = a.rp[r]; k < a.rp[r + 1]; ++k) {
                 int c = a.col[k];
-                if (c == r || (c >= cs && c < r)) continue;
+                if (c == r || chained<BACK>(a, r, c)) continue;
                 acc -= a.val[k] * (c < a.ncl ? a.x[c] : a.xh[c - a.ncl]);
             }
             for (int k = a.rp[r]; k < a.rp[r + 1]; ++k) {
                 int c = a.col[k];
-                if (c >= cs && c < r) acc -= a.val[k] * a.y[c];
+                if (chained<BACK>(a, r, c)) acc -= a.val[k] * a.y[c];
             }
             a.y[r] = acc * a.dinv[r];
         }
@@ -282,14 +294,13 @@ __global__ __launch_bounds__(kTPB) void hybrid_gs_kernel(GsArgs a) {
     }
     __syncthreads();
     for (int r = r0 + tid; r < r1; r += kTPB) {
-        const int cs = chunk_start(a, r);
         const int e0 = a.rp[r] - k0, e1 = a.rp[r + 1] - k0;
         double acc = a.b[r];
         int lb = -1, le = -1;
         for (int k = e0; k < e1; ++k) {
             int c = lcl[k];
             if (c == r) continue;
-            if (c >= cs && c < r) {
+            if (chained<BACK>(a, r, c)) {  // contiguous in the sorted row
                 if (lb < 0) lb = k;
                 le = k + 1;
                 prod[k] = a.val[k0 + k];  // keep a_ij for the chain
@@ -302,14 +313,15 @@ __global__ __launch_bounds__(kTPB) void hybrid_gs_kernel(GsArgs a) {
         loe[r - r0] = le;
     }
     __syncthreads();
-    // chains: lane t walks chunk t of this block
+    // chains: lane t walks chunk t of this block (descending rows when BACK)
     const long long g0 = (a.first_row + r0) / a.B;
     const long long gl = (a.first_row + r1 - 1) / a.B;
     if (tid <= gl - g0) {
         const long long g = g0 + tid;
         long long cb = g * a.B - a.first_row, ce = cb + a.B;
         const int rb = (int)(cb < r0 ? r0 : cb), re = (int)(ce > r1 ? r1 : ce);
-        for (int r = rb; r < re; ++r) {
+        for (int t = 0; t < re - rb; ++t) {
+            const int r = BACK ? re - 1 - t : rb + t;
             double acc = sacc[r - r0];
             const int lb = lob[r - r0], le = loe[r - r0];
             for (int k = lb; k < le && lb >= 0; ++k) acc -= prod[k] * xnew[lcl[k] - r0];
@@ -542,11 +554,14 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
 }
 
 void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
-                      double* y) {
+                      double* y, bool backward) {
     if (A.n_gs_blocks <= 0) return;
     GsArgs a{A.gs_blocks.p, A.rp.p, A.col.p, A.val.p, x, A.halo.p, (int)A.n_cols_local,
-             b, A.dinv.p, y, (long long)A.first_row, (long long)A.gs_block};
-    hipLaunchKernelGGL(hybrid_gs_kernel, dim3(A.n_gs_blocks), dim3(kTPB), 0, s, a);
+             b, A.dinv.p, y, (long long)A.first_row, (long long)A.gs_block, (int)A.n_rows};
+    if (backward)
+        hipLaunchKernelGGL(hybrid_gs_kernel<true>, dim3(A.n_gs_blocks), dim3(kTPB), 0, s, a);
+    else
+        hipLaunchKernelGGL(hybrid_gs_kernel<false>, dim3(A.n_gs_blocks), dim3(kTPB), 0, s, a);
     HIP_CHECK(hipGetLastError());
 }
 

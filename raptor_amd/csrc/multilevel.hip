@@ -126,8 +126,10 @@ void Solver::ensure_hist(int32_t n) {
         }
 }
 
+// Hybrid GS sweeps forward before the coarse correction and backward after it (post):
+// the V-cycle is then a symmetric operator, as CG requires (oracle smooth()).
 void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_zero,
-                    bool with_norm) {
+                    bool with_norm, bool post) {
     DevMatrix& A = Amat(l);
     if (with_norm) {  // Jacobi sweep that also leaves the partials of ||b - A x||
         AMG_ASSERT(opt.smoother == AMG_SMOOTH_JACOBI && !x_zero);
@@ -135,7 +137,7 @@ void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_
         norm_finish(A, sink);
     } else if (opt.smoother == AMG_SMOOTH_HYBRID_GS) {
         if (x_zero) launch_zero(ctx->stream, A.n_rows, x);
-        par_hybrid_gs(A, x, b, tmp, opt.gs_block);
+        par_hybrid_gs(A, x, b, tmp, opt.gs_block, post);
     } else if (x_zero) {
         launch_jacobi_zero(ctx->stream, A.n_rows, b, A.dinv.p, tmp, opt.jacobi_omega);
     } else {
@@ -195,7 +197,7 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
         cycle_rec(l + 1, C.x.p, C.b.p, true, false);
         par_apply(*L.P, KM_SPMV_ADD, C.x.p, nullptr, cur, 0.0, nullptr);
     }
-    for (int k = 0; k < opt.post_sweeps; ++k) smooth(l, cur, b, tmp, false, false);
+    for (int k = 0; k < opt.post_sweeps; ++k) smooth(l, cur, b, tmp, false, false, true);
     if (cur != x)
         HIP_CHECK(hipMemcpyAsync(x, cur, A.n_rows * sizeof(double), hipMemcpyDeviceToDevice, s));
 }

@@ -263,11 +263,12 @@ void par_apply(DevMatrix& A, int mode, const double* x, const double* b, double*
     launch_csr_stream(s, mode, partial != nullptr, A, A.nb_int, A.nb_bnd, x, b, y, omega, partial);
 }
 
-void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block) {
+void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block,
+                   bool backward) {
     A.ensure_gs_blocks(block);
     const bool comm = A.halo_begin(x);
     if (comm) A.halo_wait();
-    launch_hybrid_gs(A.ctx->stream, A, x, b, y);
+    launch_hybrid_gs(A.ctx->stream, A, x, b, y, backward);
 }
 
 void norm_finish(DevMatrix& A, const NormSink& ns) {

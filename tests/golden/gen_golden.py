@@ -229,6 +229,28 @@ def hybrid_gs(A, x, b, block):
     return out
 
 
+def hybrid_gs_backward(A, x, b, block):
+    """Backward sweep: rows of each block in descending order, new values for in-block j > i."""
+    R = rows(A)
+    n = len(R)
+    out = np.zeros(n)
+    d = A.diagonal()
+    for s in range(0, n, block):
+        e = min(n, s + block)
+        for i in range(e - 1, s - 1, -1):
+            acc = b[i]
+            cols, vals = R[i]
+            for c, v in zip(cols, vals):
+                if c == i or i < c < e:
+                    continue
+                acc -= v * x[c]
+            for c, v in zip(cols, vals):
+                if i < c < e:
+                    acc -= v * out[c]
+            out[i] = acc * (1.0 / d[i])
+    return out
+
+
 def save(name, **arrays):
     np.savez_compressed(os.path.join(HERE, name), **arrays)
 
@@ -260,6 +282,8 @@ def main():
         out["jac"] = x + (2.0 / 3.0) * ((1.0 / d) * (b - A @ x))
         out["gs64"] = hybrid_gs(A, x, b, 64)
         out["gs7"] = hybrid_gs(A, x, b, 7)
+        out["gsb64"] = hybrid_gs_backward(A, x, b, 64)
+        out["gsb7"] = hybrid_gs_backward(A, x, b, 7)
         S = strength_classical(A, 0.25)
         out["S_classical_nnz"] = np.array([len(s) for s in S], np.int64)
         out["cf_rs"] = rs_split(S)

@@ -36,6 +36,19 @@ def run_ranks(n, fn):
     return out
 
 
+def level_starts(ml):
+    """first_row of every level operator on this rank (a replicated level starts at 0)."""
+    return [ml.level_matrix(l, "A").first_row for l in range(ml.num_levels)]
+
+
+def set_oracle_cuts(Ho, res):
+    """Hybrid-GS blocks are clipped at rank boundaries: give the oracle each
+    level's partition, gathered from the ranks' results (last element = level_starts)."""
+    starts = [r[-1] for r in res]
+    for l in range(Ho.num_levels):
+        Ho.set_cuts(l, sorted({s[l] for s in starts if l < len(s)}))
+
+
 @pytest.mark.parametrize("nranks", [2, 3])
 def test_slab_kernels_bit_exact(oracle, nranks):
     import raptor_amd as ra
@@ -93,14 +106,7 @@ def test_multirank_vcycle_bit_exact(oracle, nranks, kind, dims, coarsen, smoothe
                                 else O.SMOOTH_HYBRID_GS))
     n = Ao.shape[0]
     b = Ao.spmv(O.vec_uniform(n, 42))
-    xs = []
-    xo = np.zeros(n)
-    for _ in range(3):
-        xo = Ho.cycle(xo, b)
-        xs.append(xo.copy())
-    _, hist_o = Ho.solve(np.zeros(n), b, max_iter=6)
-    levels = [(Ho.matrix(l, "A"), Ho.matrix(l, "P") if l + 1 < Ho.num_levels else None)
-              for l in range(Ho.num_levels)]
+    levels = [Ho.matrix(l, "A") for l in range(Ho.num_levels)]
 
     def rank(r, nr, world):
         ctx = ra.Context.loopback(r, nr, world)
@@ -113,25 +119,32 @@ def test_multirank_vcycle_bit_exact(oracle, nranks, kind, dims, coarsen, smoothe
         for l in range(min(ml.num_levels, Ho.num_levels)):
             M = ml.level_matrix(l, "A")
             loc = M.to_scipy_local()
-            G = levels[l][0][M.first_row:M.first_row + M.local_rows]
+            G = levels[l][M.first_row:M.first_row + M.local_rows]
             if not (np.array_equal(loc.indptr, G.indptr) and np.array_equal(loc.indices, G.indices)
                     and np.array_equal(loc.data, G.data)):
                 bad.append(("A", l))
         db = to_dev(ctx, b[f:f + m])
         dx = ctx.zeros(m)
+        xs = []
         for k in range(3):
             ml.cycle(dx, db)
-            if not np.array_equal(to_host(ctx, dx), xs[k][f:f + m]):
-                bad.append(("cycle", k))
+            xs.append(to_host(ctx, dx))
         dx = ctx.zeros(m)
         _, hist = ml.solve(dx, db, max_iter=6)
-        return bad, hist
+        return bad, hist, f, m, xs, level_starts(ml)
 
     res = run_ranks(nranks, rank)
-    for bad, hist in res:
+    set_oracle_cuts(Ho, res)
+    xo = np.zeros(n)
+    for k in range(3):
+        xo = Ho.cycle(xo, b)
+        for _, _, f, m, xs, _ in res:
+            assert np.array_equal(xs[k], xo[f:f + m]), ("cycle", k)
+    _, hist_o = Ho.solve(np.zeros(n), b, max_iter=6)
+    for bad, hist, *_ in res:
         assert bad == []
         assert np.all(np.abs(hist - hist_o) <= 1e-10 * hist_o)
-    assert all(np.array_equal(res[0][1], h) for _, h in res)  # every rank reports the same
+    assert all(np.array_equal(res[0][1], r[1]) for r in res)  # every rank reports the same
 
 
 def test_uneven_partition_from_csr(oracle):

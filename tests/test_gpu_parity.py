@@ -66,6 +66,8 @@ def test_level_kernels_bit_exact(ctx, oracle, problems, name):
     for blk in (64, 17, 1, 256):
         A.hybrid_gs(dx, db, out, blk)
         assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs(x, b, blk)), blk
+        A.hybrid_gs(dx, db, out, blk, backward=True)
+        assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs_backward(x, b, blk)), blk
     rn = A.residual_norm(dx, db)
     ro = O.norm2(Ao.residual(x, b))
     assert abs(rn - ro) <= 1e-12 * ro

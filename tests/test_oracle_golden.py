@@ -50,6 +50,8 @@ def test_level_kernels_match_scipy(oracle, name):
     assert np.allclose(A.jacobi(x, b, 2.0 / 3.0), g["jac"], rtol=1e-14, atol=1e-14)
     assert np.array_equal(A.hybrid_gs(x, b, 64), g["gs64"])
     assert np.array_equal(A.hybrid_gs(x, b, 7), g["gs7"])
+    assert np.array_equal(A.hybrid_gs_backward(x, b, 64), g["gsb64"])
+    assert np.array_equal(A.hybrid_gs_backward(x, b, 7), g["gsb7"])
     y0 = np.arange(x.size, dtype=float)
     assert np.array_equal(A.spmv_add(x, y0), y0 + g["y"])
 
