@@ -211,25 +211,41 @@ void orc_jacobi(const orc_csr* A, const double* x, const double* b, double* xout
  * blocks Jacobi.  acc = b_i; acc -= a_ij*x_j over "old" entries (j != i, j outside
  * [block_start, i)) in CSR order; then acc -= a_ij*xnew_j over in-block lower entries in
  * CSR order; xnew_i = acc * dinv_i. */
-/* one GS block [s, e): Jacobi for couplings outside it, Gauss-Seidel inside.  Forward:
- * rows s..e-1, new values for in-block j < i.  Backward: rows e-1..s, new values for
- * in-block j > i.  Old-value couplings first, then new-value couplings, each in CSR order. */
+/* one GS block [s, e) of the l1 hybrid Gauss-Seidel: Gauss-Seidel inside the
+ * block, Jacobi for couplings outside it, and the diagonal augmented by the l1 norm of the
+ * outside couplings, d_i = a_ii + sum_{j outside} |a_ij| (summed in CSR order), applied in
+ * correction form x_i' = x_i + r_i / d_i, which makes the sweep convergent for any SPD A.  Forward: rows s..e-1, new values for in-block j < i;
+ * backward: rows e-1..s, new values for in-block j > i.  Old-value couplings are subtracted
+ * first in CSR order, then new-value couplings in sweep order (ascending j forward,
+ * descending j backward). */
 static void gs_block_rows(const orc_csr* A, const double* x, const double* b, double* xout,
                           int64_t s, int64_t e, int backward) {
     for (int64_t t = 0; t < e - s; ++t) {
         int64_t i = backward ? e - 1 - t : s + t;
         int64_t lo = backward ? i + 1 : s, hi = backward ? e : i; /* new-value range [lo, hi) */
-        double acc = b[i], dinv = 1.0 / diag_of(A, i);
+        double acc = b[i], l1 = 0.0;
         for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
             int64_t j = A->col[k];
-            if (j == i || (j >= lo && j < hi)) continue;
-            acc -= A->val[k] * x[j];
+            if (j < s || j >= e) l1 += fabs(A->val[k]);
         }
+        double dinv = 1.0 / (diag_of(A, i) + l1);
         for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
             int64_t j = A->col[k];
-            if (j >= lo && j < hi) acc -= A->val[k] * xout[j];
+            if (j >= lo && j < hi) continue;
+            acc -= A->val[k] * x[j]; /* includes the diagonal, old x_i */
         }
-        xout[i] = acc * dinv;
+        if (!backward) {
+            for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
+                int64_t j = A->col[k];
+                if (j >= lo && j < hi) acc -= A->val[k] * xout[j];
+            }
+        } else {
+            for (int64_t k = A->rp[i + 1] - 1; k >= A->rp[i]; --k) {
+                int64_t j = A->col[k];
+                if (j >= lo && j < hi) acc -= A->val[k] * xout[j];
+            }
+        }
+        xout[i] = x[i] + acc * dinv; /* correction form: the fixed point solves A x = b */
     }
 }
 

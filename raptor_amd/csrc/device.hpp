@@ -124,10 +124,17 @@ struct DevMatrix {
     // csr-stream variant bits (kernels.hip): 2 = XCD block order, 4 = gather (no x tile).
     // Set at build: x tile for square operators; gather + XCD order for rectangular ones.
     int default_variant = 0;
-    // hybrid-GS blocks (built on first use for a given block size)
-    DevBuf<int2> gs_blocks;
-    int n_gs_blocks = 0;
+    // l1 hybrid GS (built on first use for a given block size B <= 64): GS chunks = global
+    // multiples of B clipped to this rank, packed whole into slabs of <= 64 rows (one
+    // wavefront each, lane = row).  Each slab's rows are stored sliced-ELL, column-major
+    // (entry k of lane l at (off + k) * 64 + l; col -1 = padding) so a lane's walk of its
+    // row is a coalesced stream.  gs_dinv = 1 / (a_ii + sum of |a_ij| outside the chunk).
+    DevBuf<int4> gs_slabs;  // {first row, rows, offset / 64, width}
+    DevBuf<int> gs_col;
+    DevBuf<double> gs_val, gs_dinv;
+    int n_gs_slabs = 0;
     int64_t gs_block = 0;
+    int64_t gs_bytes = 0;  // sliced-ELL bytes streamed per sweep
     // halo (ParComm): RCCL neighbour exchange
     HaloPlan plan;
     DevBuf<int> send_idx;

@@ -217,119 +217,111 @@ __global__ __launch_bounds__(kTPB) void csr_stream_kernel(CsrArgs a, int first_b
     }
 }
 
-// Hybrid Gauss-Seidel (row a5).  Workgroup = whole GS chunks (global row multiples of B)
-// with <= kCAP nonzeros, <= 256 rows.  Phase 1 stages a_ij * x_old_j; phase 2 (lane per
-// row) subtracts the "old" terms in CSR order and marks the in-chunk lower entries
-// (contiguous just before the diagonal because columns are sorted); phase 3 (lane per
-// chunk) runs the short dependency chain in LDS.  Oversized chunks: lane 0 of the
-// workgroup walks them exactly like the oracle.
+// l1 hybrid Gauss-Seidel (row a5; definition DESIGN.md 3).  One wavefront per slab of <= 64
+// rows (whole GS chunks), lane = row.
+//  phase 1: the lane walks its row in the slab's sliced-ELL layout (entry k of all lanes is
+//           one coalesced 512-byte load) and subtracts every old-value coupling, diagonal
+//           included, in CSR order; the new-value ("chain") couplings -- in-chunk j < i
+//           forward, j > i backward -- are contiguous in the sorted row and are skipped.
+//  phase 2: the in-chunk triangular solve, column-oriented: at step t the row finishing now
+//           (lane t forward, lane n-1-t backward) has its final value; it is broadcast with
+//           v_readlane and every lane whose next chain column is that row subtracts
+//           a_ij * x_j.  Each lane keeps its next four chain entries in registers and
+//           refills from the (cache-hot) sliced-ELL arrays, so chain couplings are consumed
+//           in sweep order (ascending j forward, descending j backward) exactly like the
+//           oracle, with no LDS and no barrier.
+//  x_i' = x_i + acc * dinv_l1.
 struct GsArgs {
-    const int2* blocks;
-    const int* rp;
-    const int* col;
+    const int4* slabs;
+    const int* col;      // sliced-ELL, -1 = padding
     const double* val;
     const double* x;
-    const double* xh;
+    const double* xh;    // halo values (columns >= ncl)
     int ncl;
     const double* b;
-    const double* dinv;
+    const double* dinv;  // l1 diagonal inverse
     double* y;
     long long first_row;
     long long B;
-    int n;  // local rows (chunks are clipped to the rank)
+    int n;               // local rows (chunks are clipped to the rank)
+    int nslab;
 };
 
-__device__ __forceinline__ int chunk_start(const GsArgs& a, int r) {
-    long long g = a.first_row + r;
-    long long cs = (g / a.B) * a.B - a.first_row;
-    return cs < 0 ? 0 : (int)cs;
-}
-__device__ __forceinline__ int chunk_end(const GsArgs& a, int r) {
-    long long g = a.first_row + r;
-    long long ce = (g / a.B + 1) * a.B - a.first_row;
-    return ce > a.n ? a.n : (int)ce;
-}
-// in-chunk couplings that take the NEW value: j < i (forward) or j > i (backward)
-template <bool BACK>
-__device__ __forceinline__ bool chained(const GsArgs& a, int r, int c) {
-    return BACK ? (c > r && c < chunk_end(a, r)) : (c >= chunk_start(a, r) && c < r);
+__device__ __forceinline__ double bcast_lane(double v, int lane) {
+    const long long bits = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)bits, lane);
+    const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
 template <bool BACK>
-__global__ __launch_bounds__(kTPB) void hybrid_gs_kernel(GsArgs a) {
-    __shared__ double prod[kCAP];
-    __shared__ int lcl[kCAP];
-    __shared__ double sacc[kTPB];
-    __shared__ double xnew[kTPB];
-    __shared__ int lob[kTPB], loe[kTPB];
-    const int2 br = a.blocks[blockIdx.x];
-    const int r0 = br.x, r1 = br.y;
-    const int k0 = a.rp[r0];
-    const int nnz = a.rp[r1] - k0;
-    const int tid = threadIdx.x;
-    if (nnz > kCAP || r1 - r0 > kTPB) {
-        if (tid != 0) return;
-        for (int t = 0; t < r1 - r0; ++t) {
-            const int r = BACK ? r1 - 1 - t : r0 + t;
-            double acc = a.b[r];
-            for (int k = a.rp[r]; k < a.rp[r + 1]; ++k) {
-                int c = a.col[k];
-                if (c == r || chained<BACK>(a, r, c)) continue;
-                acc -= a.val[k] * (c < a.ncl ? a.x[c] : a.xh[c - a.ncl]);
-            }
-            for (int k = a.rp[r]; k < a.rp[r + 1]; ++k) {
-                int c = a.col[k];
-                if (chained<BACK>(a, r, c)) acc -= a.val[k] * a.y[c];
-            }
-            a.y[r] = acc * a.dinv[r];
+__global__ __launch_bounds__(256) void hybrid_gs_kernel(GsArgs a) {
+    // wave index made provably uniform: slab fields land in SGPRs, the step loop is scalar
+    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    if (wave >= a.nslab) return;
+    const int lane = threadIdx.x & 63;
+    const int4 sl = a.slabs[wave];
+    const int r = sl.x + lane;
+    const bool live = lane < sl.y;
+    int lo = 0, hi = 0;  // chain (new-value) column range [lo, hi)
+    double acc = 0.0, xi = 0.0, dinv = 0.0;
+    if (live) {
+        const long long g = a.first_row + r;
+        long long cs = (g / a.B) * a.B - a.first_row, ce = cs + a.B;
+        cs = cs < 0 ? 0 : cs;
+        ce = ce > a.n ? a.n : ce;
+        lo = BACK ? r + 1 : (int)cs;
+        hi = BACK ? (int)ce : r;
+        acc = a.b[r];
+        xi = a.x[r];
+        dinv = a.dinv[r];
+    }
+    const size_t base = (size_t)sl.z * 64 + lane;
+    const int* colp = a.col + base;
+    const double* valp = a.val + base;
+    int kf = -1, kl = -1;  // first / last chain entry of the row
+    for (int k = 0; k < sl.w; ++k) {
+        const int c = __builtin_nontemporal_load(colp + (size_t)k * 64);
+        const double v = __builtin_nontemporal_load(valp + (size_t)k * 64);
+        if (c < 0) continue;  // padding (also every entry of a dead lane)
+        if (c >= lo && c < hi) {
+            kf = kf < 0 ? k : kf;
+            kl = k;
+            continue;
         }
-        return;
+        acc -= v * (c < a.ncl ? a.x[c] : a.xh[c - a.ncl]);
     }
-    for (int k = tid; k < nnz; k += kTPB) {
-        int c = __builtin_nontemporal_load(a.col + k0 + k);
-        double v = __builtin_nontemporal_load(a.val + k0 + k);
-        const double* p = c < a.ncl ? a.x + c : a.xh + (c - a.ncl);
-        prod[k] = v * *p;
-        lcl[k] = c;
-    }
-    __syncthreads();
-    for (int r = r0 + tid; r < r1; r += kTPB) {
-        const int e0 = a.rp[r] - k0, e1 = a.rp[r + 1] - k0;
-        double acc = a.b[r];
-        int lb = -1, le = -1;
-        for (int k = e0; k < e1; ++k) {
-            int c = lcl[k];
-            if (c == r) continue;
-            if (chained<BACK>(a, r, c)) {  // contiguous in the sorted row
-                if (lb < 0) lb = k;
-                le = k + 1;
-                prod[k] = a.val[k0 + k];  // keep a_ij for the chain
-                continue;
-            }
-            acc -= prod[k];
+    // register ring of the next four chain entries, in consumption order
+    int c0 = -1, c1 = -1, c2 = -1, c3 = -1;
+    double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+    int kn = BACK ? kl : kf;       // next entry to load
+    int left = kf < 0 ? 0 : kl - kf + 1;
+    auto load = [&](int& c, double& v) {
+        if (left > 0) {
+            c = colp[(size_t)kn * 64];
+            v = valp[(size_t)kn * 64];
+            kn += BACK ? -1 : 1;
+            --left;
+        } else {
+            c = -1;
         }
-        sacc[r - r0] = acc;
-        lob[r - r0] = lb;
-        loe[r - r0] = le;
-    }
-    __syncthreads();
-    // chains: lane t walks chunk t of this block (descending rows when BACK)
-    const long long g0 = (a.first_row + r0) / a.B;
-    const long long gl = (a.first_row + r1 - 1) / a.B;
-    if (tid <= gl - g0) {
-        const long long g = g0 + tid;
-        long long cb = g * a.B - a.first_row, ce = cb + a.B;
-        const int rb = (int)(cb < r0 ? r0 : cb), re = (int)(ce > r1 ? r1 : ce);
-        for (int t = 0; t < re - rb; ++t) {
-            const int r = BACK ? re - 1 - t : rb + t;
-            double acc = sacc[r - r0];
-            const int lb = lob[r - r0], le = loe[r - r0];
-            for (int k = lb; k < le && lb >= 0; ++k) acc -= prod[k] * xnew[lcl[k] - r0];
-            const double xn = acc * a.dinv[r];
-            xnew[r - r0] = xn;
-            a.y[r] = xn;
+    };
+    load(c0, v0);
+    load(c1, v1);
+    load(c2, v2);
+    load(c3, v3);
+    for (int t = 0; t < sl.y; ++t) {
+        const int j = BACK ? sl.y - 1 - t : t;  // lane whose row is final now
+        const double xj = bcast_lane(xi + acc * dinv, j);
+        if (c0 == sl.x + j) {
+            acc -= v0 * xj;
+            c0 = c1, v0 = v1;
+            c1 = c2, v1 = v2;
+            c2 = c3, v2 = v3;
+            load(c3, v3);
         }
     }
+    if (live) a.y[r] = xi + acc * dinv;
 }
 
 __global__ void jacobi_zero_kernel(long long n, const double* b, const double* dinv, double* y,
@@ -555,13 +547,15 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
 
 void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
                       double* y, bool backward) {
-    if (A.n_gs_blocks <= 0) return;
-    GsArgs a{A.gs_blocks.p, A.rp.p, A.col.p, A.val.p, x, A.halo.p, (int)A.n_cols_local,
-             b, A.dinv.p, y, (long long)A.first_row, (long long)A.gs_block, (int)A.n_rows};
+    if (A.n_gs_slabs <= 0) return;
+    GsArgs a{A.gs_slabs.p, A.gs_col.p, A.gs_val.p, x, A.halo.p, (int)A.n_cols_local, b,
+             A.gs_dinv.p, y, (long long)A.first_row, (long long)A.gs_block, (int)A.n_rows,
+             A.n_gs_slabs};
+    const dim3 grid((A.n_gs_slabs + 3) / 4);
     if (backward)
-        hipLaunchKernelGGL(hybrid_gs_kernel<true>, dim3(A.n_gs_blocks), dim3(kTPB), 0, s, a);
+        hipLaunchKernelGGL(hybrid_gs_kernel<true>, grid, dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL(hybrid_gs_kernel<false>, dim3(A.n_gs_blocks), dim3(kTPB), 0, s, a);
+        hipLaunchKernelGGL(hybrid_gs_kernel<false>, grid, dim3(256), 0, s, a);
     HIP_CHECK(hipGetLastError());
 }
 

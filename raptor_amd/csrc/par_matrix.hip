@@ -8,6 +8,7 @@
 // stream; the boundary kernel runs after the halo event.
 #include <algorithm>
 #include <climits>
+#include <cmath>
 
 #include "device.hpp"
 
@@ -198,30 +199,60 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
 
 void DevMatrix::ensure_gs_blocks(int64_t B) {
     AMG_CHECK(square, "hybrid GS needs a square matrix");
-    AMG_CHECK(B >= 1 && B <= kTPB, "hybrid GS block must be in [1, 256]");
-    if (gs_block == B && (n_gs_blocks > 0 || n_rows == 0)) return;
-    std::vector<int2> out;
-    const std::vector<int64_t>& hrp = host.rp;
-    if (n_rows > 0) {
-        int64_t q0 = first_row / B, q1 = (first_row + n_rows - 1) / B;
-        int64_t br = -1, be = -1, acc = 0;
-        for (int64_t q = q0; q <= q1; ++q) {
-            int64_t cb = std::max<int64_t>(0, q * B - first_row);
-            int64_t ce = std::min<int64_t>(n_rows, (q + 1) * B - first_row);
-            int64_t cn = hrp[ce] - hrp[cb];
-            if (br >= 0 && (acc + cn > kCAP || ce - br > kTPB)) {
-                out.push_back(make_int2((int)br, (int)be));
-                br = -1;
-            }
-            if (br < 0) br = cb, acc = 0;
-            be = ce;
-            acc += cn;
+    AMG_CHECK(B >= 1 && B <= 64, "hybrid GS block must be in [1, 64]");
+    if (gs_block == B) return;
+    const int64_t clo = first_col, chi = first_col + n_cols_local;
+    auto local_col = [&](int64_t g) -> int {
+        return g >= clo && g < chi ? (int)(g - clo) : (int)(n_cols_local + plan.find(g));
+    };
+    // chunks (global multiples of B clipped to the rank), packed whole into <= 64-row slabs
+    std::vector<int4> slabs;
+    int64_t cells = 0;
+    for (int64_t r = 0; r < n_rows;) {
+        int64_t end = r;
+        while (end < n_rows) {
+            const int64_t g = first_row + end;
+            const int64_t ce = std::min(n_rows, (g / B + 1) * B - first_row);
+            if (ce - r > 64) break;
+            end = ce;
         }
-        if (br >= 0) out.push_back(make_int2((int)br, (int)be));
+        AMG_ASSERT(end > r);
+        int w = 0;
+        for (int64_t i = r; i < end; ++i) w = std::max<int>(w, (int)(host.rp[i + 1] - host.rp[i]));
+        slabs.push_back(make_int4((int)r, (int)(end - r), (int)cells, w));
+        cells += w;
+        r = end;
     }
-    gs_blocks.upload(out.data(), out.size());
-    n_gs_blocks = (int)out.size();
+    AMG_CHECK(cells * 64 < INT_MAX, "hybrid GS: sliced-ELL too large for int32 offsets");
+    std::vector<int> sc((size_t)std::max<int64_t>(cells, 1) * 64, -1);
+    std::vector<double> sv(sc.size(), 0.0), di(n_rows);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (size_t q = 0; q < slabs.size(); ++q) {
+        const int4 sl = slabs[q];
+        for (int l = 0; l < sl.y; ++l) {
+            const int64_t i = sl.x + l, g = first_row + i;
+            const int64_t cs = std::max<int64_t>(first_row, g / B * B);
+            const int64_t ce = std::min(first_row + n_rows, (g / B + 1) * B);
+            double l1 = 0.0, d = 0.0;
+            for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) {
+                const int64_t gc = host.col[k];
+                const size_t at = ((size_t)sl.z + (size_t)(k - host.rp[i])) * 64 + l;
+                sc[at] = local_col(gc);
+                sv[at] = host.val[k];
+                if (gc < cs || gc >= ce) l1 += std::fabs(host.val[k]);
+                if (gc == g) d = host.val[k];
+            }
+            AMG_CHECK(d != 0.0 || l1 != 0.0, "hybrid GS: zero row");
+            di[i] = 1.0 / (d + l1);
+        }
+    }
+    gs_slabs.upload(slabs.data(), slabs.size());
+    gs_col.upload(sc.data(), sc.size());
+    gs_val.upload(sv.data(), sv.size());
+    gs_dinv.upload(di.data(), di.size());
+    n_gs_slabs = (int)slabs.size();
     gs_block = B;
+    gs_bytes = 12 * 64 * cells + 16 * (int64_t)slabs.size() + 32 * n_rows;
 }
 
 bool DevMatrix::halo_begin(const double* x) {

@@ -208,24 +208,36 @@ def mis2_aggregate(Sv, seed):
     return np.array(out, np.int32), len(roots)
 
 
+def _l1_gs_block(R, d, x, b, out, s, e, backward):
+    """l1 hybrid GS on block [s, e): acc = b_i - sum of old-value couplings
+    (incl. the diagonal, CSR order) - sum of new-value in-block couplings (sweep order);
+    x_i' = x_i + acc / (a_ii + sum_{j outside [s, e)} |a_ij|)."""
+    order = range(e - 1, s - 1, -1) if backward else range(s, e)
+    for i in order:
+        cols, vals = R[i]
+        lo, hi = (i + 1, e) if backward else (s, i)
+        l1 = 0.0
+        for c, v in zip(cols, vals):
+            if c < s or c >= e:
+                l1 += abs(v)
+        acc = b[i]
+        for c, v in zip(cols, vals):
+            if lo <= c < hi:
+                continue
+            acc -= v * x[c]
+        new = [(c, v) for c, v in zip(cols, vals) if lo <= c < hi]
+        for c, v in (reversed(new) if backward else new):
+            acc -= v * out[c]
+        out[i] = x[i] + acc * (1.0 / (d[i] + l1))
+
+
 def hybrid_gs(A, x, b, block):
     R = rows(A)
     n = len(R)
     out = np.zeros(n)
     d = A.diagonal()
     for s in range(0, n, block):
-        e = min(n, s + block)
-        for i in range(s, e):
-            acc = b[i]
-            cols, vals = R[i]
-            for c, v in zip(cols, vals):
-                if c == i or s <= c < i:
-                    continue
-                acc -= v * x[c]
-            for c, v in zip(cols, vals):
-                if s <= c < i:
-                    acc -= v * out[c]
-            out[i] = acc * (1.0 / d[i])
+        _l1_gs_block(R, d, x, b, out, s, min(n, s + block), False)
     return out
 
 
@@ -236,18 +248,7 @@ def hybrid_gs_backward(A, x, b, block):
     out = np.zeros(n)
     d = A.diagonal()
     for s in range(0, n, block):
-        e = min(n, s + block)
-        for i in range(e - 1, s - 1, -1):
-            acc = b[i]
-            cols, vals = R[i]
-            for c, v in zip(cols, vals):
-                if c == i or i < c < e:
-                    continue
-                acc -= v * x[c]
-            for c, v in zip(cols, vals):
-                if i < c < e:
-                    acc -= v * out[c]
-            out[i] = acc * (1.0 / d[i])
+        _l1_gs_block(R, d, x, b, out, s, min(n, s + block), True)
     return out
 
 

@@ -63,7 +63,7 @@ def test_level_kernels_bit_exact(ctx, oracle, problems, name):
     assert np.array_equal(to_host(ctx, out), Ao.residual(x, b))
     A.jacobi(dx, db, out, 2.0 / 3.0)
     assert np.array_equal(to_host(ctx, out), Ao.jacobi(x, b, 2.0 / 3.0))
-    for blk in (64, 17, 1, 256):
+    for blk in (64, 17, 1, 33):
         A.hybrid_gs(dx, db, out, blk)
         assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs(x, b, blk)), blk
         A.hybrid_gs(dx, db, out, blk, backward=True)
