@@ -787,6 +787,7 @@ void orc_dense_inverse(int64_t n, const orc_csr* A, double* inv) {
             M[c * n + j] *= ip;
             inv[c * n + j] *= ip;
         }
+#pragma omp parallel for schedule(static)
         for (int64_t r = 0; r < n; ++r) {
             if (r == c) continue;
             double f = M[r * n + c];
@@ -852,7 +853,9 @@ orc_hier* orc_hier_setup(const orc_csr* A0, const orc_options* opt) {
             P = orc_interp_classical(A, S, split);
             orc_csr_free(S);
         }
-        if (P->n_cols == 0 || P->n_cols >= n) { /* coarsening stalled */
+        /* coarsening stalled: no coarse points, no reduction, or < 20% reduction on a level
+         * small enough (<= 8192 rows) to become the dense-solved coarsest */
+        if (P->n_cols == 0 || P->n_cols >= n || (n <= 8192 && 5 * P->n_cols > 4 * n)) {
             orc_csr_free(P);
             free(split);
             break;

@@ -30,6 +30,7 @@ constexpr int kTPB = 256;   // threads per workgroup (4 waves of 64)
 constexpr int kCAP = 2048;  // nonzeros staged in LDS per workgroup (16 KiB of products)
 constexpr int kPad = 4;     // col/val padding (entries) for the 16-byte vector-load tail
 constexpr int kTileLines = 256;  // x tile per workgroup: 256 lines x 64 B = 16 KiB of LDS
+constexpr int kGsWide = 128;     // sliced-ELL width from which hybrid GS uses the wide variant
 constexpr int kDefaultVariant = 0;  // csr-stream variant (kernels.hip kernel_variant())
 int kernel_variant();
 
@@ -135,6 +136,7 @@ struct DevMatrix {
     int n_gs_slabs = 0;
     int64_t gs_block = 0;
     int64_t gs_bytes = 0;  // sliced-ELL bytes streamed per sweep
+    bool gs_wide = false;  // average slab width >= kGsWide: the LDS-chain kernel variant
     // halo (ParComm): RCCL neighbour exchange
     HaloPlan plan;
     DevBuf<int> send_idx;

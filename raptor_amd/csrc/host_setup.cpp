@@ -584,6 +584,8 @@ std::vector<double> dense_inverse_gathered(const HostComm& comm, const HostCSR& 
             M[c * n + j] *= ip;
             inv[c * n + j] *= ip;
         }
+        // rows are independent within a pivot step: parallel, same arithmetic per element
+#pragma omp parallel for schedule(static)
         for (int64_t r = 0; r < n; ++r) {
             if (r == c) continue;
             double f = M[r * n + c];
@@ -628,7 +630,9 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
             throw Error(AMG_ERR_INVALID, "unknown coarsening");
         }
         const int64_t nc = P.n_global_cols;
-        if (nc == 0 || nc >= n) break;  // coarsening stalled (same rule as the oracle)
+        // coarsening stalled (same rule as the oracle): no coarse points, no reduction, or
+        // less than 20% reduction on a level small enough to be the dense-solved coarsest
+        if (nc == 0 || nc >= n || (n <= 8192 && 5 * nc > 4 * n)) break;
         HostCSR R = transpose(comm, P);
         HostCSR AP = mm(A, P);
         HostCSR Ac = mm(R, AP);

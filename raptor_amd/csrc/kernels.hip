@@ -12,6 +12,8 @@
 // kernels are bit-identical to oracle/amg_oracle.c.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "device.hpp"
 
 namespace amg {
@@ -254,10 +256,16 @@ __device__ __forceinline__ double bcast_lane(double v, int lane) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-template <bool BACK>
-__global__ __launch_bounds__(256) void hybrid_gs_kernel(GsArgs a) {
+// WIDE (dense coarse operators, average slab width >= kGsWide): one wave per workgroup, the
+// slab's chain entries go to LDS as a 64 x 64 column-major block plus a per-lane bit mask in
+// phase 1, so the triangular solve never reloads them; phase 1 keeps 16 loads in flight.
+// Narrow: 4 waves per workgroup (no LDS), 8 loads in flight, register ring of chain entries.
+template <bool BACK, bool WIDE>
+__global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
+    constexpr int U = WIDE ? 16 : 8;
     // wave index made provably uniform: slab fields land in SGPRs, the step loop is scalar
-    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    const int wave = __builtin_amdgcn_readfirstlane(
+        (int)(WIDE ? blockIdx.x : blockIdx.x * 4 + (threadIdx.x >> 6)));
     if (wave >= a.nslab) return;
     const int lane = threadIdx.x & 63;
     const int4 sl = a.slabs[wave];
@@ -279,46 +287,86 @@ __global__ __launch_bounds__(256) void hybrid_gs_kernel(GsArgs a) {
     const size_t base = (size_t)sl.z * 64 + lane;
     const int* colp = a.col + base;
     const double* valp = a.val + base;
-    int kf = -1, kl = -1;  // first / last chain entry of the row
-    for (int k = 0; k < sl.w; ++k) {
-        const int c = __builtin_nontemporal_load(colp + (size_t)k * 64);
-        const double v = __builtin_nontemporal_load(valp + (size_t)k * 64);
-        if (c < 0) continue;  // padding (also every entry of a dead lane)
-        if (c >= lo && c < hi) {
-            kf = kf < 0 ? k : kf;
-            kl = k;
-            continue;
-        }
-        acc -= v * (c < a.ncl ? a.x[c] : a.xh[c - a.ncl]);
-    }
-    // register ring of the next four chain entries, in consumption order
-    int c0 = -1, c1 = -1, c2 = -1, c3 = -1;
-    double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
-    int kn = BACK ? kl : kf;       // next entry to load
-    int left = kf < 0 ? 0 : kl - kf + 1;
-    auto load = [&](int& c, double& v) {
-        if (left > 0) {
-            c = colp[(size_t)kn * 64];
-            v = valp[(size_t)kn * 64];
-            kn += BACK ? -1 : 1;
-            --left;
-        } else {
-            c = -1;
+    __shared__ double chainL[WIDE ? 64 * 64 : 1];
+    unsigned long long mask = 0;  // WIDE: bit t = coupling to slab row t
+    int kf = -1, kl = -1;         // narrow: first / last chain entry of the row
+    // software pipeline: block k0 + U's (col, val) stream in while block k0 gathers x
+    int cn[U];
+    double vn[U];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = k0 + u < sl.w;  // uniform
+            cn[u] = in ? __builtin_nontemporal_load(colp + (size_t)(k0 + u) * 64) : -1;
+            vn[u] = in ? __builtin_nontemporal_load(valp + (size_t)(k0 + u) * 64) : 0.0;
         }
     };
-    load(c0, v0);
-    load(c1, v1);
-    load(c2, v2);
-    load(c3, v3);
-    for (int t = 0; t < sl.y; ++t) {
-        const int j = BACK ? sl.y - 1 - t : t;  // lane whose row is final now
-        const double xj = bcast_lane(xi + acc * dinv, j);
-        if (c0 == sl.x + j) {
-            acc -= v0 * xj;
-            c0 = c1, v0 = v1;
-            c1 = c2, v1 = v2;
-            c2 = c3, v2 = v3;
-            load(c3, v3);
+    fetch(0);
+    for (int k0 = 0; k0 < sl.w; k0 += U) {
+        int c[U];
+        double v[U], xv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) c[u] = cn[u], v[u] = vn[u];
+        if (k0 + U < sl.w) fetch(k0 + U);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool old = c[u] >= 0 && !(c[u] >= lo && c[u] < hi);
+            xv[u] = old ? (c[u] < a.ncl ? a.x[c[u]] : a.xh[c[u] - a.ncl]) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (c[u] < 0) continue;  // padding (also every entry of a dead lane)
+            if (c[u] >= lo && c[u] < hi) {
+                if (WIDE) {
+                    const int t = c[u] - sl.x;
+                    chainL[t * 64 + lane] = v[u];
+                    mask |= 1ull << t;
+                } else {
+                    kf = kf < 0 ? k0 + u : kf;
+                    kl = k0 + u;
+                }
+                continue;
+            }
+            acc -= v[u] * xv[u];
+        }
+    }
+    if (WIDE) {
+        for (int t = 0; t < sl.y; ++t) {
+            const int j = BACK ? sl.y - 1 - t : t;  // lane whose row is final now
+            const double lv = chainL[j * 64 + lane];
+            const double xj = bcast_lane(xi + acc * dinv, j);
+            if ((mask >> j) & 1ull) acc -= lv * xj;
+        }
+    } else {
+        // register ring of the next four chain entries, in consumption order
+        int c0 = -1, c1 = -1, c2 = -1, c3 = -1;
+        double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+        int kn = BACK ? kl : kf;  // next entry to load
+        int left = kf < 0 ? 0 : kl - kf + 1;
+        auto load = [&](int& cc, double& vv) {
+            if (left > 0) {
+                cc = colp[(size_t)kn * 64];
+                vv = valp[(size_t)kn * 64];
+                kn += BACK ? -1 : 1;
+                --left;
+            } else {
+                cc = -1;
+            }
+        };
+        load(c0, v0);
+        load(c1, v1);
+        load(c2, v2);
+        load(c3, v3);
+        for (int t = 0; t < sl.y; ++t) {
+            const int j = BACK ? sl.y - 1 - t : t;
+            const double xj = bcast_lane(xi + acc * dinv, j);
+            if (c0 == sl.x + j) {
+                acc -= v0 * xj;
+                c0 = c1, v0 = v1;
+                c1 = c2, v1 = v2;
+                c2 = c3, v2 = v3;
+                load(c3, v3);
+            }
         }
     }
     if (live) a.y[r] = xi + acc * dinv;
@@ -551,11 +599,24 @@ void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const 
     GsArgs a{A.gs_slabs.p, A.gs_col.p, A.gs_val.p, x, A.halo.p, (int)A.n_cols_local, b,
              A.gs_dinv.p, y, (long long)A.first_row, (long long)A.gs_block, (int)A.n_rows,
              A.n_gs_slabs};
-    const dim3 grid((A.n_gs_slabs + 3) / 4);
-    if (backward)
-        hipLaunchKernelGGL(hybrid_gs_kernel<true>, grid, dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(hybrid_gs_kernel<false>, grid, dim3(256), 0, s, a);
+    static const int forced = [] {
+        const char* e = std::getenv("AMG_GS_VARIANT");  // 0 narrow, 1 wide (experiments)
+        return e ? std::atoi(e) : -1;
+    }();
+    const bool wide = forced >= 0 ? forced == 1 : A.gs_wide;
+    if (wide) {
+        const dim3 grid(A.n_gs_slabs);
+        if (backward)
+            hipLaunchKernelGGL((hybrid_gs_kernel<true, true>), grid, dim3(64), 0, s, a);
+        else
+            hipLaunchKernelGGL((hybrid_gs_kernel<false, true>), grid, dim3(64), 0, s, a);
+    } else {
+        const dim3 grid((A.n_gs_slabs + 3) / 4);
+        if (backward)
+            hipLaunchKernelGGL((hybrid_gs_kernel<true, false>), grid, dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((hybrid_gs_kernel<false, false>), grid, dim3(256), 0, s, a);
+    }
     HIP_CHECK(hipGetLastError());
 }
 

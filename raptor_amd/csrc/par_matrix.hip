@@ -253,6 +253,7 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
     n_gs_slabs = (int)slabs.size();
     gs_block = B;
     gs_bytes = 12 * 64 * cells + 16 * (int64_t)slabs.size() + 32 * n_rows;
+    gs_wide = !slabs.empty() && cells >= (int64_t)kGsWide * (int64_t)slabs.size();
 }
 
 bool DevMatrix::halo_begin(const double* x) {
