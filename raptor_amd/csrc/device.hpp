@@ -161,7 +161,7 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
                        int n_blocks, const double* x, const double* b, double* y, double omega,
                        double* partial);
 void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
-                      double* y, bool backward = false);
+                      double* y, bool backward = false, double* partial = nullptr);
 void launch_jacobi_zero(hipStream_t s, int64_t n, const double* b, const double* dinv, double* y,
                         double omega);
 void launch_pack(hipStream_t s, int64_t n, const int* idx, const double* x, double* out);
@@ -186,8 +186,9 @@ void launch_zero(hipStream_t s, int64_t n, double* y);
 // ParCSRMatrix operations with halo exchange + interior/boundary overlap
 void par_apply(DevMatrix& A, int mode, const double* x, const double* b, double* y, double omega,
                double* partial_or_null);
+// partial (forward only): per-slab sums of (b - A x)^2 for a fused residual norm
 void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block,
-                   bool backward = false);
+                   bool backward = false, double* partial = nullptr);
 // Norm plumbing: a mode-NORM level kernel leaves per-block partial sums of (b - Ax)^2 in
 // NormSink::partial; norm_finish() reduces them (fixed order), combines ranks (RCCL
 // allgather, rank order) and appends sqrt to hist[*counter] -- all on the device.
@@ -198,7 +199,8 @@ struct NormSink {
     double* hist = nullptr;
     int* counter = nullptr;
 };
-void norm_finish(DevMatrix& A, const NormSink& ns);
+// reduce `nparts` partials (default: one per CSR-stream block) and append the norm
+void norm_finish(DevMatrix& A, const NormSink& ns, int nparts = -1);
 // r = b - A x and append ||r|| (device-side) through ns
 void par_residual_norm(DevMatrix& A, const double* x, const double* b, double* r,
                        const NormSink& ns);

@@ -247,6 +247,7 @@ struct GsArgs {
     long long B;
     int n;               // local rows (chunks are clipped to the rank)
     int nslab;
+    double* partial;     // NORM: per-slab sum of (b - A x_old)^2
 };
 
 __device__ __forceinline__ double bcast_lane(double v, int lane) {
@@ -260,7 +261,7 @@ __device__ __forceinline__ double bcast_lane(double v, int lane) {
 // slab's chain entries go to LDS as a 64 x 64 column-major block plus a per-lane bit mask in
 // phase 1, so the triangular solve never reloads them; phase 1 keeps 16 loads in flight.
 // Narrow: 4 waves per workgroup (no LDS), 8 loads in flight, register ring of chain entries.
-template <bool BACK, bool WIDE>
+template <bool BACK, bool WIDE, bool NORM>
 __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
     constexpr int U = WIDE ? 16 : 8;
     // wave index made provably uniform: slab fields land in SGPRs, the step loop is scalar
@@ -288,6 +289,7 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
     const int* colp = a.col + base;
     const double* valp = a.val + base;
     __shared__ double chainL[WIDE ? 64 * 64 : 1];
+    double s_old = 0.0;           // NORM: sum_j a_ij x_j (old x), for ||b - A x||
     unsigned long long mask = 0;  // WIDE: bit t = coupling to slab row t
     int kf = -1, kl = -1;         // narrow: first / last chain entry of the row
     // software pipeline: block k0 + U's (col, val) stream in while block k0 gathers x
@@ -310,12 +312,13 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
         if (k0 + U < sl.w) fetch(k0 + U);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const bool old = c[u] >= 0 && !(c[u] >= lo && c[u] < hi);
+            const bool old = c[u] >= 0 && (NORM || !(c[u] >= lo && c[u] < hi));
             xv[u] = old ? (c[u] < a.ncl ? a.x[c[u]] : a.xh[c[u] - a.ncl]) : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (c[u] < 0) continue;  // padding (also every entry of a dead lane)
+            if (NORM) s_old += v[u] * xv[u];  // A x_old in CSR order: the residual's bits
             if (c[u] >= lo && c[u] < hi) {
                 if (WIDE) {
                     const int t = c[u] - sl.x;
@@ -370,6 +373,13 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
         }
     }
     if (live) a.y[r] = xi + acc * dinv;
+    if (NORM) {  // ||b - A x_old||^2 partial of this slab; butterfly order is fixed
+        const double rr = live ? a.b[r] - s_old : 0.0;
+        double q = rr * rr;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m);
+        if (lane == 0) a.partial[wave] = q;
+    }
 }
 
 __global__ void jacobi_zero_kernel(long long n, const double* b, const double* dinv, double* y,
@@ -594,29 +604,29 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
 }
 
 void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
-                      double* y, bool backward) {
+                      double* y, bool backward, double* partial) {
     if (A.n_gs_slabs <= 0) return;
+    AMG_ASSERT(!(backward && partial));
     GsArgs a{A.gs_slabs.p, A.gs_col.p, A.gs_val.p, x, A.halo.p, (int)A.n_cols_local, b,
              A.gs_dinv.p, y, (long long)A.first_row, (long long)A.gs_block, (int)A.n_rows,
-             A.n_gs_slabs};
+             A.n_gs_slabs, partial};
     static const int forced = [] {
         const char* e = std::getenv("AMG_GS_VARIANT");  // 0 narrow, 1 wide (experiments)
         return e ? std::atoi(e) : -1;
     }();
     const bool wide = forced >= 0 ? forced == 1 : A.gs_wide;
+    const dim3 grid(wide ? A.n_gs_slabs : (A.n_gs_slabs + 3) / 4), block(wide ? 64 : 256);
+#define AMG_GS(BK, WD, NM) hipLaunchKernelGGL((hybrid_gs_kernel<BK, WD, NM>), grid, block, 0, s, a)
     if (wide) {
-        const dim3 grid(A.n_gs_slabs);
-        if (backward)
-            hipLaunchKernelGGL((hybrid_gs_kernel<true, true>), grid, dim3(64), 0, s, a);
-        else
-            hipLaunchKernelGGL((hybrid_gs_kernel<false, true>), grid, dim3(64), 0, s, a);
+        if (backward) AMG_GS(true, true, false);
+        else if (partial) AMG_GS(false, true, true);
+        else AMG_GS(false, true, false);
     } else {
-        const dim3 grid((A.n_gs_slabs + 3) / 4);
-        if (backward)
-            hipLaunchKernelGGL((hybrid_gs_kernel<true, false>), grid, dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL((hybrid_gs_kernel<false, false>), grid, dim3(256), 0, s, a);
+        if (backward) AMG_GS(true, false, false);
+        else if (partial) AMG_GS(false, false, true);
+        else AMG_GS(false, false, false);
     }
+#undef AMG_GS
     HIP_CHECK(hipGetLastError());
 }
 

@@ -76,7 +76,10 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         levels[l].r.alloc(n);
         levels[l].t.alloc(n);
         max_blocks = std::max(max_blocks, (size_t)(Al.nb_int + Al.nb_bnd));
-        if (opt.smoother == AMG_SMOOTH_HYBRID_GS) Al.ensure_gs_blocks(opt.gs_block);
+        if (opt.smoother == AMG_SMOOTH_HYBRID_GS) {
+            Al.ensure_gs_blocks(opt.gs_block);
+            max_blocks = std::max(max_blocks, (size_t)Al.n_gs_slabs);
+        }
     }
     // norm plumbing: partials | reduction scratch | gathered rank sums
     const size_t tmpn = max_blocks / 4096 + 64;
@@ -131,7 +134,12 @@ void Solver::ensure_hist(int32_t n) {
 void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_zero,
                     bool with_norm, bool post) {
     DevMatrix& A = Amat(l);
-    if (with_norm) {  // Jacobi sweep that also leaves the partials of ||b - A x||
+    if (with_norm && opt.smoother == AMG_SMOOTH_HYBRID_GS) {
+        // forward GS sweep that also leaves the partials of ||b - A x|| (old x)
+        AMG_ASSERT(!x_zero && !post);
+        par_hybrid_gs(A, x, b, tmp, opt.gs_block, false, sink.partial);
+        norm_finish(A, sink, A.n_gs_slabs);
+    } else if (with_norm) {  // Jacobi sweep that also leaves the partials of ||b - A x||
         AMG_ASSERT(opt.smoother == AMG_SMOOTH_JACOBI && !x_zero);
         par_apply(A, KM_JACOBI, x, b, tmp, opt.jacobi_omega, sink.partial);
         norm_finish(A, sink);
@@ -203,7 +211,8 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
 }
 
 bool Solver::can_fuse_norm() const {
-    return opt.smoother == AMG_SMOOTH_JACOBI && opt.pre_sweeps >= 1 && levels.size() >= 2;
+    return (opt.smoother == AMG_SMOOTH_JACOBI || opt.smoother == AMG_SMOOTH_HYBRID_GS) &&
+           opt.pre_sweeps >= 1 && levels.size() >= 2;
 }
 
 void Solver::cycle(double* x, const double* b, bool with_norm) {

@@ -296,16 +296,16 @@ void par_apply(DevMatrix& A, int mode, const double* x, const double* b, double*
 }
 
 void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block,
-                   bool backward) {
+                   bool backward, double* partial) {
     A.ensure_gs_blocks(block);
     const bool comm = A.halo_begin(x);
     if (comm) A.halo_wait();
-    launch_hybrid_gs(A.ctx->stream, A, x, b, y, backward);
+    launch_hybrid_gs(A.ctx->stream, A, x, b, y, backward, partial);
 }
 
-void norm_finish(DevMatrix& A, const NormSink& ns) {
+void norm_finish(DevMatrix& A, const NormSink& ns, int nparts) {
     Context* c = A.ctx;
-    const int nb = A.nb_int + A.nb_bnd;
+    const int nb = nparts >= 0 ? nparts : A.nb_int + A.nb_bnd;
     const int nr = c->host.nranks;
     double* local = ns.gathered + nr;
     if (nb > 0) launch_reduce_partials(c->stream, nb, ns.partial, ns.tmp, local);
