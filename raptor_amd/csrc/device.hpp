@@ -122,6 +122,13 @@ struct DevMatrix {
     DevBuf<int> tile_ptr, tile_lines;
     DevBuf<uint16_t> lcol;
     int64_t tile_bytes = 0;  // bytes the tiled kernel streams per launch (format, not CSR)
+    // value-indexed blocks (<= 256 distinct values): per-block table offset (-1 = value
+    // stream), the tables, and lane-major 1-byte indices (kCAP per block)
+    DevBuf<int> vt_ptr;
+    DevBuf<double> vtab;
+    DevBuf<uint8_t> vidx;
+    int n_vi_blocks = 0;
+    int64_t vi_nnz = 0;  // nonzeros in value-indexed blocks
     // csr-stream variant bits (kernels.hip): 2 = XCD block order, 4 = gather (no x tile).
     // Set at build: x tile for square operators; gather + XCD order for rectangular ones.
     int default_variant = 0;

@@ -159,6 +159,16 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
 uint64_t mix64(uint64_t z);
 uint32_t hash32(int64_t gid, uint64_t seed);
 
+// Setup phase timing: with AMG_TIMING=1 in the environment, rank 0 prints
+// "[amg] <label> <ms>" to stderr for every phase (host wall clock).
+struct PhaseTimer {
+    static bool enabled();
+    explicit PhaseTimer(const HostComm& comm);
+    void lap(const std::string& label);  // time since construction / the previous lap
+    int rank;
+    double t0;
+};
+
 // ---- inputs beyond the stencils (host_io.cpp, row f2) ----------------------------
 // seeded unstructured graph Laplacian (G3_circuit substitute), even row partition
 HostCSR graph_laplacian_slab(const HostComm& comm, int64_t nx, int64_t ny, uint64_t seed);

@@ -7,6 +7,10 @@
 #include <cstring>
 #include <numeric>
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
 #include "host.hpp"
 
 namespace amg {
@@ -19,6 +23,24 @@ uint64_t mix64(uint64_t z) {
 }
 uint32_t hash32(int64_t gid, uint64_t seed) {
     return (uint32_t)(mix64((uint64_t)gid ^ (seed * 0x9E3779B97F4A7C15ull)) >> 32);
+}
+
+static double wall_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+bool PhaseTimer::enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("AMG_TIMING");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+PhaseTimer::PhaseTimer(const HostComm& comm) : rank(comm.rank), t0(wall_ms()) {}
+void PhaseTimer::lap(const std::string& label) {
+    const double t = wall_ms();
+    if (enabled() && rank == 0) std::fprintf(stderr, "[amg] %-28s %9.1f ms\n", label.c_str(), t - t0);
+    t0 = t;
 }
 
 // ----------------------------------------------------------------------------------

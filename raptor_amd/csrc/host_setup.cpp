@@ -608,24 +608,32 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
     H.levels.clear();
     H.A0 = &A0;
     H.levels.emplace_back();
+    PhaseTimer tm(comm);
     for (int l = 0;; ++l) {
         const HostCSR& A = H.A(l);
+        const std::string L = "L" + std::to_string(l) + " ";
         const int64_t n = A.n_global_rows;
         if (l + 1 >= opt.max_levels || n <= opt.max_coarse) break;
         HostCSR P;
         std::vector<int32_t> split(A.nrows());
         if (opt.coarsen == AMG_COARSEN_SA) {
             HostCSR S = strength_symmetric(comm, A, std::ldexp(opt.strong_threshold, -l));
+            tm.lap(L + "strength");
             int64_t na = 0;
             std::vector<int64_t> astarts;
             std::vector<int64_t> agg = mis2_aggregate(comm, S, opt.seed + (uint64_t)l, &na, &astarts);
             for (size_t i = 0; i < agg.size(); ++i) split[i] = (int32_t)agg[i];
+            tm.lap(L + "aggregate");
             P = sa_prolongator(comm, A, agg, na, astarts);
+            tm.lap(L + "prolongator");
         } else if (opt.coarsen == AMG_COARSEN_RS || opt.coarsen == AMG_COARSEN_PMIS) {
             HostCSR S = strength_classical(comm, A, opt.strong_threshold);
+            tm.lap(L + "strength");
             split = opt.coarsen == AMG_COARSEN_RS ? rs_split(comm, S)
                                                   : pmis_split(comm, S, opt.seed + (uint64_t)l);
+            tm.lap(L + "split");
             P = interp_classical(comm, A, S, split);
+            tm.lap(L + "interpolation");
         } else {
             throw Error(AMG_ERR_INVALID, "unknown coarsening");
         }
@@ -634,8 +642,11 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
         // less than 20% reduction on a level small enough to be the dense-solved coarsest
         if (nc == 0 || nc >= n || (n <= 8192 && 5 * nc > 4 * n)) break;
         HostCSR R = transpose(comm, P);
+        tm.lap(L + "transpose");
         HostCSR AP = mm(A, P);
+        tm.lap(L + "A*P");
         HostCSR Ac = mm(R, AP);
+        tm.lap(L + "R*(AP)");
         H.levels[l].split = std::move(split);
         H.levels[l].P = std::move(P);
         H.levels[l].R = std::move(R);
@@ -646,6 +657,7 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
     AMG_CHECK(Ac.n_global_rows <= 20000,
               "coarsest level too large for the dense solve (raise max_levels / max_coarse?)");
     H.coarse_inv = dense_inverse_gathered(comm, Ac);
+    tm.lap("coarse dense inverse n=" + std::to_string(Ac.n_global_rows));
 }
 
 }  // namespace amg

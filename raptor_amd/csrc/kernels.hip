@@ -38,6 +38,9 @@ struct CsrArgs {
     const uint16_t* lcol;
     int hl0;                 // first halo line id = ceil(ncl / 8)
     int nhalo;
+    const int* vt_ptr;       // value-indexed blocks: table offset, -1 = value stream
+    const double* vtab;
+    const uint8_t* vidx;     // lane-major 1-byte indices (8 per lane per block)
 };
 
 __device__ __forceinline__ double xload(const CsrArgs& a, int c) {
@@ -73,7 +76,12 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 // x tile (the block's distinct 64-byte lines, coalesced: 8 lanes per line) into LDS while the
 // val / 16-bit tile-index streams are in flight; products then read x from LDS.  Same
 // products, same order: bit-identical to the gather path and the oracle.
-template <int MODE, bool NORM, bool XCD, bool TILE>
+//
+// VI (value-indexed CSR): a block whose nonzeros take at most 256 distinct values (by bit
+// pattern) streams a 1-byte index per nonzero (lane-major, one 8-byte load per lane) and
+// reads the values from its small table (L1/L2-resident) instead of streaming 8 bytes per
+// nonzero.  The table holds the exact fp64 bits, so products are unchanged.
+template <int MODE, bool NORM, bool XCD, bool TILE, bool VI>
 __global__ __launch_bounds__(kTPB) void csr_stream_kernel(CsrArgs a, int first_block) {
     // one 16 KiB stage: first the x tile, then (after the products are in registers) the
     // products -- the same LDS footprint as the gather path, so the same occupancy
@@ -107,6 +115,26 @@ __global__ __launch_bounds__(kTPB) void csr_stream_kernel(CsrArgs a, int first_b
     if (nnz <= kCAP && (!TILE || ntl <= kTileLines)) {
         constexpr int U = kCAP / kTPB;  // 8 nonzeros per lane
         double v[U];
+        const int vt = VI ? a.vt_ptr[bid] : -1;  // block-uniform
+        auto load_vals = [&]() {
+            if (VI && vt >= 0) {
+                typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+                const v2u q = __builtin_nontemporal_load(
+                    (const v2u*)(a.vidx + (size_t)bid * kCAP + (size_t)tid * U));
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const unsigned w = u < 4 ? q.x : q.y;
+                    const int k = tid + u * kTPB;
+                    if (k < nnz) v[u] = a.vtab[vt + ((w >> (8 * (u & 3))) & 0xffu)];
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int k = tid + u * kTPB;
+                    if (k < nnz) v[u] = __builtin_nontemporal_load(a.val + k0 + k);
+                }
+            }
+        };
         if (TILE) {
             static_assert(U == 8, "lane-major tile indices assume 8 entries per lane");
             typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -114,11 +142,7 @@ __global__ __launch_bounds__(kTPB) void csr_stream_kernel(CsrArgs a, int first_b
                 (const v4u*)(a.lcol + (size_t)bid * kCAP + (size_t)tid * U));
             const unsigned li[U] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16,
                                     q.z & 0xffffu, q.z >> 16, q.w & 0xffffu, q.w >> 16};
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int k = tid + u * kTPB;
-                if (k < nnz) v[u] = __builtin_nontemporal_load(a.val + k0 + k);
-            }
+            load_vals();
             // x tile: element e of line L is column 8L + e (local) or halo entry 8(L - hl0) + e
             // fixed 8 slots per lane, fully unrolled: all line ids, then all x loads in flight
             constexpr int TU = kTileLines * 8 / kTPB;
@@ -165,11 +189,9 @@ __global__ __launch_bounds__(kTPB) void csr_stream_kernel(CsrArgs a, int first_b
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int k = tid + u * kTPB;
-                if (k < nnz) {
-                    c[u] = __builtin_nontemporal_load(a.col + k0 + k);
-                    v[u] = __builtin_nontemporal_load(a.val + k0 + k);
-                }
+                if (k < nnz) c[u] = __builtin_nontemporal_load(a.col + k0 + k);
             }
+            load_vals();
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int k = tid + u * kTPB;
@@ -568,22 +590,38 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
     if (n_blocks <= 0) return;
     CsrArgs a{A.blocks.p, A.rp.p, A.col.p, A.val.p, x, A.halo.p, (int)A.n_cols_local,
               b, A.dinv.p, y, omega, partial, A.tile_ptr.p, A.tile_lines.p, A.lcol.p,
-              (int)((A.n_cols_local + 7) / 8), (int)A.n_halo()};
+              (int)((A.n_cols_local + 7) / 8), (int)A.n_halo(), A.vt_ptr.p, A.vtab.p, A.vidx.p};
     dim3 g(n_blocks), t(kTPB);
     // variant bits: 2 = XCD-ordered blocks, 4 = gather path (no x tile).  Default: x tile;
     // XCD order for rectangular operators (P, R: +5..17% measured), plain order for square
     // ones (neutral).  (A 16-byte vector-load variant measured 15-20% slower on every level,
     // profiles/r1b_spmv_variants.txt, and was removed.)
-    const char* ev = getenv("AMG_KERNEL_VARIANT");
-    const int var = ev ? atoi(ev) : A.default_variant;
-#define AMG_L1(M, N, X, T) hipLaunchKernelGGL((csr_stream_kernel<M, N, X, T>), g, t, 0, s, a, first_block)
-#define AMG_L(M, N)                                                   \
+    // bit 8 = value-indexed blocks (set at build when any block qualifies; AMG_NO_VI=1
+    // disables it for experiments)
+    static const int forced = [] {
+        const char* e = getenv("AMG_KERNEL_VARIANT");
+        return e ? atoi(e) : -1;
+    }();
+    static const bool no_vi = [] {
+        const char* e = getenv("AMG_NO_VI");
+        return e && *e && *e != '0';
+    }();
+    int var = forced >= 0 ? forced : A.default_variant;
+    if (A.n_vi_blocks > 0 && !no_vi) var |= 8;
+    else var &= ~8;
+#define AMG_L1(M, N, X, T, V) hipLaunchKernelGGL((csr_stream_kernel<M, N, X, T, V>), g, t, 0, s, a, first_block)
+#define AMG_L2(M, N, V)                                               \
     do {                                                              \
         const bool xo = var & 2, tl = !(var & 4);                     \
-        if (xo && tl) AMG_L1(M, N, true, true);                       \
-        else if (xo) AMG_L1(M, N, true, false);                       \
-        else if (tl) AMG_L1(M, N, false, true);                       \
-        else AMG_L1(M, N, false, false);                              \
+        if (xo && tl) AMG_L1(M, N, true, true, V);                    \
+        else if (xo) AMG_L1(M, N, true, false, V);                    \
+        else if (tl) AMG_L1(M, N, false, true, V);                    \
+        else AMG_L1(M, N, false, false, V);                           \
+    } while (0)
+#define AMG_L(M, N)                                                   \
+    do {                                                              \
+        if (var & 8) AMG_L2(M, N, true);                              \
+        else AMG_L2(M, N, false);                                     \
     } while (0)
     switch (mode) {
         case KM_SPMV: AMG_L(KM_SPMV, false); break;
@@ -599,6 +637,7 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
         default: throw Error(AMG_ERR_INTERNAL, "bad kernel mode");
     }
 #undef AMG_L
+#undef AMG_L2
 #undef AMG_L1
     HIP_CHECK(hipGetLastError());
 }

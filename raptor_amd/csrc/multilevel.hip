@@ -27,7 +27,9 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         galerkin = [this, &comm](const HostCSR& X, const HostCSR& Y) {
             return spgemm_device(*ctx, comm, X, Y);
         };
+    PhaseTimer tm(comm);
     build_hierarchy(comm, A.host, opt, H, galerkin);
+    tm.lap("hierarchy (host + SpGEMM)");
     // replicated coarse levels (multi-rank): from the first level with <= replicate_below
     // global rows on, every rank holds the whole operators and cycles them locally
     rep_level = -1;
@@ -49,10 +51,12 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
             return d;
         };
         if (l > 0) levels[l].A = make(hl.A);
+        tm.lap("L" + std::to_string(l) + " device A build");
         if (l + 1 < H.levels.size()) {
             levels[l].split = std::move(hl.split);
             levels[l].P = make(hl.P);
             levels[l].R = make(hl.R);
+            tm.lap("L" + std::to_string(l) + " device P/R build");
         }
     }
     if (rep_level > 0) {  // transition: distributed R output -> whole vector on every rank
@@ -78,6 +82,7 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         max_blocks = std::max(max_blocks, (size_t)(Al.nb_int + Al.nb_bnd));
         if (opt.smoother == AMG_SMOOTH_HYBRID_GS) {
             Al.ensure_gs_blocks(opt.gs_block);
+            tm.lap("L" + std::to_string(l) + " GS sliced-ELL build");
             max_blocks = std::max(max_blocks, (size_t)Al.n_gs_slabs);
         }
     }
@@ -110,6 +115,7 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
             for (int64_t i = 0; i < nl; ++i) invT[jp * nl + i] = inv[(f + i) * coarse_n + j];
         }
     this->invT.upload(invT.data(), invT.size());
+    tm.lap("coarse inverse upload");
     coarse_counts.assign(1, (int)cmax);
     if (!serial_coarse) {
         bfull.alloc((size_t)npad + (size_t)cmax);  // gathered + local padded send slot

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstring>
 
 #include "device.hpp"
 
@@ -112,6 +113,61 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
     return out;
 }
 
+// Value-indexed CSR (Kourtis et al., CF'08): blocks whose nonzeros take <= 256 distinct
+// values (exact bit patterns) get a table of those values and a 1-byte index per nonzero,
+// lane-major like the tile indices (entry j of the block -> lane j % kTPB, slot j / kTPB).
+static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const BlockBuild& bb) {
+    const size_t nbk = bb.blocks.size();
+    std::vector<std::vector<uint64_t>> tabs(nbk);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (size_t q = 0; q < nbk; ++q) {
+        const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
+        if (nz > kCAP || nz == 0) continue;
+        std::vector<uint64_t> t(nz);
+        std::memcpy(t.data(), M.host.val.data() + kb, sizeof(double) * (size_t)nz);
+        std::sort(t.begin(), t.end());
+        t.erase(std::unique(t.begin(), t.end()), t.end());
+        if (t.size() <= 256) tabs[q] = std::move(t);
+    }
+    std::vector<int> ptr(std::max<size_t>(nbk, 1), -1);
+    int64_t total = 0, vin = 0;
+    int nvi = 0;
+    for (size_t q = 0; q < nbk; ++q)
+        if (!tabs[q].empty()) {
+            ptr[q] = (int)total;
+            total += (int64_t)tabs[q].size();
+            vin += hrp[bb.blocks[q].y] - hrp[bb.blocks[q].x];
+            ++nvi;
+        }
+    M.n_vi_blocks = nvi;
+    M.vi_nnz = vin;
+    if (nvi == 0) {
+        M.vt_ptr.reset();
+        M.vtab.reset();
+        M.vidx.reset();
+        return;
+    }
+    AMG_CHECK(total < INT_MAX, "value tables too large");
+    std::vector<double> tab((size_t)total);
+    std::vector<uint8_t> idx(nbk * (size_t)kCAP, 0);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (size_t q = 0; q < nbk; ++q) {
+        if (tabs[q].empty()) continue;
+        const std::vector<uint64_t>& t = tabs[q];
+        std::memcpy(tab.data() + ptr[q], t.data(), sizeof(double) * t.size());
+        const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
+        for (int j = 0; j < nz; ++j) {
+            uint64_t bits;
+            std::memcpy(&bits, M.host.val.data() + kb + j, sizeof(bits));
+            const size_t at = std::lower_bound(t.begin(), t.end(), bits) - t.begin();
+            idx[q * kCAP + (size_t)(j % kTPB) * (kCAP / kTPB) + j / kTPB] = (uint8_t)at;
+        }
+    }
+    M.vt_ptr.upload(ptr.data(), ptr.size());
+    M.vtab.upload(tab.data(), tab.size());
+    M.vidx.upload(idx.data(), idx.size());
+}
+
 void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
     ctx = c;
     host = std::move(h);
@@ -181,6 +237,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 perm[q * kCAP + (size_t)(j % kTPB) * (kCAP / kTPB) + j / kTPB] = bb.lcol[kb + j];
         }
         lcol.upload(perm.data(), perm.size());
+        build_value_index(*this, hrp, bb);
         tile_bytes = 8 * nnz + 2 * kCAP * (int64_t)nbk + 4 * (n_rows + 1) +
                      8 * (int64_t)nbk + 4 * (int64_t)bb.tile_lines.size();
         // measured (profiles/r1c_spmv_variants_tiled.txt, r1d): x tiles win on every square
