@@ -596,19 +596,11 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
     // XCD order for rectangular operators (P, R: +5..17% measured), plain order for square
     // ones (neutral).  (A 16-byte vector-load variant measured 15-20% slower on every level,
     // profiles/r1b_spmv_variants.txt, and was removed.)
-    // bit 8 = value-indexed blocks (set at build when any block qualifies; AMG_NO_VI=1
-    // disables it for experiments)
-    static const int forced = [] {
-        const char* e = getenv("AMG_KERNEL_VARIANT");
-        return e ? atoi(e) : -1;
-    }();
-    static const bool no_vi = [] {
-        const char* e = getenv("AMG_NO_VI");
-        return e && *e && *e != '0';
-    }();
-    int var = forced >= 0 ? forced : A.default_variant;
-    if (A.n_vi_blocks > 0 && !no_vi) var |= 8;
-    else var &= ~8;
+    // bit 8 = value-indexed blocks (default on when any block qualifies).  The environment
+    // override (experiments, scripts/spmv_variants.py) gives all bits explicitly.
+    const char* ev = getenv("AMG_KERNEL_VARIANT");
+    int var = ev ? atoi(ev) : (A.default_variant | (A.n_vi_blocks > 0 ? 8 : 0));
+    if (A.n_vi_blocks == 0) var &= ~8;
 #define AMG_L1(M, N, X, T, V) hipLaunchKernelGGL((csr_stream_kernel<M, N, X, T, V>), g, t, 0, s, a, first_block)
 #define AMG_L2(M, N, V)                                               \
     do {                                                              \
