@@ -10,8 +10,10 @@ problem.  Timed: K steps of amg_solver_solve (no host sync inside), barrier + de
 both sides, max over ranks.  value = V-cycles/s x (global rows / 256^3): 256^3-equivalent
 V-cycles per second, the whole-job aggregate (equals plain iterations/s at N=1).
 
-roofline: the level-0 ParCSRMatrix::mult kernel (csr_stream<SPMV>), timed live with HIP
-events on the context stream; algorithmic bytes = 12 nnz + 4 (n+1) + 16 n.
+roofline: the level-0 ParCSRMatrix::mult kernel (csr_block_kernel<SPMV>), timed live with HIP
+events on the context stream; bytes = the stored format's HBM bytes per launch (DESIGN.md 4;
+value-indexed blocks stream 1-byte indices instead of fp64 values), with the plain-CSR
+equivalent 12 nnz + 4 (n+1) + 16 n reported beside it.
 cpu_baseline (rank 0, N=1): the oracle's V-cycle (C, OpenMP) on the same hierarchy and
 inputs, timed for --cpu-seconds; "port" = this repo's CPU restatement (the reference
 has no AMG code).
@@ -163,8 +165,12 @@ def main():
     else:
         cyc_bytes = float(cyc_bytes_local)
 
-    # roofline: level-0 SpMV, HIP events on the context stream
-    spmv_bytes = 12 * A.nnz + 4 * (n + 1) + 16 * n
+    # roofline: level-0 SpMV, HIP events on the context stream.  Numerator = the bytes the
+    # kernel must move in the stored format (A.info["spmv_bytes"]: block headers, x-tile ids,
+    # 16-bit tile indices, 1-byte value indices + tables or fp64 values, row_ptr, x, y); the
+    # plain-CSR figure 12 nnz + 4 (n+1) + 16 n is reported beside it (csr_equiv_*)
+    csr_bytes = 12 * A.nnz + 4 * (n + 1) + 16 * n
+    spmv_bytes = int(A.info["spmv_bytes"])
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     for _ in range(5):
@@ -178,6 +184,7 @@ def main():
     e1.synchronize()
     spmv_ms = e0.elapsed_time(e1) / args.spmv_reps
     achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
+    csr_equiv = csr_bytes / (spmv_ms * 1e-3) / 1e9
     barrier()
 
     traffic = None
@@ -242,7 +249,7 @@ def main():
             "vcycle_effective_GBps": round(cyc_bytes * iters_per_s / 1e9, 1),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "csr_stream_kernel<SPMV> (level-0 ParCSRMatrix::mult, rank 0)",
+                "kernel": "csr_block_kernel<SPMV> (level-0 ParCSRMatrix::mult, rank 0)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -250,7 +257,11 @@ def main():
                 "traffic": None if traffic is None else round(traffic, 1),
                 "traffic_source": traffic_src,
                 "bytes_per_launch": spmv_bytes,
+                "bytes_definition": "stored-format HBM bytes per launch (DESIGN.md 4)",
                 "avg_launch_ms": round(spmv_ms, 5),
+                "vi_blocks_frac": round(A.info["n_vi_blocks"] / max(1, A.info["n_blocks"]), 4),
+                "csr_equiv_bytes_per_launch": csr_bytes,
+                "csr_equiv_GBps": round(csr_equiv, 1),
             },
             "cpu_baseline": cpu,
         }

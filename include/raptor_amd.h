@@ -113,6 +113,9 @@ typedef struct amg_matrix_info {
     int64_t n_send;        /* entries sent per mult                                      */
     int32_t n_neighbors;   /* ranks exchanged with                                       */
     int32_t n_blocks;      /* CSR-stream row blocks                                      */
+    int32_t n_vi_blocks;   /* row blocks stored value-indexed (<= 256 distinct values)   */
+    int64_t spmv_bytes;    /* HBM bytes one mult() moves in the stored format: headers,  *
+                            * index/value streams, row_ptr, x (once), y                  */
 } amg_matrix_info;
 int amg_par_csr_info(amg_matrix A, amg_matrix_info* info);
 /* Host copy of the local rows (global column ids). */

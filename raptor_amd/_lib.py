@@ -56,6 +56,8 @@ class MatrixInfo(C.Structure):
         ("n_send", C.c_int64),
         ("n_neighbors", C.c_int32),
         ("n_blocks", C.c_int32),
+        ("n_vi_blocks", C.c_int32),
+        ("spmv_bytes", C.c_int64),
     ]
 
 

@@ -277,6 +277,8 @@ int amg_par_csr_info(amg_matrix A, amg_matrix_info* info) {
         info->n_send = (int64_t)m.plan.send_idx.size();
         info->n_neighbors = (int32_t)std::max(m.plan.send_procs.size(), m.plan.recv_procs.size());
         info->n_blocks = m.nb_int + m.nb_bnd;
+        info->n_vi_blocks = m.n_vi_blocks;
+        info->spmv_bytes = m.spmv_fmt_bytes;
     });
 }
 

@@ -28,11 +28,9 @@ namespace amg {
 // kernel geometry shared by host-side block building and the kernels
 constexpr int kTPB = 256;   // threads per workgroup (4 waves of 64)
 constexpr int kCAP = 2048;  // nonzeros staged in LDS per workgroup (16 KiB of products)
-constexpr int kPad = 4;     // col/val padding (entries) for the 16-byte vector-load tail
+constexpr int kPad = kCAP;  // col/val padding (entries): unconditional loads past a block's end
 constexpr int kTileLines = 256;  // x tile per workgroup: 256 lines x 64 B = 16 KiB of LDS
 constexpr int kGsWide = 128;     // sliced-ELL width from which hybrid GS uses the wide variant
-constexpr int kDefaultVariant = 0;  // csr-stream variant (kernels.hip kernel_variant())
-int kernel_variant();
 
 template <class T>
 struct DevBuf {
@@ -117,14 +115,20 @@ struct DevMatrix {
     // touch halo columns.  Each block is {row begin, row end}.
     DevBuf<int2> blocks;
     int nb_int = 0, nb_bnd = 0;
-    // x tiles: per block the sorted distinct 64-byte lines of x it reads (tile_ptr[nb+1],
-    // tile_lines) and per nonzero a 16-bit index into that tile (lcol)
-    DevBuf<int> tile_ptr, tile_lines;
+    // per block 2 x int4 = {r0, r1, k0, nnz}, {diag slot, tile lines, value-table offset
+    // (-1: value stream), value-table size}: everything a block needs before its bulk loads
+    DevBuf<int4> hdr;
+    // x tiles: per block the sorted distinct 64-byte lines of x it reads (tile_fixed:
+    // kTileLines ids per block, padded with the last) and per nonzero a 16-bit index into
+    // that tile (lcol, lane-major)
+    DevBuf<int> tile_fixed;
     DevBuf<uint16_t> lcol;
-    int64_t tile_bytes = 0;  // bytes the tiled kernel streams per launch (format, not CSR)
-    // value-indexed blocks (<= 256 distinct values): per-block table offset (-1 = value
-    // stream), the tables, and lane-major 1-byte indices (kCAP per block)
-    DevBuf<int> vt_ptr;
+    // HBM bytes of one SpMV launch in the stored format with the default kernel variant
+    // (headers, tile ids, 16-bit tile indices, VI indices + tables or values, columns for the
+    // gather path, row_ptr, x once, y): the roofline numerator, DESIGN.md section 4
+    int64_t spmv_fmt_bytes = 0;
+    // value-indexed blocks (<= 256 distinct values): the tables (offsets in hdr) and
+    // lane-major 1-byte indices (kCAP per block)
     DevBuf<double> vtab;
     DevBuf<uint8_t> vidx;
     int n_vi_blocks = 0;

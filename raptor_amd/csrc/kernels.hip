@@ -21,26 +21,26 @@ namespace amg {
 namespace {
 
 struct CsrArgs {
-    const int2* blocks;
+    const int4* hdr;         // 2 x int4 per block (par_matrix.hip): {r0, r1, k0, nnz},
+                             // {diag slot, tile lines, value-table offset (-1), table size}
+    const int* tile_ids;     // kTileLines x-tile line ids per block (padded with the last)
+    const uint16_t* lcol;    // lane-major 16-bit tile indices (kCAP per block)
+    const uint8_t* vidx;     // lane-major 1-byte value indices (kCAP per block)
+    const double* vtab;      // value tables
     const int* rp;
     const int* col;
     const double* val;
     const double* x;   // local part of x
     const double* xh;  // halo part of x
     int ncl;           // number of local columns
+    int nhalo;
+    int hl0;           // first halo line id = ceil(ncl / 8)
+    int wide_x;        // ncl >= 2 and nhalo != 1: 16-byte x-tile loads are in bounds
     const double* b;
     const double* dinv;
     double* y;
     double omega;
     double* partial;
-    const int* tile_ptr;     // x tiles (par_matrix.hip build_row_blocks)
-    const int* tile_lines;
-    const uint16_t* lcol;
-    int hl0;                 // first halo line id = ceil(ncl / 8)
-    int nhalo;
-    const int* vt_ptr;       // value-indexed blocks: table offset, -1 = value stream
-    const double* vtab;
-    const uint8_t* vidx;     // lane-major 1-byte indices (8 per lane per block)
 };
 
 __device__ __forceinline__ double xload(const CsrArgs& a, int c) {
@@ -68,167 +68,199 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
     return x * q + min(x, rem) + (b >> 3);
 }
 
-// Blocks hold <= kTPB rows, so lane t owns at most row r0 + t.  Its row bounds and
-// epilogue operands are loaded at entry, in flight together with the phase-1 stream, so
-// the epilogue costs no extra memory round trip after the barrier.
+typedef unsigned int v2u_t __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+typedef double v2d_t __attribute__((ext_vector_type(2)));
+
+// Entries [q, q+1] of a vector of n >= 2 doubles: a 16-byte load at min(q, n - 2); when q is
+// the last entry its value is the second half.  Entries past n are garbage (never used).
+__device__ __forceinline__ v2d_t load_pair(const double* base, int q, int n) {
+    const int st = min(q, n - 2);
+    const v2d_t v = *(const v2d_t*)(base + st);
+    return v2d_t{q == st ? v.x : v.y, v.y};
+}
+
+// One workgroup per row block (<= kCAP nonzeros, <= kTPB rows).  Bit-identical to the oracle:
+// products a_ij * x_j are formed in registers, staged in LDS, and lane r sums its row's
+// products in CSR order before the fused epilogue.
 //
-// TILE: instead of gathering x from global memory per nonzero, the workgroup first loads its
-// x tile (the block's distinct 64-byte lines, coalesced: 8 lanes per line) into LDS while the
-// val / 16-bit tile-index streams are in flight; products then read x from LDS.  Same
-// products, same order: bit-identical to the gather path and the oracle.
+// The kernel is built for memory-level parallelism.  Every load is unconditional and issued
+// in dependency batches with no divergent branch between them (out-of-range lanes re-read
+// the block's last entry -- the same address, merged by the TA -- and results are masked only
+// at the LDS / y stores); an earlier form guarded each load with its own bounds test, the
+// compiler wrapped each in a branch and drained vmcnt at every join, and the kernel was
+// latency-bound (profiles/r1h_variants.txt: 278 -> 184 us on the 256^3 level-0 SpMV).
+//   batch 1 (block id only): header (scalar), one x-tile line id per lane (fixed stride),
+//            16-bit tile indices, VI indices
+//   batch 2: x tile (16-byte loads, 4 per lane; line ids via ds_bpermute), values or VI
+//            table, row bounds and epilogue operands  [gather: columns, then x]
+// PMC (SQ_WAIT_INST_ANY ~42% of wave cycles) showed the VMEM issue queue, not HBM, as the
+// limit, so the per-wave vector-memory instruction count is kept low (10 for SpMV).
 //
-// VI (value-indexed CSR): a block whose nonzeros take at most 256 distinct values (by bit
-// pattern) streams a 1-byte index per nonzero (lane-major, one 8-byte load per lane) and
-// reads the values from its small table (L1/L2-resident) instead of streaming 8 bytes per
-// nonzero.  The table holds the exact fp64 bits, so products are unchanged.
-template <int MODE, bool NORM, bool XCD, bool TILE, bool VI>
-__global__ __launch_bounds__(kTPB) void csr_stream_kernel(CsrArgs a, int first_block) {
-    // one 16 KiB stage: first the x tile, then (after the products are in registers) the
-    // products -- the same LDS footprint as the gather path, so the same occupancy
-    static_assert(kTileLines * 8 <= kCAP, "x tile must fit the product stage");
-    __shared__ double prod[kCAP];
-    double* const xt = prod;
-    __shared__ double red[kTPB / 64];
-    const int bid = first_block + (XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x);
-    const int2 br = a.blocks[bid];
-    const int r0 = br.x, r1 = br.y;
-    const int tid = threadIdx.x;
+// TILE: the block's distinct 64-byte lines of x go to LDS; products read x from LDS through a
+// 16-bit index per nonzero.  Jacobi reads x[r] from the tile too when the block's own lines
+// are consecutive in it (header diag slot).  VIB: the block's nonzeros take <= 256 distinct
+// values; a 1-byte index per nonzero selects from the table staged in LDS.  NU: lane slots
+// in use (8 = full; the gather path of sparse rectangular blocks uses fewer).
+template <int MODE, bool NORM, bool TILE, bool VIB, int NU>
+__device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* stage, double* tabl) {
+    constexpr int U = kCAP / kTPB;  // 8 lane slots
+    static_assert(NU >= 1 && NU <= U && (TILE ? NU == U : true), "tile blocks use every slot");
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int tid_line = 0;
+    if (TILE) {
+        // lane l of wave w fetches line 16w + (l & 15) + 64 (l >> 4): the 64 lines wave w's
+        // 16-byte tile slots need (slot j of lane l: line 16w + (l >> 2) + 64j)
+        tid_line = a.tile_ids[(size_t)bid * kTileLines + 16 * wv + (lane & 15) + 64 * (lane >> 4)];
+    }
+    v4u_t lq = {0u, 0u, 0u, 0u};
+    if (TILE) lq = __builtin_nontemporal_load((const v4u_t*)(a.lcol + (size_t)bid * kCAP + (size_t)tid * U));
+    v2u_t vq = {0u, 0u};
+    if (VIB) vq = __builtin_nontemporal_load((const v2u_t*)(a.vidx + (size_t)bid * kCAP + (size_t)tid * U));
+    const int4 h0 = a.hdr[2 * bid], h1 = a.hdr[2 * bid + 1];
+    const int r0 = h0.x, r1 = h0.y, k0 = h0.z, nnz = h0.w;
     const int r = r0 + tid;
     const bool own = r < r1;
-    const int k0 = a.rp[r0];
-    const int nnz = a.rp[r1] - k0;
-    int e0 = 0, e1 = 0;
-    double pb = 0.0, pd = 0.0, px = 0.0;
-    if (own) {
-        e0 = a.rp[r] - k0;
-        e1 = a.rp[r + 1] - k0;
-        if (MODE == KM_SPMV_ADD) px = a.y[r];
-        if (MODE == KM_RESID || MODE == KM_JACOBI) pb = a.b[r];
-        if (MODE == KM_JACOBI) {
-            pd = a.dinv[r];
-            px = a.x[r];
-        }
+    int c[U];
+    if (!TILE) {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) c[u] = __builtin_nontemporal_load(a.col + k0 + min(tid + u * kTPB, nnz - 1));
     }
-    double sq = 0.0;
-    const int t0 = TILE ? a.tile_ptr[bid] : 0;
-    const int ntl = TILE ? a.tile_ptr[bid + 1] - t0 : 0;
-    if (nnz <= kCAP && (!TILE || ntl <= kTileLines)) {
-        constexpr int U = kCAP / kTPB;  // 8 nonzeros per lane
-        double v[U];
-        const int vt = VI ? a.vt_ptr[bid] : -1;  // block-uniform
-        auto load_vals = [&]() {
-            if (VI && vt >= 0) {
-                typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-                const v2u q = __builtin_nontemporal_load(
-                    (const v2u*)(a.vidx + (size_t)bid * kCAP + (size_t)tid * U));
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const unsigned w = u < 4 ? q.x : q.y;
-                    const int k = tid + u * kTPB;
-                    if (k < nnz) v[u] = a.vtab[vt + ((w >> (8 * (u & 3))) & 0xffu)];
-                }
-            } else {
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int k = tid + u * kTPB;
-                    if (k < nnz) v[u] = __builtin_nontemporal_load(a.val + k0 + k);
-                }
-            }
-        };
-        if (TILE) {
-            static_assert(U == 8, "lane-major tile indices assume 8 entries per lane");
-            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-            const v4u q = __builtin_nontemporal_load(
-                (const v4u*)(a.lcol + (size_t)bid * kCAP + (size_t)tid * U));
-            const unsigned li[U] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16,
-                                    q.z & 0xffffu, q.z >> 16, q.w & 0xffffu, q.w >> 16};
-            load_vals();
-            // x tile: element e of line L is column 8L + e (local) or halo entry 8(L - hl0) + e
-            // fixed 8 slots per lane, fully unrolled: all line ids, then all x loads in flight
-            constexpr int TU = kTileLines * 8 / kTPB;
-            const int nt = ntl * 8;
-            int Ls[TU];
-#pragma unroll
-            for (int j = 0; j < TU; ++j) {
-                const int idx = tid + j * kTPB;
-                Ls[j] = idx < nt ? a.tile_lines[t0 + (idx >> 3)] : 0;
-            }
-            double xs[TU];
-#pragma unroll
-            for (int j = 0; j < TU; ++j) {
-                const int idx = tid + j * kTPB, e = idx & 7, L = Ls[j];
-                const double* p = nullptr;
-                if (idx < nt) {
-                    if (L < a.hl0) {
-                        const int c = L * 8 + e;
-                        if (c < a.ncl) p = a.x + c;
-                    } else {
-                        const int h = (L - a.hl0) * 8 + e;
-                        if (h < a.nhalo) p = a.xh + h;
-                    }
-                }
-                xs[j] = p ? *p : 0.0;
-            }
-#pragma unroll
-            for (int j = 0; j < TU; ++j) {
-                const int idx = tid + j * kTPB;
-                if (idx < nt) xt[idx] = xs[j];
-            }
-            __syncthreads();
-            double pr[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) pr[u] = v[u] * xt[li[u]];
-            __syncthreads();  // every lane has read the tile; reuse it for the products
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int k = tid + u * kTPB;
-                if (k < nnz) prod[k] = pr[u];
-            }
-        } else {
-            int c[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int k = tid + u * kTPB;
-                if (k < nnz) c[u] = __builtin_nontemporal_load(a.col + k0 + k);
-            }
-            load_vals();
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int k = tid + u * kTPB;
-                if (k < nnz) prod[k] = v[u] * xload(a, c[u]);
-            }
-        }
-        __syncthreads();
-        if (own) {
-            double s = 0.0;
-            for (int k = e0; k < e1; ++k) s += prod[k];
-            double out;
-            if (MODE == KM_SPMV) {
-                out = s;
-            } else if (MODE == KM_SPMV_ADD) {
-                out = px + s;
-            } else {
-                const double t = pb - s;
-                if (NORM) sq = t * t;
-                out = MODE == KM_RESID ? t : px + a.omega * (pd * t);
-            }
-            a.y[r] = out;
-        }
+    double v[U], tv = 0.0;
+    if (VIB) {
+        tv = a.vtab[h1.z + min(tid, h1.w - 1)];
     } else {
-        // one row longer than the LDS stage: chunked, summed by lane 0 in CSR order
+#pragma unroll
+        for (int u = 0; u < NU; ++u)
+            v[u] = __builtin_nontemporal_load(a.val + k0 + min(tid + u * kTPB, nnz - 1));
+    }
+    // row operands (lanes past the block re-read row r0)
+    const int rr = own ? r : r0;
+    const int e0 = a.rp[rr] - k0, e1 = a.rp[rr + 1] - k0;
+    const bool px_tile = TILE && MODE == KM_JACOBI && h1.x >= 0;  // block-uniform
+    double pb = 0.0, pd = 0.0, px = 0.0;
+    if (MODE == KM_SPMV_ADD) px = a.y[rr];
+    if (MODE == KM_RESID || MODE == KM_JACOBI) pb = a.b[rr];
+    if (MODE == KM_JACOBI) {
+        pd = a.dinv[rr];
+        if (!px_tile) px = a.x[rr];
+    }
+    // the scheduling barrier keeps every earlier load issued before the first x load waits
+    // for its line / column id
+    __builtin_amdgcn_sched_barrier(0);
+    double xs[U];
+    if (TILE) {
+        // slot pair j of lane l: line 16w + (l >> 2) + 64j, elements e, e + 1 with e = 2 (l & 3);
+        // element e of line L is column 8L + e (local) or halo entry 8(L - hl0) + e
+        const int e = 2 * (lane & 3);
+        if (a.wide_x) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int L = __shfl(tid_line, (lane >> 2) + 16 * j, 64);
+                const v2d_t p2 = L < a.hl0 ? load_pair(a.x, L * 8 + e, a.ncl)
+                                           : load_pair(a.xh, (L - a.hl0) * 8 + e, a.nhalo);
+                xs[2 * j] = p2.x;
+                xs[2 * j + 1] = p2.y;
+            }
+        } else {  // a vector of one entry: 8-byte loads (degenerate coarse partitions)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int L = __shfl(tid_line, (lane >> 2) + 16 * j, 64);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const double* p = L < a.hl0 ? a.x + min(L * 8 + e + h, a.ncl - 1)
+                                                : a.xh + min((L - a.hl0) * 8 + e + h, a.nhalo - 1);
+                    xs[2 * j + h] = *p;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *(v2d_t*)(stage + 2 * tid + 512 * j) = v2d_t{xs[2 * j], xs[2 * j + 1]};
+    } else {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) xs[u] = xload(a, c[u]);
+    }
+    if (VIB) tabl[tid] = tv;
+    if (TILE || VIB) __syncthreads();
+    if (px_tile) px = stage[(h1.x + (rr >> 3) - (r0 >> 3)) * 8 + (rr & 7)];
+    if (VIB) {
+        const unsigned w[2] = {vq.x, vq.y};
+#pragma unroll
+        for (int u = 0; u < NU; ++u) v[u] = tabl[(w[u >> 2] >> (8 * (u & 3))) & 0xffu];
+    }
+    double pr[U];
+    if (TILE) {
+        const unsigned li[U] = {lq.x & 0xffffu, lq.x >> 16, lq.y & 0xffffu, lq.y >> 16,
+                                lq.z & 0xffffu, lq.z >> 16, lq.w & 0xffffu, lq.w >> 16};
+#pragma unroll
+        for (int u = 0; u < U; ++u) pr[u] = v[u] * stage[li[u]];
+        __syncthreads();  // every lane has read the tile; reuse it for the products
+    } else {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) pr[u] = v[u] * xs[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) stage[tid + u * kTPB] = pr[u];
+    __syncthreads();
+    double s = 0.0;
+    for (int k = e0; k < e1; ++k) s += stage[k];
+    double out, sq = 0.0;
+    if (MODE == KM_SPMV) {
+        out = s;
+    } else if (MODE == KM_SPMV_ADD) {
+        out = px + s;
+    } else {
+        const double t = pb - s;
+        if (NORM) sq = own ? t * t : 0.0;
+        out = MODE == KM_RESID ? t : px + a.omega * (pd * t);
+    }
+    if (own) a.y[r] = out;
+    return sq;
+}
+
+template <int MODE, bool NORM, bool TILE, bool VIB>
+__device__ __forceinline__ double block_dispatch(const CsrArgs& a, int bid, int nnz, double* stage,
+                                                 double* tabl) {
+    if constexpr (TILE) {
+        return block_main<MODE, NORM, TILE, VIB, 8>(a, bid, stage, tabl);
+    } else {
+        if (nnz > 4 * kTPB) return block_main<MODE, NORM, TILE, VIB, 8>(a, bid, stage, tabl);
+        if (nnz > 2 * kTPB) return block_main<MODE, NORM, TILE, VIB, 4>(a, bid, stage, tabl);
+        return block_main<MODE, NORM, TILE, VIB, 2>(a, bid, stage, tabl);
+    }
+}
+
+template <int MODE, bool NORM, bool XCD, bool TILE, bool VI>
+__global__ __launch_bounds__(kTPB) void csr_block_kernel(CsrArgs a, int first_block) {
+    static_assert(kCAP / kTPB == 8 && kTileLines * 8 == kCAP && kTPB == 256,
+                  "lane-major layouts assume 8 entries per lane, 4 waves");
+    __shared__ __attribute__((aligned(16))) double stage[kCAP];  // x tile, then products
+    __shared__ double tabl[VI ? 256 : 1];
+    __shared__ double red[kTPB / 64];
+    const int tid = threadIdx.x;
+    const int bid = first_block + (XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x);
+    const int4 h0 = a.hdr[2 * bid], h1 = a.hdr[2 * bid + 1];
+    const int r0 = h0.x, r1 = h0.y, k0 = h0.z, nnz = h0.w;
+    double sq = 0.0;
+    if (nnz <= kCAP && (!TILE || h1.y <= kTileLines) && nnz > 0) {
+        if (VI && h1.z >= 0) sq = block_dispatch<MODE, NORM, TILE, true>(a, bid, nnz, stage, tabl);
+        else sq = block_dispatch<MODE, NORM, TILE, false>(a, bid, nnz, stage, tabl);
+    } else {
+        // empty block, or one row longer than the LDS stage / a tile: chunked, lane 0 sums
         double s = 0.0;
         for (int base = 0; base < nnz; base += kCAP) {
             const int cnt = min(kCAP, nnz - base);
             for (int k = tid; k < cnt; k += kTPB)
-                prod[k] = a.val[k0 + base + k] * xload(a, a.col[k0 + base + k]);
+                stage[k] = a.val[k0 + base + k] * xload(a, a.col[k0 + base + k]);
             __syncthreads();
             if (tid == 0)
-                for (int k = 0; k < cnt; ++k) s += prod[k];
+                for (int k = 0; k < cnt; ++k) s += stage[k];
             __syncthreads();
         }
-        if (tid == 0) {
+        const int r = r0 + tid;
+        if (r < r1 && (tid == 0 || nnz == 0)) {  // nnz == 0: every row of the block is empty
             double res = 0.0;
-            a.y[r0] = epilogue<MODE>(a, r0, s, &res);
+            a.y[r] = epilogue<MODE>(a, r, s, &res);
             if (NORM) sq = res * res;
         }
     }
@@ -577,31 +609,24 @@ void launch_append(hipStream_t s, const double* v, double* hist, int* counter) {
     HIP_CHECK(hipGetLastError());
 }
 
-// CSR-stream variant: bit 0 = 16-byte vector loads, bit 1 = XCD-aware block order.
-// AMG_KERNEL_VARIANT overrides the default (A/B timing; results are identical).
-int kernel_variant() {
-    const char* e = getenv("AMG_KERNEL_VARIANT");
-    return e ? (atoi(e) & 3) : kDefaultVariant;
-}
-
 void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, int first_block,
                        int n_blocks, const double* x, const double* b, double* y, double omega,
                        double* partial) {
     if (n_blocks <= 0) return;
-    CsrArgs a{A.blocks.p, A.rp.p, A.col.p, A.val.p, x, A.halo.p, (int)A.n_cols_local,
-              b, A.dinv.p, y, omega, partial, A.tile_ptr.p, A.tile_lines.p, A.lcol.p,
-              (int)((A.n_cols_local + 7) / 8), (int)A.n_halo(), A.vt_ptr.p, A.vtab.p, A.vidx.p};
+    const int ncl = (int)A.n_cols_local, nh = (int)A.n_halo();
+    CsrArgs a{A.hdr.p, A.tile_fixed.p, A.lcol.p, A.vidx.p, A.vtab.p, A.rp.p, A.col.p, A.val.p,
+              x, A.halo.p, ncl, nh, (ncl + 7) / 8, (ncl >= 2 && nh != 1) ? 1 : 0,
+              b, A.dinv.p, y, omega, partial};
     dim3 g(n_blocks), t(kTPB);
-    // variant bits: 2 = XCD-ordered blocks, 4 = gather path (no x tile).  Default: x tile;
-    // XCD order for rectangular operators (P, R: +5..17% measured), plain order for square
-    // ones (neutral).  (A 16-byte vector-load variant measured 15-20% slower on every level,
-    // profiles/r1b_spmv_variants.txt, and was removed.)
-    // bit 8 = value-indexed blocks (default on when any block qualifies).  The environment
-    // override (experiments, scripts/spmv_variants.py) gives all bits explicitly.
+    // variant bits: 2 = XCD-ordered blocks, 4 = gather path (no x tile), 8 = value-indexed
+    // blocks (when any block qualifies).  Default: x tile for square operators, gather in
+    // XCD order for rectangular ones (profiles/r1h_variants.txt: P0 -33%, R0 -9% vs tiles;
+    // XCD order +5..17% on P/R, neutral on square operators).  AMG_KERNEL_VARIANT overrides
+    // all bits (experiments, scripts/spmv_variants.py; results are identical).
     const char* ev = getenv("AMG_KERNEL_VARIANT");
     int var = ev ? atoi(ev) : (A.default_variant | (A.n_vi_blocks > 0 ? 8 : 0));
     if (A.n_vi_blocks == 0) var &= ~8;
-#define AMG_L1(M, N, X, T, V) hipLaunchKernelGGL((csr_stream_kernel<M, N, X, T, V>), g, t, 0, s, a, first_block)
+#define AMG_L1(M, N, X, T, V) hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V>), g, t, 0, s, a, first_block)
 #define AMG_L2(M, N, V)                                               \
     do {                                                              \
         const bool xo = var & 2, tl = !(var & 4);                     \

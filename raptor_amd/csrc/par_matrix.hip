@@ -116,7 +116,9 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
 // Value-indexed CSR (Kourtis et al., CF'08): blocks whose nonzeros take <= 256 distinct
 // values (exact bit patterns) get a table of those values and a 1-byte index per nonzero,
 // lane-major like the tile indices (entry j of the block -> lane j % kTPB, slot j / kTPB).
-static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const BlockBuild& bb) {
+// Returns per-block table offset (-1: value stream) and table size for the block headers.
+static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const BlockBuild& bb,
+                              std::vector<int>& vt_off, std::vector<int>& vt_len) {
     const size_t nbk = bb.blocks.size();
     std::vector<std::vector<uint64_t>> tabs(nbk);
 #pragma omp parallel for schedule(dynamic, 64)
@@ -141,8 +143,11 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
         }
     M.n_vi_blocks = nvi;
     M.vi_nnz = vin;
+    vt_off.assign(nbk, -1);
+    vt_len.assign(nbk, 0);
+    for (size_t q = 0; q < nbk; ++q)
+        if (!tabs[q].empty()) vt_off[q] = ptr[q], vt_len[q] = (int)tabs[q].size();
     if (nvi == 0) {
-        M.vt_ptr.reset();
         M.vtab.reset();
         M.vidx.reset();
         return;
@@ -163,7 +168,6 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
             idx[q * kCAP + (size_t)(j % kTPB) * (kCAP / kTPB) + j / kTPB] = (uint8_t)at;
         }
     }
-    M.vt_ptr.upload(ptr.data(), ptr.size());
     M.vtab.upload(tab.data(), tab.size());
     M.vidx.upload(idx.data(), idx.size());
 }
@@ -223,12 +227,21 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         nb_int = bb.nb_int;
         nb_bnd = bb.nb_bnd;
         blocks.upload(bb.blocks.data(), bb.blocks.size());
-        tile_ptr.upload(bb.tile_ptr.data(), bb.tile_ptr.size());
-        if (bb.tile_lines.empty()) bb.tile_lines.push_back(0);
-        tile_lines.upload(bb.tile_lines.data(), bb.tile_lines.size());
+        const size_t nbk = bb.blocks.size();
+        {
+            // x-tile line ids at a fixed stride (kTileLines per block, padded with the block's
+            // last line), so the kernel loads them without waiting for the block header
+            std::vector<int> fx(std::max<size_t>(nbk, 1) * kTileLines, 0);
+            for (size_t q = 0; q < nbk; ++q) {
+                const int t0 = bb.tile_ptr[q], nt = bb.tile_ptr[q + 1] - t0;
+                if (nt <= 0 || nt > kTileLines) continue;
+                for (int j = 0; j < kTileLines; ++j)
+                    fx[q * kTileLines + j] = bb.tile_lines[t0 + std::min(j, nt - 1)];
+            }
+            tile_fixed.upload(fx.data(), fx.size());
+        }
         // lane-major per block: lane t's indices for entries t + 256u (u = 0..7) are 16
         // contiguous bytes, so the kernel reads them with one 16-byte load per lane
-        const size_t nbk = bb.blocks.size();
         std::vector<uint16_t> perm(std::max<size_t>(nbk, 1) * kCAP, 0);
         for (size_t q = 0; q < nbk; ++q) {
             const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
@@ -237,13 +250,50 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 perm[q * kCAP + (size_t)(j % kTPB) * (kCAP / kTPB) + j / kTPB] = bb.lcol[kb + j];
         }
         lcol.upload(perm.data(), perm.size());
-        build_value_index(*this, hrp, bb);
-        tile_bytes = 8 * nnz + 2 * kCAP * (int64_t)nbk + 4 * (n_rows + 1) +
-                     8 * (int64_t)nbk + 4 * (int64_t)bb.tile_lines.size();
+        std::vector<int> vt_off, vt_len;
+        build_value_index(*this, hrp, bb, vt_off, vt_len);
+        // 32-byte block headers (two scalar loads per block):
+        //   {r0, r1, k0, nnz}, {diag slot, tile lines, value-table offset (-1), table size}
+        // diag slot (square operators): tile position of line r0 / 8 when the lines of the
+        // block's own rows are consecutive in its tile, so x[r] is read from the tile; else -1
+        std::vector<int4> hh(std::max<size_t>(2 * nbk, 2), make_int4(0, 0, 0, 0));
+        for (size_t q = 0; q < nbk; ++q) {
+            const int2 b = bb.blocks[q];
+            const int t0 = bb.tile_ptr[q], nt = bb.tile_ptr[q + 1] - t0;
+            int dslot = -1;
+            if (square && nt > 0 && nt <= kTileLines) {
+                const int l0 = b.x >> 3, l1 = (b.y - 1) >> 3;
+                const int* tl = bb.tile_lines.data() + t0;
+                const int pos = (int)(std::lower_bound(tl, tl + nt, l0) - tl);
+                bool ok = pos + (l1 - l0) < nt;
+                for (int k = 0; ok && k <= l1 - l0; ++k) ok = tl[pos + k] == l0 + k;
+                if (ok) dslot = pos;
+            }
+            hh[2 * q] = make_int4(b.x, b.y, hrp[b.x], hrp[b.y] - hrp[b.x]);
+            hh[2 * q + 1] = make_int4(dslot, nt, vt_off[q], vt_len[q]);
+        }
+        hdr.upload(hh.data(), hh.size());
         // measured (profiles/r1c_spmv_variants_tiled.txt, r1d): x tiles win on every square
         // level operator (A0 -17%, A1/A2 -40%); the rectangular transfer operators are faster
         // with gathers in XCD order (P0: ~2 nnz/row, R0: lines spread over +-nx*ny)
         default_variant = square ? 0 : (4 | 2);
+        // format bytes of one default-variant SpMV (the kernel reads every lane slot of the
+        // fixed-stride streams, so their padding counts)
+        int64_t fb = 4 * (n_rows + 1) + 8 * (n_cols_local + plan.n_halo()) + 8 * n_rows;
+        for (size_t q = 0; q < nbk; ++q) {
+            const int nz = hh[2 * q].w, nt = hh[2 * q + 1].y;
+            fb += 32;
+            if (nz == 0) continue;
+            if (nz > kCAP || (square && nt > kTileLines)) {  // long row: CSR stream
+                fb += 12 * (int64_t)nz;
+                continue;
+            }
+            if (square) fb += 4 * kTileLines + 2 * kCAP;    // tile ids, tile indices
+            else fb += 4 * (int64_t)nz;                     // columns
+            if (hh[2 * q + 1].z >= 0) fb += kCAP + 8 * (int64_t)hh[2 * q + 1].w;
+            else fb += 8 * (int64_t)nz;
+        }
+        spmv_fmt_bytes = fb;
     }
     std::vector<int> sidx(plan.send_idx.begin(), plan.send_idx.end());
     send_idx.upload(sidx.data(), sidx.size());

@@ -24,7 +24,7 @@ def main(prefix, out):
     f, meta = per_dispatch(f"{prefix}_FETCH_SIZE/run_counter_collection.csv")
     w, _ = per_dispatch(f"{prefix}_WRITE_SIZE/run_counter_collection.csv")
     # level-0 operator = first matrix in pmc_levels.py: its first 3 csr_stream launches are SpMV
-    ds = [d for d in sorted(meta) if "csr_stream_kernel<0" in meta[d][0]][:3]
+    ds = [d for d in sorted(meta) if "csr_block_kernel<0" in meta[d][0]][:3]
     fetch = sum(f[d]["FETCH_SIZE"] for d in ds) / len(ds) * 1024
     write = sum(w[d]["WRITE_SIZE"] for d in ds) / len(ds) * 1024
     res = {"kernel": meta[ds[0]][0].split("(amg::")[0], "grid": meta[ds[0]][1], "launches": len(ds),
