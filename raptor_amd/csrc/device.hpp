@@ -122,6 +122,10 @@ struct DevMatrix {
     // kTileLines ids per block, padded with the last) and per nonzero a 16-bit index into
     // that tile (lcol, lane-major)
     DevBuf<int> tile_fixed;
+    // per row: end of its nonzeros relative to its block's first (16 bits; the kernel's row
+    // bounds) and, for value-indexed square operators, the table index of its diagonal
+    DevBuf<uint16_t> rend;
+    DevBuf<uint8_t> dvi;
     DevBuf<uint16_t> lcol;
     // HBM bytes of one SpMV launch in the stored format with the default kernel variant
     // (headers, tile ids, 16-bit tile indices, VI indices + tables or values, columns for the

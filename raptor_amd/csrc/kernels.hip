@@ -27,6 +27,8 @@ struct CsrArgs {
     const uint16_t* lcol;    // lane-major 16-bit tile indices (kCAP per block)
     const uint8_t* vidx;     // lane-major 1-byte value indices (kCAP per block)
     const double* vtab;      // value tables
+    const uint16_t* rend;    // per row: end of its nonzeros relative to the block's first
+    const uint8_t* dvi;      // per row of a VI square operator: table index of a_ii
     const int* rp;
     const int* col;
     const double* val;
@@ -103,7 +105,8 @@ __device__ __forceinline__ v2d_t load_pair(const double* base, int q, int n) {
 // values; a 1-byte index per nonzero selects from the table staged in LDS.  NU: lane slots
 // in use (8 = full; the gather path of sparse rectangular blocks uses fewer).
 template <int MODE, bool NORM, bool TILE, bool VIB, int NU>
-__device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* stage, double* tabl) {
+__device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* stage, double* tabl,
+                                             int* rends) {
     constexpr int U = kCAP / kTPB;  // 8 lane slots
     static_assert(NU >= 1 && NU <= U && (TILE ? NU == U : true), "tile blocks use every slot");
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -134,15 +137,20 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
         for (int u = 0; u < NU; ++u)
             v[u] = __builtin_nontemporal_load(a.val + k0 + min(tid + u * kTPB, nnz - 1));
     }
-    // row operands (lanes past the block re-read row r0)
+    // row operands (lanes past the block re-read row r0); row start = previous lane's end,
+    // exchanged through LDS behind the first barrier
     const int rr = own ? r : r0;
-    const int e0 = a.rp[rr] - k0, e1 = a.rp[rr + 1] - k0;
-    const bool px_tile = TILE && MODE == KM_JACOBI && h1.x >= 0;  // block-uniform
+    const int e1 = a.rend[rr];
+    rends[tid] = e1;
+    const bool px_tile = TILE && MODE == KM_JACOBI && h1.x >= 0;       // block-uniform
+    const bool pd_tab = VIB && MODE == KM_JACOBI && (h1.y >> 16) != 0;  // block-uniform
     double pb = 0.0, pd = 0.0, px = 0.0;
+    int dv = 0;
     if (MODE == KM_SPMV_ADD) px = a.y[rr];
     if (MODE == KM_RESID || MODE == KM_JACOBI) pb = a.b[rr];
     if (MODE == KM_JACOBI) {
-        pd = a.dinv[rr];
+        if (pd_tab) dv = a.dvi[rr];
+        else pd = a.dinv[rr];
         if (!px_tile) px = a.x[rr];
     }
     // the scheduling barrier keeps every earlier load issued before the first x load waits
@@ -183,6 +191,8 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     if (VIB) tabl[tid] = tv;
     if (TILE || VIB) __syncthreads();
     if (px_tile) px = stage[(h1.x + (rr >> 3) - (r0 >> 3)) * 8 + (rr & 7)];
+    // 1 / a_ii from the table: the same correctly rounded division the host does for dinv
+    if (pd_tab) pd = 1.0 / tabl[dv];
     if (VIB) {
         const unsigned w[2] = {vq.x, vq.y};
 #pragma unroll
@@ -202,6 +212,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
 #pragma unroll
     for (int u = 0; u < NU; ++u) stage[tid + u * kTPB] = pr[u];
     __syncthreads();
+    const int e0 = tid ? rends[tid - 1] : 0;
     double s = 0.0;
     for (int k = e0; k < e1; ++k) s += stage[k];
     double out, sq = 0.0;
@@ -220,31 +231,32 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
 
 template <int MODE, bool NORM, bool TILE, bool VIB>
 __device__ __forceinline__ double block_dispatch(const CsrArgs& a, int bid, int nnz, double* stage,
-                                                 double* tabl) {
+                                                 double* tabl, int* rends) {
     if constexpr (TILE) {
-        return block_main<MODE, NORM, TILE, VIB, 8>(a, bid, stage, tabl);
+        return block_main<MODE, NORM, TILE, VIB, 8>(a, bid, stage, tabl, rends);
     } else {
-        if (nnz > 4 * kTPB) return block_main<MODE, NORM, TILE, VIB, 8>(a, bid, stage, tabl);
-        if (nnz > 2 * kTPB) return block_main<MODE, NORM, TILE, VIB, 4>(a, bid, stage, tabl);
-        return block_main<MODE, NORM, TILE, VIB, 2>(a, bid, stage, tabl);
+        if (nnz > 4 * kTPB) return block_main<MODE, NORM, TILE, VIB, 8>(a, bid, stage, tabl, rends);
+        if (nnz > 2 * kTPB) return block_main<MODE, NORM, TILE, VIB, 4>(a, bid, stage, tabl, rends);
+        return block_main<MODE, NORM, TILE, VIB, 2>(a, bid, stage, tabl, rends);
     }
 }
 
 template <int MODE, bool NORM, bool XCD, bool TILE, bool VI>
-__global__ __launch_bounds__(kTPB) void csr_block_kernel(CsrArgs a, int first_block) {
+__global__ __launch_bounds__(kTPB, 8) void csr_block_kernel(CsrArgs a, int first_block) {
     static_assert(kCAP / kTPB == 8 && kTileLines * 8 == kCAP && kTPB == 256,
                   "lane-major layouts assume 8 entries per lane, 4 waves");
     __shared__ __attribute__((aligned(16))) double stage[kCAP];  // x tile, then products
     __shared__ double tabl[VI ? 256 : 1];
+    __shared__ int rends[kTPB];
     __shared__ double red[kTPB / 64];
     const int tid = threadIdx.x;
     const int bid = first_block + (XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x);
     const int4 h0 = a.hdr[2 * bid], h1 = a.hdr[2 * bid + 1];
     const int r0 = h0.x, r1 = h0.y, k0 = h0.z, nnz = h0.w;
     double sq = 0.0;
-    if (nnz <= kCAP && (!TILE || h1.y <= kTileLines) && nnz > 0) {
-        if (VI && h1.z >= 0) sq = block_dispatch<MODE, NORM, TILE, true>(a, bid, nnz, stage, tabl);
-        else sq = block_dispatch<MODE, NORM, TILE, false>(a, bid, nnz, stage, tabl);
+    if (nnz <= kCAP && (!TILE || (h1.y & 0xffff) <= kTileLines) && nnz > 0) {
+        if (VI && h1.z >= 0) sq = block_dispatch<MODE, NORM, TILE, true>(a, bid, nnz, stage, tabl, rends);
+        else sq = block_dispatch<MODE, NORM, TILE, false>(a, bid, nnz, stage, tabl, rends);
     } else {
         // empty block, or one row longer than the LDS stage / a tile: chunked, lane 0 sums
         double s = 0.0;
@@ -492,7 +504,16 @@ __global__ void dense_gemv_kernel(long long nl, long long n, const double* invT,
     long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nl) return;
     double s = 0.0;
-    for (long long j = 0; j < n; ++j) s += invT[j * nl + i] * bfull[j];
+    long long j = 0;
+    // 8 products' loads in flight per step; the sum stays sequential in j
+    for (; j + 8 <= n; j += 8) {
+        double p[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) p[u] = invT[(j + u) * nl + i] * bfull[j + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += p[u];
+    }
+    for (; j < n; ++j) s += invT[j * nl + i] * bfull[j];
     x[i] = s;
 }
 
@@ -614,7 +635,8 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
                        double* partial) {
     if (n_blocks <= 0) return;
     const int ncl = (int)A.n_cols_local, nh = (int)A.n_halo();
-    CsrArgs a{A.hdr.p, A.tile_fixed.p, A.lcol.p, A.vidx.p, A.vtab.p, A.rp.p, A.col.p, A.val.p,
+    CsrArgs a{A.hdr.p, A.tile_fixed.p, A.lcol.p, A.vidx.p, A.vtab.p, A.rend.p, A.dvi.p,
+              A.rp.p, A.col.p, A.val.p,
               x, A.halo.p, ncl, nh, (ncl + 7) / 8, (ncl >= 2 && nh != 1) ? 1 : 0,
               b, A.dinv.p, y, omega, partial};
     dim3 g(n_blocks), t(kTPB);

@@ -117,8 +117,12 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
 // values (exact bit patterns) get a table of those values and a 1-byte index per nonzero,
 // lane-major like the tile indices (entry j of the block -> lane j % kTPB, slot j / kTPB).
 // Returns per-block table offset (-1: value stream) and table size for the block headers.
+// For square operators also the table index of each row's diagonal (dvi, 1 byte per row) and
+// per block whether every row has one (then Jacobi forms 1 / a_ii from the table in-kernel
+// instead of streaming dinv: 1 byte per row instead of 8).
 static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const BlockBuild& bb,
-                              std::vector<int>& vt_off, std::vector<int>& vt_len) {
+                              std::vector<int>& vt_off, std::vector<int>& vt_len,
+                              std::vector<uint8_t>& dvi, std::vector<char>& dvi_ok) {
     const size_t nbk = bb.blocks.size();
     std::vector<std::vector<uint64_t>> tabs(nbk);
 #pragma omp parallel for schedule(dynamic, 64)
@@ -145,6 +149,8 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
     M.vi_nnz = vin;
     vt_off.assign(nbk, -1);
     vt_len.assign(nbk, 0);
+    dvi.assign(M.square ? (size_t)M.n_rows + 1 : 0, 0);
+    dvi_ok.assign(nbk, 0);
     for (size_t q = 0; q < nbk; ++q)
         if (!tabs[q].empty()) vt_off[q] = ptr[q], vt_len[q] = (int)tabs[q].size();
     if (nvi == 0) {
@@ -167,6 +173,21 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
             const size_t at = std::lower_bound(t.begin(), t.end(), bits) - t.begin();
             idx[q * kCAP + (size_t)(j % kTPB) * (kCAP / kTPB) + j / kTPB] = (uint8_t)at;
         }
+        if (!M.square) continue;
+        bool ok = true;
+        for (int r = bb.blocks[q].x; r < bb.blocks[q].y; ++r) {
+            int64_t k = M.host.rp[r], e = M.host.rp[r + 1];
+            const int64_t g = M.first_row + r;
+            while (k < e && M.host.col[k] < g) ++k;
+            if (k == e || M.host.col[k] != g || M.host.val[k] == 0.0) {
+                ok = false;
+                continue;
+            }
+            uint64_t bits;
+            std::memcpy(&bits, M.host.val.data() + k, sizeof(bits));
+            dvi[r] = (uint8_t)(std::lower_bound(t.begin(), t.end(), bits) - t.begin());
+        }
+        dvi_ok[q] = ok;
     }
     M.vtab.upload(tab.data(), tab.size());
     M.vidx.upload(idx.data(), idx.size());
@@ -251,9 +272,24 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         }
         lcol.upload(perm.data(), perm.size());
         std::vector<int> vt_off, vt_len;
-        build_value_index(*this, hrp, bb, vt_off, vt_len);
+        std::vector<uint8_t> hdvi;
+        std::vector<char> dvi_ok;
+        build_value_index(*this, hrp, bb, vt_off, vt_len, hdvi, dvi_ok);
+        if (n_vi_blocks > 0 && square) dvi.upload(hdvi.data(), hdvi.size());
+        else dvi.reset();
+        {
+            // per row: end of its nonzeros relative to its block's first (<= kCAP: 16 bits)
+            std::vector<uint16_t> re((size_t)n_rows + 1, 0);
+            for (size_t q = 0; q < nbk; ++q) {
+                const int2 b = bb.blocks[q];
+                if (hrp[b.y] - hrp[b.x] > kCAP) continue;
+                for (int r = b.x; r < b.y; ++r) re[r] = (uint16_t)(hrp[r + 1] - hrp[b.x]);
+            }
+            rend.upload(re.data(), re.size());
+        }
         // 32-byte block headers (two scalar loads per block):
-        //   {r0, r1, k0, nnz}, {diag slot, tile lines, value-table offset (-1), table size}
+        //   {r0, r1, k0, nnz}, {diag slot, tile lines | dvi flag << 16, value-table offset (-1),
+        //   table size}
         // diag slot (square operators): tile position of line r0 / 8 when the lines of the
         // block's own rows are consecutive in its tile, so x[r] is read from the tile; else -1
         std::vector<int4> hh(std::max<size_t>(2 * nbk, 2), make_int4(0, 0, 0, 0));
@@ -270,7 +306,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 if (ok) dslot = pos;
             }
             hh[2 * q] = make_int4(b.x, b.y, hrp[b.x], hrp[b.y] - hrp[b.x]);
-            hh[2 * q + 1] = make_int4(dslot, nt, vt_off[q], vt_len[q]);
+            hh[2 * q + 1] = make_int4(dslot, nt | (dvi_ok[q] ? 1 << 16 : 0), vt_off[q], vt_len[q]);
         }
         hdr.upload(hh.data(), hh.size());
         // measured (profiles/r1c_spmv_variants_tiled.txt, r1d): x tiles win on every square
@@ -279,9 +315,9 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         default_variant = square ? 0 : (4 | 2);
         // format bytes of one default-variant SpMV (the kernel reads every lane slot of the
         // fixed-stride streams, so their padding counts)
-        int64_t fb = 4 * (n_rows + 1) + 8 * (n_cols_local + plan.n_halo()) + 8 * n_rows;
+        int64_t fb = 2 * n_rows + 8 * (n_cols_local + plan.n_halo()) + 8 * n_rows;
         for (size_t q = 0; q < nbk; ++q) {
-            const int nz = hh[2 * q].w, nt = hh[2 * q + 1].y;
+            const int nz = hh[2 * q].w, nt = hh[2 * q + 1].y & 0xffff;
             fb += 32;
             if (nz == 0) continue;
             if (nz > kCAP || (square && nt > kTileLines)) {  // long row: CSR stream
