@@ -38,6 +38,7 @@ struct CsrArgs {
     int nhalo;
     int hl0;           // first halo line id = ceil(ncl / 8)
     int wide_x;        // ncl >= 2 and nhalo != 1: 16-byte x-tile loads are in bounds
+    int vi_packed;     // rectangular operator: VI indices packed NU per lane at header field 0
     const double* b;
     const double* dinv;
     double* y;
@@ -119,8 +120,17 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     v4u_t lq = {0u, 0u, 0u, 0u};
     if (TILE) lq = __builtin_nontemporal_load((const v4u_t*)(a.lcol + (size_t)bid * kCAP + (size_t)tid * U));
     v2u_t vq = {0u, 0u};
-    if (VIB) vq = __builtin_nontemporal_load((const v2u_t*)(a.vidx + (size_t)bid * kCAP + (size_t)tid * U));
     const int4 h0 = a.hdr[2 * bid], h1 = a.hdr[2 * bid + 1];
+    if (VIB) {
+        if (!a.vi_packed) {
+            vq = __builtin_nontemporal_load((const v2u_t*)(a.vidx + (size_t)bid * kCAP + (size_t)tid * U));
+        } else {  // gather blocks: NU bytes per lane at the block's offset
+            const uint8_t* p = a.vidx + (size_t)(unsigned)h1.x + (size_t)tid * NU;
+            if (NU == 8) vq = __builtin_nontemporal_load((const v2u_t*)p);
+            else if (NU == 4) vq.x = __builtin_nontemporal_load((const unsigned*)p);
+            else vq.x = __builtin_nontemporal_load((const unsigned short*)p);
+        }
+    }
     const int r0 = h0.x, r1 = h0.y, k0 = h0.z, nnz = h0.w;
     const int r = r0 + tid;
     const bool own = r < r1;
@@ -637,17 +647,18 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
     const int ncl = (int)A.n_cols_local, nh = (int)A.n_halo();
     CsrArgs a{A.hdr.p, A.tile_fixed.p, A.lcol.p, A.vidx.p, A.vtab.p, A.rend.p, A.dvi.p,
               A.rp.p, A.col.p, A.val.p,
-              x, A.halo.p, ncl, nh, (ncl + 7) / 8, (ncl >= 2 && nh != 1) ? 1 : 0,
+              x, A.halo.p, ncl, nh, (ncl + 7) / 8, (ncl >= 2 && nh != 1) ? 1 : 0, A.square ? 0 : 1,
               b, A.dinv.p, y, omega, partial};
     dim3 g(n_blocks), t(kTPB);
     // variant bits: 2 = XCD-ordered blocks, 4 = gather path (no x tile), 8 = value-indexed
-    // blocks (when any block qualifies).  Default: x tile for square operators, gather in
-    // XCD order for rectangular ones (profiles/r1h_variants.txt: P0 -33%, R0 -9% vs tiles;
-    // XCD order +5..17% on P/R, neutral on square operators).  AMG_KERNEL_VARIANT overrides
-    // all bits (experiments, scripts/spmv_variants.py; results are identical).
+    // blocks (when any block qualifies).  Default (DevMatrix::default_variant): x tile for
+    // square operators, gather for rectangular ones (stored without tiles), both in XCD
+    // order (profiles/r1m_variants.txt).  AMG_KERNEL_VARIANT overrides the bits (experiments,
+    // scripts/spmv_variants.py; results are identical).
     const char* ev = getenv("AMG_KERNEL_VARIANT");
     int var = ev ? atoi(ev) : (A.default_variant | (A.n_vi_blocks > 0 ? 8 : 0));
     if (A.n_vi_blocks == 0) var &= ~8;
+    if (!A.square) var |= 4;  // rectangular operators are stored for the gather kernel only
 #define AMG_L1(M, N, X, T, V) hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V>), g, t, 0, s, a, first_block)
 #define AMG_L2(M, N, V)                                               \
     do {                                                              \

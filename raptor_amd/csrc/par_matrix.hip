@@ -120,9 +120,16 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
 // For square operators also the table index of each row's diagonal (dvi, 1 byte per row) and
 // per block whether every row has one (then Jacobi forms 1 / a_ii from the table in-kernel
 // instead of streaming dinv: 1 byte per row instead of 8).
+// Index layout: lane-major, entry j of a block -> lane j % kTPB, slot j / kTPB.  Square
+// operators (x-tile kernel, 8 slots): kCAP bytes per block at bid * kCAP.  Rectangular ones
+// (gather kernel): NU = 2, 4 or 8 slots by block size (the kernel's choice), packed, block
+// offset in vofs (header field 0, unused by the gather kernel otherwise).
+static int gather_slots(int nz) { return nz > 4 * kTPB ? 8 : nz > 2 * kTPB ? 4 : 2; }
+
 static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const BlockBuild& bb,
                               std::vector<int>& vt_off, std::vector<int>& vt_len,
-                              std::vector<uint8_t>& dvi, std::vector<char>& dvi_ok) {
+                              std::vector<uint8_t>& dvi, std::vector<char>& dvi_ok,
+                              std::vector<int64_t>& vofs) {
     const size_t nbk = bb.blocks.size();
     std::vector<std::vector<uint64_t>> tabs(nbk);
 #pragma omp parallel for schedule(dynamic, 64)
@@ -160,7 +167,13 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
     }
     AMG_CHECK(total < INT_MAX, "value tables too large");
     std::vector<double> tab((size_t)total);
-    std::vector<uint8_t> idx(nbk * (size_t)kCAP, 0);
+    vofs.assign(nbk + 1, 0);
+    for (size_t q = 0; q < nbk; ++q) {
+        const int nz = hrp[bb.blocks[q].y] - hrp[bb.blocks[q].x];
+        vofs[q + 1] = vofs[q] + (M.square ? kCAP : tabs[q].empty() ? 0 : gather_slots(nz) * kTPB);
+    }
+    AMG_CHECK(vofs[nbk] < INT_MAX, "value index stream too large");
+    std::vector<uint8_t> idx((size_t)vofs[nbk] + 16, 0);
 #pragma omp parallel for schedule(dynamic, 64)
     for (size_t q = 0; q < nbk; ++q) {
         if (tabs[q].empty()) continue;
@@ -171,7 +184,8 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
             uint64_t bits;
             std::memcpy(&bits, M.host.val.data() + kb + j, sizeof(bits));
             const size_t at = std::lower_bound(t.begin(), t.end(), bits) - t.begin();
-            idx[q * kCAP + (size_t)(j % kTPB) * (kCAP / kTPB) + j / kTPB] = (uint8_t)at;
+            const int nu = M.square ? kCAP / kTPB : gather_slots(nz);
+            idx[(size_t)vofs[q] + (size_t)(j % kTPB) * nu + j / kTPB] = (uint8_t)at;
         }
         if (!M.square) continue;
         bool ok = true;
@@ -249,7 +263,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         nb_bnd = bb.nb_bnd;
         blocks.upload(bb.blocks.data(), bb.blocks.size());
         const size_t nbk = bb.blocks.size();
-        {
+        if (square) {  // x tiles: the square-operator kernel only
             // x-tile line ids at a fixed stride (kTileLines per block, padded with the block's
             // last line), so the kernel loads them without waiting for the block header
             std::vector<int> fx(std::max<size_t>(nbk, 1) * kTileLines, 0);
@@ -260,21 +274,25 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                     fx[q * kTileLines + j] = bb.tile_lines[t0 + std::min(j, nt - 1)];
             }
             tile_fixed.upload(fx.data(), fx.size());
+            // lane-major per block: lane t's indices for entries t + 256u (u = 0..7) are 16
+            // contiguous bytes, so the kernel reads them with one 16-byte load per lane
+            std::vector<uint16_t> perm(std::max<size_t>(nbk, 1) * kCAP, 0);
+            for (size_t q = 0; q < nbk; ++q) {
+                const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
+                if (nz > kCAP) continue;
+                for (int j = 0; j < nz; ++j)
+                    perm[q * kCAP + (size_t)(j % kTPB) * (kCAP / kTPB) + j / kTPB] = bb.lcol[kb + j];
+            }
+            lcol.upload(perm.data(), perm.size());
+        } else {
+            tile_fixed.reset();
+            lcol.reset();
         }
-        // lane-major per block: lane t's indices for entries t + 256u (u = 0..7) are 16
-        // contiguous bytes, so the kernel reads them with one 16-byte load per lane
-        std::vector<uint16_t> perm(std::max<size_t>(nbk, 1) * kCAP, 0);
-        for (size_t q = 0; q < nbk; ++q) {
-            const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
-            if (nz > kCAP) continue;
-            for (int j = 0; j < nz; ++j)
-                perm[q * kCAP + (size_t)(j % kTPB) * (kCAP / kTPB) + j / kTPB] = bb.lcol[kb + j];
-        }
-        lcol.upload(perm.data(), perm.size());
         std::vector<int> vt_off, vt_len;
         std::vector<uint8_t> hdvi;
         std::vector<char> dvi_ok;
-        build_value_index(*this, hrp, bb, vt_off, vt_len, hdvi, dvi_ok);
+        std::vector<int64_t> vofs;
+        build_value_index(*this, hrp, bb, vt_off, vt_len, hdvi, dvi_ok, vofs);
         if (n_vi_blocks > 0 && square) dvi.upload(hdvi.data(), hdvi.size());
         else dvi.reset();
         {
@@ -306,13 +324,15 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 if (ok) dslot = pos;
             }
             hh[2 * q] = make_int4(b.x, b.y, hrp[b.x], hrp[b.y] - hrp[b.x]);
-            hh[2 * q + 1] = make_int4(dslot, nt | (dvi_ok[q] ? 1 << 16 : 0), vt_off[q], vt_len[q]);
+            // rectangular (gather) operators: field 0 = the block's offset in the VI index stream
+            const int f0 = square ? dslot : (vofs.empty() ? 0 : (int)vofs[q]);
+            hh[2 * q + 1] = make_int4(f0, nt | (dvi_ok[q] ? 1 << 16 : 0), vt_off[q], vt_len[q]);
         }
         hdr.upload(hh.data(), hh.size());
-        // measured (profiles/r1c_spmv_variants_tiled.txt, r1d): x tiles win on every square
-        // level operator (A0 -17%, A1/A2 -40%); the rectangular transfer operators are faster
-        // with gathers in XCD order (P0: ~2 nnz/row, R0: lines spread over +-nx*ny)
-        default_variant = square ? 0 : (4 | 2);
+        // measured (profiles/r1m_variants.txt): x tiles in XCD order on square operators (A0
+        // -6..8%, A1 -6..8%, A2 +1% vs plain order; gathers are 1.3-1.9x slower); gathers in
+        // XCD order on the rectangular P / R (R0 -10% vs plain order)
+        default_variant = square ? 2 : (4 | 2);
         // format bytes of one default-variant SpMV (the kernel reads every lane slot of the
         // fixed-stride streams, so their padding counts)
         int64_t fb = 2 * n_rows + 8 * (n_cols_local + plan.n_halo()) + 8 * n_rows;
@@ -326,8 +346,10 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             }
             if (square) fb += 4 * kTileLines + 2 * kCAP;    // tile ids, tile indices
             else fb += 4 * (int64_t)nz;                     // columns
-            if (hh[2 * q + 1].z >= 0) fb += kCAP + 8 * (int64_t)hh[2 * q + 1].w;
-            else fb += 8 * (int64_t)nz;
+            if (hh[2 * q + 1].z >= 0)
+                fb += (square ? kCAP : gather_slots(nz) * kTPB) + 8 * (int64_t)hh[2 * q + 1].w;
+            else
+                fb += 8 * (int64_t)nz;
         }
         spmv_fmt_bytes = fb;
     }
