@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-lib_path = os.path.join(_HERE, "libraptor_amd.so")
+lib_path = os.environ.get("RAPTOR_AMD_LIB") or os.path.join(_HERE, "libraptor_amd.so")  # override: A/B builds
 
 AMG_OK = 0
 AMG_STENCIL_5PT, AMG_STENCIL_7PT, AMG_STENCIL_27PT = 0, 1, 2

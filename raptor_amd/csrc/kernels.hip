@@ -74,6 +74,8 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 typedef unsigned int v2u_t __attribute__((ext_vector_type(2)));
 typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
 typedef double v2d_t __attribute__((ext_vector_type(2)));
+typedef int v2i_t __attribute__((ext_vector_type(2)));
+
 
 // Entries [q, q+1] of a vector of n >= 2 doubles: a 16-byte load at min(q, n - 2); when q is
 // the last entry its value is the second half.  Entries past n are garbage (never used).
@@ -109,7 +111,7 @@ template <int MODE, bool NORM, bool TILE, bool VIB, int NU>
 __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* stage, double* tabl,
                                              int* rends) {
     constexpr int U = kCAP / kTPB;  // 8 lane slots
-    static_assert(NU >= 1 && NU <= U && (TILE ? NU == U : true), "tile blocks use every slot");
+    static_assert(NU >= 2 && NU % 2 == 0 && NU <= U && (TILE ? NU == U : true), "slot pairs");
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int tid_line = 0;
     if (TILE) {
@@ -134,14 +136,28 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     const int r0 = h0.x, r1 = h0.y, k0 = h0.z, nnz = h0.w;
     const int r = r0 + tid;
     const bool own = r < r1;
+    // Entry-to-lane map.  TILE: lane t holds entries 512 p + 2 t + {0, 1} (p < 4) of the
+    // block-aligned val stream (k0 even): 16-byte value loads (profiles/r1o_libab.txt: A2
+    // SpMV / Jacobi -8% / -9%).  Gather: lane t holds entries t + 256 u, so one wave-
+    // instruction's x gathers cover consecutive nonzeros (pairs measured 5-7% slower on P/R).
+    // Lanes past the block re-read its last entry / pair.
     int c[U];
     if (!TILE) {
 #pragma unroll
-        for (int u = 0; u < NU; ++u) c[u] = __builtin_nontemporal_load(a.col + k0 + min(tid + u * kTPB, nnz - 1));
+        for (int u = 0; u < NU; ++u)
+            c[u] = __builtin_nontemporal_load(a.col + k0 + min(tid + u * kTPB, nnz - 1));
     }
     double v[U], tv = 0.0;
     if (VIB) {
         tv = a.vtab[h1.z + min(tid, h1.w - 1)];
+    } else if (TILE) {
+        const int plast = (nnz - 1) & ~1;
+#pragma unroll
+        for (int p = 0; p < U / 2; ++p) {
+            const v2d_t vv = __builtin_nontemporal_load((const v2d_t*)(a.val + k0 + min(2 * tid + 2 * kTPB * p, plast)));
+            v[2 * p] = vv.x;
+            v[2 * p + 1] = vv.y;
+        }
     } else {
 #pragma unroll
         for (int u = 0; u < NU; ++u)
@@ -193,7 +209,8 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
             }
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) *(v2d_t*)(stage + 2 * tid + 512 * j) = v2d_t{xs[2 * j], xs[2 * j + 1]};
+        for (int j = 0; j < 4; ++j)
+            *(v2d_t*)(stage + 2 * tid + 512 * j) = v2d_t{xs[2 * j], xs[2 * j + 1]};
     } else {
 #pragma unroll
         for (int u = 0; u < NU; ++u) xs[u] = xload(a, c[u]);
@@ -219,8 +236,13 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
 #pragma unroll
         for (int u = 0; u < NU; ++u) pr[u] = v[u] * xs[u];
     }
+    if (TILE) {
 #pragma unroll
-    for (int u = 0; u < NU; ++u) stage[tid + u * kTPB] = pr[u];
+        for (int p = 0; p < U / 2; ++p) *(v2d_t*)(stage + 2 * tid + 2 * kTPB * p) = v2d_t{pr[2 * p], pr[2 * p + 1]};
+    } else {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) stage[tid + u * kTPB] = pr[u];
+    }
     __syncthreads();
     const int e0 = tid ? rends[tid - 1] : 0;
     double s = 0.0;
@@ -297,10 +319,15 @@ __global__ __launch_bounds__(kTPB, 8) void csr_block_kernel(CsrArgs a, int first
 
 // l1 hybrid Gauss-Seidel (row a5; definition DESIGN.md 3).  One wavefront per slab of <= 64
 // rows (whole GS chunks), lane = row.
-//  phase 1: the lane walks its row in the slab's sliced-ELL layout (entry k of all lanes is
-//           one coalesced 512-byte load) and subtracts every old-value coupling, diagonal
-//           included, in CSR order; the new-value ("chain") couplings -- in-chunk j < i
-//           forward, j > i backward -- are contiguous in the sorted row and are skipped.
+//  layout:  sliced-ELL in entry pairs -- entries k, k+1 (k even) of lane l at
+//           (off + k) * 64 + 2 l and +1 -- so a lane loads 16-byte value pairs and 8-byte
+//           column pairs (8-byte accesses stream at 0.54-0.70x the 16-byte rate,
+//           MI355X_MICROARCH.md), half the load instructions of one entry per load.
+//  phase 1: the lane walks its row (entry pairs of all lanes are one coalesced 1 KiB load)
+//           and subtracts every old-value coupling, diagonal included, in CSR order; the
+//           new-value ("chain") couplings -- in-chunk j < i forward, j > i backward -- are
+//           contiguous in the sorted row and are skipped.  Every load is unconditional
+//           (clamped into the slab, results masked): no divergent branch between loads.
 //  phase 2: the in-chunk triangular solve, column-oriented: at step t the row finishing now
 //           (lane t forward, lane n-1-t backward) has its final value; it is broadcast with
 //           v_readlane and every lane whose next chain column is that row subtracts
@@ -346,24 +373,24 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
     if (wave >= a.nslab) return;
     const int lane = threadIdx.x & 63;
     const int4 sl = a.slabs[wave];
-    const int r = sl.x + lane;
     const bool live = lane < sl.y;
-    int lo = 0, hi = 0;  // chain (new-value) column range [lo, hi)
-    double acc = 0.0, xi = 0.0, dinv = 0.0;
-    if (live) {
+    const int r = sl.x + (live ? lane : 0);  // dead lanes re-read the slab's first row
+    int lo = 0, hi = 0;  // chain (new-value) column range [lo, hi); empty on dead lanes
+    {
         const long long g = a.first_row + r;
         long long cs = (g / a.B) * a.B - a.first_row, ce = cs + a.B;
         cs = cs < 0 ? 0 : cs;
         ce = ce > a.n ? a.n : ce;
-        lo = BACK ? r + 1 : (int)cs;
-        hi = BACK ? (int)ce : r;
-        acc = a.b[r];
-        xi = a.x[r];
-        dinv = a.dinv[r];
+        lo = live ? (BACK ? r + 1 : (int)cs) : 0;
+        hi = live ? (BACK ? (int)ce : r) : 0;
     }
-    const size_t base = (size_t)sl.z * 64 + lane;
+    double acc = a.b[r];
+    const double xi = a.x[r], dinv = a.dinv[r];
+    // entry k of this lane's row sits at (off + (k & ~1)) * 64 + 2 lane + (k & 1)
+    const size_t base = (size_t)sl.z * 64 + 2 * lane;
     const int* colp = a.col + base;
     const double* valp = a.val + base;
+    auto at = [](int k) { return (size_t)(k & ~1) * 64 + (size_t)(k & 1); };
     __shared__ double chainL[WIDE ? 64 * 64 : 1];
     double s_old = 0.0;           // NORM: sum_j a_ij x_j (old x), for ||b - A x||
     unsigned long long mask = 0;  // WIDE: bit t = coupling to slab row t
@@ -371,12 +398,18 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
     // software pipeline: block k0 + U's (col, val) stream in while block k0 gathers x
     int cn[U];
     double vn[U];
+    const int klast = sl.w > 0 ? (sl.w - 1) & ~1 : 0;  // last pair of the slab
     auto fetch = [&](int k0) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool in = k0 + u < sl.w;  // uniform
-            cn[u] = in ? __builtin_nontemporal_load(colp + (size_t)(k0 + u) * 64) : -1;
-            vn[u] = in ? __builtin_nontemporal_load(valp + (size_t)(k0 + u) * 64) : 0.0;
+        for (int p = 0; p < U / 2; ++p) {
+            const int k = k0 + 2 * p;
+            const size_t o = (size_t)min(k, klast) * 64;
+            const v2i_t cc = __builtin_nontemporal_load((const v2i_t*)(colp + o));
+            const v2d_t vv = __builtin_nontemporal_load((const v2d_t*)(valp + o));
+            cn[2 * p] = k < sl.w ? cc.x : -1;  // uniform tests: pairs past the row masked
+            cn[2 * p + 1] = k + 1 < sl.w ? cc.y : -1;
+            vn[2 * p] = vv.x;
+            vn[2 * p + 1] = vv.y;
         }
     };
     fetch(0);
@@ -385,11 +418,12 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
         double v[U], xv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) c[u] = cn[u], v[u] = vn[u];
-        if (k0 + U < sl.w) fetch(k0 + U);
+        fetch(k0 + U);  // the next step's pairs (past the row: clamped re-reads, masked)
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool old = c[u] >= 0 && (NORM || !(c[u] >= lo && c[u] < hi));
-            xv[u] = old ? (c[u] < a.ncl ? a.x[c[u]] : a.xh[c[u] - a.ncl]) : 0.0;
+        for (int u = 0; u < U; ++u) {  // x of every entry; padding re-reads x[r]
+            const int cu = c[u];
+            const double* p = cu < 0 ? a.x + r : cu < a.ncl ? a.x + cu : a.xh + (cu - a.ncl);
+            xv[u] = *p;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -422,15 +456,13 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
         double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
         int kn = BACK ? kl : kf;  // next entry to load
         int left = kf < 0 ? 0 : kl - kf + 1;
-        auto load = [&](int& cc, double& vv) {
-            if (left > 0) {
-                cc = colp[(size_t)kn * 64];
-                vv = valp[(size_t)kn * 64];
-                kn += BACK ? -1 : 1;
-                --left;
-            } else {
-                cc = -1;
-            }
+        auto load = [&](int& cc, double& vv) {  // unconditional, clamped into the row
+            const int kk = min(max(kn, 0), max(sl.w - 1, 0));
+            const int c_ = colp[at(kk)];
+            vv = valp[at(kk)];
+            cc = left > 0 ? c_ : -1;
+            kn += left > 0 ? (BACK ? -1 : 1) : 0;
+            left -= left > 0 ? 1 : 0;
         };
         load(c0, v0);
         load(c1, v1);
@@ -658,7 +690,9 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
     const char* ev = getenv("AMG_KERNEL_VARIANT");
     int var = ev ? atoi(ev) : (A.default_variant | (A.n_vi_blocks > 0 ? 8 : 0));
     if (A.n_vi_blocks == 0) var &= ~8;
-    if (!A.square) var |= 4;  // rectangular operators are stored for the gather kernel only
+    // each operator is stored for one kernel: square -> x tile, rectangular -> gather
+    if (A.square) var &= ~4;
+    else var |= 4;
 #define AMG_L1(M, N, X, T, V) hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V>), g, t, 0, s, a, first_block)
 #define AMG_L2(M, N, V)                                               \
     do {                                                              \

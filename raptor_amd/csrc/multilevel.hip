@@ -2,6 +2,7 @@
 // SURVEY.md 8a rows a6-a10.  The cycle mirrors oracle/amg_oracle.c cycle_rec() operation
 // for operation, so the iterates are bit-identical to the oracle's.
 #include <cmath>
+#include <cstdlib>
 
 #include "device.hpp"
 
@@ -20,6 +21,7 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     ctx = A.ctx;
     opt = o;
     A0 = &A;
+
     const HostComm& comm = ctx->host;
     HostHierarchy H;
     SpgemmFn galerkin = nullptr;

@@ -120,9 +120,15 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
 // For square operators also the table index of each row's diagonal (dvi, 1 byte per row) and
 // per block whether every row has one (then Jacobi forms 1 / a_ii from the table in-kernel
 // instead of streaming dinv: 1 byte per row instead of 8).
-// Index layout: lane-major, entry j of a block -> lane j % kTPB, slot j / kTPB.  Square
-// operators (x-tile kernel, 8 slots): kCAP bytes per block at bid * kCAP.  Rectangular ones
-// (gather kernel): NU = 2, 4 or 8 slots by block size (the kernel's choice), packed, block
+// Lane-major position of entry j of a block whose lanes hold nu entries each, as pairs:
+// entry j = 512 p + 2 t + h sits at lane t, slot 2 p + h (p < nu / 2).
+static inline size_t lane_pos(int j, int nu) {
+    return (size_t)((j & (2 * kTPB - 1)) >> 1) * (size_t)nu + 2 * (size_t)(j / (2 * kTPB)) + (size_t)(j & 1);
+}
+
+// Index layout.  Square operators (x-tile kernel, 8 slots, entry pairs: lane_pos): kCAP
+// bytes per block at bid * kCAP.  Rectangular ones (gather kernel, entry j at lane j % kTPB,
+// slot j / kTPB): NU = 2, 4 or 8 slots by block size (the kernel's choice), packed, block
 // offset in vofs (header field 0, unused by the gather kernel otherwise).
 static int gather_slots(int nz) { return nz > 4 * kTPB ? 8 : nz > 2 * kTPB ? 4 : 2; }
 
@@ -184,8 +190,11 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
             uint64_t bits;
             std::memcpy(&bits, M.host.val.data() + kb + j, sizeof(bits));
             const size_t at = std::lower_bound(t.begin(), t.end(), bits) - t.begin();
-            const int nu = M.square ? kCAP / kTPB : gather_slots(nz);
-            idx[(size_t)vofs[q] + (size_t)(j % kTPB) * nu + j / kTPB] = (uint8_t)at;
+            // square (x-tile kernel): entry pairs; rectangular (gather kernel): entry j at
+            // lane j % kTPB, slot j / kTPB, NU slots per lane
+            const size_t pos = M.square ? lane_pos(j, kCAP / kTPB)
+                                        : (size_t)(j % kTPB) * gather_slots(nz) + (size_t)(j / kTPB);
+            idx[(size_t)vofs[q] + pos] = (uint8_t)at;
         }
         if (!M.square) continue;
         bool ok = true;
@@ -244,14 +253,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         cls[i] = b;
     }
     rp.upload(hrp.data(), hrp.size());
-    // padded by kPad zero entries: the vector-load tail of the last block stays in bounds
     hcol.resize(nnz + kPad, 0);
-    col.upload(hcol.data(), hcol.size());
-    {
-        std::vector<double> hv(host.val);
-        hv.resize(nnz + kPad, 0.0);
-        val.upload(hv.data(), hv.size());
-    }
     if (square) {
         std::vector<double> d = diagonal(comm, host), di(n_rows);
         for (int64_t i = 0; i < n_rows; ++i) di[i] = 1.0 / d[i];
@@ -263,6 +265,24 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         nb_bnd = bb.nb_bnd;
         blocks.upload(bb.blocks.data(), bb.blocks.size());
         const size_t nbk = bb.blocks.size();
+        // device col / val: block-aligned copies -- block q's entries at an even offset
+        // koff[q] (16-byte aligned values), so the kernel reads them as (2t, 2t + 1) pairs
+        std::vector<int64_t> koff(nbk + 1, 0);
+        for (size_t q = 0; q < nbk; ++q)
+            koff[q + 1] = koff[q] + (int64_t)(hrp[bb.blocks[q].y] - hrp[bb.blocks[q].x] + 1) / 2 * 2;
+        AMG_CHECK(koff[nbk] + kPad < INT_MAX, "local matrix exceeds int32 indexing");
+        {
+            std::vector<int> cb((size_t)(koff[nbk] + kPad), 0);
+            std::vector<double> vb(cb.size(), 0.0);
+#pragma omp parallel for schedule(dynamic, 256)
+            for (size_t q = 0; q < nbk; ++q) {
+                const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
+                std::copy(hcol.begin() + kb, hcol.begin() + kb + nz, cb.begin() + koff[q]);
+                std::copy(host.val.begin() + kb, host.val.begin() + kb + nz, vb.begin() + koff[q]);
+            }
+            col.upload(cb.data(), cb.size());
+            val.upload(vb.data(), vb.size());
+        }
         if (square) {  // x tiles: the square-operator kernel only
             // x-tile line ids at a fixed stride (kTileLines per block, padded with the block's
             // last line), so the kernel loads them without waiting for the block header
@@ -274,14 +294,14 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                     fx[q * kTileLines + j] = bb.tile_lines[t0 + std::min(j, nt - 1)];
             }
             tile_fixed.upload(fx.data(), fx.size());
-            // lane-major per block: lane t's indices for entries t + 256u (u = 0..7) are 16
-            // contiguous bytes, so the kernel reads them with one 16-byte load per lane
+            // lane-major per block (lane_pos): lane t's 8 indices are 16 contiguous bytes,
+            // one 16-byte load per lane
             std::vector<uint16_t> perm(std::max<size_t>(nbk, 1) * kCAP, 0);
             for (size_t q = 0; q < nbk; ++q) {
                 const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
                 if (nz > kCAP) continue;
                 for (int j = 0; j < nz; ++j)
-                    perm[q * kCAP + (size_t)(j % kTPB) * (kCAP / kTPB) + j / kTPB] = bb.lcol[kb + j];
+                    perm[q * kCAP + lane_pos(j, kCAP / kTPB)] = bb.lcol[kb + j];
             }
             lcol.upload(perm.data(), perm.size());
         } else {
@@ -306,7 +326,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             rend.upload(re.data(), re.size());
         }
         // 32-byte block headers (two scalar loads per block):
-        //   {r0, r1, k0, nnz}, {diag slot, tile lines | dvi flag << 16, value-table offset (-1),
+        //   {r0, r1, koff, nnz}, {diag slot, tile lines | dvi flag << 16, value-table offset (-1),
         //   table size}
         // diag slot (square operators): tile position of line r0 / 8 when the lines of the
         // block's own rows are consecutive in its tile, so x[r] is read from the tile; else -1
@@ -323,7 +343,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 for (int k = 0; ok && k <= l1 - l0; ++k) ok = tl[pos + k] == l0 + k;
                 if (ok) dslot = pos;
             }
-            hh[2 * q] = make_int4(b.x, b.y, hrp[b.x], hrp[b.y] - hrp[b.x]);
+            hh[2 * q] = make_int4(b.x, b.y, (int)koff[q], hrp[b.y] - hrp[b.x]);
             // rectangular (gather) operators: field 0 = the block's offset in the VI index stream
             const int f0 = square ? dslot : (vofs.empty() ? 0 : (int)vofs[q]);
             hh[2 * q + 1] = make_int4(f0, nt | (dvi_ok[q] ? 1 << 16 : 0), vt_off[q], vt_len[q]);
@@ -385,11 +405,11 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
         int w = 0;
         for (int64_t i = r; i < end; ++i) w = std::max<int>(w, (int)(host.rp[i + 1] - host.rp[i]));
         slabs.push_back(make_int4((int)r, (int)(end - r), (int)cells, w));
-        cells += w;
+        cells += (w + 1) & ~1;  // entry pairs: every slab starts at an even cell
         r = end;
     }
-    AMG_CHECK(cells * 64 < INT_MAX, "hybrid GS: sliced-ELL too large for int32 offsets");
-    std::vector<int> sc((size_t)std::max<int64_t>(cells, 1) * 64, -1);
+    AMG_CHECK((cells + 2) * 64 < INT_MAX, "hybrid GS: sliced-ELL too large for int32 offsets");
+    std::vector<int> sc((size_t)(cells + 2) * 64, -1);  // + one pair of cells: clamped reads
     std::vector<double> sv(sc.size(), 0.0), di(n_rows);
 #pragma omp parallel for schedule(dynamic, 64)
     for (size_t q = 0; q < slabs.size(); ++q) {
@@ -401,7 +421,8 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
             double l1 = 0.0, d = 0.0;
             for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) {
                 const int64_t gc = host.col[k];
-                const size_t at = ((size_t)sl.z + (size_t)(k - host.rp[i])) * 64 + l;
+                const int64_t kk = k - host.rp[i];  // pair layout (kernels.hip hybrid_gs_kernel)
+                const size_t at = ((size_t)sl.z + (size_t)(kk & ~1)) * 64 + 2 * (size_t)l + (size_t)(kk & 1);
                 sc[at] = local_col(gc);
                 sv[at] = host.val[k];
                 if (gc < cs || gc >= ce) l1 += std::fabs(host.val[k]);

@@ -30,9 +30,12 @@ def run_ranks(n, fn):
         t.start()
     for t in th:
         t.join(timeout=600)
-    for e in errs:
-        if e is not None:
-            raise e
+    # a rank that fails leaves its peers timing out at the next loopback barrier: report
+    # the root cause first
+    bad = [e for e in errs if e is not None]
+    bad.sort(key=lambda e: "barrier timed out" in str(e))
+    if bad:
+        raise bad[0]
     return out
 
 
