@@ -142,10 +142,9 @@ struct DevMatrix {
     int default_variant = 0;
     // l1 hybrid GS (built on first use for a given block size B <= 64): GS chunks = global
     // multiples of B clipped to this rank, packed whole into slabs of <= 64 rows (one
-    // wavefront each, lane = row).  Each slab's rows are stored sliced-ELL in entry pairs
-    // (entries k, k+1 of lane l at (off + k) * 64 + 2 l and +1, k and off even; col -1 =
-    // padding) so a lane's walk of its row is a coalesced stream of 16-byte value pairs.
-    // gs_dinv = 1 / (a_ii + sum of |a_ij| outside the chunk).
+    // wavefront each, lane = row).  Each slab's rows are stored sliced-ELL, column-major
+    // (entry k of lane l at (off + k) * 64 + l; col -1 = padding) so a lane's walk of its
+    // row is a coalesced stream.  gs_dinv = 1 / (a_ii + sum of |a_ij| outside the chunk).
     DevBuf<int4> gs_slabs;  // {first row, rows, offset / 64, width}
     DevBuf<int> gs_col;
     DevBuf<double> gs_val, gs_dinv;

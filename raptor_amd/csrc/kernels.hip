@@ -319,15 +319,10 @@ __global__ __launch_bounds__(kTPB, 8) void csr_block_kernel(CsrArgs a, int first
 
 // l1 hybrid Gauss-Seidel (row a5; definition DESIGN.md 3).  One wavefront per slab of <= 64
 // rows (whole GS chunks), lane = row.
-//  layout:  sliced-ELL in entry pairs -- entries k, k+1 (k even) of lane l at
-//           (off + k) * 64 + 2 l and +1 -- so a lane loads 16-byte value pairs and 8-byte
-//           column pairs (8-byte accesses stream at 0.54-0.70x the 16-byte rate,
-//           MI355X_MICROARCH.md), half the load instructions of one entry per load.
-//  phase 1: the lane walks its row (entry pairs of all lanes are one coalesced 1 KiB load)
-//           and subtracts every old-value coupling, diagonal included, in CSR order; the
-//           new-value ("chain") couplings -- in-chunk j < i forward, j > i backward -- are
-//           contiguous in the sorted row and are skipped.  Every load is unconditional
-//           (clamped into the slab, results masked): no divergent branch between loads.
+//  phase 1: the lane walks its row in the slab's sliced-ELL layout (entry k of all lanes is
+//           one coalesced 512-byte load) and subtracts every old-value coupling, diagonal
+//           included, in CSR order; the new-value ("chain") couplings -- in-chunk j < i
+//           forward, j > i backward -- are contiguous in the sorted row and are skipped.
 //  phase 2: the in-chunk triangular solve, column-oriented: at step t the row finishing now
 //           (lane t forward, lane n-1-t backward) has its final value; it is broadcast with
 //           v_readlane and every lane whose next chain column is that row subtracts
@@ -373,24 +368,24 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
     if (wave >= a.nslab) return;
     const int lane = threadIdx.x & 63;
     const int4 sl = a.slabs[wave];
+    const int r = sl.x + lane;
     const bool live = lane < sl.y;
-    const int r = sl.x + (live ? lane : 0);  // dead lanes re-read the slab's first row
-    int lo = 0, hi = 0;  // chain (new-value) column range [lo, hi); empty on dead lanes
-    {
+    int lo = 0, hi = 0;  // chain (new-value) column range [lo, hi)
+    double acc = 0.0, xi = 0.0, dinv = 0.0;
+    if (live) {
         const long long g = a.first_row + r;
         long long cs = (g / a.B) * a.B - a.first_row, ce = cs + a.B;
         cs = cs < 0 ? 0 : cs;
         ce = ce > a.n ? a.n : ce;
-        lo = live ? (BACK ? r + 1 : (int)cs) : 0;
-        hi = live ? (BACK ? (int)ce : r) : 0;
+        lo = BACK ? r + 1 : (int)cs;
+        hi = BACK ? (int)ce : r;
+        acc = a.b[r];
+        xi = a.x[r];
+        dinv = a.dinv[r];
     }
-    double acc = a.b[r];
-    const double xi = a.x[r], dinv = a.dinv[r];
-    // entry k of this lane's row sits at (off + (k & ~1)) * 64 + 2 lane + (k & 1)
-    const size_t base = (size_t)sl.z * 64 + 2 * lane;
+    const size_t base = (size_t)sl.z * 64 + lane;
     const int* colp = a.col + base;
     const double* valp = a.val + base;
-    auto at = [](int k) { return (size_t)(k & ~1) * 64 + (size_t)(k & 1); };
     __shared__ double chainL[WIDE ? 64 * 64 : 1];
     double s_old = 0.0;           // NORM: sum_j a_ij x_j (old x), for ||b - A x||
     unsigned long long mask = 0;  // WIDE: bit t = coupling to slab row t
@@ -398,18 +393,12 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
     // software pipeline: block k0 + U's (col, val) stream in while block k0 gathers x
     int cn[U];
     double vn[U];
-    const int klast = sl.w > 0 ? (sl.w - 1) & ~1 : 0;  // last pair of the slab
     auto fetch = [&](int k0) {
 #pragma unroll
-        for (int p = 0; p < U / 2; ++p) {
-            const int k = k0 + 2 * p;
-            const size_t o = (size_t)min(k, klast) * 64;
-            const v2i_t cc = __builtin_nontemporal_load((const v2i_t*)(colp + o));
-            const v2d_t vv = __builtin_nontemporal_load((const v2d_t*)(valp + o));
-            cn[2 * p] = k < sl.w ? cc.x : -1;  // uniform tests: pairs past the row masked
-            cn[2 * p + 1] = k + 1 < sl.w ? cc.y : -1;
-            vn[2 * p] = vv.x;
-            vn[2 * p + 1] = vv.y;
+        for (int u = 0; u < U; ++u) {
+            const bool in = k0 + u < sl.w;  // uniform
+            cn[u] = in ? __builtin_nontemporal_load(colp + (size_t)(k0 + u) * 64) : -1;
+            vn[u] = in ? __builtin_nontemporal_load(valp + (size_t)(k0 + u) * 64) : 0.0;
         }
     };
     fetch(0);
@@ -418,12 +407,11 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
         double v[U], xv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) c[u] = cn[u], v[u] = vn[u];
-        fetch(k0 + U);  // the next step's pairs (past the row: clamped re-reads, masked)
+        if (k0 + U < sl.w) fetch(k0 + U);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {  // x of every entry; padding re-reads x[r]
-            const int cu = c[u];
-            const double* p = cu < 0 ? a.x + r : cu < a.ncl ? a.x + cu : a.xh + (cu - a.ncl);
-            xv[u] = *p;
+        for (int u = 0; u < U; ++u) {
+            const bool old = c[u] >= 0 && (NORM || !(c[u] >= lo && c[u] < hi));
+            xv[u] = old ? (c[u] < a.ncl ? a.x[c[u]] : a.xh[c[u] - a.ncl]) : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -456,13 +444,15 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
         double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
         int kn = BACK ? kl : kf;  // next entry to load
         int left = kf < 0 ? 0 : kl - kf + 1;
-        auto load = [&](int& cc, double& vv) {  // unconditional, clamped into the row
-            const int kk = min(max(kn, 0), max(sl.w - 1, 0));
-            const int c_ = colp[at(kk)];
-            vv = valp[at(kk)];
-            cc = left > 0 ? c_ : -1;
-            kn += left > 0 ? (BACK ? -1 : 1) : 0;
-            left -= left > 0 ? 1 : 0;
+        auto load = [&](int& cc, double& vv) {
+            if (left > 0) {
+                cc = colp[(size_t)kn * 64];
+                vv = valp[(size_t)kn * 64];
+                kn += BACK ? -1 : 1;
+                --left;
+            } else {
+                cc = -1;
+            }
         };
         load(c0, v0);
         load(c1, v1);

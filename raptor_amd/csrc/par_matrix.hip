@@ -405,11 +405,11 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
         int w = 0;
         for (int64_t i = r; i < end; ++i) w = std::max<int>(w, (int)(host.rp[i + 1] - host.rp[i]));
         slabs.push_back(make_int4((int)r, (int)(end - r), (int)cells, w));
-        cells += (w + 1) & ~1;  // entry pairs: every slab starts at an even cell
+        cells += w;
         r = end;
     }
-    AMG_CHECK((cells + 2) * 64 < INT_MAX, "hybrid GS: sliced-ELL too large for int32 offsets");
-    std::vector<int> sc((size_t)(cells + 2) * 64, -1);  // + one pair of cells: clamped reads
+    AMG_CHECK(cells * 64 < INT_MAX, "hybrid GS: sliced-ELL too large for int32 offsets");
+    std::vector<int> sc((size_t)std::max<int64_t>(cells, 1) * 64, -1);
     std::vector<double> sv(sc.size(), 0.0), di(n_rows);
 #pragma omp parallel for schedule(dynamic, 64)
     for (size_t q = 0; q < slabs.size(); ++q) {
@@ -421,8 +421,7 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
             double l1 = 0.0, d = 0.0;
             for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) {
                 const int64_t gc = host.col[k];
-                const int64_t kk = k - host.rp[i];  // pair layout (kernels.hip hybrid_gs_kernel)
-                const size_t at = ((size_t)sl.z + (size_t)(kk & ~1)) * 64 + 2 * (size_t)l + (size_t)(kk & 1);
+                const size_t at = ((size_t)sl.z + (size_t)(k - host.rp[i])) * 64 + l;
                 sc[at] = local_col(gc);
                 sv[at] = host.val[k];
                 if (gc < cs || gc >= ce) l1 += std::fabs(host.val[k]);
