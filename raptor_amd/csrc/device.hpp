@@ -152,6 +152,13 @@ struct DevMatrix {
     int64_t gs_block = 0;
     int64_t gs_bytes = 0;  // sliced-ELL bytes streamed per sweep
     bool gs_wide = false;  // average slab width >= kGsWide: the LDS-chain kernel variant
+    // value dictionary (the whole local operator takes <= 256 distinct values, e.g. a
+    // constant-coefficient stencil): 1-byte indices instead of gs_val, four entries of a
+    // lane per dword -- entry k of lane l at (off + (k & ~3)) * 64 + 4 l + (k & 3) -- and
+    // the table (gs_ndict values) staged in LDS by the kernel
+    DevBuf<uint8_t> gs_vid;
+    DevBuf<double> gs_vtab;
+    int gs_ndict = 0;
     // halo (ParComm): RCCL neighbour exchange
     HaloPlan plan;
     DevBuf<int> send_idx;

@@ -346,6 +346,9 @@ struct GsArgs {
     int n;               // local rows (chunks are clipped to the rank)
     int nslab;
     double* partial;     // NORM: per-slab sum of (b - A x_old)^2
+    const uint8_t* vid;  // DICT: 1-byte value indices (4 entries of a lane per dword)
+    const double* vtab;  // DICT: the value table
+    int ndict;
 };
 
 __device__ __forceinline__ double bcast_lane(double v, int lane) {
@@ -359,9 +362,17 @@ __device__ __forceinline__ double bcast_lane(double v, int lane) {
 // slab's chain entries go to LDS as a 64 x 64 column-major block plus a per-lane bit mask in
 // phase 1, so the triangular solve never reloads them; phase 1 keeps 16 loads in flight.
 // Narrow: 4 waves per workgroup (no LDS), 8 loads in flight, register ring of chain entries.
-template <bool BACK, bool WIDE, bool NORM>
+// DICT: the operator's values come from a <= 256-entry table staged in LDS, through 1-byte
+// indices loaded four entries per dword (5 B per ELL cell instead of 12).
+template <bool BACK, bool WIDE, bool NORM, bool DICT>
 __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
     constexpr int U = WIDE ? 16 : 8;
+    static_assert(U % 4 == 0, "dictionary dwords hold 4 entries");
+    __shared__ double dtab[DICT ? 256 : 1];
+    if (DICT) {
+        for (int i = threadIdx.x; i < a.ndict; i += blockDim.x) dtab[i] = a.vtab[i];
+        __syncthreads();
+    }
     // wave index made provably uniform: slab fields land in SGPRs, the step loop is scalar
     const int wave = __builtin_amdgcn_readfirstlane(
         (int)(WIDE ? blockIdx.x : blockIdx.x * 4 + (threadIdx.x >> 6)));
@@ -386,6 +397,8 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
     const size_t base = (size_t)sl.z * 64 + lane;
     const int* colp = a.col + base;
     const double* valp = a.val + base;
+    const uint8_t* vidp = a.vid + (size_t)sl.z * 64 + 4 * (size_t)lane;  // DICT
+    auto vbyte = [&](int k) { return (int)vidp[(size_t)(k & ~3) * 64 + (k & 3)]; };
     __shared__ double chainL[WIDE ? 64 * 64 : 1];
     double s_old = 0.0;           // NORM: sum_j a_ij x_j (old x), for ||b - A x||
     unsigned long long mask = 0;  // WIDE: bit t = coupling to slab row t
@@ -393,12 +406,20 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
     // software pipeline: block k0 + U's (col, val) stream in while block k0 gathers x
     int cn[U];
     double vn[U];
+    unsigned wn[U / 4];  // DICT: the next step's value-index dwords (looked up when consumed)
     auto fetch = [&](int k0) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const bool in = k0 + u < sl.w;  // uniform
             cn[u] = in ? __builtin_nontemporal_load(colp + (size_t)(k0 + u) * 64) : -1;
-            vn[u] = in ? __builtin_nontemporal_load(valp + (size_t)(k0 + u) * 64) : 0.0;
+            if (!DICT) vn[u] = in ? __builtin_nontemporal_load(valp + (size_t)(k0 + u) * 64) : 0.0;
+        }
+        if (DICT) {
+#pragma unroll
+            for (int q = 0; q < U / 4; ++q)
+                wn[q] = k0 + 4 * q < sl.w
+                            ? __builtin_nontemporal_load((const unsigned*)(vidp + (size_t)(k0 + 4 * q) * 64))
+                            : 0u;
         }
     };
     fetch(0);
@@ -406,7 +427,14 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
         int c[U];
         double v[U], xv[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) c[u] = cn[u], v[u] = vn[u];
+        for (int u = 0; u < U; ++u) c[u] = cn[u];
+        if (DICT) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = dtab[(wn[u >> 2] >> (8 * (u & 3))) & 0xffu];
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = vn[u];
+        }
         if (k0 + U < sl.w) fetch(k0 + U);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -447,7 +475,7 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
         auto load = [&](int& cc, double& vv) {
             if (left > 0) {
                 cc = colp[(size_t)kn * 64];
-                vv = valp[(size_t)kn * 64];
+                vv = DICT ? dtab[vbyte(kn)] : valp[(size_t)kn * 64];
                 kn += BACK ? -1 : 1;
                 --left;
             } else {
@@ -722,14 +750,18 @@ void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const 
     AMG_ASSERT(!(backward && partial));
     GsArgs a{A.gs_slabs.p, A.gs_col.p, A.gs_val.p, x, A.halo.p, (int)A.n_cols_local, b,
              A.gs_dinv.p, y, (long long)A.first_row, (long long)A.gs_block, (int)A.n_rows,
-             A.n_gs_slabs, partial};
+             A.n_gs_slabs, partial, A.gs_vid.p, A.gs_vtab.p, A.gs_ndict};
     static const int forced = [] {
         const char* e = std::getenv("AMG_GS_VARIANT");  // 0 narrow, 1 wide (experiments)
         return e ? std::atoi(e) : -1;
     }();
     const bool wide = forced >= 0 ? forced == 1 : A.gs_wide;
     const dim3 grid(wide ? A.n_gs_slabs : (A.n_gs_slabs + 3) / 4), block(wide ? 64 : 256);
-#define AMG_GS(BK, WD, NM) hipLaunchKernelGGL((hybrid_gs_kernel<BK, WD, NM>), grid, block, 0, s, a)
+#define AMG_GS(BK, WD, NM)                                                                          \
+    do {                                                                                            \
+        if (A.gs_ndict > 0) hipLaunchKernelGGL((hybrid_gs_kernel<BK, WD, NM, true>), grid, block, 0, s, a); \
+        else hipLaunchKernelGGL((hybrid_gs_kernel<BK, WD, NM, false>), grid, block, 0, s, a);      \
+    } while (0)
     if (wide) {
         if (backward) AMG_GS(true, true, false);
         else if (partial) AMG_GS(false, true, true);

@@ -7,6 +7,7 @@
 // "boundary" lists: the interior kernel runs while RCCL moves the halo on a second
 // stream; the boundary kernel runs after the halo event.
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cmath>
 #include <cstring>
@@ -405,11 +406,11 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
         int w = 0;
         for (int64_t i = r; i < end; ++i) w = std::max<int>(w, (int)(host.rp[i + 1] - host.rp[i]));
         slabs.push_back(make_int4((int)r, (int)(end - r), (int)cells, w));
-        cells += w;
+        cells += (w + 3) & ~3;  // slabs start at multiples of 4 cells (dictionary dwords)
         r = end;
     }
-    AMG_CHECK(cells * 64 < INT_MAX, "hybrid GS: sliced-ELL too large for int32 offsets");
-    std::vector<int> sc((size_t)std::max<int64_t>(cells, 1) * 64, -1);
+    AMG_CHECK((cells + 4) * 64 < INT_MAX, "hybrid GS: sliced-ELL too large for int32 offsets");
+    std::vector<int> sc((size_t)(cells + 4) * 64, -1);
     std::vector<double> sv(sc.size(), 0.0), di(n_rows);
 #pragma omp parallel for schedule(dynamic, 64)
     for (size_t q = 0; q < slabs.size(); ++q) {
@@ -431,13 +432,64 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
             di[i] = 1.0 / (d + l1);
         }
     }
+    // value dictionary: <= 256 distinct values (bit patterns) in the local operator; each
+    // thread scans a chunk into a small set and gives up past 256
+    std::vector<uint64_t> dict;
+    {
+        const int64_t nz = (int64_t)host.val.size();
+        std::atomic<bool> over{false};
+#pragma omp parallel
+        {
+            std::vector<uint64_t> mine;
+#pragma omp for schedule(static) nowait
+            for (int64_t k = 0; k < nz; ++k) {
+                if (over.load(std::memory_order_relaxed)) continue;
+                uint64_t bits;
+                std::memcpy(&bits, &host.val[k], sizeof(bits));
+                if (std::find(mine.begin(), mine.end(), bits) == mine.end()) {
+                    mine.push_back(bits);
+                    if (mine.size() > 256) over.store(true, std::memory_order_relaxed);
+                }
+            }
+#pragma omp critical
+            if (!over.load()) dict.insert(dict.end(), mine.begin(), mine.end());
+        }
+        std::sort(dict.begin(), dict.end());
+        dict.erase(std::unique(dict.begin(), dict.end()), dict.end());
+        if (over.load() || dict.size() > 256) dict.clear();
+    }
+    gs_ndict = (int)dict.size();
+    if (gs_ndict > 0) {
+        std::vector<uint8_t> vid(sc.size(), 0);
+#pragma omp parallel for schedule(dynamic, 64)
+        for (size_t q = 0; q < slabs.size(); ++q) {
+            const int4 sl = slabs[q];
+            for (int l = 0; l < sl.y; ++l)
+                for (int k = 0; k < sl.w; ++k) {
+                    const size_t at = ((size_t)sl.z + (size_t)k) * 64 + (size_t)l;
+                    if (sc[at] < 0) continue;
+                    uint64_t bits;
+                    std::memcpy(&bits, &sv[at], sizeof(bits));
+                    vid[((size_t)sl.z + (size_t)(k & ~3)) * 64 + 4 * (size_t)l + (size_t)(k & 3)] =
+                        (uint8_t)(std::lower_bound(dict.begin(), dict.end(), bits) - dict.begin());
+                }
+        }
+        std::vector<double> tab(dict.size());
+        std::memcpy(tab.data(), dict.data(), sizeof(double) * dict.size());
+        gs_vid.upload(vid.data(), vid.size());
+        gs_vtab.upload(tab.data(), tab.size());
+        gs_val.reset();
+    } else {
+        gs_vid.reset();
+        gs_vtab.reset();
+        gs_val.upload(sv.data(), sv.size());
+    }
     gs_slabs.upload(slabs.data(), slabs.size());
     gs_col.upload(sc.data(), sc.size());
-    gs_val.upload(sv.data(), sv.size());
     gs_dinv.upload(di.data(), di.size());
     n_gs_slabs = (int)slabs.size();
     gs_block = B;
-    gs_bytes = 12 * 64 * cells + 16 * (int64_t)slabs.size() + 32 * n_rows;
+    gs_bytes = (gs_ndict > 0 ? 5 : 12) * 64 * cells + 16 * (int64_t)slabs.size() + 32 * n_rows;
     gs_wide = !slabs.empty() && cells >= (int64_t)kGsWide * (int64_t)slabs.size();
 }
 

@@ -201,3 +201,41 @@ def test_multirank_pcg(oracle):
 
     for hist in run_ranks(3, rank):
         assert np.all(np.abs(hist - hist_o) <= 1e-9 * hist_o[0])
+
+
+@pytest.mark.parametrize("values", ["stencil", "random"])
+def test_one_row_per_rank(oracle, values):
+    """Degenerate partition: one row and one local column per rank with one or two halo
+    entries -- the kernel's 8-byte x-tile path (a local or halo vector of one entry);
+    value-indexed ("stencil") and value-stream ("random") blocks."""
+    import scipy.sparse as sp
+
+    import raptor_amd as ra
+
+    O = oracle
+    n = 3
+    M = sp.diags([-np.ones(n - 1), 2 * np.ones(n), -np.ones(n - 1)], [-1, 0, 1]).tocsr()
+    if values == "random":
+        M.data = 1.0 + np.random.default_rng(3).random(M.nnz)
+    M.sort_indices()
+    Ao = O.Csr.from_scipy(M)
+    x, b = O.vec_uniform(n, 7), O.vec_uniform(n, 8)
+    ref = {"y": Ao.spmv(x), "r": Ao.residual(x, b), "j": Ao.jacobi(x, b, 2.0 / 3.0)}
+
+    def rank(r, nr, world):
+        ctx = ra.Context.loopback(r, nr, world)
+        A = ra.ParCSRMatrix.from_scipy_local(ctx, M[r:r + 1], n, r)
+        dx, db, out = to_dev(ctx, x[r:r + 1]), to_dev(ctx, b[r:r + 1]), ctx.empty(1)
+        A.mult(dx, out)
+        got = {"y": to_host(ctx, out)}
+        A.residual(dx, db, out)
+        got["r"] = to_host(ctx, out)
+        A.jacobi(dx, db, out)
+        got["j"] = to_host(ctx, out)
+        return got, A.info["n_halo"]
+
+    res = run_ranks(n, rank)
+    assert [h for _, h in res] == [1, 2, 1]
+    for r, (got, _) in enumerate(res):
+        for k in ("y", "r", "j"):
+            assert np.array_equal(got[k], ref[k][r:r + 1]), (k, r)
