@@ -351,7 +351,7 @@ int amg_par_csr_residual_norm(amg_matrix A, const double* x, const double* b, do
         AMG_CHECK(A && out, "null argument");
         Context& c = *A->m->ctx;
         set_device(c);
-        const size_t nb = (size_t)(A->m->nb_int + A->m->nb_bnd), tmpn = nb / 4096 + 64;
+        const size_t nb = (size_t)(A->m->nb_int + A->m->nb_bnd) * kNormParts, tmpn = nb / 4096 + 64;
         DevBuf<double> r, buf;
         DevBuf<int> cnt;
         r.alloc((size_t)std::max<int64_t>(A->m->n_rows, 1));

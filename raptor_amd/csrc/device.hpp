@@ -30,6 +30,7 @@ constexpr int kTPB = 256;   // threads per workgroup (4 waves of 64)
 constexpr int kCAP = 2048;  // nonzeros staged in LDS per workgroup (16 KiB of products)
 constexpr int kPad = kCAP;  // col/val padding (entries): unconditional loads past a block's end
 constexpr int kTileLines = 256;  // x tile per workgroup: 256 lines x 64 B = 16 KiB of LDS
+constexpr int kNormParts = kTPB / 64;  // norm partials per CSR block (one per wave)
 constexpr int kGsWide = 128;     // sliced-ELL width from which hybrid GS uses the wide variant
 
 template <class T>

@@ -280,7 +280,6 @@ __global__ __launch_bounds__(kTPB, 8) void csr_block_kernel(CsrArgs a, int first
     __shared__ __attribute__((aligned(16))) double stage[kCAP];  // x tile, then products
     __shared__ double tabl[VI ? 256 : 1];
     __shared__ int rends[kTPB];
-    __shared__ double red[kTPB / 64];
     const int tid = threadIdx.x;
     const int bid = first_block + (XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x);
     const int4 h0 = a.hdr[2 * bid], h1 = a.hdr[2 * bid + 1];
@@ -309,11 +308,10 @@ __global__ __launch_bounds__(kTPB, 8) void csr_block_kernel(CsrArgs a, int first
         }
     }
     if (NORM) {
-        // fixed-shape reduction: wave butterfly then 4 wave sums in order
+        // fixed-shape wave reduction, one partial per wave (kNormParts per block): no
+        // block barrier at the end of the kernel; the partials are summed in fixed order
         for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
-        if ((tid & 63) == 0) red[tid >> 6] = sq;
-        __syncthreads();
-        if (tid == 0) a.partial[bid] = (red[0] + red[1]) + (red[2] + red[3]);
+        if ((tid & 63) == 0) a.partial[bid * kNormParts + (tid >> 6)] = sq;
     }
 }
 

@@ -542,7 +542,7 @@ void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, in
 
 void norm_finish(DevMatrix& A, const NormSink& ns, int nparts) {
     Context* c = A.ctx;
-    const int nb = nparts >= 0 ? nparts : A.nb_int + A.nb_bnd;
+    const int nb = nparts >= 0 ? nparts : (A.nb_int + A.nb_bnd) * kNormParts;
     const int nr = c->host.nranks;
     double* local = ns.gathered + nr;
     if (nb > 0) launch_reduce_partials(c->stream, nb, ns.partial, ns.tmp, local);
