@@ -10,7 +10,7 @@ problem.  Timed: K steps of amg_solver_solve (no host sync inside), barrier + de
 both sides, max over ranks.  value = V-cycles/s x (global rows / 256^3): 256^3-equivalent
 V-cycles per second, the whole-job aggregate (equals plain iterations/s at N=1).
 
-roofline: the level-0 ParCSRMatrix::mult kernel (csr_block_kernel<SPMV>), timed live with HIP
+roofline: the level-0 ParCSRMatrix::mult kernel (tpl_kernel / csr_block_kernel), timed live with HIP
 events on the context stream; bytes = the stored format's HBM bytes per launch (DESIGN.md 4;
 value-indexed blocks stream 1-byte indices instead of fp64 values), with the plain-CSR
 equivalent 12 nnz + 4 (n+1) + 16 n reported beside it.
@@ -249,7 +249,11 @@ def main():
             "vcycle_effective_GBps": round(cyc_bytes * iters_per_s / 1e9, 1),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "csr_block_kernel<SPMV> (level-0 ParCSRMatrix::mult, rank 0)",
+                "kernel": ("tpl_kernel<SPMV> (row templates" +
+                           (")" if A.info["template_rows"] == A.local_rows else " + csr_block_kernel)") +
+                           " level-0 ParCSRMatrix::mult, rank 0"
+                           if A.info["template_rows"] > 0 else
+                           "csr_block_kernel<SPMV> (level-0 ParCSRMatrix::mult, rank 0)"),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -260,6 +264,8 @@ def main():
                 "bytes_definition": "stored-format HBM bytes per launch (DESIGN.md 4)",
                 "avg_launch_ms": round(spmv_ms, 5),
                 "vi_blocks_frac": round(A.info["n_vi_blocks"] / max(1, A.info["n_blocks"]), 4),
+                "row_templates": A.info["n_templates"],
+                "template_rows_frac": round(A.info["template_rows"] / max(1, A.local_rows), 4),
                 "csr_equiv_bytes_per_launch": csr_bytes,
                 "csr_equiv_GBps": round(csr_equiv, 1),
             },

@@ -116,6 +116,8 @@ typedef struct amg_matrix_info {
     int32_t n_vi_blocks;   /* row blocks stored value-indexed (<= 256 distinct values)   */
     int64_t spmv_bytes;    /* HBM bytes one mult() moves in the stored format: headers,  *
                             * index/value streams, row_ptr, x (once), y                  */
+    int32_t n_templates;   /* row templates built (0: none; <= 255)                      */
+    int64_t template_rows; /* rows mult() runs through the row-template kernel           */
 } amg_matrix_info;
 int amg_par_csr_info(amg_matrix A, amg_matrix_info* info);
 /* Host copy of the local rows (global column ids). */

@@ -58,6 +58,8 @@ class MatrixInfo(C.Structure):
         ("n_blocks", C.c_int32),
         ("n_vi_blocks", C.c_int32),
         ("spmv_bytes", C.c_int64),
+        ("n_templates", C.c_int32),
+        ("template_rows", C.c_int64),
     ]
 
 

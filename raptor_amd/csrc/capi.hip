@@ -278,7 +278,9 @@ int amg_par_csr_info(amg_matrix A, amg_matrix_info* info) {
         info->n_neighbors = (int32_t)std::max(m.plan.send_procs.size(), m.plan.recv_procs.size());
         info->n_blocks = m.nb_int + m.nb_bnd;
         info->n_vi_blocks = m.n_vi_blocks;
-        info->spmv_bytes = m.spmv_fmt_bytes;
+        info->spmv_bytes = m.tpl_on() ? m.spmv_fmt_bytes : m.csr_fmt_bytes;
+        info->n_templates = m.n_tpl;
+        info->template_rows = m.tpl_on() ? m.tpl_rows : 0;
     });
 }
 
@@ -351,7 +353,7 @@ int amg_par_csr_residual_norm(amg_matrix A, const double* x, const double* b, do
         AMG_CHECK(A && out, "null argument");
         Context& c = *A->m->ctx;
         set_device(c);
-        const size_t nb = (size_t)(A->m->nb_int + A->m->nb_bnd) * kNormParts, tmpn = nb / 4096 + 64;
+        const size_t nb = (size_t)A->m->norm_parts_max(), tmpn = nb / 4096 + 64;
         DevBuf<double> r, buf;
         DevBuf<int> cnt;
         r.alloc((size_t)std::max<int64_t>(A->m->n_rows, 1));

@@ -32,6 +32,18 @@ constexpr int kPad = kCAP;  // col/val padding (entries): unconditional loads pa
 constexpr int kTileLines = 256;  // x tile per workgroup: 256 lines x 64 B = 16 KiB of LDS
 constexpr int kNormParts = kTPB / 64;  // norm partials per CSR block (one per wave)
 constexpr int kGsWide = 128;     // sliced-ELL width from which hybrid GS uses the wide variant
+// row templates: 1-byte template id per row (kTplNone = row not templated)
+constexpr int kTplNone = 255;
+constexpr int kTplMax = 255;       // templates per operator
+constexpr int kTplEntries = 1024;  // entries over all templates (staged in LDS per workgroup)
+constexpr int kTplMaxLen = 64;     // entries per template
+#ifndef AMG_TPL_RPL  // build-time knob for same-box A/B builds (scripts/gpu_libab.sh)
+#define AMG_TPL_RPL 2
+#endif
+constexpr int kTplRPL = AMG_TPL_RPL;  // rows per lane of the template kernel
+constexpr int kTplBands = 8;       // x-window bands
+constexpr int kTplWin = 16 * 256;  // x-window doubles per workgroup (32 KiB of LDS)
+constexpr int kTplRows = kTPB * kTplRPL;  // rows per template-kernel workgroup
 
 template <class T>
 struct DevBuf {
@@ -160,6 +172,28 @@ struct DevMatrix {
     DevBuf<uint8_t> gs_vid;
     DevBuf<double> gs_vtab;
     int gs_ndict = 0;
+    // row templates (square operators): rows whose columns are all local, written as
+    // (column - row) offsets, values and 1/a_ii; rows with identical triples share a template.
+    // tpl_id per row (kTplNone: the CSR block kernel handles the row); per template
+    // tpl_hdr = start | len << 16 | diag entry << 24 (255: none), tpl_pd = 1/a_ii; entries
+    // tpl_off / tpl_val.  CSR blocks [0, nb_skip) hold only templated rows: the block kernel
+    // skips them while templates are active (tpl_on()).
+    DevBuf<uint8_t> tpl_id;
+    DevBuf<int> tpl_hdr, tpl_off;
+    // x window: bands of template offsets; per entry its window slot (tpl_ldo);
+    // tpl_win = window size in doubles, 0 = the bands do not fit (global x loads)
+    std::vector<int> tpl_blo, tpl_bbase;
+    DevBuf<int> tpl_ldo;
+    int tpl_win = 0;
+    DevBuf<double> tpl_val, tpl_pd;
+    int n_tpl = 0, n_tpl_ent = 0, nb_skip = 0;
+    int64_t tpl_rows = 0;  // rows the template kernel handles
+    int64_t csr_fmt_bytes = 0;  // spmv_fmt_bytes with templates off (AMG_KERNEL_VARIANT)
+    bool tpl_on() const;
+    int tpl_blocks() const { return n_tpl > 0 ? (int)((n_rows + kTplRows - 1) / kTplRows) : 0; }
+    // norm partials one NORM-mode application leaves (and the most either path can leave)
+    int norm_parts() const;
+    int norm_parts_max() const { return (nb_int + nb_bnd + tpl_blocks()) * kNormParts; }
     // halo (ParComm): RCCL neighbour exchange
     HaloPlan plan;
     DevBuf<int> send_idx;
@@ -180,9 +214,16 @@ struct DevMatrix {
 enum KernelMode { KM_SPMV = 0, KM_SPMV_ADD = 1, KM_RESID = 2, KM_JACOBI = 3 };
 
 // launchers (kernels.hip); all enqueue on s
+// csr-stream variant bits in effect for A (DevMatrix::default_variant, VI and template bits,
+// or AMG_KERNEL_VARIANT): 2 XCD order, 4 gather, 8 value-indexed, 32 row templates
+int kernel_variant(const DevMatrix& A);
+// partial slot of block bid's wave w: part_off + bid * kNormParts + w
 void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, int first_block,
                        int n_blocks, const double* x, const double* b, double* y, double omega,
-                       double* partial);
+                       double* partial, int part_off = 0);
+// template rows of A (all of them, one launch); partials at [0, tpl_blocks() * kNormParts)
+void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const double* x,
+                const double* b, double* y, double omega, double* partial);
 void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
                       double* y, bool backward = false, double* partial = nullptr);
 void launch_jacobi_zero(hipStream_t s, int64_t n, const double* b, const double* dinv, double* y,

@@ -44,6 +44,7 @@ struct CsrArgs {
     double* y;
     double omega;
     double* partial;
+    int part_off;      // partial slot of block bid's wave w: part_off + bid * kNormParts + w
 };
 
 __device__ __forceinline__ double xload(const CsrArgs& a, int c) {
@@ -311,7 +312,179 @@ __global__ __launch_bounds__(kTPB, 8) void csr_block_kernel(CsrArgs a, int first
         // fixed-shape wave reduction, one partial per wave (kNormParts per block): no
         // block barrier at the end of the kernel; the partials are summed in fixed order
         for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
-        if ((tid & 63) == 0) a.partial[bid * kNormParts + (tid >> 6)] = sq;
+        if ((tid & 63) == 0) a.partial[a.part_off + bid * kNormParts + (tid >> 6)] = sq;
+    }
+}
+
+// Row-template kernel.  A templated row is (column - row) offsets, values and
+// 1/a_ii shared with every row of the same shape -- for a constant-coefficient stencil a few
+// dozen templates cover the operator -- so the kernel streams 1 byte per row (its template
+// id) plus the vectors, instead of per-nonzero indices and values.  Lane = row, kTplRPL rows
+// per lane (rows r0 + lane + kTPB j of the workgroup's kTplRows).  Each row's sum runs in CSR
+// order from 0.0 -- the oracle's order, so the results are bit-identical.
+//
+// x window (NPL > 0): the template offsets, merged into a few bands [lo, hi], tell which x
+// every workgroup reads: x[r0 + lo, r0 + kTplRows + hi] per band.  The workgroup loads the
+// bands into LDS once (NPL 8-byte loads per lane, all issued before the first is used; 512
+// contiguous bytes per wave-instruction) and every product reads x from LDS through the
+// entry's window slot (tpl_ldo).  Without the window (operators whose bands do not fit) each
+// product loads x from global memory, 8 entries per batch.  Measured on the 7-pt 256^3
+// operator: window 5x fewer vector-memory instructions than the global loads, which were
+// latency-bound at ~1/4 of the HBM rate (profiles/r1t_*).
+struct TplArgs {
+    const uint8_t* id;   // per row (kTplNone: not templated here)
+    const int* hdr;      // per template: start | len << 16 | diag entry << 24
+    const int* off;      // per entry: window slot (NPL > 0) or column - row
+    const double* val;   // per entry
+    const double* pd;    // per template: 1/a_ii (Jacobi)
+    int ntpl, nent, n;
+    int nband, win;            // x-window bands, window size (doubles)
+    int blo[kTplBands];        // band b covers x[r0 + blo[b] + i], i < bbase[b+1] - bbase[b]
+    int bbase[kTplBands + 1];  // first window slot of band b
+    const double* x;
+    const double* b;
+    double* y;
+    double omega;
+    double* partial;
+};
+
+// dynamic LDS: window | values | 1/a_ii | entry slots or offsets | headers
+inline size_t tpl_lds_bytes(int win, int nent) {
+    return 8 * ((size_t)win + (size_t)nent + kTplMax + 1) + 4 * ((size_t)nent + kTplMax + 1);
+}
+
+template <int MODE, bool NORM, int NPL>
+__global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
+    constexpr int R = kTplRPL, C = 8;  // C: global-path loads per batch
+    extern __shared__ double tpl_lds[];
+    double* s_win = tpl_lds;
+    double* s_val = s_win + a.win;
+    double* s_pd = s_val + a.nent;
+    int* s_off = (int*)(s_pd + kTplMax + 1);
+    int* s_hdr = s_off + a.nent;
+    const int tid = threadIdx.x;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int r0 = blk * kTplRows;
+    // x through a buffer descriptor: 32-bit offsets, out-of-range loads return 0 (window
+    // slots before row 0 / past row n - 1 are never read)
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.x, (short)0, (int)((unsigned)a.n * 8u), 0x00020000);
+    // batch 1: row operands and the x window (independent of each other and of the table)
+    int id[R], rr[R];
+    double pb[R], py[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int r = r0 + kTPB * j + tid;
+        rr[j] = min(r, a.n - 1);
+        const int t = a.id[rr[j]];
+        id[j] = r < a.n ? t : kTplNone;
+        pb[j] = 0.0;
+        py[j] = 0.0;
+        if (MODE == KM_RESID || MODE == KM_JACOBI) pb[j] = a.b[rr[j]];
+        if (MODE == KM_SPMV_ADD) py[j] = a.y[rr[j]];
+    }
+    double wv[NPL > 0 ? NPL : 1];
+#pragma unroll
+    for (int u = 0; u < NPL; ++u) {
+        const int i = tid + kTPB * u;
+        // band of slot i: selects, no branch (bands past nband start at win)
+        int lo = a.blo[0], bb = a.bbase[0];
+#pragma unroll
+        for (int q = 1; q < kTplBands; ++q) {
+            const bool in = i >= a.bbase[q];
+            lo = in ? a.blo[q] : lo;
+            bb = in ? a.bbase[q] : bb;
+        }
+        const int g = r0 + lo + (i - bb);
+        const int vo = i < a.win ? g * 8 : -8;  // negative: past num_records, returns 0
+        wv[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xrs, vo, 0, 0));
+    }
+    // template table (L2-resident)
+    for (int k = tid; k < a.nent; k += kTPB) {
+        s_off[k] = a.off[k];
+        s_val[k] = a.val[k];
+    }
+    if (tid < a.ntpl) {
+        s_hdr[tid] = a.hdr[tid];
+        if (MODE == KM_JACOBI) s_pd[tid] = a.pd[tid];
+    }
+    if (tid == kTplNone) s_hdr[kTplNone] = (int)(255u << 24);  // length 0, no diagonal
+#pragma unroll
+    for (int u = 0; u < NPL; ++u) {
+        const int i = tid + kTPB * u;
+        if (i < a.win) s_win[i] = wv[u];
+    }
+    __syncthreads();
+    // per row: template fields (global path: both rows of the lane advance together, C entries
+    // per batch, every load of a batch issued before its first product)
+    int st[R], ln[R], dk[R], L = 0;
+    double s[R], xr[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const unsigned h = (unsigned)s_hdr[id[j]];
+        st[j] = (int)(h & 0xffffu);
+        ln[j] = (int)((h >> 16) & 0xffu);
+        dk[j] = (int)(h >> 24);
+        L = max(L, ln[j]);
+        s[j] = 0.0;
+        xr[j] = 0.0;
+        // Jacobi needs x[r]; a template without a diagonal entry reads it here (rare)
+        if (MODE == KM_JACOBI && dk[j] == 255 && id[j] != kTplNone) xr[j] = a.x[rr[j]];
+    }
+    if (NPL > 0) {
+        // window: one entry at a time per row (measured faster than 4-entry batches,
+        // profiles/r1t_tpl.txt)
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            for (int k = 0; k < ln[j]; ++k) {
+                const double xv = s_win[s_off[st[j] + k] + kTPB * j + tid];
+                s[j] = s[j] + s_val[st[j] + k] * xv;
+                if (MODE == KM_JACOBI) xr[j] = k == dk[j] ? xv : xr[j];
+            }
+    } else {
+        const int elast = a.nent - 1;
+        for (int k0 = 0; k0 < L; k0 += C) {
+            double xv[C][R];
+#pragma unroll
+            for (int u = 0; u < C; ++u)
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const int k = k0 + u;
+                    const int o = k < ln[j] ? s_off[min(st[j] + k, elast)] : 0;
+                    xv[u][j] = __builtin_bit_cast(
+                        double, __builtin_amdgcn_raw_buffer_load_b64(xrs, (rr[j] + o) * 8, 0, 0));
+                }
+            __builtin_amdgcn_sched_barrier(0);  // values read after the loads (register budget)
+#pragma unroll
+            for (int u = 0; u < C; ++u)
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const int k = k0 + u;
+                    const double p = s_val[min(st[j] + k, elast)] * xv[u][j];
+                    s[j] = k < ln[j] ? s[j] + p : s[j];
+                    if (MODE == KM_JACOBI) xr[j] = k == dk[j] ? xv[u][j] : xr[j];
+                }
+        }
+    }
+    double sq = 0.0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const bool own = id[j] != kTplNone;
+        double out;
+        if (MODE == KM_SPMV) {
+            out = s[j];
+        } else if (MODE == KM_SPMV_ADD) {
+            out = py[j] + s[j];
+        } else {
+            const double t = pb[j] - s[j];
+            if (NORM) sq += own ? t * t : 0.0;
+            out = MODE == KM_RESID ? t : xr[j] + a.omega * (s_pd[MODE == KM_JACOBI ? id[j] : 0] * t);
+        }
+        if (own) a.y[r0 + kTPB * j + tid] = out;
+    }
+    if (NORM) {
+        for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
+        if ((tid & 63) == 0) a.partial[blk * kNormParts + (tid >> 6)] = sq;
     }
 }
 
@@ -688,27 +861,103 @@ void launch_append(hipStream_t s, const double* v, double* hist, int* counter) {
     HIP_CHECK(hipGetLastError());
 }
 
+int kernel_variant(const DevMatrix& A) {
+    // variant bits: 2 = XCD-ordered blocks, 4 = gather path (no x tile), 8 = value-indexed
+    // blocks (when any block qualifies), 32 = row templates (when built).  Default
+    // (DevMatrix::default_variant): x tile for square operators, gather for rectangular ones
+    // (stored without tiles), both in XCD order (profiles/r1m_variants.txt), VI and templates
+    // where built.  AMG_KERNEL_VARIANT overrides the bits (experiments,
+    // scripts/spmv_variants.py; results are identical).
+    const char* ev = getenv("AMG_KERNEL_VARIANT");
+    int var = ev ? atoi(ev) : (A.default_variant | (A.n_vi_blocks > 0 ? 8 : 0) | (A.n_tpl > 0 ? 32 : 0));
+    if (A.n_vi_blocks == 0) var &= ~8;
+    if (A.n_tpl == 0) var &= ~32;
+    // each operator is stored for one kernel: square -> x tile, rectangular -> gather
+    if (A.square) var &= ~4;
+    else var |= 4;
+    return var;
+}
+
+bool DevMatrix::tpl_on() const { return n_tpl > 0 && (kernel_variant(*this) & 32); }
+
+int DevMatrix::norm_parts() const {
+    return tpl_on() ? (tpl_blocks() + nb_int + nb_bnd - nb_skip) * kNormParts
+                    : (nb_int + nb_bnd) * kNormParts;
+}
+
+void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const double* x,
+                const double* b, double* y, double omega, double* partial) {
+    const int g = A.tpl_blocks();
+    if (g <= 0) return;
+    AMG_ASSERT(A.square && A.n_tpl > 0 && A.n_tpl <= kTplMax && A.n_tpl_ent <= kTplEntries);
+    // AMG_TPL_WINDOW=0: global x loads even where the window fits (experiments)
+    static const bool allow_win = [] {
+        const char* e = std::getenv("AMG_TPL_WINDOW");
+        return !(e && std::atoi(e) == 0);
+    }();
+    const bool win = allow_win && A.tpl_win > 0;
+    TplArgs a{};
+    a.id = A.tpl_id.p;
+    a.hdr = A.tpl_hdr.p;
+    a.off = win ? A.tpl_ldo.p : A.tpl_off.p;
+    a.val = A.tpl_val.p;
+    a.pd = A.tpl_pd.p;
+    a.ntpl = A.n_tpl;
+    a.nent = A.n_tpl_ent;
+    a.n = (int)A.n_rows;
+    a.nband = win ? (int)A.tpl_blo.size() : 0;
+    a.win = win ? A.tpl_win : 0;
+    for (int q = 0; q < a.nband; ++q) a.blo[q] = A.tpl_blo[q], a.bbase[q] = A.tpl_bbase[q];
+    a.bbase[a.nband] = a.win;
+    for (int q = a.nband; q < kTplBands; ++q) a.blo[q] = 0, a.bbase[q + 1] = a.win;
+    a.x = x;
+    a.b = b;
+    a.y = y;
+    a.omega = omega;
+    a.partial = partial;
+    const int npl = !win ? 0 : a.win <= 4 * kTPB ? 4 : a.win <= 8 * kTPB ? 8 : a.win <= 12 * kTPB ? 12 : 16;
+    AMG_ASSERT(a.win <= npl * kTPB && a.win <= kTplWin);
+    const size_t lds = tpl_lds_bytes(a.win, a.nent);
+#define AMG_T2(M, N, P) hipLaunchKernelGGL((tpl_kernel<M, N, P>), dim3(g), dim3(kTPB), lds, s, a)
+#define AMG_T(M, N)                              \
+    do {                                         \
+        switch (npl) {                           \
+            case 4: AMG_T2(M, N, 4); break;      \
+            case 8: AMG_T2(M, N, 8); break;      \
+            case 12: AMG_T2(M, N, 12); break;    \
+            case 16: AMG_T2(M, N, 16); break;    \
+            default: AMG_T2(M, N, 0); break;     \
+        }                                        \
+    } while (0)
+    switch (mode) {
+        case KM_SPMV: AMG_T(KM_SPMV, false); break;
+        case KM_SPMV_ADD: AMG_T(KM_SPMV_ADD, false); break;
+        case KM_RESID:
+            if (norm) AMG_T(KM_RESID, true);
+            else AMG_T(KM_RESID, false);
+            break;
+        case KM_JACOBI:
+            if (norm) AMG_T(KM_JACOBI, true);
+            else AMG_T(KM_JACOBI, false);
+            break;
+        default: throw Error(AMG_ERR_INTERNAL, "bad kernel mode");
+    }
+#undef AMG_T
+#undef AMG_T2
+    HIP_CHECK(hipGetLastError());
+}
+
 void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, int first_block,
                        int n_blocks, const double* x, const double* b, double* y, double omega,
-                       double* partial) {
+                       double* partial, int part_off) {
     if (n_blocks <= 0) return;
     const int ncl = (int)A.n_cols_local, nh = (int)A.n_halo();
     CsrArgs a{A.hdr.p, A.tile_fixed.p, A.lcol.p, A.vidx.p, A.vtab.p, A.rend.p, A.dvi.p,
               A.rp.p, A.col.p, A.val.p,
               x, A.halo.p, ncl, nh, (ncl + 7) / 8, (ncl >= 2 && nh != 1) ? 1 : 0, A.square ? 0 : 1,
-              b, A.dinv.p, y, omega, partial};
+              b, A.dinv.p, y, omega, partial, part_off};
     dim3 g(n_blocks), t(kTPB);
-    // variant bits: 2 = XCD-ordered blocks, 4 = gather path (no x tile), 8 = value-indexed
-    // blocks (when any block qualifies).  Default (DevMatrix::default_variant): x tile for
-    // square operators, gather for rectangular ones (stored without tiles), both in XCD
-    // order (profiles/r1m_variants.txt).  AMG_KERNEL_VARIANT overrides the bits (experiments,
-    // scripts/spmv_variants.py; results are identical).
-    const char* ev = getenv("AMG_KERNEL_VARIANT");
-    int var = ev ? atoi(ev) : (A.default_variant | (A.n_vi_blocks > 0 ? 8 : 0));
-    if (A.n_vi_blocks == 0) var &= ~8;
-    // each operator is stored for one kernel: square -> x tile, rectangular -> gather
-    if (A.square) var &= ~4;
-    else var |= 4;
+    const int var = kernel_variant(A);
 #define AMG_L1(M, N, X, T, V) hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V>), g, t, 0, s, a, first_block)
 #define AMG_L2(M, N, V)                                               \
     do {                                                              \

@@ -81,7 +81,7 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         }
         levels[l].r.alloc(n);
         levels[l].t.alloc(n);
-        max_blocks = std::max(max_blocks, (size_t)(Al.nb_int + Al.nb_bnd) * kNormParts);
+        max_blocks = std::max(max_blocks, (size_t)Al.norm_parts_max());
         if (opt.smoother == AMG_SMOOTH_HYBRID_GS) {
             Al.ensure_gs_blocks(opt.gs_block);
             tm.lap("L" + std::to_string(l) + " GS sliced-ELL build");

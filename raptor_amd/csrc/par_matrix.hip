@@ -10,7 +10,9 @@
 #include <atomic>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <unordered_map>
 
 #include "device.hpp"
 
@@ -31,15 +33,18 @@ Context::~Context() {
 // 16-bit index into the tile: slot * 8 + (column & 7).  A single row touching more lines
 // than a tile holds becomes a block of its own and takes the untiled path.
 struct BlockBuild {
-    std::vector<int2> blocks;     // interior blocks, then boundary blocks
+    std::vector<int2> blocks;     // interior all-templated, other interior, then boundary blocks
     std::vector<int> tile_ptr;    // nb + 1
     std::vector<int> tile_lines;  // global line ids per block
     std::vector<uint16_t> lcol;   // per nonzero (nnz + kPad)
-    int nb_int = 0, nb_bnd = 0;
+    int nb_int = 0, nb_bnd = 0, nb_skip = 0;  // nb_skip: leading interior all-templated blocks
 };
 
+// tplf (optional): per row 1 = handled by the template kernel; blocks then also break where it
+// changes, and all-templated interior blocks come first
 static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector<int>& col,
-                                   const std::vector<uint8_t>& cls, int64_t ncl, int64_t nhalo) {
+                                   const std::vector<uint8_t>& cls, int64_t ncl, int64_t nhalo,
+                                   const std::vector<uint8_t>* tplf = nullptr) {
     const int n = (int)rp.size() - 1;
     const int64_t hl0 = (ncl + 7) / 8;
     auto line_of = [&](int c) -> int64_t { return c < ncl ? c >> 3 : hl0 + ((c - ncl) >> 3); };
@@ -47,7 +52,7 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
     struct Rec {
         int r0, r1;
         std::vector<int> lines;
-        bool bnd;
+        bool bnd, tpl;
     };
     std::vector<Rec> recs;
     BlockBuild out;
@@ -65,7 +70,8 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
             const int e = c < ncl ? (c & 7) : (int)((c - ncl) & 7);  // element within its line
             out.lcol[k] = tiled ? (uint16_t)(slot[line_of(c)] * 8 + e) : (uint16_t)0;
         }
-        recs.push_back({a, b, tiled ? lines : std::vector<int>(), cls[a] != 0});
+        recs.push_back({a, b, tiled ? lines : std::vector<int>(), cls[a] != 0,
+                        tplf != nullptr && (*tplf)[a] != 0});
         if (!tiled) recs.back().lines.assign(kTileLines + 1, 0);  // marker: untiled
         lines.clear();
         ++blk;
@@ -87,7 +93,7 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
         const long long len = rp[r + 1] - rp[r];
         collect(r, 2 * (int64_t)r);
         if (r > r0 && (cls[r] != cls[r0] || acc + len > kCAP || r - r0 >= kTPB ||
-                       nl + (int)cand.size() > kTileLines)) {
+                       nl + (int)cand.size() > kTileLines || (tplf && (*tplf)[r] != (*tplf)[r0]))) {
             emit(r0, r);  // closes [r0, r); blk advances
             r0 = r;
             acc = 0;
@@ -102,13 +108,15 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
         acc += len;
     }
     emit(r0, n);
-    for (int pass = 0; pass < 2; ++pass)
+    for (int pass = 0; pass < 3; ++pass)
         for (const Rec& R : recs) {
-            if (R.bnd != (pass == 1)) continue;
+            const int p = R.bnd ? 2 : R.tpl ? 0 : 1;
+            if (p != pass) continue;
             out.blocks.push_back(make_int2(R.r0, R.r1));
             out.tile_ptr.push_back((int)out.tile_lines.size());
             out.tile_lines.insert(out.tile_lines.end(), R.lines.begin(), R.lines.end());
-            (pass ? out.nb_bnd : out.nb_int)++;
+            (pass == 2 ? out.nb_bnd : out.nb_int)++;
+            if (pass == 0) out.nb_skip++;
         }
     out.tile_ptr.push_back((int)out.tile_lines.size());
     return out;
@@ -217,6 +225,148 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
     M.vidx.upload(idx.data(), idx.size());
 }
 
+
+// Row templates.  A row qualifies when all its columns are local and it has
+// 1..kTplMaxLen entries; its key is (column - row offsets, value bits, 1/a_ii bits).  Rows
+// with equal keys share a template.  Each thread scans a contiguous chunk into a local
+// dictionary; the chunk dictionaries merge in chunk order into <= kTplMax templates of
+// <= kTplEntries entries (later shapes beyond either cap stay untemplated).
+struct TplBuild {
+    std::vector<uint8_t> id;  // per row, kTplNone = not templated
+    std::vector<int> hdr, off;
+    std::vector<double> val, pd;
+    int64_t rows = 0;
+};
+
+static TplBuild build_templates(const std::vector<int>& rp, const std::vector<int>& col,
+                                const std::vector<double>& val, const std::vector<double>& dinv,
+                                int64_t ncl) {
+    const int n = (int)rp.size() - 1;
+    TplBuild T;
+    T.id.assign((size_t)n, (uint8_t)kTplNone);
+    if (n <= 0) return T;
+    auto bits = [](double v) {
+        uint64_t u;
+        std::memcpy(&u, &v, sizeof(u));
+        return u;
+    };
+    auto qualifies = [&](int r) {
+        const int len = rp[r + 1] - rp[r];
+        if (len <= 0 || len > kTplMaxLen) return false;
+        for (int k = rp[r]; k < rp[r + 1]; ++k)
+            if (col[k] >= ncl) return false;
+        return true;
+    };
+    auto key_hash = [&](int r) {
+        uint64_t h = 0x9E3779B97F4A7C15ull * (uint64_t)(rp[r + 1] - rp[r] + 1);
+        auto mix = [&](uint64_t v) {
+            h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+            h *= 0xBF58476D1CE4E5B9ull;
+        };
+        for (int k = rp[r]; k < rp[r + 1]; ++k) {
+            mix((uint64_t)(uint32_t)(col[k] - r));
+            mix(bits(val[k]));
+        }
+        mix(bits(dinv[r]));
+        return h;
+    };
+    auto same = [&](int a, int b) {
+        const int la = rp[a + 1] - rp[a];
+        if (la != rp[b + 1] - rp[b] || bits(dinv[a]) != bits(dinv[b])) return false;
+        for (int k = 0; k < la; ++k)
+            if (col[rp[a] + k] - a != col[rp[b] + k] - b || bits(val[rp[a] + k]) != bits(val[rp[b] + k]))
+                return false;
+        return true;
+    };
+    const int nch = std::max(1, std::min(256, n / 16384));
+    std::vector<std::vector<int>> reps(nch);       // representative row per local template
+    std::vector<std::vector<uint64_t>> hashes(nch);
+    std::vector<int16_t> lid((size_t)n, -1);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int c = 0; c < nch; ++c) {
+        const int r0 = (int)((int64_t)n * c / nch), r1 = (int)((int64_t)n * (c + 1) / nch);
+        std::unordered_map<uint64_t, std::vector<int>> m;
+        std::vector<int>& R = reps[c];
+        int last = -1;
+        for (int r = r0; r < r1; ++r) {
+            if (!qualifies(r)) continue;
+            if (last >= 0 && same(R[last], r)) {
+                lid[r] = (int16_t)last;
+                continue;
+            }
+            const uint64_t h = key_hash(r);
+            int found = -1;
+            auto it = m.find(h);
+            if (it != m.end())
+                for (int t : it->second)
+                    if (same(R[t], r)) {
+                        found = t;
+                        break;
+                    }
+            if (found < 0) {
+                if ((int)R.size() >= kTplMax) continue;
+                found = (int)R.size();
+                R.push_back(r);
+                hashes[c].push_back(h);
+                m[h].push_back(found);
+            }
+            lid[r] = (int16_t)found;
+            last = found;
+        }
+    }
+    // merge (chunk order) into the global dictionary
+    std::vector<std::vector<int>> gmap(nch);
+    std::vector<int> grep;
+    std::unordered_map<uint64_t, std::vector<int>> gm;
+    int ent = 0;
+    for (int c = 0; c < nch; ++c) {
+        gmap[c].assign(reps[c].size(), -1);
+        for (size_t t = 0; t < reps[c].size(); ++t) {
+            const int r = reps[c][t];
+            const uint64_t h = hashes[c][t];
+            int g = -1;
+            auto it = gm.find(h);
+            if (it != gm.end())
+                for (int q : it->second)
+                    if (same(grep[q], r)) {
+                        g = q;
+                        break;
+                    }
+            const int len = rp[r + 1] - rp[r];
+            if (g < 0 && (int)grep.size() < kTplMax && ent + len <= kTplEntries) {
+                g = (int)grep.size();
+                grep.push_back(r);
+                gm[h].push_back(g);
+                ent += len;
+            }
+            gmap[c][t] = g;
+        }
+    }
+    int64_t rows = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : rows)
+    for (int c = 0; c < nch; ++c) {
+        const int r0 = (int)((int64_t)n * c / nch), r1 = (int)((int64_t)n * (c + 1) / nch);
+        for (int r = r0; r < r1; ++r)
+            if (lid[r] >= 0 && gmap[c][lid[r]] >= 0) {
+                T.id[r] = (uint8_t)gmap[c][lid[r]];
+                ++rows;
+            }
+    }
+    T.rows = rows;
+    for (int r : grep) {
+        const int start = (int)T.off.size(), len = rp[r + 1] - rp[r];
+        int dk = 255;
+        for (int k = 0; k < len; ++k) {
+            T.off.push_back(col[rp[r] + k] - r);
+            T.val.push_back(val[rp[r] + k]);
+            if (col[rp[r] + k] == r && dk == 255) dk = k;
+        }
+        T.hdr.push_back(start | len << 16 | (int)((unsigned)dk << 24));
+        T.pd.push_back(dinv[r]);
+    }
+    return T;
+}
+
 void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
     ctx = c;
     host = std::move(h);
@@ -254,16 +404,99 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         cls[i] = b;
     }
     rp.upload(hrp.data(), hrp.size());
-    hcol.resize(nnz + kPad, 0);
+    std::vector<double> di;
     if (square) {
-        std::vector<double> d = diagonal(comm, host), di(n_rows);
+        std::vector<double> d = diagonal(comm, host);
+        di.resize(n_rows);
         for (int64_t i = 0; i < n_rows; ++i) di[i] = 1.0 / d[i];
         dinv.upload(di.data(), di.size());
     }
+    // row templates: square operators whose templates cover every row, or at least half of
+    // the rows of a large operator (AMG_TPL_MIN_ROWS, default 16384; tests lower it)
+    TplBuild tb;
+    n_tpl = n_tpl_ent = nb_skip = 0;
+    tpl_rows = 0;
+    if (square && n_rows > 0) {
+        const char* e = std::getenv("AMG_TPL_MIN_ROWS");
+        const int64_t min_rows = e ? std::atoll(e) : (int64_t)16384;
+        tb = build_templates(hrp, hcol, host.val, di, n_cols_local);
+        const bool use = tb.rows == n_rows || (n_rows >= min_rows && 2 * tb.rows >= n_rows);
+        if (!use) tb = TplBuild();
+    }
+    hcol.resize(nnz + kPad, 0);
     {
-        BlockBuild bb = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo());
+        std::vector<uint8_t> tplf;
+        if (!tb.hdr.empty()) {
+            tplf.resize(n_rows);
+            for (int64_t i = 0; i < n_rows; ++i) tplf[i] = tb.id[i] != kTplNone && cls[i] == 0;
+        }
+        BlockBuild bb = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(),
+                                         tplf.empty() ? nullptr : &tplf);
         nb_int = bb.nb_int;
         nb_bnd = bb.nb_bnd;
+        if (!tb.hdr.empty()) {
+            // rows of blocks the CSR kernel still runs are not the template kernel's
+            std::vector<char> keep(n_rows, 0);
+            for (int q = 0; q < bb.nb_skip; ++q)
+                for (int r = bb.blocks[q].x; r < bb.blocks[q].y; ++r) keep[r] = 1;
+            int64_t rows = 0;
+            for (int64_t i = 0; i < n_rows; ++i) {
+                if (!keep[i]) tb.id[i] = (uint8_t)kTplNone;
+                rows += tb.id[i] != kTplNone;
+            }
+            nb_skip = bb.nb_skip;
+            tpl_rows = rows;
+            n_tpl = (int)tb.hdr.size();
+            n_tpl_ent = (int)tb.off.size();
+            tpl_id.upload(tb.id.data(), tb.id.size());
+            tpl_hdr.upload(tb.hdr.data(), tb.hdr.size());
+            tpl_off.upload(tb.off.data(), tb.off.size());
+            tpl_val.upload(tb.val.data(), tb.val.size());
+            tpl_pd.upload(tb.pd.data(), tb.pd.size());
+            // x window: distinct offsets merged into bands while a gap is shorter than a
+            // workgroup's rows (a new band would load kTplRows more doubles than the gap)
+            std::vector<int> offs(tb.off);
+            std::sort(offs.begin(), offs.end());
+            offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
+            std::vector<int2> bands;  // {lo, hi}
+            for (int o : offs) {
+                if (!bands.empty() && (int64_t)o - bands.back().y < kTplRows) bands.back().y = o;
+                else bands.push_back(make_int2(o, o));
+            }
+            int64_t w = 0;
+            for (const int2& bd : bands) w += kTplRows + (int64_t)bd.y - bd.x;
+            tpl_blo.clear();
+            tpl_bbase.clear();
+            tpl_win = 0;
+            tpl_ldo.reset();
+            if ((int)bands.size() <= kTplBands && w <= kTplWin) {
+                std::vector<int> ldo(tb.off.size());
+                int base = 0;
+                for (const int2& bd : bands) {
+                    tpl_blo.push_back(bd.x);
+                    tpl_bbase.push_back(base);
+                    base += kTplRows + bd.y - bd.x;
+                }
+                for (size_t k = 0; k < tb.off.size(); ++k) {
+                    const int o = tb.off[k];
+                    size_t q = 0;
+                    while (q + 1 < bands.size() && o > bands[q].y) ++q;
+                    ldo[k] = tpl_bbase[q] + (o - bands[q].x);
+                }
+                tpl_win = base;
+                tpl_ldo.upload(ldo.data(), ldo.size());
+            }
+        } else {
+            tpl_blo.clear();
+            tpl_bbase.clear();
+            tpl_win = 0;
+            tpl_ldo.reset();
+            tpl_id.reset();
+            tpl_hdr.reset();
+            tpl_off.reset();
+            tpl_val.reset();
+            tpl_pd.reset();
+        }
         blocks.upload(bb.blocks.data(), bb.blocks.size());
         const size_t nbk = bb.blocks.size();
         // device col / val: block-aligned copies -- block q's entries at an even offset
@@ -356,9 +589,15 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         default_variant = square ? 2 : (4 | 2);
         // format bytes of one default-variant SpMV (the kernel reads every lane slot of the
         // fixed-stride streams, so their padding counts)
-        int64_t fb = 2 * n_rows + 8 * (n_cols_local + plan.n_halo()) + 8 * n_rows;
+        // with templates: the skipped blocks cost nothing; template rows cost 1 byte (id) and
+        // every template workgroup stages the table (tpl_blocks() * table bytes, L2-resident)
+        const int64_t xy = 8 * (n_cols_local + plan.n_halo()) + 8 * n_rows;
+        int64_t fb = 2 * n_rows + xy, fb_tpl = xy;
+        if (n_tpl > 0)
+            fb_tpl += n_rows + (int64_t)tpl_blocks() * (12 * (int64_t)n_tpl_ent + 4 * (int64_t)n_tpl);
         for (size_t q = 0; q < nbk; ++q) {
             const int nz = hh[2 * q].w, nt = hh[2 * q + 1].y & 0xffff;
+            const int64_t fb0 = fb;
             fb += 32;
             if (nz == 0) continue;
             if (nz > kCAP || (square && nt > kTileLines)) {  // long row: CSR stream
@@ -371,8 +610,10 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 fb += (square ? kCAP : gather_slots(nz) * kTPB) + 8 * (int64_t)hh[2 * q + 1].w;
             else
                 fb += 8 * (int64_t)nz;
+            if ((int)q >= nb_skip) fb_tpl += fb - fb0 + 2 * (int64_t)(bb.blocks[q].y - bb.blocks[q].x);
         }
-        spmv_fmt_bytes = fb;
+        csr_fmt_bytes = fb;
+        spmv_fmt_bytes = n_tpl > 0 ? fb_tpl : fb;
     }
     std::vector<int> sidx(plan.send_idx.begin(), plan.send_idx.end());
     send_idx.upload(sidx.data(), sidx.size());
@@ -527,9 +768,16 @@ void par_apply(DevMatrix& A, int mode, const double* x, const double* b, double*
     if (mode == KM_JACOBI || mode == KM_RESID) AMG_CHECK(A.square, "Jacobi/residual need a square matrix");
     const bool comm = A.halo_begin(x);
     hipStream_t s = A.ctx->stream;
-    launch_csr_stream(s, mode, partial != nullptr, A, 0, A.nb_int, x, b, y, omega, partial);
+    const bool norm = partial != nullptr;
+    // template rows never touch the halo: they run with the interior blocks; the CSR kernel's
+    // partials follow the template kernel's
+    const bool tp = A.tpl_on();
+    const int c0 = tp ? A.nb_skip : 0;
+    const int poff = tp ? (A.tpl_blocks() - A.nb_skip) * kNormParts : 0;
+    if (tp) launch_tpl(s, mode, norm, A, x, b, y, omega, partial);
+    launch_csr_stream(s, mode, norm, A, c0, A.nb_int - c0, x, b, y, omega, partial, poff);
     if (comm) A.halo_wait();
-    launch_csr_stream(s, mode, partial != nullptr, A, A.nb_int, A.nb_bnd, x, b, y, omega, partial);
+    launch_csr_stream(s, mode, norm, A, A.nb_int, A.nb_bnd, x, b, y, omega, partial, poff);
 }
 
 void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block,
@@ -542,7 +790,7 @@ void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, in
 
 void norm_finish(DevMatrix& A, const NormSink& ns, int nparts) {
     Context* c = A.ctx;
-    const int nb = nparts >= 0 ? nparts : (A.nb_int + A.nb_bnd) * kNormParts;
+    const int nb = nparts >= 0 ? nparts : A.norm_parts();
     const int nr = c->host.nranks;
     double* local = ns.gathered + nr;
     if (nb > 0) launch_reduce_partials(c->stream, nb, ns.partial, ns.tmp, local);

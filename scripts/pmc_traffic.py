@@ -2,7 +2,7 @@
 
 traffic = 2 x FETCH_SIZE + WRITE_SIZE (bytes; FETCH_SIZE reads half the bytes of wide
 streaming loads on gfx950, MI355X_MICROARCH.md "HBM"), averaged over the SpMV launches of
-the 7-pt 256^3 level-0 operator (grid 65536 workgroups, SPMV instantiation).  Writes a JSON
+the 7-pt 256^3 level-0 operator (SPMV instantiation of its first kernel).  Writes a JSON
 that bench.py reports as roofline.traffic."""
 import csv
 import json
@@ -23,8 +23,11 @@ def per_dispatch(path):
 def main(prefix, out):
     f, meta = per_dispatch(f"{prefix}_FETCH_SIZE/run_counter_collection.csv")
     w, _ = per_dispatch(f"{prefix}_WRITE_SIZE/run_counter_collection.csv")
-    # level-0 operator = first matrix in pmc_levels.py: its first 3 csr_stream launches are SpMV
-    ds = [d for d in sorted(meta) if "csr_block_kernel<0" in meta[d][0]][:3]
+    # level-0 operator = first matrix in pmc_levels.py: its first 3 SpMV launches (the
+    # row-template kernel where the operator is templated, else the CSR block kernel)
+    spmv = [d for d in sorted(meta)
+            if any(k in meta[d][0] for k in ("tpl_kernel<0", "csr_block_kernel<0"))]
+    ds = [d for d in spmv if meta[d] == meta[spmv[0]]][:3]
     fetch = sum(f[d]["FETCH_SIZE"] for d in ds) / len(ds) * 1024
     write = sum(w[d]["WRITE_SIZE"] for d in ds) / len(ds) * 1024
     res = {"kernel": meta[ds[0]][0].split("(amg::")[0], "grid": meta[ds[0]][1], "launches": len(ds),

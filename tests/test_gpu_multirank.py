@@ -52,9 +52,15 @@ def set_oracle_cuts(Ho, res):
         Ho.set_cuts(l, sorted({s[l] for s in starts if l < len(s)}))
 
 
+@pytest.mark.parametrize("tpl", [False, True], ids=["csr", "templates"])
 @pytest.mark.parametrize("nranks", [2, 3])
-def test_slab_kernels_bit_exact(oracle, nranks):
+def test_slab_kernels_bit_exact(oracle, monkeypatch, nranks, tpl):
+    """templates: interior rows on the row-template kernel, halo rows on the CSR block
+    kernel (size floor lowered so the small slabs qualify)."""
     import raptor_amd as ra
+
+    if tpl:
+        monkeypatch.setenv("AMG_TPL_MIN_ROWS", "0")
 
     O = oracle
     dims = (14, 13, 17)
@@ -79,6 +85,7 @@ def test_slab_kernels_bit_exact(oracle, nranks):
         got["j"] = to_host(ctx, out)
         got["rn"] = A.residual_norm(dx, db)
         got["halo"] = A.info["n_halo"]
+        got["tpl_rows"] = A.info["template_rows"]
         return f, m, got
 
     res = run_ranks(nranks, rank)
@@ -88,6 +95,7 @@ def test_slab_kernels_bit_exact(oracle, nranks):
             assert np.array_equal(got[k], ref[k][f:f + m]), k
         assert abs(got["rn"] - rn_ref) <= 1e-12 * rn_ref
         assert got["halo"] > 0
+        assert (0 < got["tpl_rows"] < m) if tpl else got["tpl_rows"] == 0
 
 
 CASES = [(2, "7pt", (16, 15, 18), "pmis", "jacobi"),

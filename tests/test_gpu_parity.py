@@ -73,6 +73,66 @@ def test_level_kernels_bit_exact(ctx, oracle, problems, name):
     assert abs(rn - ro) <= 1e-12 * ro
 
 
+def _all_modes_equal(ctx, O, A, Ao, seed=3):
+    n = Ao.shape[0]
+    x, b, y0 = O.vec_uniform(n, seed), O.vec_uniform(n, seed + 1), O.vec_uniform(n, seed + 2)
+    dx, db = to_dev(ctx, x), to_dev(ctx, b)
+    out = ctx.empty(n)
+    A.mult(dx, out)
+    assert np.array_equal(to_host(ctx, out), Ao.spmv(x))
+    dy = to_dev(ctx, y0)
+    A.mult_add(dx, dy)
+    assert np.array_equal(to_host(ctx, dy), Ao.spmv_add(x, y0))
+    A.residual(dx, db, out)
+    assert np.array_equal(to_host(ctx, out), Ao.residual(x, b))
+    A.jacobi(dx, db, out, 2.0 / 3.0)
+    assert np.array_equal(to_host(ctx, out), Ao.jacobi(x, b, 2.0 / 3.0))
+    rn = A.residual_norm(dx, db)
+    ro = O.norm2(Ao.residual(x, b))
+    assert abs(rn - ro) <= 1e-12 * ro
+
+
+@pytest.mark.parametrize("name,ntpl", [("7pt_20", 27), ("5pt_37x29", 9), ("27pt_13", 27)])
+def test_row_templates_bit_exact(ctx, oracle, problems, monkeypatch, name, ntpl):
+    """Stencil operators are stored as row templates: one template per boundary
+    class, every row on the template kernel; all four modes bit-identical to the oracle, and
+    to the CSR block kernel (AMG_KERNEL_VARIANT without bit 32)."""
+    import raptor_amd as ra
+
+    Ao = problems[name]
+    A = _dev_matrix(ra, ctx, Ao)
+    assert A.info["n_templates"] == ntpl
+    assert A.info["template_rows"] == Ao.shape[0]
+    _all_modes_equal(ctx, oracle, A, Ao)
+    monkeypatch.setenv("AMG_KERNEL_VARIANT", "10")
+    _all_modes_equal(ctx, oracle, A, Ao)
+
+
+def test_row_templates_partial_cover(ctx, oracle, monkeypatch):
+    """Mixed operator: more distinct row shapes than templates (300 perturbed diagonals), a
+    row longer than a template holds (100 entries) and an empty row.  With the size floor
+    lowered, the template kernel takes the covered rows and the CSR block kernel the rest,
+    in one application; results bit-identical, norm partials from both kernels."""
+    import raptor_amd as ra
+
+    O = oracle
+    monkeypatch.setenv("AMG_TPL_MIN_ROWS", "0")
+    M = O.gen_7pt(24, 23, 22).to_scipy().tolil()
+    n = M.shape[0]
+    rng = np.random.default_rng(5)
+    for k, r in enumerate(rng.choice(n, 300, replace=False)):
+        M[r, r] = 6.0 + (k + 1) * 1e-3
+    M[77, :100] = rng.standard_normal(100)
+    M[4000, :] = 0
+    M = M.tocsr()
+    M.sort_indices()
+    Ao = O.Csr.from_scipy(M)
+    A = _dev_matrix(ra, ctx, Ao)
+    assert 27 < A.info["n_templates"] <= 255  # capped by kTplEntries (1024 entries)
+    assert n // 2 <= A.info["template_rows"] < n
+    _all_modes_equal(ctx, O, A, Ao, seed=21)
+
+
 @pytest.mark.parametrize("name", ["7pt_20", "27pt_13", "ragged"])
 def test_spgemm_bit_exact(ctx, oracle, problems, name):
     """Device Galerkin SpGEMM == oracle SpGEMM bit for bit (all LDS table bins; the ragged
