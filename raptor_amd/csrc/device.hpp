@@ -184,7 +184,7 @@ struct DevMatrix {
     // tpl_win = window size in doubles, 0 = the bands do not fit (global x loads)
     std::vector<int> tpl_blo, tpl_bbase;
     DevBuf<int> tpl_ldo;
-    int tpl_win = 0;
+    int tpl_win = 0, tpl_wend = 0;
     DevBuf<double> tpl_val, tpl_pd;
     int n_tpl = 0, n_tpl_ent = 0, nb_skip = 0;
     int64_t tpl_rows = 0;  // rows the template kernel handles

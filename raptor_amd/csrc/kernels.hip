@@ -338,7 +338,8 @@ struct TplArgs {
     const double* val;   // per entry
     const double* pd;    // per template: 1/a_ii (Jacobi)
     int ntpl, nent, n;
-    int nband, win;            // x-window bands, window size (doubles)
+    int nband, win;            // x-window bands, window size (doubles, even)
+    int wend;                  // window end relative to r0 (last band's end)
     int blo[kTplBands];        // band b covers x[r0 + blo[b] + i], i < bbase[b+1] - bbase[b]
     int bbase[kTplBands + 1];  // first window slot of band b
     const double* x;
@@ -383,21 +384,44 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
         if (MODE == KM_RESID || MODE == KM_JACOBI) pb[j] = a.b[rr[j]];
         if (MODE == KM_SPMV_ADD) py[j] = a.y[rr[j]];
     }
-    double wv[NPL > 0 ? NPL : 1];
+    // window loads.  Workgroups whose window lies inside x (all but the first and last few)
+    // load slot pairs with 16-byte loads (bands start at even offsets and hold an even number
+    // of slots); the others load single slots, out-of-range ones returning 0.
+    const bool pairs = r0 + a.blo[0] >= 0 && r0 + a.wend <= a.n;  // workgroup-uniform
+    constexpr int NP = NPL > 0 ? NPL : 1;
+    double wv[NP];
+    if (NPL > 0 && pairs) {
 #pragma unroll
-    for (int u = 0; u < NPL; ++u) {
-        const int i = tid + kTPB * u;
-        // band of slot i: selects, no branch (bands past nband start at win)
-        int lo = a.blo[0], bb = a.bbase[0];
+        for (int u = 0; u < NP / 2; ++u) {
+            const int i = 2 * (tid + kTPB * u);
+            int lo = a.blo[0], bb = a.bbase[0];
 #pragma unroll
-        for (int q = 1; q < kTplBands; ++q) {
-            const bool in = i >= a.bbase[q];
-            lo = in ? a.blo[q] : lo;
-            bb = in ? a.bbase[q] : bb;
+            for (int q = 1; q < kTplBands; ++q) {
+                const bool in = i >= a.bbase[q];
+                lo = in ? a.blo[q] : lo;
+                bb = in ? a.bbase[q] : bb;
+            }
+            const int vo = i < a.win ? (r0 + lo + (i - bb)) * 8 : -16;
+            const v2d_t p2 = __builtin_bit_cast(v2d_t, __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, 0, 0));
+            wv[2 * u] = p2.x;
+            wv[2 * u + 1] = p2.y;
         }
-        const int g = r0 + lo + (i - bb);
-        const int vo = i < a.win ? g * 8 : -8;  // negative: past num_records, returns 0
-        wv[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xrs, vo, 0, 0));
+    } else if (NPL > 0) {
+#pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            const int i = tid + kTPB * u;
+            // band of slot i: selects, no branch (bands past nband start at win)
+            int lo = a.blo[0], bb = a.bbase[0];
+#pragma unroll
+            for (int q = 1; q < kTplBands; ++q) {
+                const bool in = i >= a.bbase[q];
+                lo = in ? a.blo[q] : lo;
+                bb = in ? a.bbase[q] : bb;
+            }
+            const int g = r0 + lo + (i - bb);
+            const int vo = i < a.win ? g * 8 : -8;  // negative: past num_records, returns 0
+            wv[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xrs, vo, 0, 0));
+        }
     }
     // template table (L2-resident)
     for (int k = tid; k < a.nent; k += kTPB) {
@@ -409,10 +433,18 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
         if (MODE == KM_JACOBI) s_pd[tid] = a.pd[tid];
     }
     if (tid == kTplNone) s_hdr[kTplNone] = (int)(255u << 24);  // length 0, no diagonal
+    if (NPL > 0 && pairs) {
 #pragma unroll
-    for (int u = 0; u < NPL; ++u) {
-        const int i = tid + kTPB * u;
-        if (i < a.win) s_win[i] = wv[u];
+        for (int u = 0; u < NP / 2; ++u) {
+            const int i = 2 * (tid + kTPB * u);
+            if (i < a.win) *(v2d_t*)(s_win + i) = v2d_t{wv[2 * u], wv[2 * u + 1]};
+        }
+    } else if (NPL > 0) {
+#pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            const int i = tid + kTPB * u;
+            if (i < a.win) s_win[i] = wv[u];
+        }
     }
     __syncthreads();
     // per row: template fields (global path: both rows of the lane advance together, C entries
@@ -907,6 +939,7 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
     a.n = (int)A.n_rows;
     a.nband = win ? (int)A.tpl_blo.size() : 0;
     a.win = win ? A.tpl_win : 0;
+    a.wend = win ? A.tpl_wend : 0;
     for (int q = 0; q < a.nband; ++q) a.blo[q] = A.tpl_blo[q], a.bbase[q] = A.tpl_bbase[q];
     a.bbase[a.nband] = a.win;
     for (int q = a.nband; q < kTplBands; ++q) a.blo[q] = 0, a.bbase[q + 1] = a.win;

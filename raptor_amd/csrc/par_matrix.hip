@@ -463,11 +463,14 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 if (!bands.empty() && (int64_t)o - bands.back().y < kTplRows) bands.back().y = o;
                 else bands.push_back(make_int2(o, o));
             }
+            // even band starts and lengths: slot pairs map to 16-byte aligned pairs of x
+            for (int2& bd : bands) bd.x &= ~1;
+            auto blen = [](const int2& bd) { return (int64_t)(kTplRows + bd.y - bd.x + 1) & ~(int64_t)1; };
             int64_t w = 0;
-            for (const int2& bd : bands) w += kTplRows + (int64_t)bd.y - bd.x;
+            for (const int2& bd : bands) w += blen(bd);
             tpl_blo.clear();
             tpl_bbase.clear();
-            tpl_win = 0;
+            tpl_win = tpl_wend = 0;
             tpl_ldo.reset();
             if ((int)bands.size() <= kTplBands && w <= kTplWin) {
                 std::vector<int> ldo(tb.off.size());
@@ -475,8 +478,9 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 for (const int2& bd : bands) {
                     tpl_blo.push_back(bd.x);
                     tpl_bbase.push_back(base);
-                    base += kTplRows + bd.y - bd.x;
+                    base += (int)blen(bd);
                 }
+                tpl_wend = bands.back().x + (int)blen(bands.back());
                 for (size_t k = 0; k < tb.off.size(); ++k) {
                     const int o = tb.off[k];
                     size_t q = 0;
@@ -489,7 +493,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         } else {
             tpl_blo.clear();
             tpl_bbase.clear();
-            tpl_win = 0;
+            tpl_win = tpl_wend = 0;
             tpl_ldo.reset();
             tpl_id.reset();
             tpl_hdr.reset();
