@@ -12,6 +12,7 @@
 // kernels are bit-identical to oracle/amg_oracle.c.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "device.hpp"
@@ -354,110 +355,155 @@ inline size_t tpl_lds_bytes(int win, int nent) {
     return 8 * ((size_t)win + (size_t)nent + kTplMax + 1) + 4 * ((size_t)nent + kTplMax + 1);
 }
 
-template <int MODE, bool NORM, int NPL>
-__global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
-    constexpr int R = kTplRPL, C = 8;  // C: global-path loads per batch
+struct TplLds {
+    double* win;
+    double* val;
+    double* pd;
+    int* off;
+    int* hdr;
+};
+
+__device__ __forceinline__ TplLds tpl_lds_layout(const TplArgs& a) {
     extern __shared__ double tpl_lds[];
-    double* s_win = tpl_lds;
-    double* s_val = s_win + a.win;
-    double* s_pd = s_val + a.nent;
-    int* s_off = (int*)(s_pd + kTplMax + 1);
-    int* s_hdr = s_off + a.nent;
+    TplLds L;
+    L.win = tpl_lds;
+    L.val = L.win + a.win;
+    L.pd = L.val + a.nent;
+    L.off = (int*)(L.pd + kTplMax + 1);
+    L.hdr = L.off + a.nent;
+    return L;
+}
+
+// x through a buffer descriptor: 32-bit offsets, out-of-range loads return 0 (window slots
+// before row 0 / past row n - 1 are never read)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tpl_xrs(const TplArgs& a) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, (int)((unsigned)a.n * 8u), 0x00020000);
+}
+
+// template table into LDS (L2-resident; the caller's barrier publishes it)
+template <int MODE>
+__device__ __forceinline__ void tpl_stage_table(const TplArgs& a, const TplLds& L) {
     const int tid = threadIdx.x;
-    const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const int r0 = blk * kTplRows;
-    // x through a buffer descriptor: 32-bit offsets, out-of-range loads return 0 (window
-    // slots before row 0 / past row n - 1 are never read)
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)a.x, (short)0, (int)((unsigned)a.n * 8u), 0x00020000);
-    // batch 1: row operands and the x window (independent of each other and of the table)
-    int id[R], rr[R];
-    double pb[R], py[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-        const int r = r0 + kTPB * j + tid;
-        rr[j] = min(r, a.n - 1);
-        const int t = a.id[rr[j]];
-        id[j] = r < a.n ? t : kTplNone;
-        pb[j] = 0.0;
-        py[j] = 0.0;
-        if (MODE == KM_RESID || MODE == KM_JACOBI) pb[j] = a.b[rr[j]];
-        if (MODE == KM_SPMV_ADD) py[j] = a.y[rr[j]];
-    }
-    // window loads.  Workgroups whose window lies inside x (all but the first and last few)
-    // load slot pairs with 16-byte loads (bands start at even offsets and hold an even number
-    // of slots); the others load single slots, out-of-range ones returning 0.
-    const bool pairs = r0 + a.blo[0] >= 0 && r0 + a.wend <= a.n;  // workgroup-uniform
-    constexpr int NP = NPL > 0 ? NPL : 1;
-    double wv[NP];
-    if (NPL > 0 && pairs) {
-#pragma unroll
-        for (int u = 0; u < NP / 2; ++u) {
-            const int i = 2 * (tid + kTPB * u);
-            int lo = a.blo[0], bb = a.bbase[0];
-#pragma unroll
-            for (int q = 1; q < kTplBands; ++q) {
-                const bool in = i >= a.bbase[q];
-                lo = in ? a.blo[q] : lo;
-                bb = in ? a.bbase[q] : bb;
-            }
-            const int vo = i < a.win ? (r0 + lo + (i - bb)) * 8 : -16;
-            const v2d_t p2 = __builtin_bit_cast(v2d_t, __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, 0, 0));
-            wv[2 * u] = p2.x;
-            wv[2 * u + 1] = p2.y;
-        }
-    } else if (NPL > 0) {
-#pragma unroll
-        for (int u = 0; u < NP; ++u) {
-            const int i = tid + kTPB * u;
-            // band of slot i: selects, no branch (bands past nband start at win)
-            int lo = a.blo[0], bb = a.bbase[0];
-#pragma unroll
-            for (int q = 1; q < kTplBands; ++q) {
-                const bool in = i >= a.bbase[q];
-                lo = in ? a.blo[q] : lo;
-                bb = in ? a.bbase[q] : bb;
-            }
-            const int g = r0 + lo + (i - bb);
-            const int vo = i < a.win ? g * 8 : -8;  // negative: past num_records, returns 0
-            wv[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xrs, vo, 0, 0));
-        }
-    }
-    // template table (L2-resident)
     for (int k = tid; k < a.nent; k += kTPB) {
-        s_off[k] = a.off[k];
-        s_val[k] = a.val[k];
+        L.off[k] = a.off[k];
+        L.val[k] = a.val[k];
     }
     if (tid < a.ntpl) {
-        s_hdr[tid] = a.hdr[tid];
-        if (MODE == KM_JACOBI) s_pd[tid] = a.pd[tid];
+        L.hdr[tid] = a.hdr[tid];
+        if (MODE == KM_JACOBI) L.pd[tid] = a.pd[tid];
     }
-    if (tid == kTplNone) s_hdr[kTplNone] = (int)(255u << 24);  // length 0, no diagonal
-    if (NPL > 0 && pairs) {
+    if (tid == kTplNone) L.hdr[kTplNone] = (int)(255u << 24);  // length 0, no diagonal
+}
+
+// the row operands and x window of the rows block starting at r0, into registers
+template <int MODE, int NPL>
+struct TplFetch {
+    static constexpr int R = kTplRPL, NP = NPL > 0 ? NPL : 1;
+    int id[R], rr[R];
+    double pb[R], py[R], wv[NP];
+    bool pairs;
+
+    __device__ __forceinline__ void issue(const TplArgs& a, __amdgpu_buffer_rsrc_t xrs, int r0) {
+        issue_ids(a, r0);
+        issue_operands(a);
+        issue_window(a, xrs, r0);
+    }
+
+    __device__ __forceinline__ void issue_ids(const TplArgs& a, int r0) {
 #pragma unroll
-        for (int u = 0; u < NP / 2; ++u) {
-            const int i = 2 * (tid + kTPB * u);
-            if (i < a.win) *(v2d_t*)(s_win + i) = v2d_t{wv[2 * u], wv[2 * u + 1]};
-        }
-    } else if (NPL > 0) {
-#pragma unroll
-        for (int u = 0; u < NP; ++u) {
-            const int i = tid + kTPB * u;
-            if (i < a.win) s_win[i] = wv[u];
+        for (int j = 0; j < R; ++j) {
+            const int r = r0 + kTPB * j + (int)threadIdx.x;
+            rr[j] = min(r, a.n - 1);
+            const int t = a.id[rr[j]];
+            id[j] = r < a.n ? t : kTplNone;
         }
     }
-    __syncthreads();
-    // per row: template fields (global path: both rows of the lane advance together, C entries
-    // per batch, every load of a batch issued before its first product)
-    int st[R], ln[R], dk[R], L = 0;
+
+    // b / y: needed only by the epilogue
+    __device__ __forceinline__ void issue_operands(const TplArgs& a) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            pb[j] = 0.0;
+            py[j] = 0.0;
+            if (MODE == KM_RESID || MODE == KM_JACOBI) pb[j] = a.b[rr[j]];
+            if (MODE == KM_SPMV_ADD) py[j] = a.y[rr[j]];
+        }
+    }
+
+    __device__ __forceinline__ void issue_window(const TplArgs& a, __amdgpu_buffer_rsrc_t xrs, int r0) {
+        const int tid = threadIdx.x;
+        // Blocks whose window lies inside x (all but the first and last few) load slot pairs
+        // with 16-byte loads (bands start at even offsets and hold an even number of slots);
+        // the others load single slots, out-of-range ones returning 0.
+        pairs = r0 + a.blo[0] >= 0 && r0 + a.wend <= a.n;  // workgroup-uniform
+        if (NPL > 0 && pairs) {
+#pragma unroll
+            for (int u = 0; u < NP / 2; ++u) {
+                const int i = 2 * (tid + kTPB * u);
+                int lo = a.blo[0], bb = a.bbase[0];
+#pragma unroll
+                for (int q = 1; q < kTplBands; ++q) {  // band of slot i: selects, no branch
+                    const bool in = i >= a.bbase[q];
+                    lo = in ? a.blo[q] : lo;
+                    bb = in ? a.bbase[q] : bb;
+                }
+                const int vo = i < a.win ? (r0 + lo + (i - bb)) * 8 : -16;
+                const v2d_t p2 = __builtin_bit_cast(v2d_t, __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, 0, 0));
+                wv[2 * u] = p2.x;
+                wv[2 * u + 1] = p2.y;
+            }
+        } else if (NPL > 0) {
+#pragma unroll
+            for (int u = 0; u < NP; ++u) {
+                const int i = tid + kTPB * u;
+                int lo = a.blo[0], bb = a.bbase[0];
+#pragma unroll
+                for (int q = 1; q < kTplBands; ++q) {
+                    const bool in = i >= a.bbase[q];
+                    lo = in ? a.blo[q] : lo;
+                    bb = in ? a.bbase[q] : bb;
+                }
+                const int vo = i < a.win ? (r0 + lo + (i - bb)) * 8 : -8;  // negative: returns 0
+                wv[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xrs, vo, 0, 0));
+            }
+        }
+    }
+
+    __device__ __forceinline__ void commit(const TplArgs& a, const TplLds& L) const {
+        const int tid = threadIdx.x;
+        if (NPL > 0 && pairs) {
+#pragma unroll
+            for (int u = 0; u < NP / 2; ++u) {
+                const int i = 2 * (tid + kTPB * u);
+                if (i < a.win) *(v2d_t*)(L.win + i) = v2d_t{wv[2 * u], wv[2 * u + 1]};
+            }
+        } else if (NPL > 0) {
+#pragma unroll
+            for (int u = 0; u < NP; ++u) {
+                const int i = tid + kTPB * u;
+                if (i < a.win) L.win[i] = wv[u];
+            }
+        }
+    }
+};
+
+// the rows of one block: sums in CSR order, fused epilogue, y stores; returns the lane's
+// (b - Ax)^2 sum for the norm
+template <int MODE, bool NORM, int NPL>
+__device__ __forceinline__ double tpl_rows(const TplArgs& a, const TplLds& L, __amdgpu_buffer_rsrc_t xrs,
+                                           int r0, const int* id, const int* rr, const double* pb,
+                                           const double* py) {
+    constexpr int R = kTplRPL, C = 8;  // C: global-path loads per batch
+    const int tid = threadIdx.x;
+    int st[R], ln[R], dk[R], Lm = 0;
     double s[R], xr[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-        const unsigned h = (unsigned)s_hdr[id[j]];
+        const unsigned h = (unsigned)L.hdr[id[j]];
         st[j] = (int)(h & 0xffffu);
         ln[j] = (int)((h >> 16) & 0xffu);
         dk[j] = (int)(h >> 24);
-        L = max(L, ln[j]);
+        Lm = max(Lm, ln[j]);
         s[j] = 0.0;
         xr[j] = 0.0;
         // Jacobi needs x[r]; a template without a diagonal entry reads it here (rare)
@@ -469,20 +515,22 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
 #pragma unroll
         for (int j = 0; j < R; ++j)
             for (int k = 0; k < ln[j]; ++k) {
-                const double xv = s_win[s_off[st[j] + k] + kTPB * j + tid];
-                s[j] = s[j] + s_val[st[j] + k] * xv;
+                const double xv = L.win[L.off[st[j] + k] + kTPB * j + tid];
+                s[j] = s[j] + L.val[st[j] + k] * xv;
                 if (MODE == KM_JACOBI) xr[j] = k == dk[j] ? xv : xr[j];
             }
     } else {
+        // global x: both rows of the lane advance together, C entries per batch, every load
+        // of a batch issued before its first product
         const int elast = a.nent - 1;
-        for (int k0 = 0; k0 < L; k0 += C) {
+        for (int k0 = 0; k0 < Lm; k0 += C) {
             double xv[C][R];
 #pragma unroll
             for (int u = 0; u < C; ++u)
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
                     const int k = k0 + u;
-                    const int o = k < ln[j] ? s_off[min(st[j] + k, elast)] : 0;
+                    const int o = k < ln[j] ? L.off[min(st[j] + k, elast)] : 0;
                     xv[u][j] = __builtin_bit_cast(
                         double, __builtin_amdgcn_raw_buffer_load_b64(xrs, (rr[j] + o) * 8, 0, 0));
                 }
@@ -492,7 +540,7 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
                     const int k = k0 + u;
-                    const double p = s_val[min(st[j] + k, elast)] * xv[u][j];
+                    const double p = L.val[min(st[j] + k, elast)] * xv[u][j];
                     s[j] = k < ln[j] ? s[j] + p : s[j];
                     if (MODE == KM_JACOBI) xr[j] = k == dk[j] ? xv[u][j] : xr[j];
                 }
@@ -510,13 +558,72 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
         } else {
             const double t = pb[j] - s[j];
             if (NORM) sq += own ? t * t : 0.0;
-            out = MODE == KM_RESID ? t : xr[j] + a.omega * (s_pd[MODE == KM_JACOBI ? id[j] : 0] * t);
+            out = MODE == KM_RESID ? t : xr[j] + a.omega * (L.pd[MODE == KM_JACOBI ? id[j] : 0] * t);
         }
         if (own) a.y[r0 + kTPB * j + tid] = out;
     }
+    return sq;
+}
+
+template <bool NORM>
+__device__ __forceinline__ void tpl_partial(const TplArgs& a, int blk, double sq) {
     if (NORM) {
         for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
-        if ((tid & 63) == 0) a.partial[blk * kNormParts + (tid >> 6)] = sq;
+        if ((threadIdx.x & 63) == 0) a.partial[blk * kNormParts + (threadIdx.x >> 6)] = sq;
+    }
+}
+
+// one workgroup per block of kTplRows rows
+template <int MODE, bool NORM, int NPL>
+__global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
+    const TplLds L = tpl_lds_layout(a);
+    const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int r0 = blk * kTplRows;
+    TplFetch<MODE, NPL> f;
+    f.issue(a, xrs, r0);  // row operands and window first: independent of the table
+    tpl_stage_table<MODE>(a, L);
+    f.commit(a, L);
+    __syncthreads();
+    tpl_partial<NORM>(a, blk, tpl_rows<MODE, NORM, NPL>(a, L, xrs, r0, f.id, f.rr, f.pb, f.py));
+}
+
+// Persistent form of the window path: a grid of resident workgroups (a multiple of 8), XCD
+// x = blockIdx % 8 owning a contiguous 1/8 of the blocks, its workgroups sweeping them side by
+// side (iteration i: blocks start_x + i * per + lw), so an XCD's L2 holds the planes its
+// workgroups share.  The table is staged once; the next block's row operands and window are
+// fetched into registers while the current block is computed from LDS (double buffering
+// through registers), so the load latency overlaps the arithmetic.
+template <int MODE, bool NORM, int NPL>
+__global__ __launch_bounds__(kTPB, 6) void tpl_persist_kernel(TplArgs a, int nblk) {
+    static_assert(NPL > 0, "window path only");
+    const TplLds L = tpl_lds_layout(a);
+    const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
+    const int x = blockIdx.x & 7, lw = blockIdx.x >> 3, per = gridDim.x >> 3;
+    const int q = nblk >> 3, rem = nblk & 7;
+    const int b0 = x * q + min(x, rem), b1 = b0 + q + (x < rem ? 1 : 0);
+    int blk = b0 + lw;
+    if (blk >= b1) return;  // workgroup-uniform: no barrier is skipped by part of a group
+    // f: the next block's ids and window (registers); c: the current block's row operands
+    TplFetch<MODE, NPL> f, c;
+    f.issue_ids(a, blk * kTplRows);
+    f.issue_window(a, xrs, blk * kTplRows);
+    tpl_stage_table<MODE>(a, L);
+    for (;;) {
+        f.commit(a, L);
+#pragma unroll
+        for (int j = 0; j < kTplRPL; ++j) c.id[j] = f.id[j], c.rr[j] = f.rr[j];
+        c.issue_operands(a);  // b / y: needed only at the end of the rows below
+        __syncthreads();      // window (and, first time, table) visible
+        const int nxt = blk + per;
+        if (nxt < b1) {  // in flight during the rows below
+            f.issue_ids(a, nxt * kTplRows);
+            f.issue_window(a, xrs, nxt * kTplRows);
+        }
+        tpl_partial<NORM>(a, blk, tpl_rows<MODE, NORM, NPL>(a, L, xrs, blk * kTplRows, c.id, c.rr, c.pb, c.py));
+        if (nxt >= b1) break;
+        __syncthreads();  // every wave is done reading the window before it is overwritten
+        blk = nxt;
     }
 }
 
@@ -917,6 +1024,37 @@ int DevMatrix::norm_parts() const {
                     : (nb_int + nb_bnd) * kNormParts;
 }
 
+// window path: the persistent kernel with a grid of exactly the resident workgroups (its
+// blocks are split statically, so a workgroup that waited for a slot would double the tail),
+// or one workgroup per block when that is no more (AMG_TPL_PERSIST=0: always one per block)
+template <int M, bool N, int P>
+static void launch_tpl_window(hipStream_t s, const TplArgs& a, int g, size_t lds) {
+    static const bool allow_persist = [] {
+        const char* e = std::getenv("AMG_TPL_PERSIST");
+        return !(e && std::atoi(e) == 0);
+    }();
+    if constexpr (P > 8) {  // larger windows: the persistent form exceeds the VGPR budget
+        hipLaunchKernelGGL((tpl_kernel<M, N, P>), dim3(g), dim3(kTPB), lds, s, a);
+        return;
+    }
+    thread_local int cus = 0, occ = 0;
+    thread_local size_t occ_lds = 0;
+    if (cus == 0) {
+        int dev = 0;
+        HIP_CHECK(hipGetDevice(&dev));
+        HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    if (occ_lds != lds) {
+        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tpl_persist_kernel<M, N, P>, kTPB, lds));
+        occ_lds = lds;
+    }
+    const int gp = std::min(g, cus * occ) / 8 * 8;
+    if (allow_persist && gp >= 8 && g > gp)
+        hipLaunchKernelGGL((tpl_persist_kernel<M, N, P>), dim3(gp), dim3(kTPB), lds, s, a, g);
+    else
+        hipLaunchKernelGGL((tpl_kernel<M, N, P>), dim3(g), dim3(kTPB), lds, s, a);
+}
+
 void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const double* x,
                 const double* b, double* y, double omega, double* partial) {
     const int g = A.tpl_blocks();
@@ -951,7 +1089,7 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
     const int npl = !win ? 0 : a.win <= 4 * kTPB ? 4 : a.win <= 8 * kTPB ? 8 : a.win <= 12 * kTPB ? 12 : 16;
     AMG_ASSERT(a.win <= npl * kTPB && a.win <= kTplWin);
     const size_t lds = tpl_lds_bytes(a.win, a.nent);
-#define AMG_T2(M, N, P) hipLaunchKernelGGL((tpl_kernel<M, N, P>), dim3(g), dim3(kTPB), lds, s, a)
+#define AMG_T2(M, N, P) launch_tpl_window<M, N, P>(s, a, g, lds)
 #define AMG_T(M, N)                              \
     do {                                         \
         switch (npl) {                           \
@@ -959,7 +1097,7 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
             case 8: AMG_T2(M, N, 8); break;      \
             case 12: AMG_T2(M, N, 12); break;    \
             case 16: AMG_T2(M, N, 16); break;    \
-            default: AMG_T2(M, N, 0); break;     \
+            default: hipLaunchKernelGGL((tpl_kernel<M, N, 0>), dim3(g), dim3(kTPB), lds, s, a); break; \
         }                                        \
     } while (0)
     switch (mode) {
