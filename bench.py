@@ -185,6 +185,22 @@ def main():
     spmv_ms = e0.elapsed_time(e1) / args.spmv_reps
     achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
     csr_equiv = csr_bytes / (spmv_ms * 1e-3) / 1e9
+    # measured STREAM-copy ceiling on this box (report it beside the spec peak):
+    # 1 GiB fp64 device-to-device copy, read + write bytes over HIP-event time
+    copy_gbs = None
+    if rank == 0:
+        with torch.cuda.stream(ctx.stream):
+            src = torch.empty(1 << 27, dtype=torch.float64, device="cuda").fill_(1.0)
+            dst = torch.empty_like(src)
+            for _ in range(3):
+                dst.copy_(src)
+            e0.record(ctx.stream)
+            for _ in range(10):
+                dst.copy_(src)
+            e1.record(ctx.stream)
+        e1.synchronize()
+        copy_gbs = 2 * src.numel() * 8 / (e0.elapsed_time(e1) / 10 * 1e-3) / 1e9
+        del src, dst
     barrier()
 
     traffic = None
@@ -258,6 +274,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "stream_copy_GBps": None if copy_gbs is None else round(copy_gbs, 1),
+                "frac_of_stream_copy": None if copy_gbs is None else round(achieved / copy_gbs, 4),
                 "traffic": None if traffic is None else round(traffic, 1),
                 "traffic_source": traffic_src,
                 "bytes_per_launch": spmv_bytes,

@@ -37,6 +37,9 @@ constexpr int kTplNone = 255;
 constexpr int kTplMax = 255;       // templates per operator
 constexpr int kTplEntries = 1024;  // entries over all templates (staged in LDS per workgroup)
 constexpr int kTplMaxLen = 64;     // entries per template
+#ifndef AMG_TPL_BATCH  // build-time knob: window entries per batch in the template kernel (0: one)
+#define AMG_TPL_BATCH 0
+#endif
 #ifndef AMG_TPL_RPL  // build-time knob for same-box A/B builds (scripts/gpu_libab.sh)
 #define AMG_TPL_RPL 2
 #endif

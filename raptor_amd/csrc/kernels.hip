@@ -509,7 +509,34 @@ __device__ __forceinline__ double tpl_rows(const TplArgs& a, const TplLds& L, __
         // Jacobi needs x[r]; a template without a diagonal entry reads it here (rare)
         if (MODE == KM_JACOBI && dk[j] == 255 && id[j] != kTplNone) xr[j] = a.x[rr[j]];
     }
-    if (NPL > 0) {
+    if constexpr (NPL > 0 && AMG_TPL_BATCH > 0) {
+        // window, batched: both rows of the lane advance together, B entries per batch; the
+        // slot reads of a batch are all issued before the window reads that depend on them,
+        // so a batch waits on LDS twice instead of once per entry (A/B build knob)
+        constexpr int B = AMG_TPL_BATCH > 0 ? AMG_TPL_BATCH : 1;
+        const int elast = a.nent - 1;
+        for (int k0 = 0; k0 < Lm; k0 += B) {
+            int o[B][R];
+            double xv[B][R];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+#pragma unroll
+                for (int j = 0; j < R; ++j) o[u][j] = L.off[min(st[j] + k0 + u, elast)];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+#pragma unroll
+                for (int j = 0; j < R; ++j) xv[u][j] = L.win[o[u][j] + kTPB * j + tid];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const int k = k0 + u;
+                    const double p = L.val[min(st[j] + k, elast)] * xv[u][j];
+                    s[j] = k < ln[j] ? s[j] + p : s[j];
+                    if (MODE == KM_JACOBI) xr[j] = k == dk[j] ? xv[u][j] : xr[j];
+                }
+        }
+    } else if constexpr (NPL > 0) {
         // window: one entry at a time per row (measured faster than 4-entry batches,
         // profiles/r1t_tpl.txt)
 #pragma unroll

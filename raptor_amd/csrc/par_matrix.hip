@@ -593,12 +593,13 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         default_variant = square ? 2 : (4 | 2);
         // format bytes of one default-variant SpMV (the kernel reads every lane slot of the
         // fixed-stride streams, so their padding counts)
-        // with templates: the skipped blocks cost nothing; template rows cost 1 byte (id) and
-        // every template workgroup stages the table (tpl_blocks() * table bytes, L2-resident)
+        // with templates: the skipped blocks cost nothing; template rows cost 1 byte (id); the
+        // table (offsets, values, headers, 1/a_ii) is read from HBM once -- every further
+        // workgroup's staging copy of it is an L2 hit, not HBM traffic
         const int64_t xy = 8 * (n_cols_local + plan.n_halo()) + 8 * n_rows;
         int64_t fb = 2 * n_rows + xy, fb_tpl = xy;
         if (n_tpl > 0)
-            fb_tpl += n_rows + (int64_t)tpl_blocks() * (12 * (int64_t)n_tpl_ent + 4 * (int64_t)n_tpl);
+            fb_tpl += n_rows + 12 * (int64_t)n_tpl_ent + 12 * (int64_t)n_tpl;
         for (size_t q = 0; q < nbk; ++q) {
             const int nz = hh[2 * q].w, nt = hh[2 * q + 1].y & 0xffff;
             const int64_t fb0 = fb;

@@ -29,7 +29,7 @@ def main(prefix):
           f"{'x2_MB':>8s} {'WRITE_MB':>9s} {'L2hit%':>7s}")
     for d in sorted(meta):
         k, g, us, vg, sg, lds = meta[d]
-        if "csr_block" not in k and "gs" not in k:
+        if "csr_block" not in k and "gs" not in k and "tpl" not in k:
             continue
         fe = f[d].get("FETCH_SIZE", 0) / 1024
         wr = w.get(d, {}).get("WRITE_SIZE", 0) / 1024

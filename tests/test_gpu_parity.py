@@ -103,6 +103,9 @@ def test_row_templates_bit_exact(ctx, oracle, problems, monkeypatch, name, ntpl)
     A = _dev_matrix(ra, ctx, Ao)
     assert A.info["n_templates"] == ntpl
     assert A.info["template_rows"] == Ao.shape[0]
+    # roofline numerator: 1-byte id + x + y per row, the table counted once
+    n = Ao.shape[0]
+    assert 17 * n < A.info["spmv_bytes"] <= 17 * n + 12 * (1024 + 255)
     _all_modes_equal(ctx, oracle, A, Ao)
     monkeypatch.setenv("AMG_KERNEL_VARIANT", "10")
     _all_modes_equal(ctx, oracle, A, Ao)
