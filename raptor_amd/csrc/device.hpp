@@ -37,6 +37,9 @@ constexpr int kTplNone = 255;
 constexpr int kTplMax = 255;       // templates per operator
 constexpr int kTplEntries = 1024;  // entries over all templates (staged in LDS per workgroup)
 constexpr int kTplMaxLen = 64;     // entries per template
+#ifndef AMG_CSR_PERSIST_WAVES  // build-time knob: waves/SIMD bound of the persistent x-tile kernel
+#define AMG_CSR_PERSIST_WAVES 6
+#endif
 #ifndef AMG_TPL_BATCH  // build-time knob: window entries per batch in the template kernel (0: one)
 #define AMG_TPL_BATCH 0
 #endif

@@ -109,22 +109,56 @@ __device__ __forceinline__ v2d_t load_pair(const double* base, int q, int n) {
 // are consecutive in it (header diag slot).  VIB: the block's nonzeros take <= 256 distinct
 // values; a 1-byte index per nonzero selects from the table staged in LDS.  NU: lane slots
 // in use (8 = full; the gather path of sparse rectangular blocks uses fewer).
-template <int MODE, bool NORM, bool TILE, bool VIB, int NU>
+// Batch 1 of an x-tile block (depends on the block id only): what the persistent kernel
+// prefetches for its next block while the current one runs.
+struct CsrPre {
+    int4 h0, h1;
+    int tid_line;
+    v4u_t lq;
+    v2u_t vq;
+};
+
+template <bool VI>
+__device__ __forceinline__ void csr_pre_tile(const CsrArgs& a, int bid, CsrPre& p) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    p.h0 = a.hdr[2 * bid];
+    p.h1 = a.hdr[2 * bid + 1];
+    p.tid_line = a.tile_ids[(size_t)bid * kTileLines + 16 * wv + (lane & 15) + 64 * (lane >> 4)];
+    p.lq = __builtin_nontemporal_load((const v4u_t*)(a.lcol + (size_t)bid * kCAP + (size_t)tid * (kCAP / kTPB)));
+    p.vq = v2u_t{0u, 0u};
+    // square operators with value-indexed blocks hold kCAP index bytes for every block
+    if (VI) p.vq = __builtin_nontemporal_load((const v2u_t*)(a.vidx + (size_t)bid * kCAP + (size_t)tid * (kCAP / kTPB)));
+}
+
+// PRE: 0 = load batch 1 here; 1 / 2 = batch 1 comes in *pre, which is then refilled with
+// block nxt's batch 1 (2: with VI indices) unless nxt < 0
+template <int MODE, bool NORM, bool TILE, bool VIB, int NU, int PRE = 0>
 __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* stage, double* tabl,
-                                             int* rends) {
+                                             int* rends, CsrPre* pre = nullptr, int nxt = -1) {
     constexpr int U = kCAP / kTPB;  // 8 lane slots
     static_assert(NU >= 2 && NU % 2 == 0 && NU <= U && (TILE ? NU == U : true), "slot pairs");
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    static_assert(!PRE || TILE, "prefetched batch 1: x-tile path only");
     int tid_line = 0;
+    v4u_t lq = {0u, 0u, 0u, 0u};
+    v2u_t vq = {0u, 0u};
+    int4 h0, h1;
+    if constexpr (PRE > 0) {
+        tid_line = pre->tid_line;
+        lq = pre->lq;
+        vq = pre->vq;
+        h0 = pre->h0;
+        h1 = pre->h1;
+        if (nxt >= 0) csr_pre_tile<PRE == 2>(a, nxt, *pre);  // in flight during this block
+    } else {
     if (TILE) {
         // lane l of wave w fetches line 16w + (l & 15) + 64 (l >> 4): the 64 lines wave w's
         // 16-byte tile slots need (slot j of lane l: line 16w + (l >> 2) + 64j)
         tid_line = a.tile_ids[(size_t)bid * kTileLines + 16 * wv + (lane & 15) + 64 * (lane >> 4)];
     }
-    v4u_t lq = {0u, 0u, 0u, 0u};
     if (TILE) lq = __builtin_nontemporal_load((const v4u_t*)(a.lcol + (size_t)bid * kCAP + (size_t)tid * U));
-    v2u_t vq = {0u, 0u};
-    const int4 h0 = a.hdr[2 * bid], h1 = a.hdr[2 * bid + 1];
+    h0 = a.hdr[2 * bid];
+    h1 = a.hdr[2 * bid + 1];
     if (VIB) {
         if (!a.vi_packed) {
             vq = __builtin_nontemporal_load((const v2u_t*)(a.vidx + (size_t)bid * kCAP + (size_t)tid * U));
@@ -134,6 +168,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
             else if (NU == 4) vq.x = __builtin_nontemporal_load((const unsigned*)p);
             else vq.x = __builtin_nontemporal_load((const unsigned short*)p);
         }
+    }
     }
     const int r0 = h0.x, r1 = h0.y, k0 = h0.z, nnz = h0.w;
     const int r = r0 + tid;
@@ -275,6 +310,40 @@ __device__ __forceinline__ double block_dispatch(const CsrArgs& a, int bid, int 
     }
 }
 
+// empty block, or one row longer than the LDS stage / a tile: chunked, lane 0 sums
+template <int MODE, bool NORM>
+__device__ __forceinline__ double block_long(const CsrArgs& a, int4 h0, double* stage) {
+    const int tid = threadIdx.x;
+    const int r0 = h0.x, r1 = h0.y, k0 = h0.z, nnz = h0.w;
+    double s = 0.0, sq = 0.0;
+    for (int base = 0; base < nnz; base += kCAP) {
+        const int cnt = min(kCAP, nnz - base);
+        for (int k = tid; k < cnt; k += kTPB)
+            stage[k] = a.val[k0 + base + k] * xload(a, a.col[k0 + base + k]);
+        __syncthreads();
+        if (tid == 0)
+            for (int k = 0; k < cnt; ++k) s += stage[k];
+        __syncthreads();
+    }
+    const int r = r0 + tid;
+    if (r < r1 && (tid == 0 || nnz == 0)) {  // nnz == 0: every row of the block is empty
+        double res = 0.0;
+        a.y[r] = epilogue<MODE>(a, r, s, &res);
+        if (NORM) sq = res * res;
+    }
+    return sq;
+}
+
+// fixed-shape wave reduction, one partial per wave (kNormParts per block): no block barrier
+// at the end of the kernel; the partials are summed in fixed order
+template <bool NORM>
+__device__ __forceinline__ void block_partial(const CsrArgs& a, int bid, double sq) {
+    if (NORM) {
+        for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
+        if ((threadIdx.x & 63) == 0) a.partial[a.part_off + bid * kNormParts + (threadIdx.x >> 6)] = sq;
+    }
+}
+
 template <int MODE, bool NORM, bool XCD, bool TILE, bool VI>
 __global__ __launch_bounds__(kTPB, 8) void csr_block_kernel(CsrArgs a, int first_block) {
     static_assert(kCAP / kTPB == 8 && kTileLines * 8 == kCAP && kTPB == 256,
@@ -282,38 +351,53 @@ __global__ __launch_bounds__(kTPB, 8) void csr_block_kernel(CsrArgs a, int first
     __shared__ __attribute__((aligned(16))) double stage[kCAP];  // x tile, then products
     __shared__ double tabl[VI ? 256 : 1];
     __shared__ int rends[kTPB];
-    const int tid = threadIdx.x;
     const int bid = first_block + (XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x);
     const int4 h0 = a.hdr[2 * bid], h1 = a.hdr[2 * bid + 1];
-    const int r0 = h0.x, r1 = h0.y, k0 = h0.z, nnz = h0.w;
-    double sq = 0.0;
+    const int nnz = h0.w;
+    double sq;
     if (nnz <= kCAP && (!TILE || (h1.y & 0xffff) <= kTileLines) && nnz > 0) {
         if (VI && h1.z >= 0) sq = block_dispatch<MODE, NORM, TILE, true>(a, bid, nnz, stage, tabl, rends);
         else sq = block_dispatch<MODE, NORM, TILE, false>(a, bid, nnz, stage, tabl, rends);
     } else {
-        // empty block, or one row longer than the LDS stage / a tile: chunked, lane 0 sums
-        double s = 0.0;
-        for (int base = 0; base < nnz; base += kCAP) {
-            const int cnt = min(kCAP, nnz - base);
-            for (int k = tid; k < cnt; k += kTPB)
-                stage[k] = a.val[k0 + base + k] * xload(a, a.col[k0 + base + k]);
-            __syncthreads();
-            if (tid == 0)
-                for (int k = 0; k < cnt; ++k) s += stage[k];
-            __syncthreads();
-        }
-        const int r = r0 + tid;
-        if (r < r1 && (tid == 0 || nnz == 0)) {  // nnz == 0: every row of the block is empty
-            double res = 0.0;
-            a.y[r] = epilogue<MODE>(a, r, s, &res);
-            if (NORM) sq = res * res;
-        }
+        sq = block_long<MODE, NORM>(a, h0, stage);
     }
-    if (NORM) {
-        // fixed-shape wave reduction, one partial per wave (kNormParts per block): no
-        // block barrier at the end of the kernel; the partials are summed in fixed order
-        for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
-        if ((tid & 63) == 0) a.partial[a.part_off + bid * kNormParts + (tid >> 6)] = sq;
+    block_partial<NORM>(a, bid, sq);
+}
+
+// Persistent form of the x-tile path (variant bit 64): a resident grid (a multiple of 8), XCD
+// x = blockIdx % 8 owning a contiguous 1/8 of the blocks, its workgroups sweeping them side by
+// side.  Each workgroup issues the next block's batch 1 (header, tile line ids, tile and VI
+// indices) before the current block's batch 2, so a block waits on one round of loads
+// instead of two.  Same blocks, same per-block code: bit-identical results and partials.
+template <int MODE, bool NORM, bool VI>
+__global__ __launch_bounds__(kTPB, AMG_CSR_PERSIST_WAVES) void csr_persist_kernel(CsrArgs a, int first_block, int nblk) {
+    __shared__ __attribute__((aligned(16))) double stage[kCAP];
+    __shared__ double tabl[VI ? 256 : 1];
+    __shared__ int rends[kTPB];
+    const int x = blockIdx.x & 7, lw = blockIdx.x >> 3, per = gridDim.x >> 3;
+    const int q = nblk >> 3, rem = nblk & 7;
+    const int b0 = x * q + min(x, rem), b1 = b0 + q + (x < rem ? 1 : 0);
+    int blk = b0 + lw;
+    if (blk >= b1) return;  // workgroup-uniform
+    constexpr int PV = VI ? 2 : 1;
+    CsrPre f;
+    csr_pre_tile<VI>(a, first_block + blk, f);
+    for (;;) {
+        const int bid = first_block + blk, nxt = blk + per;
+        const int nb = nxt < b1 ? first_block + nxt : -1;
+        const int4 h0 = f.h0, h1 = f.h1;
+        double sq;
+        if (h0.w <= kCAP && (h1.y & 0xffff) <= kTileLines && h0.w > 0) {
+            if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV>(a, bid, stage, tabl, rends, &f, nb);
+            else sq = block_main<MODE, NORM, true, false, 8, PV>(a, bid, stage, tabl, rends, &f, nb);
+        } else {
+            if (nb >= 0) csr_pre_tile<VI>(a, nb, f);
+            sq = block_long<MODE, NORM>(a, h0, stage);
+        }
+        block_partial<NORM>(a, bid, sq);
+        if (nxt >= b1) break;
+        __syncthreads();  // stage / tabl / rends are rewritten by the next block
+        blk = nxt;
     }
 }
 
@@ -1145,6 +1229,41 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
     HIP_CHECK(hipGetLastError());
 }
 
+template <int M, bool N, bool V>
+static void launch_csr_persist_t(hipStream_t s, const CsrArgs& a, int first_block, int nb) {
+    static int occ = 0;  // resident workgroups per CU (same for every operator)
+    if (occ == 0) HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, csr_persist_kernel<M, N, V>, kTPB, 0));
+    int dev = 0, ncu = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const int g = std::max(8, std::min(nb, std::max(1, occ) * ncu) / 8 * 8);
+    hipLaunchKernelGGL((csr_persist_kernel<M, N, V>), dim3(g), dim3(kTPB), 0, s, a, first_block, nb);
+}
+
+static void launch_csr_persist(hipStream_t s, int mode, bool norm, const CsrArgs& a, int first_block,
+                               int nb, bool vi) {
+#define AMG_P(M, N)                                              \
+    do {                                                         \
+        if (vi) launch_csr_persist_t<M, N, true>(s, a, first_block, nb);  \
+        else launch_csr_persist_t<M, N, false>(s, a, first_block, nb);    \
+    } while (0)
+    switch (mode) {
+        case KM_SPMV: AMG_P(KM_SPMV, false); break;
+        case KM_SPMV_ADD: AMG_P(KM_SPMV_ADD, false); break;
+        case KM_RESID:
+            if (norm) AMG_P(KM_RESID, true);
+            else AMG_P(KM_RESID, false);
+            break;
+        case KM_JACOBI:
+            if (norm) AMG_P(KM_JACOBI, true);
+            else AMG_P(KM_JACOBI, false);
+            break;
+        default: throw Error(AMG_ERR_INTERNAL, "bad kernel mode");
+    }
+#undef AMG_P
+    HIP_CHECK(hipGetLastError());
+}
+
 void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, int first_block,
                        int n_blocks, const double* x, const double* b, double* y, double omega,
                        double* partial, int part_off) {
@@ -1156,6 +1275,10 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
               b, A.dinv.p, y, omega, partial, part_off};
     dim3 g(n_blocks), t(kTPB);
     const int var = kernel_variant(A);
+    if ((var & 64) && !(var & 4)) {
+        launch_csr_persist(s, mode, norm, a, first_block, n_blocks, (var & 8) != 0);
+        return;
+    }
 #define AMG_L1(M, N, X, T, V) hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V>), g, t, 0, s, a, first_block)
 #define AMG_L2(M, N, V)                                               \
     do {                                                              \

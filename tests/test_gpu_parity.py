@@ -92,6 +92,42 @@ def _all_modes_equal(ctx, O, A, Ao, seed=3):
     assert abs(rn - ro) <= 1e-12 * ro
 
 
+@pytest.mark.parametrize("var", [74, 66], ids=["persist_vi", "persist"])
+@pytest.mark.parametrize("name", ["7pt_20", "5pt_37x29", "27pt_13", "ragged"])
+def test_persistent_tile_kernel_bit_exact(ctx, oracle, problems, monkeypatch, name, var):
+    """Variant bit 64: the persistent x-tile kernel -- resident grid,
+    next block's batch 1 prefetched -- gives the oracle's bits in every mode, with and
+    without value-indexed blocks, including the long-row and empty-row blocks of "ragged"."""
+    import raptor_amd as ra
+
+    monkeypatch.setenv("AMG_KERNEL_VARIANT", str(var))
+    Ao = problems[name]
+    A = _dev_matrix(ra, ctx, Ao)
+    _all_modes_equal(ctx, oracle, A, Ao)
+
+
+def test_persistent_tile_kernel_vcycle(ctx, monkeypatch):
+    """A PMIS V-cycle on the persistent x-tile kernel (coarse Galerkin operators: VI and
+    fp64-value blocks) reproduces the default kernels' iterates and history bit for bit."""
+    import raptor_amd as ra
+
+    A = ra.par_stencil_grid(ctx, "7pt", (40, 36, 33))
+    n = A.local_rows
+    b = ra.vector_uniform(ctx, n, 0, 7)
+    res = []
+    for var in (None, "106"):
+        if var is None:
+            monkeypatch.delenv("AMG_KERNEL_VARIANT", raising=False)
+        else:
+            monkeypatch.setenv("AMG_KERNEL_VARIANT", var)
+        ml = ra.ParRugeStubenSolver(coarsen="pmis", use_graph=False).setup(A)
+        x = ctx.zeros(n)
+        _, h = ml.solve(x, b, max_iter=4)
+        res.append((to_host(ctx, x), h))
+    assert np.array_equal(res[0][0], res[1][0])
+    assert np.array_equal(res[0][1], res[1][1])
+
+
 @pytest.mark.parametrize("name,ntpl", [("7pt_20", 27), ("5pt_37x29", 9), ("27pt_13", 27)])
 def test_row_templates_bit_exact(ctx, oracle, problems, monkeypatch, name, ntpl):
     """Stencil operators are stored as row templates: one template per boundary
