@@ -434,9 +434,11 @@ struct TplArgs {
     double* partial;
 };
 
-// dynamic LDS: window | values | 1/a_ii | entry slots or offsets | headers
-inline size_t tpl_lds_bytes(int win, int nent) {
-    return 8 * ((size_t)win + (size_t)nent + kTplMax + 1) + 4 * ((size_t)nent + kTplMax + 1);
+// dynamic LDS: window | values | 1/a_ii (Jacobi only) | entry slots or offsets | headers.
+// (Leaving out the 2 KiB of 1/a_ii outside Jacobi measured neutral on the 7-pt SpMV,
+// profiles/r1t_lds_ab.txt; kept because it costs nothing.)
+inline size_t tpl_lds_bytes(int win, int nent, bool jacobi) {
+    return 8 * ((size_t)win + (size_t)nent + (jacobi ? kTplMax + 1 : 0)) + 4 * ((size_t)nent + kTplMax + 1);
 }
 
 struct TplLds {
@@ -447,13 +449,14 @@ struct TplLds {
     int* hdr;
 };
 
+template <int MODE>
 __device__ __forceinline__ TplLds tpl_lds_layout(const TplArgs& a) {
     extern __shared__ double tpl_lds[];
     TplLds L;
     L.win = tpl_lds;
     L.val = L.win + a.win;
     L.pd = L.val + a.nent;
-    L.off = (int*)(L.pd + kTplMax + 1);
+    L.off = (int*)(L.pd + (MODE == KM_JACOBI ? kTplMax + 1 : 0));
     L.hdr = L.off + a.nent;
     return L;
 }
@@ -687,7 +690,7 @@ __device__ __forceinline__ void tpl_partial(const TplArgs& a, int blk, double sq
 // one workgroup per block of kTplRows rows
 template <int MODE, bool NORM, int NPL>
 __global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
-    const TplLds L = tpl_lds_layout(a);
+    const TplLds L = tpl_lds_layout<MODE>(a);
     const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int r0 = blk * kTplRows;
@@ -708,7 +711,7 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
 template <int MODE, bool NORM, int NPL>
 __global__ __launch_bounds__(kTPB, 6) void tpl_persist_kernel(TplArgs a, int nblk) {
     static_assert(NPL > 0, "window path only");
-    const TplLds L = tpl_lds_layout(a);
+    const TplLds L = tpl_lds_layout<MODE>(a);
     const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
     const int x = blockIdx.x & 7, lw = blockIdx.x >> 3, per = gridDim.x >> 3;
     const int q = nblk >> 3, rem = nblk & 7;
@@ -1199,7 +1202,7 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
     a.partial = partial;
     const int npl = !win ? 0 : a.win <= 4 * kTPB ? 4 : a.win <= 8 * kTPB ? 8 : a.win <= 12 * kTPB ? 12 : 16;
     AMG_ASSERT(a.win <= npl * kTPB && a.win <= kTplWin);
-    const size_t lds = tpl_lds_bytes(a.win, a.nent);
+    const size_t lds = tpl_lds_bytes(a.win, a.nent, mode == KM_JACOBI);
 #define AMG_T2(M, N, P) launch_tpl_window<M, N, P>(s, a, g, lds)
 #define AMG_T(M, N)                              \
     do {                                         \
