@@ -190,6 +190,10 @@ struct DevMatrix {
     // tpl_win = window size in doubles, 0 = the bands do not fit (global x loads)
     std::vector<int> tpl_blo, tpl_bbase;
     DevBuf<int> tpl_ldo;
+    // z-marching (variant bit 128): stride in blocks between a block and the one whose window
+    // it reuses (0: no useful shift), and per window slot the source slot (-1: load)
+    int tpl_march_s = 0;
+    DevBuf<int> tpl_wsrc;
     int tpl_win = 0, tpl_wend = 0;
     DevBuf<double> tpl_val, tpl_pd;
     int n_tpl = 0, n_tpl_ent = 0, nb_skip = 0;

@@ -432,6 +432,8 @@ struct TplArgs {
     double* y;
     double omega;
     double* partial;
+    const int* wsrc;  // march (variant bit 128): per window slot, the slot of the block one
+                      // stride back that holds the same x (-1: load it)
 };
 
 // dynamic LDS: window | values | 1/a_ii (Jacobi only) | entry slots or offsets | headers.
@@ -738,6 +740,77 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_persist_kernel(TplArgs a, int nbl
         if (nxt >= b1) break;
         __syncthreads();  // every wave is done reading the window before it is overwritten
         blk = nxt;
+    }
+}
+
+// z-marching form of the window path (variant bit 128).  Workgroup chains
+// walk blocks c, c + S, c + 2S, ... (S blocks = the shift D the host found, e.g. one plane of
+// the 7-pt operator), so the -plane band and the middle of the centre band of a block are
+// the previous block's centre and +plane bands: those slots are copied inside LDS (wsrc) and
+// only the rest is loaded -- 1024 instead of 2048 doubles per 7-pt block.  The next block's
+// loaded slots and row ids are prefetched into registers during the current block.
+template <int MODE, bool NORM, int NPL>
+__global__ __launch_bounds__(kTPB, 6) void tpl_march_kernel(TplArgs a, int nblk, int S, int nchunk) {
+    static_assert(NPL > 0, "window path only");
+    const TplLds L = tpl_lds_layout<MODE>(a);
+    const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
+    const int tid = threadIdx.x;
+    int gof[NPL], src[NPL];
+#pragma unroll
+    for (int u = 0; u < NPL; ++u) {
+        const int i = tid + kTPB * u;
+        int lo = a.blo[0], bb = a.bbase[0];
+#pragma unroll
+        for (int q = 1; q < kTplBands; ++q) {
+            const bool in = i >= a.bbase[q];
+            lo = in ? a.blo[q] : lo;
+            bb = in ? a.bbase[q] : bb;
+        }
+        gof[u] = lo + (i - bb);
+        src[u] = i < a.win ? a.wsrc[i] : -2;  // -2: slot past the window
+    }
+    tpl_stage_table<MODE>(a, L);
+    const int K = (nblk + S - 1) / S;         // blocks per column
+    const int per = (K + nchunk - 1) / nchunk;  // blocks per chain
+    TplFetch<MODE, NPL> f, c;
+    double gv[NPL];
+    for (int ch = blockIdx.x; ch < S * nchunk; ch += gridDim.x) {
+        const int col = ch % S, t0 = (ch / S) * per, t1 = min(K, t0 + per);
+        if (t0 >= t1 || col + S * t0 >= nblk) continue;  // workgroup-uniform
+        // first block of the chain: every slot from x
+        f.issue_ids(a, (col + S * t0) * kTplRows);
+#pragma unroll
+        for (int u = 0; u < NPL; ++u)
+            gv[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                xrs, src[u] != -2 ? ((col + S * t0) * kTplRows + gof[u]) * 8 : -8, 0, 0));
+        for (int t = t0; t < t1; ++t) {
+            const int blk = col + S * t;
+            if (blk >= nblk) break;  // uniform
+            const int r0 = blk * kTplRows;
+            const bool first = t == t0;
+            double wv[NPL];
+#pragma unroll
+            for (int u = 0; u < NPL; ++u) wv[u] = (!first && src[u] >= 0) ? L.win[src[u]] : gv[u];
+#pragma unroll
+            for (int j = 0; j < kTplRPL; ++j) c.id[j] = f.id[j], c.rr[j] = f.rr[j];
+            c.issue_operands(a);
+            __syncthreads();  // every wave is done with the previous window (rows and copies)
+#pragma unroll
+            for (int u = 0; u < NPL; ++u)
+                if (src[u] != -2) L.win[tid + kTPB * u] = wv[u];
+            __syncthreads();
+            const int nb = blk + S;
+            if (t + 1 < t1 && nb < nblk) {  // in flight during the rows below
+                f.issue_ids(a, nb * kTplRows);
+#pragma unroll
+                for (int u = 0; u < NPL; ++u)
+                    gv[u] = src[u] == -1 ? __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                               xrs, (nb * kTplRows + gof[u]) * 8, 0, 0))
+                                         : 0.0;
+            }
+            tpl_partial<NORM>(a, blk, tpl_rows<MODE, NORM, NPL>(a, L, xrs, r0, c.id, c.rr, c.pb, c.py));
+        }
+        __syncthreads();  // the next chain's first window overwrites this one
     }
 }
 
@@ -1169,6 +1242,20 @@ static void launch_tpl_window(hipStream_t s, const TplArgs& a, int g, size_t lds
         hipLaunchKernelGGL((tpl_kernel<M, N, P>), dim3(g), dim3(kTPB), lds, s, a);
 }
 
+template <int M, bool N, int P>
+static void launch_tpl_march(hipStream_t s, const TplArgs& a, int g, size_t lds, int S) {
+    if constexpr (P > 0) {
+        int occ = 0, dev = 0, ncu = 0;
+        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tpl_march_kernel<M, N, P>, kTPB, lds));
+        HIP_CHECK(hipGetDevice(&dev));
+        HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        const int res = std::max(1, occ) * ncu;                // resident workgroups
+        const int nchunk = std::max(1, res / S);               // chains per column
+        const int gp = std::max(1, std::min(res, S * nchunk));
+        hipLaunchKernelGGL((tpl_march_kernel<M, N, P>), dim3(gp), dim3(kTPB), lds, s, a, g, S, nchunk);
+    }
+}
+
 void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const double* x,
                 const double* b, double* y, double omega, double* partial) {
     const int g = A.tpl_blocks();
@@ -1203,7 +1290,13 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
     const int npl = !win ? 0 : a.win <= 4 * kTPB ? 4 : a.win <= 8 * kTPB ? 8 : a.win <= 12 * kTPB ? 12 : 16;
     AMG_ASSERT(a.win <= npl * kTPB && a.win <= kTplWin);
     const size_t lds = tpl_lds_bytes(a.win, a.nent, mode == KM_JACOBI);
-#define AMG_T2(M, N, P) launch_tpl_window<M, N, P>(s, a, g, lds)
+    const bool march = win && A.tpl_march_s > 0 && (kernel_variant(A) & 128);
+    if (march) a.wsrc = A.tpl_wsrc.p;
+#define AMG_T2(M, N, P)                                                     \
+    do {                                                                    \
+        if (march) launch_tpl_march<M, N, P>(s, a, g, lds, A.tpl_march_s);  \
+        else launch_tpl_window<M, N, P>(s, a, g, lds);                      \
+    } while (0)
 #define AMG_T(M, N)                              \
     do {                                         \
         switch (npl) {                           \

@@ -489,6 +489,49 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 }
                 tpl_win = base;
                 tpl_ldo.upload(ldo.data(), ldo.size());
+                // z-marching: the shift D (a multiple of kTplRows, taken from the band
+                // starts) under which the most window slots of a block are slots of the block
+                // D rows back; used when at least a quarter of the window is reused
+                const int nbd = (int)bands.size();
+                auto reuse_map = [&](int64_t D, std::vector<int>* map) {
+                    int cnt = 0;
+                    for (int q = 0; q < nbd; ++q) {
+                        const int len = (q + 1 < nbd ? tpl_bbase[q + 1] : base) - tpl_bbase[q];
+                        for (int i = 0; i < len; ++i) {
+                            const int64_t g = D + tpl_blo[q] + i;  // relative to the old r0
+                            int src = -1;
+                            for (int q2 = 0; q2 < nbd && src < 0; ++q2) {
+                                const int len2 = (q2 + 1 < nbd ? tpl_bbase[q2 + 1] : base) - tpl_bbase[q2];
+                                const int64_t j = g - tpl_blo[q2];
+                                if (j >= 0 && j < len2) src = tpl_bbase[q2] + (int)j;
+                            }
+                            if (map) (*map)[tpl_bbase[q] + i] = src;
+                            cnt += src >= 0;
+                        }
+                    }
+                    return cnt;
+                };
+                int64_t bestD = 0;
+                int best = 0;
+                std::vector<int64_t> cand;
+                for (int q = 0; q < nbd; ++q) {
+                    cand.push_back(std::abs((int64_t)tpl_blo[q]));
+                    for (int q2 = q + 1; q2 < nbd; ++q2) cand.push_back((int64_t)tpl_blo[q2] - tpl_blo[q]);
+                }
+                for (int64_t D : cand) {
+                    D -= D % kTplRows;
+                    if (D <= 0 || D / kTplRows > INT_MAX / 2) continue;
+                    const int c = reuse_map(D, nullptr);
+                    if (c > best) best = c, bestD = D;
+                }
+                tpl_march_s = 0;
+                tpl_wsrc.reset();
+                if (bestD > 0 && 4 * best >= base) {
+                    std::vector<int> map(base, -1);
+                    reuse_map(bestD, &map);
+                    tpl_march_s = (int)(bestD / kTplRows);
+                    tpl_wsrc.upload(map.data(), map.size());
+                }
             }
         } else {
             tpl_blo.clear();

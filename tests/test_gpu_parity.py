@@ -147,6 +147,45 @@ def test_row_templates_bit_exact(ctx, oracle, problems, monkeypatch, name, ntpl)
     _all_modes_equal(ctx, oracle, A, Ao)
 
 
+@pytest.mark.parametrize("dims", [(40, 40, 40), (37, 41, 29)])
+@pytest.mark.parametrize("kind", ["7pt", "27pt"])
+def test_row_templates_march_bit_exact(ctx, oracle, monkeypatch, kind, dims):
+    """Variant bit 128: z-marching template kernel -- window slots shared with
+    the block one shift back are copied inside LDS -- bit-identical in every mode.  Planes of
+    1600 / 1517 rows (not multiples of the 512-row block): the shift is the largest multiple
+    of 512 below, so only part of the window is reused, every chain start reloads it all."""
+    import raptor_amd as ra
+
+    O = oracle
+    Ao = O.gen_7pt(*dims) if kind == "7pt" else O.gen_27pt(*dims)
+    monkeypatch.setenv("AMG_KERNEL_VARIANT", "170")
+    A = _dev_matrix(ra, ctx, Ao)
+    assert A.info["template_rows"] == Ao.shape[0]
+    _all_modes_equal(ctx, O, A, Ao)
+
+
+def test_row_templates_march_vcycle(ctx, monkeypatch):
+    """PMIS V-cycle with the z-marching template kernel on level 0 (7-pt 64^3: plane = 8
+    blocks, the whole -plane band and half the centre band reused) == default kernels."""
+    import raptor_amd as ra
+
+    A = ra.par_stencil_grid(ctx, "7pt", (64, 64, 64))
+    n = A.local_rows
+    b = ra.vector_uniform(ctx, n, 0, 9)
+    res = []
+    for var in (None, "170"):
+        if var is None:
+            monkeypatch.delenv("AMG_KERNEL_VARIANT", raising=False)
+        else:
+            monkeypatch.setenv("AMG_KERNEL_VARIANT", var)
+        ml = ra.ParRugeStubenSolver(coarsen="pmis", use_graph=False).setup(A)
+        x = ctx.zeros(n)
+        _, h = ml.solve(x, b, max_iter=3)
+        res.append((to_host(ctx, x), h))
+    assert np.array_equal(res[0][0], res[1][0])
+    assert np.array_equal(res[0][1], res[1][1])
+
+
 def test_row_templates_partial_cover(ctx, oracle, monkeypatch):
     """Mixed operator: more distinct row shapes than templates (300 perturbed diagonals), a
     row longer than a template holds (100 entries) and an empty row.  With the size floor
