@@ -751,14 +751,17 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_persist_kernel(TplArgs a, int nbl
 // loaded slots and row ids are prefetched into registers during the current block.
 template <int MODE, bool NORM, int NPL>
 __global__ __launch_bounds__(kTPB, 6) void tpl_march_kernel(TplArgs a, int nblk, int S, int nchunk) {
-    static_assert(NPL > 0, "window path only");
+    static_assert(NPL > 0 && NPL % 2 == 0, "window path, slot pairs");
+    constexpr int NP = NPL / 2;  // slot pairs per lane (16-byte loads and LDS copies)
     const TplLds L = tpl_lds_layout<MODE>(a);
     const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
     const int tid = threadIdx.x;
-    int gof[NPL], src[NPL];
+    // pair u of this lane: slots i, i + 1 with i = 2 (tid + kTPB u); bands have even starts
+    // and lengths and the shift is even, so both slots of a pair share their source
+    int gof[NP], src[NP];
 #pragma unroll
-    for (int u = 0; u < NPL; ++u) {
-        const int i = tid + kTPB * u;
+    for (int u = 0; u < NP; ++u) {
+        const int i = 2 * (tid + kTPB * u);
         int lo = a.blo[0], bb = a.bbase[0];
 #pragma unroll
         for (int q = 1; q < kTplBands; ++q) {
@@ -767,46 +770,50 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_march_kernel(TplArgs a, int nblk,
             bb = in ? a.bbase[q] : bb;
         }
         gof[u] = lo + (i - bb);
-        src[u] = i < a.win ? a.wsrc[i] : -2;  // -2: slot past the window
+        src[u] = i < a.win ? a.wsrc[i] : -2;  // -2: pair past the window
     }
     tpl_stage_table<MODE>(a, L);
-    const int K = (nblk + S - 1) / S;         // blocks per column
+    const int K = (nblk + S - 1) / S;           // blocks per column
     const int per = (K + nchunk - 1) / nchunk;  // blocks per chain
+    // chains ordered (chunk, column); XCD x = blockIdx % 8 takes a contiguous 1/8 of them, so
+    // the workgroups of one XCD walk neighbouring columns of the same planes side by side
+    const int C = S * nchunk, x = blockIdx.x & 7, lw = blockIdx.x >> 3, nw = gridDim.x >> 3;
+    const int c0 = x * (C >> 3) + min(x, C & 7), c1 = c0 + (C >> 3) + (x < (C & 7) ? 1 : 0);
     TplFetch<MODE, NPL> f, c;
-    double gv[NPL];
-    for (int ch = blockIdx.x; ch < S * nchunk; ch += gridDim.x) {
+    v2d_t gv[NP];
+    for (int ch = c0 + lw; ch < c1; ch += nw) {
         const int col = ch % S, t0 = (ch / S) * per, t1 = min(K, t0 + per);
         if (t0 >= t1 || col + S * t0 >= nblk) continue;  // workgroup-uniform
-        // first block of the chain: every slot from x
+        // first block of the chain: every pair from x (out-of-range pairs load 0)
         f.issue_ids(a, (col + S * t0) * kTplRows);
 #pragma unroll
-        for (int u = 0; u < NPL; ++u)
-            gv[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
-                xrs, src[u] != -2 ? ((col + S * t0) * kTplRows + gof[u]) * 8 : -8, 0, 0));
+        for (int u = 0; u < NP; ++u)
+            gv[u] = __builtin_bit_cast(v2d_t, __builtin_amdgcn_raw_buffer_load_b128(
+                xrs, src[u] != -2 ? ((col + S * t0) * kTplRows + gof[u]) * 8 : -16, 0, 0));
         for (int t = t0; t < t1; ++t) {
             const int blk = col + S * t;
             if (blk >= nblk) break;  // uniform
             const int r0 = blk * kTplRows;
             const bool first = t == t0;
-            double wv[NPL];
+            v2d_t wv[NP];
 #pragma unroll
-            for (int u = 0; u < NPL; ++u) wv[u] = (!first && src[u] >= 0) ? L.win[src[u]] : gv[u];
+            for (int u = 0; u < NP; ++u) wv[u] = (!first && src[u] >= 0) ? *(const v2d_t*)(L.win + src[u]) : gv[u];
 #pragma unroll
             for (int j = 0; j < kTplRPL; ++j) c.id[j] = f.id[j], c.rr[j] = f.rr[j];
             c.issue_operands(a);
             __syncthreads();  // every wave is done with the previous window (rows and copies)
 #pragma unroll
-            for (int u = 0; u < NPL; ++u)
-                if (src[u] != -2) L.win[tid + kTPB * u] = wv[u];
+            for (int u = 0; u < NP; ++u)
+                if (src[u] != -2) *(v2d_t*)(L.win + 2 * (tid + kTPB * u)) = wv[u];
             __syncthreads();
             const int nb = blk + S;
             if (t + 1 < t1 && nb < nblk) {  // in flight during the rows below
                 f.issue_ids(a, nb * kTplRows);
 #pragma unroll
-                for (int u = 0; u < NPL; ++u)
-                    gv[u] = src[u] == -1 ? __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                for (int u = 0; u < NP; ++u)
+                    gv[u] = src[u] == -1 ? __builtin_bit_cast(v2d_t, __builtin_amdgcn_raw_buffer_load_b128(
                                                xrs, (nb * kTplRows + gof[u]) * 8, 0, 0))
-                                         : 0.0;
+                                         : v2d_t{0.0, 0.0};
             }
             tpl_partial<NORM>(a, blk, tpl_rows<MODE, NORM, NPL>(a, L, xrs, r0, c.id, c.rr, c.pb, c.py));
         }
@@ -1189,13 +1196,16 @@ void launch_append(hipStream_t s, const double* v, double* hist, int* counter) {
 
 int kernel_variant(const DevMatrix& A) {
     // variant bits: 2 = XCD-ordered blocks, 4 = gather path (no x tile), 8 = value-indexed
-    // blocks (when any block qualifies), 32 = row templates (when built).  Default
+    // blocks (when any block qualifies), 32 = row templates (when built), 64 = persistent
+    // x-tile kernel (off by default), 128 = z-marching template windows (when a shift with
+    // enough reuse exists; profiles/r1t_march_ab.txt).  Default
     // (DevMatrix::default_variant): x tile for square operators, gather for rectangular ones
     // (stored without tiles), both in XCD order (profiles/r1m_variants.txt), VI and templates
     // where built.  AMG_KERNEL_VARIANT overrides the bits (experiments,
     // scripts/spmv_variants.py; results are identical).
     const char* ev = getenv("AMG_KERNEL_VARIANT");
-    int var = ev ? atoi(ev) : (A.default_variant | (A.n_vi_blocks > 0 ? 8 : 0) | (A.n_tpl > 0 ? 32 : 0));
+    int var = ev ? atoi(ev) : (A.default_variant | (A.n_vi_blocks > 0 ? 8 : 0) | (A.n_tpl > 0 ? 32 : 0) |
+                                (A.tpl_march_s > 0 ? 128 : 0));
     if (A.n_vi_blocks == 0) var &= ~8;
     if (A.n_tpl == 0) var &= ~32;
     // each operator is stored for one kernel: square -> x tile, rectangular -> gather
@@ -1249,9 +1259,9 @@ static void launch_tpl_march(hipStream_t s, const TplArgs& a, int g, size_t lds,
         HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tpl_march_kernel<M, N, P>, kTPB, lds));
         HIP_CHECK(hipGetDevice(&dev));
         HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-        const int res = std::max(1, occ) * ncu;                // resident workgroups
-        const int nchunk = std::max(1, res / S);               // chains per column
-        const int gp = std::max(1, std::min(res, S * nchunk));
+        const int res = std::max(8, std::max(1, occ) * ncu / 8 * 8);  // resident workgroups
+        const int nchunk = std::max(1, res / S);                        // chains per column
+        const int gp = std::max(8, std::min(res, (S * nchunk + 7) / 8 * 8));
         hipLaunchKernelGGL((tpl_march_kernel<M, N, P>), dim3(gp), dim3(kTPB), lds, s, a, g, S, nchunk);
     }
 }

@@ -526,7 +526,8 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 }
                 tpl_march_s = 0;
                 tpl_wsrc.reset();
-                if (bestD > 0 && 4 * best >= base) {
+                // 16-byte pair loads: an even row count keeps every pair inside or outside x
+                if (bestD > 0 && 4 * best >= base && n_rows % 2 == 0) {
                     std::vector<int> map(base, -1);
                     reuse_map(bestD, &map);
                     tpl_march_s = (int)(bestD / kTplRows);

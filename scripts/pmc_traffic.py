@@ -26,7 +26,7 @@ def main(prefix, out):
     # level-0 operator = first matrix in pmc_levels.py: its first 3 SpMV launches (the
     # row-template kernel where the operator is templated, else the CSR block kernel)
     spmv = [d for d in sorted(meta)
-            if any(k in meta[d][0] for k in ("tpl_kernel<0", "tpl_persist_kernel<0", "csr_block_kernel<0"))]
+            if any(k in meta[d][0] for k in ("tpl_kernel<0", "tpl_persist_kernel<0", "tpl_march_kernel<0", "csr_block_kernel<0"))]
     ds = [d for d in spmv if meta[d] == meta[spmv[0]]][:3]
     fetch = sum(f[d]["FETCH_SIZE"] for d in ds) / len(ds) * 1024
     write = sum(w[d]["WRITE_SIZE"] for d in ds) / len(ds) * 1024

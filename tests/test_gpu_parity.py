@@ -152,8 +152,9 @@ def test_row_templates_bit_exact(ctx, oracle, problems, monkeypatch, name, ntpl)
 def test_row_templates_march_bit_exact(ctx, oracle, monkeypatch, kind, dims):
     """Variant bit 128: z-marching template kernel -- window slots shared with
     the block one shift back are copied inside LDS -- bit-identical in every mode.  Planes of
-    1600 / 1517 rows (not multiples of the 512-row block): the shift is the largest multiple
-    of 512 below, so only part of the window is reused, every chain start reloads it all."""
+    1600 rows (not a multiple of the 512-row block): the shift is the largest multiple of 512
+    below, so only part of the window is reused, every chain start reloads it all.  The odd
+    row count of 37x41x29 turns the march off (16-byte pairs): the window kernel runs."""
     import raptor_amd as ra
 
     O = oracle
