@@ -439,6 +439,8 @@ struct TplArgs {
 // dynamic LDS: window | values | 1/a_ii (Jacobi only) | entry slots or offsets | headers.
 // (Leaving out the 2 KiB of 1/a_ii outside Jacobi measured neutral on the 7-pt SpMV,
 // profiles/r1t_lds_ab.txt; kept because it costs nothing.)
+// (A 1/a_ii table of ntpl instead of 256 entries -- 8 instead of 7 Jacobi workgroups per CU
+// -- made the 7-pt Jacobi slower, 102 -> 120 us, profiles/r1u_pdtrim_ab.txt.)
 inline size_t tpl_lds_bytes(int win, int nent, bool jacobi) {
     return 8 * ((size_t)win + (size_t)nent + (jacobi ? kTplMax + 1 : 0)) + 4 * ((size_t)nent + kTplMax + 1);
 }
@@ -1197,15 +1199,17 @@ void launch_append(hipStream_t s, const double* v, double* hist, int* counter) {
 int kernel_variant(const DevMatrix& A) {
     // variant bits: 2 = XCD-ordered blocks, 4 = gather path (no x tile), 8 = value-indexed
     // blocks (when any block qualifies), 32 = row templates (when built), 64 = persistent
-    // x-tile kernel (off by default), 128 = z-marching template windows (when a shift with
-    // enough reuse exists; profiles/r1t_march_ab.txt).  Default
+    // x-tile kernel (off by default), 128 = z-marching template windows (default when a
+    // shift with enough reuse exists and the window is <= 2048 doubles: 7-pt level 0 74.5 vs
+    // 80.6 us, profiles/r1u_march_ab.txt; the 27-pt window of 3078 doubles ran 204 vs 154 us,
+    // profiles/r1u_sa27_kernel_stats.csv against r1t).  Default
     // (DevMatrix::default_variant): x tile for square operators, gather for rectangular ones
     // (stored without tiles), both in XCD order (profiles/r1m_variants.txt), VI and templates
     // where built.  AMG_KERNEL_VARIANT overrides the bits (experiments,
     // scripts/spmv_variants.py; results are identical).
     const char* ev = getenv("AMG_KERNEL_VARIANT");
     int var = ev ? atoi(ev) : (A.default_variant | (A.n_vi_blocks > 0 ? 8 : 0) | (A.n_tpl > 0 ? 32 : 0) |
-                                (A.tpl_march_s > 0 ? 128 : 0));
+                                (A.tpl_march_s > 0 && A.tpl_win <= 8 * kTPB ? 128 : 0));
     if (A.n_vi_blocks == 0) var &= ~8;
     if (A.n_tpl == 0) var &= ~32;
     // each operator is stored for one kernel: square -> x tile, rectangular -> gather
