@@ -1,0 +1,82 @@
+"""One rank of tests/test_gpu_rccl.py: the product's RCCL transport, one process per rank.
+
+Launched by the test as a child process (never imported by it) with RANK / WORLD_SIZE /
+MASTER_* set.  Every rank joins a gloo group (setup-time exchange) and an RCCL communicator
+(solve-time halo exchange, norm and coarse allgathers), runs the level kernels and a few
+V-cycles on its z-slab, and writes its slices to ``<out>.<rank>.npz``.  The parent compares
+them with the serial oracle: this is the path the bench takes for --gpus N > 1.
+
+The development boxes have one GPU and RCCL refuses two ranks on one device of one host, so
+the test gives each rank its own NCCL_HOSTID: RCCL then treats the ranks as separate hosts and
+moves the data over its socket transport on the loopback interface.  Every call the product
+makes (ncclSend/ncclRecv groups on the comm stream, ncclAllGather, graph capture of both) is
+the same call it makes over xGMI on an 8-GPU node; only the wire differs.
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    spec = json.loads(sys.argv[1])
+    out = sys.argv[2]
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    import raptor_amd as ra
+
+    ctx = ra.Context.distributed(0)
+    A = ra.par_stencil_grid(ctx, spec["kind"], spec["dims"])
+    f, m = A.first_row, A.local_rows
+    res = {"f": f, "m": m, "n_halo": A.info["n_halo"]}
+
+    def host(t):
+        ctx.synchronize()
+        return t.detach().cpu().numpy().copy()
+
+    with torch.cuda.stream(ctx.stream):
+        x = ra.vector_uniform(ctx, m, f, 3)
+        b = ra.vector_uniform(ctx, m, f, 4)
+        y = ctx.empty(m)
+    A.mult(x, y)
+    res["y"] = host(y)
+    A.residual(x, b, y)
+    res["r"] = host(y)
+    A.jacobi(x, b, y)
+    res["j"] = host(y)
+    res["rn"] = A.residual_norm(x, b)
+
+    ml = ra.ParMultilevel(coarsen=spec["coarsen"], smoother=spec["smoother"],
+                          replicate_below=spec["rep"], use_graph=spec["graph"]).setup(A)
+    res["levels"] = ml.num_levels
+    res["starts"] = np.array([ml.level_matrix(l, "A").first_row for l in range(ml.num_levels)])
+    with torch.cuda.stream(ctx.stream):
+        xs = ra.vector_uniform(ctx, m, f, 42)
+        bb = ctx.empty(m)
+    A.mult(xs, bb)
+    dx = ctx.zeros(m)
+    for k in range(3):
+        ml.cycle(dx, bb)
+        res[f"x{k}"] = host(dx)
+    dx = ctx.zeros(m)
+    _, hist = ml.solve(dx, bb, max_iter=6)
+    res["hist"] = hist
+    res["xsolve"] = host(dx)
+    dx = ctx.zeros(m)
+    _, hp = ml.pcg(dx, bb, max_iter=5)
+    res["pcg"] = hp
+    np.savez(f"{out}.{rank}.npz", **res)
+    dist.barrier()
+    del ml, A
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,109 @@
+"""The RCCL transport itself: N processes, one rank each, the
+product's ncclSend/ncclRecv halo groups and ncclAllGather norms / coarse gathers, checked
+bit-for-bit against the serial oracle (the loopback tests in test_gpu_multirank.py cover the
+same plans with device copies instead of RCCL).
+
+On a 1-GPU box RCCL refuses two ranks of one host on one device ("Duplicate GPU detected"),
+so each rank gets its own NCCL_HOSTID and RCCL connects them with its socket transport over
+`lo`; the product's calls are unchanged (tests/rccl_worker.py).  On a multi-GPU node the
+same test runs with NCCL_HOSTID unset and ranks on distinct devices would use xGMI; here all
+ranks share device 0."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_rccl(nranks, spec, tmp_path, timeout=240):
+    port = _free_port()
+    out = str(tmp_path / "rank")
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ)
+        env.update(RANK=str(r), WORLD_SIZE=str(nranks), LOCAL_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   NCCL_HOSTID=f"raptor-amd-rank-{r}", NCCL_SOCKET_IFNAME="lo",
+                   GLOO_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
+                   HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(ROOT, "tests", "rccl_worker.py"), json.dumps(spec), out],
+            env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    logs = []
+    try:
+        for p in procs:
+            o, _ = p.communicate(timeout=timeout)
+            logs.append(o.decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{logs[r][-4000:]}"
+    return [dict(np.load(f"{out}.{r}.npz")) for r in range(nranks)]
+
+
+CASES = [
+    (2, dict(kind="7pt", dims=[16, 15, 18], coarsen="pmis", smoother="jacobi", rep=0)),
+    (2, dict(kind="7pt", dims=[16, 15, 18], coarsen="pmis", smoother="jacobi", rep=800)),
+    (3, dict(kind="27pt", dims=[10, 11, 16], coarsen="sa", smoother="hybrid_gs", rep=0)),
+    (8, dict(kind="7pt", dims=[24, 24, 64], coarsen="pmis", smoother="jacobi", rep=0)),
+    (8, dict(kind="7pt", dims=[24, 24, 64], coarsen="sa", smoother="hybrid_gs", rep=65536)),
+]
+
+
+@pytest.mark.parametrize("graph", [False], ids=["eager"])
+@pytest.mark.parametrize("nranks,spec", CASES,
+                         ids=[f"{n}r-{s['kind']}-{s['coarsen']}-rep{s['rep']}" for n, s in CASES])
+def test_rccl_vcycle_bit_exact(oracle, tmp_path, nranks, spec, graph):
+    O = oracle
+    spec = dict(spec, graph=graph)
+    res = run_rccl(nranks, spec, tmp_path)
+    Ao = {"7pt": O.gen_7pt, "27pt": O.gen_27pt}[spec["kind"]](*spec["dims"])
+    n = Ao.shape[0]
+    assert sum(int(r["m"]) for r in res) == n
+    x, b = O.vec_uniform(n, 3), O.vec_uniform(n, 4)
+    ref = {"y": Ao.spmv(x), "r": Ao.residual(x, b), "j": Ao.jacobi(x, b, 2.0 / 3.0)}
+    rn = O.norm2(ref["r"])
+    for r in res:
+        f, m = int(r["f"]), int(r["m"])
+        assert int(r["n_halo"]) > 0
+        for k in ("y", "r", "j"):
+            assert np.array_equal(r[k], ref[k][f:f + m]), k
+        assert abs(float(r["rn"]) - rn) <= 1e-12 * rn
+    smoother = O.SMOOTH_JACOBI if spec["smoother"] == "jacobi" else O.SMOOTH_HYBRID_GS
+    Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS[spec["coarsen"]], smoother=smoother))
+    assert all(int(r["levels"]) == Ho.num_levels for r in res)
+    for l in range(Ho.num_levels):
+        Ho.set_cuts(l, sorted({int(r["starts"][l]) for r in res}))
+    bo = Ao.spmv(O.vec_uniform(n, 42))
+    xo = np.zeros(n)
+    for k in range(3):
+        xo = Ho.cycle(xo, bo)
+        for r in res:
+            f, m = int(r["f"]), int(r["m"])
+            assert np.array_equal(r[f"x{k}"], xo[f:f + m]), ("cycle", k)
+    xso, hist_o = Ho.solve(np.zeros(n), bo, max_iter=6)
+    _, pcg_o = Ho.pcg(np.zeros(n), bo, max_iter=5)
+    for r in res:
+        f, m = int(r["f"]), int(r["m"])
+        assert np.array_equal(r["xsolve"], xso[f:f + m])
+        assert np.all(np.abs(r["hist"] - hist_o) <= 1e-10 * hist_o)
+        assert np.all(np.abs(r["pcg"] - pcg_o) <= 1e-9 * pcg_o[0])
+        assert np.array_equal(r["hist"], res[0]["hist"])  # every rank reports the same
