@@ -10,10 +10,12 @@ problem.  Timed: K steps of amg_solver_solve (no host sync inside), barrier + de
 both sides, max over ranks.  value = V-cycles/s x (global rows / 256^3): 256^3-equivalent
 V-cycles per second, the whole-job aggregate (equals plain iterations/s at N=1).
 
-roofline: the level-0 ParCSRMatrix::mult kernel (tpl_kernel / csr_block_kernel), timed live with HIP
-events on the context stream; bytes = the stored format's HBM bytes per launch (DESIGN.md 4;
-value-indexed blocks stream 1-byte indices instead of fp64 values), with the plain-CSR
-equivalent 12 nnz + 4 (n+1) + 16 n reported beside it.
+roofline: the level-0 ParCSRMatrix::mult on the plain CSR format (csr_plain_kernel: int32 row_ptr
+/ col, fp64 val) timed live with HIP events on the context stream, scored on SURVEY.md 8(d)'s
+algorithmic bytes 12 nnz + 4 (n+1) + 16 n.  roofline_stored: the same mult in the product's
+default format (row templates / CSR-VI blocks) on the bytes that format streams.
+vcycle_kernels: every V-cycle operation of the large levels (eager, events), stored bytes and
+fraction of the 8 TB/s peak; the hipGraph'd durations are in profiles/ (rocprofv3).
 cpu_baseline (rank 0, N=1): the oracle's V-cycle (C, OpenMP) on the same hierarchy and
 inputs, timed for --cpu-seconds; "port" = this repo's CPU restatement (the reference
 has no AMG code).
@@ -155,52 +157,114 @@ def main():
     conv = float((hist[-1] / hist[0]) ** (1.0 / max(1, len(hist) - 1))) if hist[0] > 0 else None
     log(rank, f"{args.steps} V-cycles in {dt * 1e3:.2f} ms -> {iters_per_s:.1f} it/s, conv {conv}")
 
-    # algorithmic bytes of one V-cycle, all ranks (the per-iteration residual norm is fused
-    # into the next cycle's first Jacobi sweep: no extra bytes except the last one)
-    cyc_bytes_local = ml.bytes_per_cycle()
-    if world > 1:
-        t = torch.tensor([cyc_bytes_local], dtype=torch.float64)
+    # bytes of one V-cycle on all ranks: plain-CSR and stored-format (what
+    # the kernels stream).  The per-iteration residual norm is fused into the next cycle's
+    # first sweep, so a solve iteration moves one cycle's bytes.
+    def allsum(v):
+        if world == 1:
+            return float(v)
+        t = torch.tensor([float(v)], dtype=torch.float64)
         dist.all_reduce(t)
-        cyc_bytes = float(t.item())
-    else:
-        cyc_bytes = float(cyc_bytes_local)
+        return float(t.item())
 
-    # roofline: level-0 SpMV, HIP events on the context stream.  Numerator = the bytes the
-    # kernel must move in the stored format (A.info["spmv_bytes"]: block headers, x-tile ids,
-    # 16-bit tile indices, 1-byte value indices + tables or fp64 values, row_ptr, x, y); the
-    # plain-CSR figure 12 nnz + 4 (n+1) + 16 n is reported beside it (csr_equiv_*)
-    csr_bytes = 12 * A.nnz + 4 * (n + 1) + 16 * n
-    spmv_bytes = int(A.info["spmv_bytes"])
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    for _ in range(5):
-        A.mult(x, y)
-    barrier()
-    with torch.cuda.stream(ctx.stream):
-        e0.record(ctx.stream)
-        for _ in range(args.spmv_reps):
-            A.mult(x, y)
-        e1.record(ctx.stream)
-    e1.synchronize()
-    spmv_ms = e0.elapsed_time(e1) / args.spmv_reps
-    achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
-    csr_equiv = csr_bytes / (spmv_ms * 1e-3) / 1e9
-    # measured STREAM-copy ceiling on this box (report it beside the spec peak):
-    # 1 GiB fp64 device-to-device copy, read + write bytes over HIP-event time
-    copy_gbs = None
-    if rank == 0:
+    cyc_bytes = allsum(ml.bytes_per_cycle())
+    cyc_stored = allsum(sum(i["stored_bytes_per_cycle_local"] for i in infos))
+
+    # ---- level kernels, timed live with HIP events on the context stream -----------------
+    n = A.local_rows
+
+    def timed(fn, reps, flush=None):
+        """avg ms per launch of fn() over reps (HIP events on the context stream).  flush:
+        run before each launch and excluded (cache-cold timing: a 1 GiB copy evicts the
+        256 MiB Infinity Cache and the L2s)."""
         with torch.cuda.stream(ctx.stream):
-            src = torch.empty(1 << 27, dtype=torch.float64, device="cuda").fill_(1.0)
-            dst = torch.empty_like(src)
             for _ in range(3):
-                dst.copy_(src)
-            e0.record(ctx.stream)
-            for _ in range(10):
-                dst.copy_(src)
-            e1.record(ctx.stream)
-        e1.synchronize()
-        copy_gbs = 2 * src.numel() * 8 / (e0.elapsed_time(e1) / 10 * 1e-3) / 1e9
-        del src, dst
+                fn()
+            if flush is None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(ctx.stream)
+                for _ in range(reps):
+                    fn()
+                e1.record(ctx.stream)
+                e1.synchronize()
+                return e0.elapsed_time(e1) / reps
+            tot = 0.0
+            for _ in range(reps):
+                flush()
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(ctx.stream)
+                fn()
+                e1.record(ctx.stream)
+                e1.synchronize()
+                tot += e0.elapsed_time(e1)
+            return tot / reps
+
+    fl_src = ctx.empty(1 << 27)
+    fl_dst = ctx.empty(1 << 27)
+    with torch.cuda.stream(ctx.stream):
+        fl_src.fill_(1.0)
+
+    def flush():
+        ra.vector_copy(ctx, fl_src, fl_dst)
+
+    barrier()
+    # roofline (SURVEY.md 8(d)): level-0 ParCSRMatrix::mult on the plain CSR format -- int32
+    # row_ptr, int32 col, fp64 val, exactly the arrays 8(d) prices -- scored on 8(d)'s
+    # algorithmic bytes 12 nnz + 4 (n+1) + 8 (cols + halo) + 8 n
+    A.set_format("csr")
+    csr_bytes = int(A.info["csr_bytes"])
+    csr_ms = timed(lambda: A.mult(x, y), args.spmv_reps)
+    csr_cold_ms = timed(lambda: A.mult(x, y), 10, flush)
+    A.set_format("auto")
+    # the product's default format on the same operator (row templates / CSR-VI blocks),
+    # scored on the bytes that format streams
+    spmv_bytes = int(A.info["spmv_bytes"])
+    spmv_ms = timed(lambda: A.mult(x, y), args.spmv_reps)
+    spmv_cold_ms = timed(lambda: A.mult(x, y), 10, flush)
+    # measured STREAM-copy ceiling (SURVEY.md 8d): the 16-byte nontemporal copy kernel, 1 GiB
+    copy_ms = timed(flush, 10)
+    copy_gbs = 2 * fl_src.numel() * 8 / (copy_ms * 1e-3) / 1e9
+    barrier()
+
+    # per-level V-cycle kernels (rank 0's share; eager launches of the ops the cycle runs, on
+    # levels whose kernels outlast the launch overhead).  The in-graph durations are in the
+    # rocprofv3 summary committed under profiles/.
+    table = []
+    gs = sa27 or g3
+    for l in range(nlev - 1):
+        if infos[l]["n_global"] // world < 100000:  # same decision on every rank
+            break
+        Al = A if l == 0 else ml.level_matrix(l, "A")
+        nl = Al.local_rows
+        P, R = ml.level_matrix(l, "P"), ml.level_matrix(l, "R")
+        nc = P.local_cols
+        with torch.cuda.stream(ctx.stream):
+            xl, bl, tl = ra.vector_uniform(ctx, nl, 0, 5), ra.vector_uniform(ctx, nl, 0, 6), ctx.empty(nl)
+            xc, bc = ra.vector_uniform(ctx, nc, 0, 7), ctx.empty(R.local_rows)
+        ai, pi, ri = Al.info, P.info, R.info
+        if gs:
+            Al.hybrid_gs(xl, bl, tl, 64)  # builds the sliced-ELL copy if the cycle has not
+            ai = Al._info()
+            ops = [("pre GS (forward)", lambda: Al.hybrid_gs(xl, bl, tl, 64), ai["gs_bytes"]),
+                   ("residual", lambda: Al.residual(xl, bl, tl), ai["residual_bytes"]),
+                   ("restrict R r", lambda: R.mult(tl, bc), ri["spmv_bytes"]),
+                   ("interp x += P e", lambda: P.mult_add(xc, xl), pi["mult_add_bytes"]),
+                   ("post GS (backward)", lambda: Al.hybrid_gs(xl, bl, tl, 64, backward=True), ai["gs_bytes"])]
+        else:
+            ops = [("Jacobi", lambda: Al.jacobi(xl, bl, tl), ai["jacobi_bytes"]),
+                   ("residual", lambda: Al.residual(xl, bl, tl), ai["residual_bytes"]),
+                   ("restrict R r", lambda: R.mult(tl, bc), ri["spmv_bytes"]),
+                   ("interp x += P e", lambda: P.mult_add(xc, xl), pi["mult_add_bytes"])]
+        for name, fn, nbytes in ops:
+            ms = timed(fn, 10)
+            table.append({"level": l, "op": name, "us": round(ms * 1e3, 1), "stored_bytes": int(nbytes),
+                          "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                          "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+        del xl, bl, tl, xc, bc
+    dominant = max(table, key=lambda t: t["us"]) if table else None
+    del fl_src, fl_dst
     barrier()
 
     traffic = None
@@ -209,10 +273,9 @@ def main():
             and os.path.exists(args.traffic_json)):
         try:
             tj = json.load(open(args.traffic_json))
-            traffic = float(tj["traffic_bytes"]) / (spmv_ms * 1e-3) / 1e9
-            traffic_src = (f"{os.path.relpath(args.traffic_json, ROOT)}: "
-                           f"{tj['traffic_bytes'] / 1e9:.3f} GB/launch (2xFETCH_SIZE+WRITE_SIZE) "
-                           "over this run's avg launch time")
+            traffic = float(tj["traffic_bytes"])
+            traffic_src = (f"{os.path.relpath(args.traffic_json, ROOT)}: {tj.get('kernel', 'level-0 SpMV')}, "
+                           "2xFETCH_SIZE+WRITE_SIZE per launch (MI355X_MICROARCH.md correction)")
         except (OSError, KeyError, ValueError):
             traffic = None
 
@@ -261,32 +324,49 @@ def main():
             },
             "iters_per_s": round(iters_per_s, 3),
             "convergence_factor": conv,
-            "vcycle_bytes": cyc_bytes,
-            "vcycle_effective_GBps": round(cyc_bytes * iters_per_s / 1e9, 1),
+            # bytes one cycle streams in the stored formats (<= peak x time) and the plain-CSR
+            # count of SURVEY.md 8(d) (what a CSR implementation of the same cycle would move)
+            "vcycle_stored_bytes": cyc_stored,
+            "vcycle_stored_GBps": round(cyc_stored * iters_per_s / 1e9, 1),
+            "vcycle_csr_equiv_bytes": cyc_bytes,
             "roofline": {
                 "bound": "hbm",
-                "kernel": ("tpl_kernel<SPMV> (row templates" +
-                           (")" if A.info["template_rows"] == A.local_rows else " + csr_block_kernel)") +
-                           " level-0 ParCSRMatrix::mult, rank 0"
-                           if A.info["template_rows"] > 0 else
-                           "csr_block_kernel<SPMV> (level-0 ParCSRMatrix::mult, rank 0)"),
-                "achieved": round(achieved, 1),
+                "kernel": "csr_plain_kernel<SPMV> -- level-0 ParCSRMatrix::mult, plain CSR "
+                          "(AMG_FORMAT_CSR: int32 row_ptr/col, fp64 val), rank 0",
+                "achieved": round(csr_bytes / (csr_ms * 1e-3) / 1e9, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "stream_copy_GBps": None if copy_gbs is None else round(copy_gbs, 1),
-                "frac_of_stream_copy": None if copy_gbs is None else round(achieved / copy_gbs, 4),
-                "traffic": None if traffic is None else round(traffic, 1),
+                "frac": round(csr_bytes / (csr_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "traffic": None if traffic is None else round(traffic / 1e9, 4),
+                "traffic_unit": "GB per launch",
                 "traffic_source": traffic_src,
+                "bytes_per_launch": csr_bytes,
+                "bytes_definition": "SURVEY.md 8(d): 12 nnz + 4 (n+1) + 8 (local + halo cols) + 8 n",
+                "avg_launch_ms": round(csr_ms, 5),
+                "cold_avg_launch_ms": round(csr_cold_ms, 5),
+                "cold_GBps": round(csr_bytes / (csr_cold_ms * 1e-3) / 1e9, 1),
+                "stream_copy_GBps": round(copy_gbs, 1),
+                "frac_of_stream_copy": round(csr_bytes / (csr_ms * 1e-3) / 1e9 / copy_gbs, 4),
+            },
+            "roofline_stored": {
+                "kernel": (("tpl_march_kernel" if A.info["tpl_march_shift"] > 0 else "tpl_kernel") +
+                           "<SPMV> (row templates" +
+                           (")" if A.info["template_rows"] == A.local_rows else " + csr_block_kernel)")
+                           if A.info["template_rows"] > 0 else "csr_block_kernel<SPMV> (CSR-VI blocks)") +
+                          " -- level-0 mult, default format, rank 0",
+                "achieved": round(spmv_bytes / (spmv_ms * 1e-3) / 1e9, 1),
+                "frac": round(spmv_bytes / (spmv_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "bytes_per_launch": spmv_bytes,
                 "bytes_definition": "stored-format HBM bytes per launch (DESIGN.md 4)",
                 "avg_launch_ms": round(spmv_ms, 5),
-                "vi_blocks_frac": round(A.info["n_vi_blocks"] / max(1, A.info["n_blocks"]), 4),
+                "cold_avg_launch_ms": round(spmv_cold_ms, 5),
+                "csr_speedup": round(csr_ms / spmv_ms, 3),
                 "row_templates": A.info["n_templates"],
                 "template_rows_frac": round(A.info["template_rows"] / max(1, A.local_rows), 4),
-                "csr_equiv_bytes_per_launch": csr_bytes,
-                "csr_equiv_GBps": round(csr_equiv, 1),
+                "vi_blocks_frac": round(A.info["n_vi_blocks"] / max(1, A.info["n_blocks"]), 4),
             },
+            "vcycle_kernels": table,
+            "vcycle_dominant_kernel": dominant,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
@@ -294,8 +374,22 @@ def main():
         dist.destroy_process_group()
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(ml, b, seconds, scale, hybrid_gs=False):
-    """Oracle V-cycle (C, OpenMP) on the product's own level operators, rank 0, N=1."""
+    """Oracle V-cycle (C, OpenMP) on the product's own level operators, rank 0, N=1.
+
+    Threads = OpenMP's default team (OMP_NUM_THREADS, which the GPU box sets to its CPU
+    share of 16); `nproc` and the affinity mask are recorded beside it (the box's nproc
+    counts the whole machine, which this job does not own)."""
     import numpy as np
 
     from oracle import oracle as O
@@ -326,13 +420,23 @@ def cpu_baseline(ml, b, seconds, scale, hybrid_gs=False):
         if el >= seconds:
             break
     rate = k / el * scale
+    threads = int(O.lib().orc_num_threads())
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return {
         "value": round(rate, 4),
         "unit": "V-cycles/s" if scale == 1.0 else "V-cycles/s (256^3-equivalent)",
-        "cores": int(O.lib().orc_num_threads()),
+        "cores": threads,
         "kind": "port",
-        "sample": f"{k} oracle V-cycles (C/OpenMP, same hierarchy and b) in {el:.1f}s; "
-                  "reference has no AMG CPU path (SURVEY.md 0)",
+        "cpu_model": _cpu_model(),
+        "nproc": os.cpu_count(),
+        "affinity_cpus": affinity,
+        "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+        "sample": f"{k} oracle V-cycles (C/OpenMP, {threads} threads, same hierarchy and b) in "
+                  f"{el:.1f}s; build CPU restatement, not RAPtor (the reference has no AMG CPU "
+                  "path, SURVEY.md 0)",
     }
 
 

@@ -118,8 +118,29 @@ typedef struct amg_matrix_info {
                             * index/value streams, row_ptr, x (once), y                  */
     int32_t n_templates;   /* row templates built (0: none; <= 255)                      */
     int64_t template_rows; /* rows mult() runs through the row-template kernel           */
+    int32_t format;        /* AMG_FORMAT_* in effect                                     */
+    int32_t kernel_variant;/* level-kernel variant bits in effect           */
+    int64_t csr_bytes;     /* SURVEY.md 8(d) plain-CSR SpMV bytes: 12 nnz + 4 (n+1) +     *
+                            * 8 (local + halo columns) + 8 n                              */
+    int32_t tpl_window;    /* template x window, doubles per workgroup (0: none)         */
+    int32_t tpl_lanes;     /* window doubles loaded per lane (4, 8, 12, 16; 0: none)      */
+    int32_t tpl_march_shift; /* z-marching shift in 512-row blocks (0: no march)          */
+    int64_t mult_add_bytes;  /* stored-format bytes of mult_add / residual / jacobi        */
+    int64_t residual_bytes;
+    int64_t jacobi_bytes;
+    int64_t gs_bytes;        /* sliced-ELL bytes of one hybrid GS sweep (0: not built)     */
 } amg_matrix_info;
 int amg_par_csr_info(amg_matrix A, amg_matrix_info* info);
+
+/* Storage format the level kernels of A use (rows a2-a4).  AUTO (default): row templates
+ * where rows share a shape, CSR blocks with x tiles and value indexing elsewhere
+ * (DESIGN.md 4.0-4.1).  BLOCKS: CSR blocks on every row.  CSR: plain CSR -- int32 row_ptr,
+ * int32 col, fp64 val, exactly the arrays SURVEY.md 8(d) prices (the roofline leg; DESIGN.md
+ * 4.5); selecting it uploads those arrays once.  Results are bit-identical in every format. */
+#define AMG_FORMAT_AUTO 0
+#define AMG_FORMAT_CSR 1
+#define AMG_FORMAT_BLOCKS 2
+int amg_par_csr_set_format(amg_matrix A, int32_t format);
 /* Host copy of the local rows (global column ids). */
 int amg_par_csr_export(amg_matrix A, int64_t* row_ptr, int64_t* col_global, double* val);
 
@@ -179,7 +200,10 @@ typedef struct amg_level_info {
     int64_t n_global, nnz_global;          /* A_l                                        */
     int64_t n_local, nnz_local;
     int64_t p_nnz_local, r_nnz_local;      /* P_l, R_l (0 on the coarsest level)         */
-    int64_t bytes_per_cycle_local;         /* algorithmic HBM bytes this level moves     */
+    int64_t bytes_per_cycle_local;         /* plain-CSR bytes of the level's
+                                              share of one V-cycle                         */
+    int64_t stored_bytes_per_cycle_local;  /* the same, in the stored formats the kernels
+                                              stream (templates, CSR-VI blocks, sliced ELL) */
 } amg_level_info;
 int amg_solver_level_info(amg_solver S, int32_t level, amg_level_info* info);
 /* which: 0 = A_l, 1 = P_l, 2 = R_l.  Borrowed handle, valid while S lives. */
@@ -242,6 +266,9 @@ int amg_host_csr_destroy(amg_host_csr A);
 /* out[i] = uniform(-1,1) from splitmix64(seed, first_gid + i) on the device. */
 int amg_vector_uniform(amg_context ctx, int64_t n, int64_t first_gid, uint64_t seed,
                        double* out);
+/* dst = src on the context stream (16-byte nontemporal copy kernel; 16-byte aligned device
+ * pointers).  bench.py times it as the box's STREAM-copy ceiling. */
+int amg_vector_copy(amg_context ctx, int64_t n, const double* src, double* dst);
 
 #ifdef __cplusplus
 }

@@ -23,6 +23,9 @@ import os
 import numpy as np
 
 from ._lib import (  # noqa: F401  (re-exported constants)
+    AMG_FORMAT_AUTO,
+    AMG_FORMAT_BLOCKS,
+    AMG_FORMAT_CSR,
     AMG_COARSEN_PMIS,
     AMG_REORDER_RCM,
     AMG_COARSEN_RS,
@@ -243,6 +246,16 @@ class ParCSRMatrix:
         return ParCSRMatrix(self.ctx, h), perm
 
     # ---- level kernels (ParCSRMatrix::mult & friends) -------------------------------
+    _FORMATS = {"auto": AMG_FORMAT_AUTO, "csr": AMG_FORMAT_CSR, "blocks": AMG_FORMAT_BLOCKS}
+
+    def set_format(self, fmt: str):
+        """Storage format of the level kernels: "auto" (row templates + CSR blocks, default),
+        "blocks" (CSR blocks with x tiles / value indexing on every row) or "csr" (plain
+        row_ptr / col / val, the SURVEY.md 8(d) format).  Results are identical."""
+        check(lib().amg_par_csr_set_format(self.h, self._FORMATS[fmt]))
+        self.info = self._info()
+        return self
+
     def mult(self, x, y):
         check(lib().amg_par_csr_mult(self.h, _ptr(x), _ptr(y)))
         return y
@@ -320,6 +333,14 @@ def read_par_matrix(ctx: Context, path) -> ParCSRMatrix:
     h = C.c_void_p()
     check(lib().amg_par_csr_read(ctx.h, os.fsencode(path), C.byref(h)))
     return ParCSRMatrix(ctx, h)
+
+
+def vector_copy(ctx: Context, src, dst):
+    """dst = src with the 16-byte nontemporal copy kernel (the bench's copy ceiling)."""
+    if src.numel() != dst.numel():
+        raise ValueError("vector_copy: sizes differ")
+    check(lib().amg_vector_copy(ctx.h, int(src.numel()), _ptr(src), _ptr(dst)))
+    return dst
 
 
 def vector_uniform(ctx: Context, n: int, first_gid: int = 0, seed: int = 42):

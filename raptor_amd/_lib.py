@@ -16,6 +16,7 @@ AMG_COARSEN_RS, AMG_COARSEN_PMIS, AMG_COARSEN_SA = 0, 1, 2
 AMG_SMOOTH_JACOBI, AMG_SMOOTH_HYBRID_GS = 0, 1
 AMG_PRESET_PMIS_JACOBI, AMG_PRESET_RS_JACOBI, AMG_PRESET_SA_HYBRID_GS = 0, 1, 2
 AMG_REORDER_RCM = 1
+AMG_FORMAT_AUTO, AMG_FORMAT_CSR, AMG_FORMAT_BLOCKS = 0, 1, 2
 
 ERROR_NAMES = {1: "INVALID", 2: "HIP", 3: "RCCL", 4: "COMM", 5: "INTERNAL", 6: "NOMEM"}
 
@@ -60,6 +61,16 @@ class MatrixInfo(C.Structure):
         ("spmv_bytes", C.c_int64),
         ("n_templates", C.c_int32),
         ("template_rows", C.c_int64),
+        ("format", C.c_int32),
+        ("kernel_variant", C.c_int32),
+        ("csr_bytes", C.c_int64),
+        ("tpl_window", C.c_int32),
+        ("tpl_lanes", C.c_int32),
+        ("tpl_march_shift", C.c_int32),
+        ("mult_add_bytes", C.c_int64),
+        ("residual_bytes", C.c_int64),
+        ("jacobi_bytes", C.c_int64),
+        ("gs_bytes", C.c_int64),
     ]
 
 
@@ -72,6 +83,7 @@ class LevelInfo(C.Structure):
         ("p_nnz_local", C.c_int64),
         ("r_nnz_local", C.c_int64),
         ("bytes_per_cycle_local", C.c_int64),
+        ("stored_bytes_per_cycle_local", C.c_int64),
     ]
 
 
@@ -98,6 +110,7 @@ SIGNATURES = {
     "amg_par_stencil_create": (C.c_int, [_vp, C.c_int, _i64, _i64, _i64, _pf64, C.POINTER(_vp)]),
     "amg_par_csr_info": (C.c_int, [_vp, C.POINTER(MatrixInfo)]),
     "amg_par_csr_export": (C.c_int, [_vp, _pi64, _pi64, _pf64]),
+    "amg_par_csr_set_format": (C.c_int, [_vp, _i32]),
     "amg_par_graph_laplacian_create": (C.c_int, [_vp, _i64, _i64, C.c_uint64, C.POINTER(_vp)]),
     "amg_par_csr_read": (C.c_int, [_vp, C.c_char_p, C.POINTER(_vp)]),
     "amg_par_csr_write": (C.c_int, [_vp, C.c_char_p]),
@@ -123,6 +136,7 @@ SIGNATURES = {
     "amg_solver_set_graph": (C.c_int, [_vp, _i32]),
     "amg_solver_destroy": (C.c_int, [_vp]),
     "amg_vector_uniform": (C.c_int, [_vp, _i64, _i64, C.c_uint64, _vp]),
+    "amg_vector_copy": (C.c_int, [_vp, _i64, _vp, _vp]),
     "amg_host_hierarchy_build": (C.c_int, [C.c_int, C.c_int, ALLTOALLV_FN, _vp, _i64, _i64, _i64,
                                            _pi64, _pi64, _pf64, C.POINTER(Options),
                                            C.POINTER(_vp)]),

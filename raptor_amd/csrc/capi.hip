@@ -278,9 +278,31 @@ int amg_par_csr_info(amg_matrix A, amg_matrix_info* info) {
         info->n_neighbors = (int32_t)std::max(m.plan.send_procs.size(), m.plan.recv_procs.size());
         info->n_blocks = m.nb_int + m.nb_bnd;
         info->n_vi_blocks = m.n_vi_blocks;
-        info->spmv_bytes = m.tpl_on() ? m.spmv_fmt_bytes : m.csr_fmt_bytes;
+        info->spmv_bytes = m.mode_bytes(KM_SPMV);
         info->n_templates = m.n_tpl;
         info->template_rows = m.tpl_on() ? m.tpl_rows : 0;
+        info->format = m.format;
+        info->kernel_variant = kernel_variant(m);
+        info->csr_bytes = m.csr_plain_bytes();
+        if (m.format == AMG_FORMAT_CSR) info->template_rows = 0;
+        const bool tpl = m.tpl_on();
+        info->tpl_window = tpl ? m.tpl_win : 0;
+        const int w = info->tpl_window;
+        info->tpl_lanes = w <= 0 ? 0 : w <= 4 * kTPB ? 4 : w <= 8 * kTPB ? 8 : w <= 12 * kTPB ? 12 : 16;
+        info->tpl_march_shift = tpl && (info->kernel_variant & 128) ? m.tpl_march_s : 0;
+        info->mult_add_bytes = m.mode_bytes(KM_SPMV_ADD);
+        info->residual_bytes = m.square ? m.mode_bytes(KM_RESID) : 0;
+        info->jacobi_bytes = m.square ? m.mode_bytes(KM_JACOBI) : 0;
+        info->gs_bytes = m.n_gs_slabs > 0 ? m.gs_bytes : 0;
+    });
+}
+
+int amg_par_csr_set_format(amg_matrix A, int32_t format) {
+    return guard([&] {
+        AMG_CHECK(A, "null matrix");
+        set_device(*A->m->ctx);
+        HIP_CHECK(hipStreamSynchronize(A->m->ctx->stream));
+        A->m->set_format(format);
     });
 }
 
@@ -445,6 +467,7 @@ int amg_solver_level_info(amg_solver S, int32_t l, amg_level_info* info) {
         info->p_nnz_local = L.P ? L.P->nnz : 0;
         info->r_nnz_local = L.R ? L.R->nnz : 0;
         info->bytes_per_cycle_local = S->s.bytes_per_cycle(l);
+        info->stored_bytes_per_cycle_local = S->s.stored_bytes_per_cycle(l);
     });
 }
 
@@ -683,6 +706,15 @@ int amg_host_csr_export(amg_host_csr A, int64_t* row_ptr, int64_t* col_global, d
 
 int amg_host_csr_destroy(amg_host_csr A) {
     return guard([&] { delete A; });
+}
+
+int amg_vector_copy(amg_context ctx, int64_t n, const double* src, double* dst) {
+    return guard([&] {
+        AMG_CHECK(ctx && n >= 0, "bad argument");
+        AMG_CHECK(n == 0 || (src && dst), "null vector");
+        set_device(ctx->c);
+        launch_copy(ctx->c.stream, n, src, dst);
+    });
 }
 
 int amg_vector_uniform(amg_context ctx, int64_t n, int64_t first_gid, uint64_t seed, double* out) {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <memory>
 #include <string>
 #include <vector>
@@ -199,11 +200,31 @@ struct DevMatrix {
     int n_tpl = 0, n_tpl_ent = 0, nb_skip = 0;
     int64_t tpl_rows = 0;  // rows the template kernel handles
     int64_t csr_fmt_bytes = 0;  // spmv_fmt_bytes with templates off (AMG_KERNEL_VARIANT)
+    // storage format the level kernels use (AMG_FORMAT_*, amg_par_csr_set_format):
+    // AUTO = templates + CSR blocks (default), BLOCKS = CSR blocks only, CSR = plain CSR
+    // (row_ptr / col / val exactly as SURVEY.md 8(d) prices them; pcol / pval are built when
+    // the format is first selected: local | halo column numbering, 2 padding entries)
+    int format = AMG_FORMAT_AUTO;
+    DevBuf<int> pcol;
+    DevBuf<double> pval;
+    int plain_blocks() const { return (int)((n_rows + kTPB - 1) / kTPB); }
+    // SURVEY.md 8(d) plain-CSR SpMV bytes: 12 nnz + 4 (n + 1) + 8 (local + halo columns) + 8 n
+    int64_t csr_plain_bytes() const {
+        return 12 * nnz + 4 * (n_rows + 1) + 8 * (n_cols_local + plan.n_halo()) + 8 * n_rows;
+    }
+    void set_format(int f);
+    // stored-format HBM bytes of one application in `mode` (KernelMode) with the format and
+    // kernel variant in effect (the bench's per-kernel roofline table)
+    int64_t mode_bytes(int mode) const;
+    int64_t jac_extra_all = 0, jac_extra_csr = 0;  // Jacobi operand bytes of the CSR-kernel rows
+    static int64_t format_generation;  // bumped by every set_format: captured graphs go stale
     bool tpl_on() const;
     int tpl_blocks() const { return n_tpl > 0 ? (int)((n_rows + kTplRows - 1) / kTplRows) : 0; }
     // norm partials one NORM-mode application leaves (and the most either path can leave)
     int norm_parts() const;
-    int norm_parts_max() const { return (nb_int + nb_bnd + tpl_blocks()) * kNormParts; }
+    int norm_parts_max() const {
+        return std::max(nb_int + nb_bnd + tpl_blocks(), plain_blocks()) * kNormParts;
+    }
     // halo (ParComm): RCCL neighbour exchange
     HaloPlan plan;
     DevBuf<int> send_idx;
@@ -236,6 +257,12 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
                 const double* b, double* y, double omega, double* partial);
 void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
                       double* y, bool backward = false, double* partial = nullptr);
+// plain CSR (AMG_FORMAT_CSR): all rows, one launch; partials at [0, plain_blocks() * kNormParts)
+void launch_csr_plain(hipStream_t s, int mode, bool norm, const DevMatrix& A, const double* x,
+                      const double* b, double* y, double omega, double* partial);
+// dst = src (16-byte nontemporal copy kernel; the bench's STREAM-copy ceiling)
+void launch_copy(hipStream_t s, int64_t n, const double* src, double* dst);
+int tpl_march_chunk_cap();
 void launch_jacobi_zero(hipStream_t s, int64_t n, const double* b, const double* dinv, double* y,
                         double omega);
 void launch_pack(hipStream_t s, int64_t n, const int* idx, const double* x, double* out);
@@ -308,6 +335,7 @@ struct Solver {
         hipGraphExec_t exec = nullptr;
         const double* x = nullptr;
         const double* b = nullptr;
+        int64_t fmt_gen = -1;
     } graphs[2];  // [0] plain cycle, [1] cycle that also appends ||b - A x_in||
 
     DevMatrix& Amat(size_t l) { return l == 0 ? *A0 : *levels[l].A; }
@@ -327,6 +355,9 @@ struct Solver {
     DevBuf<double> pcg_vec, pcg_scratch;  // r | z | p | q ; dot partials | tmp | gathered | scalars
     void dot(const double* a, const double* b, double* dst, bool take_sqrt);
     int64_t bytes_per_cycle(size_t l) const;
+    // the bytes level l's share of a cycle streams in the stored formats (<= what HBM can
+    // move in the measured time)
+    int64_t stored_bytes_per_cycle(size_t l) const;
     ~Solver();
 };
 

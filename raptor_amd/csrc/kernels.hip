@@ -401,6 +401,104 @@ __global__ __launch_bounds__(kTPB, AMG_CSR_PERSIST_WAVES) void csr_persist_kerne
     }
 }
 
+// Plain CSR (AMG_FORMAT_CSR): exactly the arrays SURVEY.md 8(d) prices --
+// int32 row_ptr, int32 col, fp64 val -- and nothing else (no headers, tiles, value indexing
+// or templates).  It is the roofline leg scored on 8(d)'s algorithmic bytes, and the path for
+// callers that hand over a matrix to be used as stored.  One 256-lane workgroup per 256
+// consecutive rows (XCD-remapped, so neighbouring row blocks share an L2).  The workgroup
+// streams its nonzero range [rp[r0], rp[r1]) in chunks of kCAP entries: lane t takes entries
+// base + 2t + 512p (p < 4) as a 16-byte value pair and an 8-byte column pair, both
+// nontemporal (each byte is read once), gathers x (L2-resident), and stages the products in
+// LDS; lane r then sums its row's products over the chunk in CSR order.  Rows never straddle
+// a workgroup, so every row sum runs from 0.0 in the oracle's order: bit-identical.
+struct PlainArgs {
+    const int* rp;
+    const int* col;     // local | halo numbering, 2 padding entries
+    const double* val;  // 2 padding entries
+    const double* x;
+    const double* xh;
+    int ncl, n;
+    const double* b;
+    const double* dinv;
+    double* y;
+    double omega;
+    double* partial;
+};
+
+__device__ __forceinline__ double plain_x(const PlainArgs& a, int c) {
+    return c < a.ncl ? a.x[c] : a.xh[c - a.ncl];
+}
+
+template <int MODE, bool NORM>
+__global__ __launch_bounds__(kTPB, 8) void csr_plain_kernel(PlainArgs a) {
+    __shared__ __attribute__((aligned(16))) double stage[kCAP];
+    const int tid = threadIdx.x;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int r0 = bid * kTPB, r1 = min(a.n, r0 + kTPB), r = r0 + tid;
+    const bool own = r < r1;
+    const int rr = own ? r : r1 - 1;
+    const int k0 = a.rp[r0], k1 = a.rp[r1];  // workgroup-uniform (scalar loads)
+    const int rs = a.rp[rr], re = a.rp[rr + 1];
+    double pb = 0.0, pd = 0.0, px = 0.0;
+    if (MODE == KM_SPMV_ADD) px = a.y[rr];
+    if (MODE == KM_RESID || MODE == KM_JACOBI) pb = a.b[rr];
+    if (MODE == KM_JACOBI) {
+        pd = a.dinv[rr];
+        px = a.x[rr];
+    }
+    const int plast = max(k1 - 1, 0) & ~1;  // last pair holding a real entry (padding after)
+    double s = 0.0;
+    for (int base = k0 & ~1; base < k1; base += kCAP) {
+        v2d_t vv[4];
+        v2i_t cc[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int q = min(base + 2 * tid + 2 * kTPB * p, plast);
+            vv[p] = __builtin_nontemporal_load((const v2d_t*)(a.val + q));
+            cc[p] = __builtin_nontemporal_load((const v2i_t*)(a.col + q));
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+            *(v2d_t*)(stage + 2 * tid + 2 * kTPB * p) =
+                v2d_t{vv[p].x * plain_x(a, cc[p].x), vv[p].y * plain_x(a, cc[p].y)};
+        __syncthreads();
+        const int lo = max(rs, base) - base, hi = min(re, base + kCAP) - base;
+        for (int k = lo; k < hi; ++k) s += stage[k];
+        __syncthreads();  // the next chunk overwrites the stage
+    }
+    double out, sq = 0.0;
+    if (MODE == KM_SPMV) {
+        out = s;
+    } else if (MODE == KM_SPMV_ADD) {
+        out = px + s;
+    } else {
+        const double t = pb - s;
+        if (NORM) sq = own ? t * t : 0.0;
+        out = MODE == KM_RESID ? t : px + a.omega * (pd * t);
+    }
+    if (own) a.y[r] = out;
+    if (NORM) {
+        for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
+        if ((tid & 63) == 0) a.partial[bid * kNormParts + (tid >> 6)] = sq;
+    }
+}
+
+// STREAM-copy ceiling (bench.py): 16-byte nontemporal loads and stores, 4 pairs in flight
+// per lane, grid-stride.  MI355X_MICROARCH.md records ~6.3 TB/s for such a copy.
+__global__ __launch_bounds__(kTPB) void copy_kernel(long long npair, const v2d_t* __restrict__ src,
+                                                     v2d_t* __restrict__ dst) {
+    const long long stride = (long long)gridDim.x * kTPB;
+    long long i = (long long)blockIdx.x * kTPB + threadIdx.x;
+    for (; i + 3 * stride < npair; i += 4 * stride) {
+        v2d_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+    }
+    for (; i < npair; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
 // Row-template kernel.  A templated row is (column - row) offsets, values and
 // 1/a_ii shared with every row of the same shape -- for a constant-coefficient stencil a few
 // dozen templates cover the operator -- so the kernel streams 1 byte per row (its template
@@ -1212,6 +1310,8 @@ int kernel_variant(const DevMatrix& A) {
                                 (A.tpl_march_s > 0 && A.tpl_win <= 8 * kTPB ? 128 : 0));
     if (A.n_vi_blocks == 0) var &= ~8;
     if (A.n_tpl == 0) var &= ~32;
+    // AMG_FORMAT_BLOCKS: the CSR block kernel on every row (no templates)
+    if (A.format == AMG_FORMAT_BLOCKS) var &= ~(32 | 128);
     // each operator is stored for one kernel: square -> x tile, rectangular -> gather
     if (A.square) var &= ~4;
     else var |= 4;
@@ -1221,6 +1321,7 @@ int kernel_variant(const DevMatrix& A) {
 bool DevMatrix::tpl_on() const { return n_tpl > 0 && (kernel_variant(*this) & 32); }
 
 int DevMatrix::norm_parts() const {
+    if (format == AMG_FORMAT_CSR) return plain_blocks() * kNormParts;
     return tpl_on() ? (tpl_blocks() + nb_int + nb_bnd - nb_skip) * kNormParts
                     : (nb_int + nb_bnd) * kNormParts;
 }
@@ -1256,15 +1357,33 @@ static void launch_tpl_window(hipStream_t s, const TplArgs& a, int g, size_t lds
         hipLaunchKernelGGL((tpl_kernel<M, N, P>), dim3(g), dim3(kTPB), lds, s, a);
 }
 
+// AMG_TPL_MARCH_CHUNKS caps the chains per column (tests: longer chains, so the LDS reuse
+// branch runs on small grids; 0 = no cap)
+int tpl_march_chunk_cap() {
+    const char* e = std::getenv("AMG_TPL_MARCH_CHUNKS");
+    return e ? std::max(0, std::atoi(e)) : 0;
+}
+
 template <int M, bool N, int P>
 static void launch_tpl_march(hipStream_t s, const TplArgs& a, int g, size_t lds, int S) {
     if constexpr (P > 0) {
-        int occ = 0, dev = 0, ncu = 0;
-        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tpl_march_kernel<M, N, P>, kTPB, lds));
-        HIP_CHECK(hipGetDevice(&dev));
-        HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        // CU count and occupancy per LDS size cached per instantiation (no runtime queries
+        // on the eager multi-rank path)
+        thread_local int ncu = 0, occ = 0;
+        thread_local size_t occ_lds = 0;
+        if (ncu == 0) {
+            int dev = 0;
+            HIP_CHECK(hipGetDevice(&dev));
+            HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        }
+        if (occ_lds != lds) {
+            HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tpl_march_kernel<M, N, P>, kTPB, lds));
+            occ_lds = lds;
+        }
         const int res = std::max(8, std::max(1, occ) * ncu / 8 * 8);  // resident workgroups
-        const int nchunk = std::max(1, res / S);                        // chains per column
+        int nchunk = std::max(1, res / S);                              // chains per column
+        const int cap = tpl_march_chunk_cap();
+        if (cap > 0) nchunk = std::min(nchunk, cap);
         const int gp = std::max(8, std::min(res, (S * nchunk + 7) / 8 * 8));
         hipLaunchKernelGGL((tpl_march_kernel<M, N, P>), dim3(gp), dim3(kTPB), lds, s, a, g, S, nchunk);
     }
@@ -1420,6 +1539,43 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
 #undef AMG_L2
 #undef AMG_L1
     HIP_CHECK(hipGetLastError());
+}
+
+void launch_csr_plain(hipStream_t s, int mode, bool norm, const DevMatrix& A, const double* x,
+                      const double* b, double* y, double omega, double* partial) {
+    const int g = A.plain_blocks();
+    if (g <= 0) return;
+    AMG_ASSERT(A.pcol.p != nullptr && A.pval.p != nullptr);
+    PlainArgs a{A.rp.p, A.pcol.p, A.pval.p, x, A.halo.p, (int)A.n_cols_local, (int)A.n_rows,
+                b, A.dinv.p, y, omega, partial};
+#define AMG_PL(M, N) hipLaunchKernelGGL((csr_plain_kernel<M, N>), dim3(g), dim3(kTPB), 0, s, a)
+    switch (mode) {
+        case KM_SPMV: AMG_PL(KM_SPMV, false); break;
+        case KM_SPMV_ADD: AMG_PL(KM_SPMV_ADD, false); break;
+        case KM_RESID:
+            if (norm) AMG_PL(KM_RESID, true);
+            else AMG_PL(KM_RESID, false);
+            break;
+        case KM_JACOBI:
+            if (norm) AMG_PL(KM_JACOBI, true);
+            else AMG_PL(KM_JACOBI, false);
+            break;
+        default: throw Error(AMG_ERR_INTERNAL, "bad kernel mode");
+    }
+#undef AMG_PL
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_copy(hipStream_t s, int64_t n, const double* src, double* dst) {
+    if (n <= 0) return;
+    AMG_CHECK(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0, "copy: 16-byte aligned vectors");
+    const long long np = n / 2;
+    if (np > 0) {
+        const int g = (int)std::min<long long>(256 * 8, (np + kTPB - 1) / kTPB);
+        hipLaunchKernelGGL(copy_kernel, dim3(g), dim3(kTPB), 0, s, np, (const v2d_t*)src, (v2d_t*)dst);
+        HIP_CHECK(hipGetLastError());
+    }
+    if (n & 1) HIP_CHECK(hipMemcpyAsync(dst + n - 1, src + n - 1, sizeof(double), hipMemcpyDeviceToDevice, s));
 }
 
 void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,

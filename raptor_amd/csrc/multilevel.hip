@@ -231,7 +231,7 @@ void Solver::cycle(double* x, const double* b, bool with_norm) {
     }
     hipStream_t s = ctx->stream;
     Graph& G = graphs[with_norm ? 1 : 0];
-    if (!G.exec || G.x != x || G.b != b) {
+    if (!G.exec || G.x != x || G.b != b || G.fmt_gen != DevMatrix::format_generation) {
         if (G.exec) HIP_CHECK(hipGraphExecDestroy(G.exec));
         G.exec = nullptr;
         hipGraph_t g = nullptr;
@@ -248,6 +248,7 @@ void Solver::cycle(double* x, const double* b, bool with_norm) {
         HIP_CHECK(hipGraphDestroy(g));
         G.x = x;
         G.b = b;
+        G.fmt_gen = DevMatrix::format_generation;
     }
     HIP_CHECK(hipGraphLaunch(G.exec, s));
 }
@@ -397,6 +398,36 @@ int64_t Solver::bytes_per_cycle(size_t l) const {
     b += opt.post_sweeps * jac;
     sweeps += opt.post_sweeps;
     if (sweeps % 2 == 1) b += 16 * n;                     // copy back
+    return b;
+}
+
+}  // namespace amg
+
+namespace amg {
+
+// Mirrors cycle_rec(): per operation the stored-format bytes of the kernel that runs it
+// (DevMatrix::mode_bytes, the sliced-ELL stream for hybrid GS), plus the vector-only passes.
+int64_t Solver::stored_bytes_per_cycle(size_t l) const {
+    const DevMatrix& A = const_cast<Solver*>(this)->Amat(l);
+    const int64_t n = A.n_rows;
+    if (l + 1 == levels.size()) return 8 * coarse_n * n + 8 * coarse_n + 8 * n;
+    const bool gs = opt.smoother == AMG_SMOOTH_HYBRID_GS;
+    const int64_t sweep = gs ? A.gs_bytes : A.mode_bytes(KM_JACOBI);
+    int64_t b = 0;
+    bool zero = l > 0;
+    int64_t sweeps = 0;
+    for (int k = 0; k < opt.pre_sweeps; ++k, ++sweeps) {
+        if (zero && !gs) b += 24 * n;              // omega * dinv * b
+        else b += sweep + (zero ? 8 * n : 0);      // (zero fill of x first)
+        zero = false;
+    }
+    if (zero) b += 8 * n;
+    b += A.mode_bytes(KM_RESID);
+    b += levels[l].R->mode_bytes(KM_SPMV);
+    b += levels[l].P->mode_bytes(KM_SPMV_ADD);
+    b += opt.post_sweeps * sweep;
+    sweeps += opt.post_sweeps;
+    if (sweeps % 2 == 1) b += 16 * n;  // copy back
     return b;
 }
 

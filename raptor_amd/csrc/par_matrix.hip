@@ -613,6 +613,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         // diag slot (square operators): tile position of line r0 / 8 when the lines of the
         // block's own rows are consecutive in its tile, so x[r] is read from the tile; else -1
         std::vector<int4> hh(std::max<size_t>(2 * nbk, 2), make_int4(0, 0, 0, 0));
+        jac_extra_all = jac_extra_csr = 0;
         for (size_t q = 0; q < nbk; ++q) {
             const int2 b = bb.blocks[q];
             const int t0 = bb.tile_ptr[q], nt = bb.tile_ptr[q + 1] - t0;
@@ -626,6 +627,12 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 if (ok) dslot = pos;
             }
             hh[2 * q] = make_int4(b.x, b.y, (int)koff[q], hrp[b.y] - hrp[b.x]);
+            if (square) {  // Jacobi operands beyond b: 1/a_ii (table index or fp64), x[r]
+                const int64_t rows = b.y - b.x;
+                const int64_t e = rows * (dvi_ok[q] ? 1 : 8) + (dslot < 0 ? 8 * rows : 0);
+                jac_extra_all += e;
+                if ((int)q >= bb.nb_skip) jac_extra_csr += e;
+            }
             // rectangular (gather) operators: field 0 = the block's offset in the VI index stream
             const int f0 = square ? dslot : (vofs.empty() ? 0 : (int)vofs[q]);
             hh[2 * q + 1] = make_int4(f0, nt | (dvi_ok[q] ? 1 << 16 : 0), vt_off[q], vt_len[q]);
@@ -783,6 +790,43 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
     gs_wide = !slabs.empty() && cells >= (int64_t)kGsWide * (int64_t)slabs.size();
 }
 
+int64_t DevMatrix::format_generation = 0;
+
+int64_t DevMatrix::mode_bytes(int mode) const {
+    const int64_t n = n_rows;
+    if (format == AMG_FORMAT_CSR) {  // residual + 8 n (b), Jacobi + 16 n (b, dinv)
+        const int64_t base = csr_plain_bytes();
+        return base + (mode == KM_JACOBI ? 16 * n : mode == KM_SPMV ? 0 : 8 * n);
+    }
+    const bool tpl = tpl_on();
+    int64_t b = tpl ? spmv_fmt_bytes : csr_fmt_bytes;
+    if (mode != KM_SPMV) b += 8 * n;  // b, or y for y += A x
+    // template rows take 1/a_ii and x[r] from LDS; CSR-kernel rows stream them
+    if (mode == KM_JACOBI) b += tpl ? jac_extra_csr : jac_extra_all;
+    return b;
+}
+
+void DevMatrix::set_format(int f) {
+    AMG_CHECK(f == AMG_FORMAT_AUTO || f == AMG_FORMAT_CSR || f == AMG_FORMAT_BLOCKS, "bad format");
+    if (f == AMG_FORMAT_CSR && !pcol.p && nnz + 2 > 0) {
+        // plain arrays in local | halo numbering, in row order (row_ptr is `rp`); two padding
+        // entries (column 0, value 0) keep the kernel's last 16-byte pair inside the buffer
+        const int64_t clo = first_col, chi = first_col + n_cols_local;
+        std::vector<int> pc((size_t)nnz + 2, 0);
+        std::vector<double> pv((size_t)nnz + 2, 0.0);
+#pragma omp parallel for schedule(static)
+        for (int64_t k = 0; k < nnz; ++k) {
+            const int64_t g = host.col[k];
+            pc[k] = g >= clo && g < chi ? (int)(g - clo) : (int)(n_cols_local + plan.find(g));
+            pv[k] = host.val[k];
+        }
+        pcol.upload(pc.data(), pc.size());
+        pval.upload(pv.data(), pv.size());
+    }
+    if (format != f) ++format_generation;
+    format = f;
+}
+
 bool DevMatrix::halo_begin(const double* x) {
     const HostComm& comm = ctx->host;
     if (comm.nranks == 1 || replicated) return false;
@@ -818,6 +862,11 @@ void par_apply(DevMatrix& A, int mode, const double* x, const double* b, double*
     const bool comm = A.halo_begin(x);
     hipStream_t s = A.ctx->stream;
     const bool norm = partial != nullptr;
+    if (A.format == AMG_FORMAT_CSR) {  // plain CSR: one launch over every row, after the halo
+        if (comm) A.halo_wait();
+        launch_csr_plain(s, mode, norm, A, x, b, y, omega, partial);
+        return;
+    }
     // template rows never touch the halo: they run with the interior blocks; the CSR kernel's
     // partials follow the template kernel's
     const bool tp = A.tpl_on();

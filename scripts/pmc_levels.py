@@ -1,6 +1,7 @@
 """Driver for rocprofv3 --pmc passes: runs each level operator of the 7-pt 256^3 PMIS
 hierarchy 3 times (SpMV; Jacobi for A_l) so per-dispatch counters can be read per kernel
-and grid size.  See profiles/README.md for the counter recipe."""
+and grid size, then the level-0 SpMV on the plain CSR format (csr_plain_kernel<0>, the bench's
+roofline kernel).  See profiles/README.md for the counter recipe."""
 import os
 import sys
 
@@ -25,3 +26,10 @@ for name, M in mats:
             M.jacobi(x, b, y)
     ctx.synchronize()
     print(name, "rows", M.local_rows, "nnz", M.nnz, "blocks", M.info["n_blocks"], flush=True)
+A.set_format("csr")
+x = ra.vector_uniform(ctx, A.local_cols, 0, 1)
+y = ctx.empty(A.local_rows)
+for _ in range(3):
+    A.mult(x, y)
+ctx.synchronize()
+print("A0 plain CSR", A.info["csr_bytes"], flush=True)

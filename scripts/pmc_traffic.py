@@ -2,7 +2,7 @@
 
 traffic = 2 x FETCH_SIZE + WRITE_SIZE (bytes; FETCH_SIZE reads half the bytes of wide
 streaming loads on gfx950, MI355X_MICROARCH.md "HBM"), averaged over the SpMV launches of
-the 7-pt 256^3 level-0 operator (SPMV instantiation of its first kernel).  Writes a JSON
+the 7-pt 256^3 level-0 operator (by default the plain-CSR kernel csr_plain_kernel<0>).  Writes a JSON
 that bench.py reports as roofline.traffic."""
 import csv
 import json
@@ -20,13 +20,12 @@ def per_dispatch(path):
     return vals, meta
 
 
-def main(prefix, out):
+def main(prefix, out, kernels=("csr_plain_kernel<0",)):
     f, meta = per_dispatch(f"{prefix}_FETCH_SIZE/run_counter_collection.csv")
     w, _ = per_dispatch(f"{prefix}_WRITE_SIZE/run_counter_collection.csv")
     # level-0 operator = first matrix in pmc_levels.py: its first 3 SpMV launches (the
     # row-template kernel where the operator is templated, else the CSR block kernel)
-    spmv = [d for d in sorted(meta)
-            if any(k in meta[d][0] for k in ("tpl_kernel<0", "tpl_persist_kernel<0", "tpl_march_kernel<0", "csr_block_kernel<0"))]
+    spmv = [d for d in sorted(meta) if any(k in meta[d][0] for k in kernels)]
     ds = [d for d in spmv if meta[d] == meta[spmv[0]]][:3]
     fetch = sum(f[d]["FETCH_SIZE"] for d in ds) / len(ds) * 1024
     write = sum(w[d]["WRITE_SIZE"] for d in ds) / len(ds) * 1024
@@ -39,4 +38,6 @@ def main(prefix, out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    # argv[3] (optional): comma-separated kernel-name prefixes (default: the plain-CSR SpMV,
+    # the bench's roofline kernel; "tpl_march_kernel<0" for the default-format one)
+    main(sys.argv[1], sys.argv[2], *([tuple(sys.argv[3].split(","))] if len(sys.argv) > 3 else []))

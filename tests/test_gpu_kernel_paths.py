@@ -1,0 +1,250 @@
+"""Every production kernel path against the CPU oracle (VERDICT r1 "What's weak" 1).
+
+The level kernels are size-gated: the row-template kernel picks its lanes-per-row (NPL 4 / 8 /
+12 / 16) from the x-window size, switches to the persistent form when there are more blocks
+than resident workgroups, and marches along z when a reusing shift exists; the storage format
+can be the default (templates + CSR blocks), CSR blocks only, or plain CSR.
+Each test below forces one of those paths on a shape chosen to reach it, asserts through
+ParCSRMatrix.info that the path was taken, and compares all four modes and the fused norm with
+the oracle bit for bit (norm: 1e-12 relative, different reduction order).  The V-cycle tests
+compare with the oracle's cycle on the product's own level operators -- not the product with
+itself."""
+import numpy as np
+import pytest
+
+from tests.util import oracle_levels, to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(ra, ctx, Ao):
+    rp, col, val = Ao.arrays()
+    return ra.ParCSRMatrix.from_csr(ctx, Ao.shape[0], 0, rp, col, val)
+
+
+def all_modes_equal(ctx, O, A, Ao, seed=3):
+    n = Ao.shape[0]
+    x, b, y0 = O.vec_uniform(n, seed), O.vec_uniform(n, seed + 1), O.vec_uniform(n, seed + 2)
+    dx, db = to_dev(ctx, x), to_dev(ctx, b)
+    out = ctx.empty(n)
+    A.mult(dx, out)
+    assert np.array_equal(to_host(ctx, out), Ao.spmv(x)), "mult"
+    dy = to_dev(ctx, y0)
+    A.mult_add(dx, dy)
+    assert np.array_equal(to_host(ctx, dy), Ao.spmv_add(x, y0)), "mult_add"
+    A.residual(dx, db, out)
+    assert np.array_equal(to_host(ctx, out), Ao.residual(x, b)), "residual"
+    A.jacobi(dx, db, out, 2.0 / 3.0)
+    assert np.array_equal(to_host(ctx, out), Ao.jacobi(x, b, 2.0 / 3.0)), "jacobi"
+    rn = A.residual_norm(dx, db)
+    ro = O.norm2(Ao.residual(x, b))
+    assert abs(rn - ro) <= 1e-12 * ro, "norm"
+
+
+def _ragged(O):
+    import scipy.sparse as sp
+
+    rng = np.random.default_rng(7)
+    n = 3000
+    M = sp.random(n, n, density=0.002, random_state=11, format="lil")
+    M[5, :] = 0
+    M[17, :] = 0
+    M[100, :] = rng.standard_normal(n)  # one row of 3000 entries: chunked in the plain kernel
+    M = (M + sp.eye(n) * 10.0).tocsr()
+    M.sort_indices()
+    return O.Csr.from_scipy(M)
+
+
+# ---- storage formats ------------------------------------------------------------------
+@pytest.mark.parametrize("fmt", ["csr", "blocks"])
+@pytest.mark.parametrize("name", ["7pt_20", "5pt_37x29", "27pt_13", "ragged", "7pt_odd"])
+def test_formats_bit_exact(ctx, oracle, name, fmt):
+    """AMG_FORMAT_CSR (plain row_ptr / col / val) and AMG_FORMAT_BLOCKS (CSR
+    blocks on every row, templates off): all modes bit-identical to the oracle, including
+    empty rows, a 3000-entry row (two LDS chunks) and an odd nonzero count (padding pair)."""
+    import raptor_amd as ra
+
+    O = oracle
+    Ao = {"7pt_20": lambda: O.gen_7pt(20, 20, 20), "5pt_37x29": lambda: O.gen_5pt(37, 29),
+          "27pt_13": lambda: O.gen_27pt(13, 13, 13), "ragged": lambda: _ragged(O),
+          "7pt_odd": lambda: O.gen_7pt(7, 5, 3)}[name]()
+    A = _dev(ra, ctx, Ao).set_format(fmt)
+    n = Ao.shape[0]
+    inf = A.info
+    assert inf["format"] == {"csr": ra.AMG_FORMAT_CSR, "blocks": ra.AMG_FORMAT_BLOCKS}[fmt]
+    assert inf["template_rows"] == 0
+    assert inf["csr_bytes"] == 12 * Ao.nnz + 4 * (n + 1) + 16 * n
+    if fmt == "csr":
+        assert inf["spmv_bytes"] == inf["csr_bytes"]
+    all_modes_equal(ctx, O, A, Ao)
+    A.set_format("auto")
+    all_modes_equal(ctx, O, A, Ao, seed=11)
+
+
+def test_plain_csr_full_size_bytes(ctx, oracle):
+    """the plain-CSR SpMV of 7-pt 256^3 moves 1,740,111,876 bytes."""
+    import raptor_amd as ra
+
+    A = ra.par_stencil_grid(ctx, "7pt", (256, 256, 256)).set_format("csr")
+    assert A.info["csr_bytes"] == 1740111876 == A.info["spmv_bytes"]
+    n = A.local_rows
+    ones = to_dev(ctx, np.ones(n))
+    y = ctx.empty(n)
+    A.mult(ones, y)
+    g = np.arange(n)
+    i, j, k = g % 256, (g // 256) % 256, g // 65536
+    expect = sum((c == 0).astype(float) + (c == 255).astype(float) for c in (i, j, k))
+    assert np.array_equal(to_host(ctx, y), expect)
+
+
+# ---- row-template windows: NPL 12 / 16 (sa27's level 0), persistent, march --------------
+# 27-pt: window = 3 bands of about 514 + 2 nx doubles -> NPL 12 from nx ~ 171, NPL 16 from 256
+WIDE = [("27pt", (200, 8, 8), 12), ("27pt", (260, 8, 8), 16), ("27pt", (256, 16, 16), 16),
+        ("27pt", (40, 40, 40), 8), ("7pt", (40, 40, 40), 8), ("5pt", (200, 60), 4)]
+
+
+@pytest.mark.parametrize("path", ["window", "march"])
+@pytest.mark.parametrize("kind,dims,npl", WIDE, ids=[f"{k}-{'x'.join(map(str, d))}" for k, d, _ in WIDE])
+def test_template_window_lanes(ctx, oracle, monkeypatch, kind, dims, npl, path):
+    """tpl_kernel<*, *, NPL> (window) and tpl_march_kernel<*, *, NPL> (forced by variant bit
+    128, chains capped at one per column so every block after a chain's first copies its
+    reused slots inside LDS) at every lanes-per-row instantiation, all modes + norm."""
+    import raptor_amd as ra
+
+    O = oracle
+    if path == "march" and npl == 4:
+        pytest.skip("a window of <= 1024 doubles is one band: no reusing shift exists")
+    gen = {"7pt": O.gen_7pt, "27pt": O.gen_27pt, "5pt": O.gen_5pt}[kind]
+    Ao = gen(*dims)
+    if path == "march":
+        monkeypatch.setenv("AMG_KERNEL_VARIANT", "170")
+        monkeypatch.setenv("AMG_TPL_MARCH_CHUNKS", "1")
+    A = _dev(ra, ctx, Ao)
+    inf = A.info
+    assert inf["template_rows"] == Ao.shape[0]
+    assert inf["tpl_lanes"] == npl, inf
+    if path == "march":
+        S = inf["tpl_march_shift"]
+        assert S > 0, "no reusing shift found"
+        blocks = -(-Ao.shape[0] // 512)
+        assert blocks >= 2 * S, "chains of one block: the reuse branch would not run"
+    all_modes_equal(ctx, O, A, Ao)
+
+
+@pytest.mark.parametrize("kind,dims", [("7pt", (128, 128, 80)), ("27pt", (80, 120, 120))])
+def test_template_persistent_kernel(ctx, oracle, monkeypatch, kind, dims):
+    """More 512-row blocks than resident workgroups (2048 on 256 CUs): with the march off
+    (variant 42 = templates + VI + XCD order) the persistent window kernel
+    tpl_persist_kernel<*, *, 8> runs, every workgroup sweeping several blocks."""
+    import raptor_amd as ra
+
+    O = oracle
+    Ao = (O.gen_7pt if kind == "7pt" else O.gen_27pt)(*dims)
+    assert Ao.shape[0] // 512 > 2048
+    monkeypatch.setenv("AMG_KERNEL_VARIANT", "42")
+    A = _dev(ra, ctx, Ao)
+    assert A.info["tpl_lanes"] in (4, 8) and A.info["tpl_march_shift"] == 0
+    all_modes_equal(ctx, O, A, Ao)
+
+
+@pytest.mark.parametrize("dims", [(64, 64, 24), (40, 40, 40), (72, 40, 30)],
+                         ids=["exact-plane", "partial-plane", "partial-plane-2"])
+@pytest.mark.parametrize("kind", ["7pt", "27pt"])
+def test_march_reuse_shapes(ctx, oracle, monkeypatch, kind, dims):
+    """the march's LDS-reuse branch on a plane that is a whole number of 512-row
+    blocks (64x64: shift = one plane) and on planes that are not (1600, 2880 rows: the shift
+    is the largest block multiple below, only part of the window is reused)."""
+    import raptor_amd as ra
+
+    O = oracle
+    Ao = (O.gen_7pt if kind == "7pt" else O.gen_27pt)(*dims)
+    monkeypatch.setenv("AMG_KERNEL_VARIANT", "170")
+    monkeypatch.setenv("AMG_TPL_MARCH_CHUNKS", "1")
+    A = _dev(ra, ctx, Ao)
+    S = A.info["tpl_march_shift"]
+    assert S > 0 and -(-Ao.shape[0] // 512) >= 2 * S
+    all_modes_equal(ctx, O, A, Ao, seed=31)
+
+
+# ---- V-cycles on forced paths, against the oracle ----------------------------------------
+VPATHS = {"persist_csr": {"AMG_KERNEL_VARIANT": "106"},
+          "march_chained": {"AMG_KERNEL_VARIANT": "170", "AMG_TPL_MARCH_CHUNKS": "1"},
+          "blocks_only": {"AMG_KERNEL_VARIANT": "10"},
+          "eager": {}}
+
+
+@pytest.mark.parametrize("path", list(VPATHS))
+def test_vcycle_paths_vs_oracle(ctx, oracle, monkeypatch, path):
+    """PMIS V-cycles with the level kernels forced onto one path (persistent x-tile kernel,
+    chained march, CSR blocks only, eager launches instead of the hipGraph): iterates
+    bit-identical to the oracle's cycle on the product's own operators, history <= 1e-10."""
+    import raptor_amd as ra
+
+    O = oracle
+    for k, v in VPATHS[path].items():
+        monkeypatch.setenv(k, v)
+    A = ra.par_stencil_grid(ctx, "7pt", (64, 64, 40))
+    ml = ra.ParRugeStubenSolver(coarsen="pmis", use_graph=path != "eager").setup(A)
+    H = O.Hierarchy(None, levels=oracle_levels(O, ml))
+    n = A.local_rows
+    b = O.vec_uniform(n, 9)
+    db = to_dev(ctx, b)
+    dx = ctx.zeros(n)
+    xo = np.zeros(n)
+    for _ in range(2):
+        ml.cycle(dx, db)
+        xo = H.cycle(xo, b)
+        assert np.array_equal(to_host(ctx, dx), xo)
+    _, h = ml.solve(ctx.zeros(n), db, max_iter=4)
+    _, ho = H.solve(np.zeros(n), b, max_iter=4)
+    assert np.all(np.abs(h - ho) <= 1e-10 * ho)
+
+
+def test_sa27_npl16_vcycle_vs_oracle(ctx, oracle):
+    """configs[2]'s kernel mix at a cheap size: 27-pt 256x24x16 (level-0 window > 3072
+    doubles: the NPL-16 template kernel for residuals and norms), smoothed aggregation,
+    hybrid GS on the value dictionary.  Hierarchy built independently by the oracle."""
+    import raptor_amd as ra
+
+    O = oracle
+    dims = (256, 24, 16)
+    Ao = O.gen_27pt(*dims)
+    A = ra.par_stencil_grid(ctx, "27pt", dims)
+    assert A.info["tpl_lanes"] == 16
+    ml = ra.ParSmoothedAggregationSolver().setup(A)
+    Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS["sa"], smoother=O.SMOOTH_HYBRID_GS))
+    assert ml.num_levels == Ho.num_levels
+    n = Ao.shape[0]
+    b = Ao.spmv(O.vec_uniform(n, 42))
+    db = to_dev(ctx, b)
+    dx = ctx.zeros(n)
+    xo = np.zeros(n)
+    for _ in range(2):
+        ml.cycle(dx, db)
+        xo = Ho.cycle(xo, b)
+        assert np.array_equal(to_host(ctx, dx), xo)
+    _, h = ml.solve(ctx.zeros(n), db, max_iter=5)
+    _, ho = Ho.solve(np.zeros(n), b, max_iter=5)
+    assert np.all(np.abs(h - ho) <= 1e-10 * ho)
+
+
+@pytest.mark.slow
+def test_full_size_27pt_256(ctx, oracle):
+    """BASELINE.json configs[2] size: 27-pt 256^3 (449M nnz).  The level-0 kernels the sa27
+    bench runs -- the NPL-16 template kernel in every mode with the norm, and the l1 hybrid
+    GS on the 1-byte value dictionary, forward and backward -- bit-identical to the oracle."""
+    import raptor_amd as ra
+
+    O = oracle
+    N = 256
+    A = ra.par_stencil_grid(ctx, "27pt", (N, N, N))
+    assert A.info["tpl_lanes"] == 16 and A.info["template_rows"] == N ** 3
+    Ao = O.gen_27pt(N, N, N)
+    all_modes_equal(ctx, O, A, Ao, seed=17)
+    n = N ** 3
+    x, b = O.vec_uniform(n, 5), O.vec_uniform(n, 6)
+    dx, db, out = to_dev(ctx, x), to_dev(ctx, b), ctx.empty(n)
+    A.hybrid_gs(dx, db, out, 64)
+    assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs(x, b, 64))
+    A.hybrid_gs(dx, db, out, 64, backward=True)
+    assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs_backward(x, b, 64))

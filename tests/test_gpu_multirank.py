@@ -52,14 +52,15 @@ def set_oracle_cuts(Ho, res):
         Ho.set_cuts(l, sorted({s[l] for s in starts if l < len(s)}))
 
 
-@pytest.mark.parametrize("tpl", [False, True], ids=["csr", "templates"])
+@pytest.mark.parametrize("tpl", [False, True, "plain"], ids=["csr", "templates", "plain"])
 @pytest.mark.parametrize("nranks", [2, 3])
 def test_slab_kernels_bit_exact(oracle, monkeypatch, nranks, tpl):
     """templates: interior rows on the row-template kernel, halo rows on the CSR block
-    kernel (size floor lowered so the small slabs qualify)."""
+    kernel (size floor lowered so the small slabs qualify).  plain: AMG_FORMAT_CSR, the plain
+    CSR kernel over local | halo columns after the exchange."""
     import raptor_amd as ra
 
-    if tpl:
+    if tpl is True:
         monkeypatch.setenv("AMG_TPL_MIN_ROWS", "0")
 
     O = oracle
@@ -74,6 +75,8 @@ def test_slab_kernels_bit_exact(oracle, monkeypatch, nranks, tpl):
     def rank(r, nr, world):
         ctx = ra.Context.loopback(r, nr, world)
         A = ra.par_stencil_grid(ctx, "7pt", dims)
+        if tpl == "plain":
+            A.set_format("csr")
         f, m = A.first_row, A.local_rows
         dx, db = to_dev(ctx, x[f:f + m]), to_dev(ctx, b[f:f + m])
         out = ctx.empty(m)
@@ -95,13 +98,16 @@ def test_slab_kernels_bit_exact(oracle, monkeypatch, nranks, tpl):
             assert np.array_equal(got[k], ref[k][f:f + m]), k
         assert abs(got["rn"] - rn_ref) <= 1e-12 * rn_ref
         assert got["halo"] > 0
-        assert (0 < got["tpl_rows"] < m) if tpl else got["tpl_rows"] == 0
+        assert (0 < got["tpl_rows"] < m) if tpl is True else got["tpl_rows"] == 0
 
 
 CASES = [(2, "7pt", (16, 15, 18), "pmis", "jacobi"),
          (3, "7pt", (14, 14, 21), "pmis", "jacobi"),
          (4, "27pt", (10, 11, 16), "sa", "hybrid_gs"),
-         (2, "5pt", (40, 34), "pmis", "jacobi")]
+         (2, "5pt", (40, 34), "pmis", "jacobi"),
+         # configs[3]'s partition shape: 8 z-slabs
+         (8, "7pt", (48, 48, 96), "pmis", "jacobi"),
+         (8, "7pt", (48, 48, 96), "sa", "hybrid_gs")]
 
 
 @pytest.mark.parametrize("rep", [0, 800, 10 ** 9], ids=["distributed", "rep-deep", "rep-all"])
