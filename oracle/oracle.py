@@ -75,6 +75,8 @@ def lib():
             "orc_jacobi": (None, [vp, _f64p, _f64p, _f64p, C.c_double]),
             "orc_hybrid_gs": (None, [vp, _f64p, _f64p, _f64p, C.c_int64]),
             "orc_hybrid_gs_backward": (None, [vp, _f64p, _f64p, _f64p, C.c_int64]),
+            "orc_hybrid_gs_cut": (None, [vp, _f64p, _f64p, _f64p, C.c_int64, C.c_int32, C.c_int32,
+                                         _i64p]),
             "orc_norm2": (C.c_double, [C.c_int64, _f64p]),
             "orc_transpose": (vp, [vp]),
             "orc_spgemm": (vp, [vp, vp]),
@@ -197,6 +199,16 @@ class Csr:
         b = np.ascontiguousarray(b, np.float64)
         out = np.empty(self.shape[0])
         lib().orc_hybrid_gs_backward(self.h, _p(x, _f64p), _p(b, _f64p), _p(out, _f64p), block)
+        return out
+
+    def hybrid_gs_cut(self, x, b, block, backward, cuts):
+        """Hybrid GS with GS blocks clipped at the rank starts `cuts` (amg_oracle.c:255)."""
+        x = np.ascontiguousarray(x, np.float64)
+        b = np.ascontiguousarray(b, np.float64)
+        c = np.ascontiguousarray(cuts, np.int64)
+        out = np.empty(self.shape[0])
+        lib().orc_hybrid_gs_cut(self.h, _p(x, _f64p), _p(b, _f64p), _p(out, _f64p), block,
+                                1 if backward else 0, int(c.size), _p(c, _i64p))
         return out
 
     def transpose(self):

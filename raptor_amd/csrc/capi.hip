@@ -293,7 +293,7 @@ int amg_par_csr_info(amg_matrix A, amg_matrix_info* info) {
         info->mult_add_bytes = m.mode_bytes(KM_SPMV_ADD);
         info->residual_bytes = m.square ? m.mode_bytes(KM_RESID) : 0;
         info->jacobi_bytes = m.square ? m.mode_bytes(KM_JACOBI) : 0;
-        info->gs_bytes = m.n_gs_slabs > 0 ? m.gs_bytes : 0;
+        info->gs_bytes = m.gs_block > 0 ? m.gs_bytes : 0;
     });
 }
 

@@ -169,7 +169,21 @@ struct DevMatrix {
     DevBuf<int> gs_col;
     DevBuf<double> gs_val, gs_dinv;
     int n_gs_slabs = 0;
+    int n_gs_slabs_int = 0;  // slabs [0, n_gs_slabs_int) touch no halo column (run before the wait)
     int64_t gs_block = 0;
+    // hybrid GS on row templates: 512-row blocks whose rows all have a GS
+    // template = (row template, l1 diagonal) pair run tpl_gs_kernel; the sliced-ELL slabs
+    // above cover the other rows only
+    DevBuf<uint8_t> gs_tid;      // per row: GS template (kTplNone: ELL row)
+    DevBuf<int> gs_thdr;         // per GS template: its row template's header
+    DevBuf<double> gs_tdl;       // per GS template: 1 / (a_ii + l1)
+    DevBuf<int> gs_tblocks;      // the 512-row blocks on the template kernel
+    DevBuf<double> gs_tcvm, gs_tcvp;  // per GS template: value of its -1 / +1 entry (or 0)
+    DevBuf<int> gs_tcf;          // per GS template: bit 0 has a -1 entry, bit 1 a +1 entry
+    DevBuf<int> gs_tkem, gs_tkep;  // per GS template: index in the row of its -1 / +1 entry (-1)
+    DevBuf<double> gs_racc;      // per row: b - old-value couplings (acc kernel -> chain kernel)
+    int n_gs_tpl = 0, n_gs_tblk = 0;
+    int gs_norm_parts() const { return n_gs_slabs + kNormParts * n_gs_tblk; }
     int64_t gs_bytes = 0;  // sliced-ELL bytes streamed per sweep
     bool gs_wide = false;  // average slab width >= kGsWide: the LDS-chain kernel variant
     // value dictionary (the whole local operator takes <= 256 distinct values, e.g. a
@@ -186,6 +200,7 @@ struct DevMatrix {
     // tpl_off / tpl_val.  CSR blocks [0, nb_skip) hold only templated rows: the block kernel
     // skips them while templates are active (tpl_on()).
     DevBuf<uint8_t> tpl_id;
+    std::vector<uint8_t> tpl_id_host;  // host copy (GS templates are derived from it)
     DevBuf<int> tpl_hdr, tpl_off;
     // x window: bands of template offsets; per entry its window slot (tpl_ldo);
     // tpl_win = window size in doubles, 0 = the bands do not fit (global x loads)
@@ -255,8 +270,10 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
 // template rows of A (all of them, one launch); partials at [0, tpl_blocks() * kNormParts)
 void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const double* x,
                 const double* b, double* y, double omega, double* partial);
+// hybrid GS sweep over slabs [s0, s1) of the sliced-ELL copy, plus (tpl) the template blocks;
+// partials: slab q at q, template block list entry t, wave w at n_gs_slabs + 4 t + w
 void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
-                      double* y, bool backward = false, double* partial = nullptr);
+                      double* y, bool backward, double* partial, int s0, int s1, bool tpl);
 // plain CSR (AMG_FORMAT_CSR): all rows, one launch; partials at [0, plain_blocks() * kNormParts)
 void launch_csr_plain(hipStream_t s, int mode, bool norm, const DevMatrix& A, const double* x,
                       const double* b, double* y, double omega, double* partial);

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
 
 #include "device.hpp"
@@ -483,20 +484,22 @@ __global__ __launch_bounds__(kTPB, 8) void csr_plain_kernel(PlainArgs a) {
     }
 }
 
-// STREAM-copy ceiling (bench.py): 16-byte nontemporal loads and stores, 4 pairs in flight
-// per lane, grid-stride.  MI355X_MICROARCH.md records ~6.3 TB/s for such a copy.
+// STREAM-copy ceiling (bench.py): one pass, 4 x 16-byte pairs per lane (1 KiB-strided, so a
+// wave instruction moves 1 KiB), plain loads and stores.  Same-box probe (profiles/
+// r2c_copy_probe.txt): 5.6 TB/s, against 4.1-5.3 TB/s for grid-stride forms and 5.2 TB/s for
+// hipMemcpyAsync.
 __global__ __launch_bounds__(kTPB) void copy_kernel(long long npair, const v2d_t* __restrict__ src,
                                                      v2d_t* __restrict__ dst) {
-    const long long stride = (long long)gridDim.x * kTPB;
-    long long i = (long long)blockIdx.x * kTPB + threadIdx.x;
-    for (; i + 3 * stride < npair; i += 4 * stride) {
+    const long long i = (long long)blockIdx.x * 4 * kTPB + threadIdx.x;
+    if (i + 3 * kTPB < npair) {
         v2d_t v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+        for (int u = 0; u < 4; ++u) v[u] = src[i + u * kTPB];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+        for (int u = 0; u < 4; ++u) dst[i + u * kTPB] = v[u];
+    } else {
+        for (long long k = i; k < npair; k += kTPB) dst[k] = src[k];
     }
-    for (; i < npair; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
 // Row-template kernel.  A templated row is (column - row) offsets, values and
@@ -953,6 +956,7 @@ struct GsArgs {
     const uint8_t* vid;  // DICT: 1-byte value indices (4 entries of a lane per dword)
     const double* vtab;  // DICT: the value table
     int ndict;
+    int slab0;           // first slab of this launch (waves index slabs slab0 + wave)
 };
 
 __device__ __forceinline__ double bcast_lane(double v, int lane) {
@@ -979,7 +983,7 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
     }
     // wave index made provably uniform: slab fields land in SGPRs, the step loop is scalar
     const int wave = __builtin_amdgcn_readfirstlane(
-        (int)(WIDE ? blockIdx.x : blockIdx.x * 4 + (threadIdx.x >> 6)));
+        (int)(WIDE ? blockIdx.x : blockIdx.x * 4 + (threadIdx.x >> 6))) + a.slab0;
     if (wave >= a.nslab) return;
     const int lane = threadIdx.x & 63;
     const int4 sl = a.slabs[wave];
@@ -1109,6 +1113,194 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m);
         if (lane == 0) a.partial[wave] = q;
+    }
+}
+
+// l1 hybrid Gauss-Seidel on row templates, for operators whose in-chunk
+// couplings are the +-1 neighbours only (a stencil with its x line along the chunk).  Rows
+// whose (template, l1 diagonal) pair is shared -- boundary class x position of the row in its
+// GS chunk -- stream a 1-byte GS-template id.  Two kernels per sweep:
+//  tpl_gs_acc_kernel  (lane = row, 512-row blocks, the template x window in LDS):
+//      acc_i = b_i - sum of the old-value couplings in CSR order (diagonal included; the
+//      chain coupling -- offset -1 forward / +1 backward when that neighbour is in the
+//      row's chunk -- skipped), stored to `racc`; NORM: (b - A x_old)^2 partials
+//  tpl_gs_chain_kernel (lane = chunk, 256 chunks per workgroup):
+//      the chunk's rows in sweep order, 8 rows of (acc, x, id) per batch in registers with
+//      the next batch in flight: acc -= a_i,i-+1 x'_prev; x'_i = x_i + acc * dinv_l1.
+// The oracle's order exactly (one chain coupling, subtracted after the old ones).  The chain
+// is a sequential recurrence per chunk; lane = chunk runs 64 chunks per wave instruction.  A
+// single-kernel form (same recurrence walked by 8 lanes of a 512-row block, or broadcast with
+// v_readlane by every row's lane) took 880-920 / 727 us per 27-pt 256^3 sweep.
+struct TplGsArgs {
+    TplArgs t;           // id = GS-template id per row; hdr = base template header per GS
+                         // template; off = window slots; val; y = racc (acc kernel)
+    const int* ke;       // per GS template: the chain entry's index in the row (-1: none)
+    const int* blocks;   // the 512-row blocks on the template path
+    int nblk;
+    long long first_row;
+    int B;
+    int part_off;        // NORM: partial of block list entry q, wave w at part_off + 4 q + w
+};
+
+template <bool BACK, bool NORM, int NPL>
+__global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
+    static_assert(NPL > 0, "window path only");
+    constexpr int R = kTplRPL;
+    const TplArgs& a = g.t;
+    const TplLds L = tpl_lds_layout<KM_RESID>(a);
+    int* loffr = L.hdr + kTplMax + 1;  // per GS template: index (in the row) of its chain entry
+    const int tid = threadIdx.x, lane = tid & 63;
+    const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
+    const int q = xcd_remap(blockIdx.x, gridDim.x);
+    const int r0 = g.blocks[q] * kTplRows;
+    TplFetch<KM_RESID, NPL> f;  // ids, b, window
+    f.issue(a, xrs, r0);
+    tpl_stage_table<KM_RESID>(a, L);
+    if (tid < a.ntpl) loffr[tid] = g.ke[tid];
+    f.commit(a, L);
+    __syncthreads();
+    double sq = 0.0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int lr = kTPB * j + tid, i = r0 + lr;
+        const unsigned h = (unsigned)L.hdr[f.id[j]];
+        const int st = (int)(h & 0xffffu), ln = (int)((h >> 16) & 0xffu);
+        // the chain neighbour is in the row's chunk (chunks = global multiples of B; the rank
+        // start is a multiple of 64 and B | 64, so pos = i mod B and only the rank end clips)
+        const int pos = i & (g.B - 1);
+        const bool chain = BACK ? (pos != g.B - 1 && i + 1 < a.n) : pos != 0;
+        const int ke = chain ? loffr[f.id[j]] : -1;  // template entry of the chain coupling
+        double acc = f.pb[j], sold = 0.0;
+        for (int k = 0; k < ln; ++k) {
+            const int e = st + k;
+            const double p = L.val[e] * L.win[L.off[e] + lr];
+            if (NORM) sold += p;
+            acc = k == ke ? acc : acc - p;
+        }
+        if (f.id[j] != kTplNone) {
+            a.y[i] = acc;
+            if (NORM) {
+                const double rr = f.pb[j] - sold;
+                sq += rr * rr;
+            }
+        }
+    }
+    if (NORM) {
+        for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
+        if (lane == 0) a.partial[g.part_off + 4 * q + (tid >> 6)] = sq;
+    }
+}
+
+struct TplGsChainArgs {
+    const double* racc;
+    const double* x;
+    const uint8_t* id;
+    const double* dl;    // per GS template: 1 / (a_ii + l1)
+    const double* cv;    // per GS template: coefficient of the chain neighbour (-1 fwd, +1 bwd)
+    const int* cf;       // per GS template: bit 0 has the -1 entry, bit 1 the +1 entry
+    int ntpl;
+    const int* blocks;
+    int nblk;
+    int B;
+    int n;
+    long long first_row;
+    double* y;
+};
+
+// One wave per 64 chunks.  Batch k = rows 8k .. 8k+7 of every chunk: the wave loads the
+// batch's 64-byte lines cooperatively (16 bytes per lane, 4 lanes per line, each line read
+// once) into LDS while the previous batch is walked, then lane c walks chunk c's 8 rows from
+// LDS.  (Lane c loading its own chunk's lines took 161 us per 27-pt 256^3 sweep: 64 distinct
+// lines per wave instruction, each fetched again by the next quarter-line load.)
+template <bool BACK>
+__global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
+    constexpr int U = 8;
+    __shared__ double sdl[kTplMax + 1], scv[kTplMax + 1];
+    __shared__ int scf[kTplMax + 1];
+    __shared__ __attribute__((aligned(16))) double sacc[64 * U], sx[64 * U];
+    __shared__ unsigned sid[64 * 2];
+    const int lane = threadIdx.x;
+    constexpr int kBit = BACK ? 2 : 1;
+    for (int k = lane; k < a.ntpl; k += 64) {
+        sdl[k] = a.dl[k];
+        scv[k] = a.cv[k];
+        scf[k] = a.cf[k] & kBit;
+    }
+    const int cpb = kTplRows / a.B;  // chunks per block
+    const long long nq = (long long)a.nblk * cpb;
+    const long long q0 = (long long)blockIdx.x * 64;
+    auto cstart = [&](long long qc) { return a.blocks[qc / cpb] * kTplRows + (int)(qc % cpb) * a.B; };
+    // my chunk
+    const long long qc = q0 + lane;
+    const bool live = qc < nq;
+    const int c0 = live ? cstart(qc) : 0;
+    const int c1 = live ? min(c0 + a.B, a.n) : 0;
+    // fast path: B % 8 == 0 and every chunk of the wave whole (wave-uniform)
+    const bool whole = a.B % U == 0 && q0 + 64 <= nq && __all(c1 - c0 == a.B);
+    __syncthreads();
+    double prev = 0.0;
+    if (whole) {
+        // load assignment u (4 per array): line of chunk 16 u + lane / 4, 16-byte piece lane % 4
+        int ls[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ls[u] = cstart(q0 + 16 * u + (lane >> 2)) + 2 * (lane & 3);
+        const int nb = a.B / U;
+        v2d_t ra[4], rx[4];
+        v2u_t ri;
+        auto load = [&](int bi) {
+            const int off = (BACK ? nb - 1 - bi : bi) * U;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                ra[u] = __builtin_nontemporal_load((const v2d_t*)(a.racc + ls[u] + off));
+                rx[u] = *(const v2d_t*)(a.x + ls[u] + off);
+            }
+            ri = *(const v2u_t*)(a.id + c0 + off);
+        };
+        load(0);
+        for (int bi = 0; bi < nb; ++bi) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int slot = (16 * u + (lane >> 2)) * U + 2 * (lane & 3);
+                *(v2d_t*)(sacc + slot) = ra[u];
+                *(v2d_t*)(sx + slot) = rx[u];
+            }
+            sid[2 * lane] = ri.x;
+            sid[2 * lane + 1] = ri.y;
+            __syncthreads();
+            if (bi + 1 < nb) load(bi + 1);  // in flight during the walk below
+            double out[U];
+            const unsigned iw[2] = {sid[2 * lane], sid[2 * lane + 1]};
+#pragma unroll
+            for (int t = 0; t < U; ++t) {
+                const int u = BACK ? U - 1 - t : t;
+                const int tp = (int)((iw[u >> 2] >> (8 * (u & 3))) & 0xffu);
+                double acc = sacc[lane * U + u];
+                // the chunk's first row in sweep order has no chain neighbour; a template
+                // without the neighbour entry (boundary row) has none either
+                if ((bi > 0 || t > 0) && scf[tp]) acc -= scv[tp] * prev;
+                prev = sx[lane * U + u] + acc * sdl[tp];
+                out[u] = prev;
+            }
+            // x' back through the stage: whole 64-byte lines per 4 lanes, like the loads
+#pragma unroll
+            for (int u = 0; u < U; ++u) sacc[lane * U + u] = out[u];
+            __syncthreads();
+            const int off = (BACK ? nb - 1 - bi : bi) * U;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                *(v2d_t*)(a.y + ls[u] + off) = *(const v2d_t*)(sacc + (16 * u + (lane >> 2)) * U + 2 * (lane & 3));
+            __syncthreads();  // the stage is rewritten by the next batch
+        }
+    } else if (live) {
+        // clipped chunk (the rank's last rows), a partial wave, or B not a multiple of 8
+        for (int t = 0; t < c1 - c0; ++t) {
+            const int i = BACK ? c1 - 1 - t : c0 + t;
+            const int tp = a.id[i];
+            double acc = a.racc[i];
+            if (t > 0 && scf[tp]) acc -= scv[tp] * prev;
+            prev = a.x[i] + acc * sdl[tp];
+            a.y[i] = prev;
+        }
     }
 }
 
@@ -1571,26 +1763,93 @@ void launch_copy(hipStream_t s, int64_t n, const double* src, double* dst) {
     AMG_CHECK(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0, "copy: 16-byte aligned vectors");
     const long long np = n / 2;
     if (np > 0) {
-        const int g = (int)std::min<long long>(256 * 8, (np + kTPB - 1) / kTPB);
-        hipLaunchKernelGGL(copy_kernel, dim3(g), dim3(kTPB), 0, s, np, (const v2d_t*)src, (v2d_t*)dst);
+        const long long g = (np + 4 * kTPB - 1) / (4 * kTPB);
+        AMG_CHECK(g < INT_MAX, "copy: vector too long");
+        hipLaunchKernelGGL(copy_kernel, dim3((unsigned)g), dim3(kTPB), 0, s, np, (const v2d_t*)src, (v2d_t*)dst);
         HIP_CHECK(hipGetLastError());
     }
     if (n & 1) HIP_CHECK(hipMemcpyAsync(dst + n - 1, src + n - 1, sizeof(double), hipMemcpyDeviceToDevice, s));
 }
 
+// acc kernel LDS: the template kernel's RESID layout + the entries' column offsets
+inline size_t tpl_gs_lds_bytes(int win, int nent) { return tpl_lds_bytes(win, nent, false) + 4 * (kTplMax + 1); }
+
+static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
+                          double* y, bool backward, double* partial) {
+    AMG_ASSERT(A.n_gs_tblk > 0 && A.tpl_win > 0 && A.n_tpl_ent <= kTplEntries);
+    AMG_ASSERT(A.gs_racc.n >= (size_t)A.n_rows);
+    TplGsArgs g{};
+    TplArgs& a = g.t;
+    a.id = A.gs_tid.p;
+    a.hdr = A.gs_thdr.p;
+    a.off = A.tpl_ldo.p;
+    a.val = A.tpl_val.p;
+    a.pd = A.gs_tdl.p;
+    a.ntpl = A.n_gs_tpl;
+    a.nent = A.n_tpl_ent;
+    a.n = (int)A.n_rows;
+    a.nband = (int)A.tpl_blo.size();
+    a.win = A.tpl_win;
+    a.wend = A.tpl_wend;
+    for (int q = 0; q < a.nband; ++q) a.blo[q] = A.tpl_blo[q], a.bbase[q] = A.tpl_bbase[q];
+    a.bbase[a.nband] = a.win;
+    for (int q = a.nband; q < kTplBands; ++q) a.blo[q] = 0, a.bbase[q + 1] = a.win;
+    a.x = x;
+    a.b = b;
+    a.y = A.gs_racc.p;
+    a.partial = partial;
+    g.ke = backward ? A.gs_tkep.p : A.gs_tkem.p;
+    g.blocks = A.gs_tblocks.p;
+    g.nblk = A.n_gs_tblk;
+    g.first_row = A.first_row;
+    g.B = (int)A.gs_block;
+    g.part_off = A.n_gs_slabs;
+    const int npl = a.win <= 4 * kTPB ? 4 : a.win <= 8 * kTPB ? 8 : a.win <= 12 * kTPB ? 12 : 16;
+    AMG_ASSERT(a.win <= npl * kTPB && a.win <= kTplWin);
+    const size_t lds = tpl_gs_lds_bytes(a.win, a.nent);
+    const bool norm = partial != nullptr;
+    const dim3 grid(g.nblk), blk(kTPB);
+#define AMG_G2(BK, NM, P) hipLaunchKernelGGL((tpl_gs_acc_kernel<BK, NM, P>), grid, blk, lds, s, g)
+#define AMG_G(BK, NM)                         \
+    do {                                      \
+        switch (npl) {                        \
+            case 4: AMG_G2(BK, NM, 4); break;   \
+            case 8: AMG_G2(BK, NM, 8); break;   \
+            case 12: AMG_G2(BK, NM, 12); break; \
+            default: AMG_G2(BK, NM, 16); break; \
+        }                                     \
+    } while (0)
+    if (backward) AMG_G(true, false);
+    else if (norm) AMG_G(false, true);
+    else AMG_G(false, false);
+#undef AMG_G
+#undef AMG_G2
+    HIP_CHECK(hipGetLastError());
+    TplGsChainArgs c{A.gs_racc.p, x, A.gs_tid.p, A.gs_tdl.p, backward ? A.gs_tcvp.p : A.gs_tcvm.p,
+                     A.gs_tcf.p, A.n_gs_tpl, A.gs_tblocks.p, A.n_gs_tblk, (int)A.gs_block, (int)A.n_rows,
+                     (long long)A.first_row, y};
+    const long long nch = (long long)A.n_gs_tblk * (kTplRows / A.gs_block);
+    const dim3 cg((unsigned)((nch + 63) / 64)), cb(64);
+    if (backward) hipLaunchKernelGGL((tpl_gs_chain_kernel<true>), cg, cb, 0, s, c);
+    else hipLaunchKernelGGL((tpl_gs_chain_kernel<false>), cg, cb, 0, s, c);
+    HIP_CHECK(hipGetLastError());
+}
+
 void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
-                      double* y, bool backward, double* partial) {
-    if (A.n_gs_slabs <= 0) return;
+                      double* y, bool backward, double* partial, int s0, int s1, bool tpl) {
     AMG_ASSERT(!(backward && partial));
+    if (tpl && A.n_gs_tblk > 0) launch_tpl_gs(s, A, x, b, y, backward, partial);
+    if (s1 <= s0) return;
     GsArgs a{A.gs_slabs.p, A.gs_col.p, A.gs_val.p, x, A.halo.p, (int)A.n_cols_local, b,
              A.gs_dinv.p, y, (long long)A.first_row, (long long)A.gs_block, (int)A.n_rows,
-             A.n_gs_slabs, partial, A.gs_vid.p, A.gs_vtab.p, A.gs_ndict};
+             s1, partial, A.gs_vid.p, A.gs_vtab.p, A.gs_ndict, s0};
     static const int forced = [] {
         const char* e = std::getenv("AMG_GS_VARIANT");  // 0 narrow, 1 wide (experiments)
         return e ? std::atoi(e) : -1;
     }();
     const bool wide = forced >= 0 ? forced == 1 : A.gs_wide;
-    const dim3 grid(wide ? A.n_gs_slabs : (A.n_gs_slabs + 3) / 4), block(wide ? 64 : 256);
+    const int ns = s1 - s0;
+    const dim3 grid(wide ? ns : (ns + 3) / 4), block(wide ? 64 : 256);
 #define AMG_GS(BK, WD, NM)                                                                          \
     do {                                                                                            \
         if (A.gs_ndict > 0) hipLaunchKernelGGL((hybrid_gs_kernel<BK, WD, NM, true>), grid, block, 0, s, a); \

@@ -85,7 +85,7 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         if (opt.smoother == AMG_SMOOTH_HYBRID_GS) {
             Al.ensure_gs_blocks(opt.gs_block);
             tm.lap("L" + std::to_string(l) + " GS sliced-ELL build");
-            max_blocks = std::max(max_blocks, (size_t)Al.n_gs_slabs);
+            max_blocks = std::max(max_blocks, (size_t)Al.gs_norm_parts());
         }
     }
     // norm plumbing: partials | reduction scratch | gathered rank sums
@@ -146,7 +146,7 @@ void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_
         // forward GS sweep that also leaves the partials of ||b - A x|| (old x)
         AMG_ASSERT(!x_zero && !post);
         par_hybrid_gs(A, x, b, tmp, opt.gs_block, false, sink.partial);
-        norm_finish(A, sink, A.n_gs_slabs);
+        norm_finish(A, sink, A.gs_norm_parts());
     } else if (with_norm) {  // Jacobi sweep that also leaves the partials of ||b - A x||
         AMG_ASSERT(opt.smoother == AMG_SMOOTH_JACOBI && !x_zero);
         par_apply(A, KM_JACOBI, x, b, tmp, opt.jacobi_omega, sink.partial);

@@ -449,6 +449,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             n_tpl = (int)tb.hdr.size();
             n_tpl_ent = (int)tb.off.size();
             tpl_id.upload(tb.id.data(), tb.id.size());
+            tpl_id_host = tb.id;
             tpl_hdr.upload(tb.hdr.data(), tb.hdr.size());
             tpl_off.upload(tb.off.data(), tb.off.size());
             tpl_val.upload(tb.val.data(), tb.val.size());
@@ -540,6 +541,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             tpl_win = tpl_wend = 0;
             tpl_ldo.reset();
             tpl_id.reset();
+            tpl_id_host.clear();
             tpl_hdr.reset();
             tpl_off.reset();
             tpl_val.reset();
@@ -688,12 +690,144 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
     auto local_col = [&](int64_t g) -> int {
         return g >= clo && g < chi ? (int)(g - clo) : (int)(n_cols_local + plan.find(g));
     };
-    // chunks (global multiples of B clipped to the rank), packed whole into <= 64-row slabs
+    // l1 diagonal of every row: d_i = a_ii + sum of |a_ij| outside the row's chunk (global
+    // multiples of B clipped to the rank), summed in CSR order like the oracle
+    std::vector<double> di(n_rows);
+    std::atomic<bool> zero_row{false};
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n_rows; ++i) {
+        const int64_t g = first_row + i;
+        const int64_t cs = std::max<int64_t>(first_row, g / B * B);
+        const int64_t ce = std::min(first_row + n_rows, (g / B + 1) * B);
+        double l1 = 0.0, d = 0.0;
+        for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) {
+            const int64_t gc = host.col[k];
+            if (gc < cs || gc >= ce) l1 += std::fabs(host.val[k]);
+            if (gc == g) d = host.val[k];
+        }
+        if (d == 0.0 && l1 == 0.0) zero_row.store(true, std::memory_order_relaxed);
+        di[i] = 1.0 / (d + l1);
+    }
+    AMG_CHECK(!zero_row.load(), "hybrid GS: zero row");
+    // GS templates: a 512-row block runs on tpl_gs_kernel when every row has
+    // a row template (all columns local) and the (template, l1 diagonal) pairs fit the table.
+    // Chunks must not straddle a wave's 64-row group: first_row % 64 == 0 and B | 64.
+    std::vector<char> tblk;
+    n_gs_tpl = n_gs_tblk = 0;
+    gs_tid.reset();
+    gs_thdr.reset();
+    gs_tdl.reset();
+    gs_tblocks.reset();
+    gs_tcvm.reset();
+    gs_tcvp.reset();
+    gs_tcf.reset();
+    gs_tkem.reset();
+    gs_tkep.reset();
+    gs_racc.reset();
+    {
+        const char* e = std::getenv("AMG_GS_TEMPLATES");
+        const bool allow = !(e && std::atoi(e) == 0);
+        // the template kernels take one chain coupling per row: every template's in-chunk
+        // offsets (0 < |o| < B) must be -1 / +1 only
+        std::vector<int> hdrs, toff;
+        std::vector<double> tval;
+        bool shape_ok = n_tpl > 0 && tpl_win > 0;
+        if (shape_ok) {
+            hdrs.resize(n_tpl);
+            toff.resize(n_tpl_ent);
+            tval.resize(n_tpl_ent);
+            HIP_CHECK(hipMemcpy(hdrs.data(), tpl_hdr.p, sizeof(int) * n_tpl, hipMemcpyDeviceToHost));
+            HIP_CHECK(hipMemcpy(toff.data(), tpl_off.p, sizeof(int) * n_tpl_ent, hipMemcpyDeviceToHost));
+            HIP_CHECK(hipMemcpy(tval.data(), tpl_val.p, sizeof(double) * n_tpl_ent, hipMemcpyDeviceToHost));
+            for (int o : toff)
+                if (o != 0 && o != -1 && o != 1 && std::llabs(o) < B) shape_ok = false;
+        }
+        if (allow && shape_ok && first_row % 64 == 0 && 64 % B == 0 &&
+            (int64_t)tpl_id_host.size() == n_rows) {
+            std::vector<uint8_t> gid((size_t)n_rows, (uint8_t)kTplNone);
+            std::vector<std::vector<std::pair<uint64_t, int>>> by_tpl(n_tpl);
+            std::vector<int> gbase;
+            std::vector<double> gdl;
+            bool ok = true;
+            for (int64_t i = 0; i < n_rows && ok; ++i) {
+                const int t = tpl_id_host[i];
+                if (t == kTplNone) continue;
+                uint64_t bits;
+                std::memcpy(&bits, &di[i], sizeof(bits));
+                int found = -1;
+                for (const auto& pr : by_tpl[t])
+                    if (pr.first == bits) {
+                        found = pr.second;
+                        break;
+                    }
+                if (found < 0) {
+                    if ((int)gbase.size() >= kTplMax) {
+                        ok = false;
+                        break;
+                    }
+                    found = (int)gbase.size();
+                    gbase.push_back(t);
+                    gdl.push_back(di[i]);
+                    by_tpl[t].push_back({bits, found});
+                }
+                gid[i] = (uint8_t)found;
+            }
+            if (ok) {
+                const int64_t nb = (n_rows + kTplRows - 1) / kTplRows;
+                tblk.assign((size_t)nb, 0);
+                std::vector<int> blist;
+                for (int64_t q = 0; q < nb; ++q) {
+                    bool all = true;
+                    for (int64_t i = q * kTplRows; i < std::min(n_rows, (q + 1) * kTplRows) && all; ++i)
+                        all = gid[i] != kTplNone;
+                    if (all) {
+                        tblk[q] = 1;
+                        blist.push_back((int)q);
+                    }
+                }
+                if (!blist.empty()) {
+                    std::vector<int> gh(gbase.size()), cf(gbase.size(), 0);
+                    std::vector<int> kem(gbase.size(), -1), kep(gbase.size(), -1);
+                    std::vector<double> cvm(gbase.size(), 0.0), cvp(gbase.size(), 0.0);
+                    for (size_t k = 0; k < gbase.size(); ++k) {
+                        const int h = hdrs[gbase[k]];
+                        gh[k] = h;
+                        const int st = h & 0xffff, ln = (h >> 16) & 0xff;
+                        for (int e = st; e < st + ln; ++e) {
+                            if (toff[e] == -1) cvm[k] = tval[e], cf[k] |= 1, kem[k] = e - st;
+                            if (toff[e] == 1) cvp[k] = tval[e], cf[k] |= 2, kep[k] = e - st;
+                        }
+                    }
+                    gs_tcvm.upload(cvm.data(), cvm.size());
+                    gs_tcvp.upload(cvp.data(), cvp.size());
+                    gs_tcf.upload(cf.data(), cf.size());
+                    gs_tkem.upload(kem.data(), kem.size());
+                    gs_tkep.upload(kep.data(), kep.size());
+                    gs_racc.alloc((size_t)n_rows);
+                    gs_tid.upload(gid.data(), gid.size());
+                    gs_thdr.upload(gh.data(), gh.size());
+                    gs_tdl.upload(gdl.data(), gdl.size());
+                    gs_tblocks.upload(blist.data(), blist.size());
+                    n_gs_tpl = (int)gbase.size();
+                    n_gs_tblk = (int)blist.size();
+                } else {
+                    tblk.clear();
+                }
+            }
+        }
+    }
+    auto on_tpl = [&](int64_t r) { return !tblk.empty() && tblk[(size_t)(r / kTplRows)] != 0; };
+    // the other rows: chunks packed whole into <= 64-row slabs; interior slabs (no halo
+    // column) first, so par_hybrid_gs runs them while the halo is in flight
     std::vector<int4> slabs;
-    int64_t cells = 0;
+    std::vector<char> sbnd;
     for (int64_t r = 0; r < n_rows;) {
+        if (on_tpl(r)) {
+            r = std::min(n_rows, (r / kTplRows + 1) * kTplRows);
+            continue;
+        }
         int64_t end = r;
-        while (end < n_rows) {
+        while (end < n_rows && !on_tpl(end)) {
             const int64_t g = first_row + end;
             const int64_t ce = std::min(n_rows, (g / B + 1) * B - first_row);
             if (ce - r > 64) break;
@@ -701,32 +835,44 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
         }
         AMG_ASSERT(end > r);
         int w = 0;
-        for (int64_t i = r; i < end; ++i) w = std::max<int>(w, (int)(host.rp[i + 1] - host.rp[i]));
-        slabs.push_back(make_int4((int)r, (int)(end - r), (int)cells, w));
-        cells += (w + 3) & ~3;  // slabs start at multiples of 4 cells (dictionary dwords)
+        char bnd = 0;
+        for (int64_t i = r; i < end; ++i) {
+            w = std::max<int>(w, (int)(host.rp[i + 1] - host.rp[i]));
+            for (int64_t k = host.rp[i]; k < host.rp[i + 1] && !bnd; ++k)
+                bnd = host.col[k] < first_col || host.col[k] >= first_col + n_cols_local;
+        }
+        slabs.push_back(make_int4((int)r, (int)(end - r), 0, w));
+        sbnd.push_back(bnd);
         r = end;
+    }
+    {
+        std::vector<int4> ordered;
+        ordered.reserve(slabs.size());
+        for (int pass = 0; pass < 2; ++pass)
+            for (size_t q = 0; q < slabs.size(); ++q)
+                if (sbnd[q] == pass) ordered.push_back(slabs[q]);
+        n_gs_slabs_int = 0;
+        for (char c : sbnd) n_gs_slabs_int += c == 0;
+        slabs.swap(ordered);
+    }
+    int64_t cells = 0;
+    for (int4& sl : slabs) {
+        sl.z = (int)cells;
+        cells += (sl.w + 3) & ~3;  // slabs start at multiples of 4 cells (dictionary dwords)
     }
     AMG_CHECK((cells + 4) * 64 < INT_MAX, "hybrid GS: sliced-ELL too large for int32 offsets");
     std::vector<int> sc((size_t)(cells + 4) * 64, -1);
-    std::vector<double> sv(sc.size(), 0.0), di(n_rows);
+    std::vector<double> sv(sc.size(), 0.0);
 #pragma omp parallel for schedule(dynamic, 64)
     for (size_t q = 0; q < slabs.size(); ++q) {
         const int4 sl = slabs[q];
         for (int l = 0; l < sl.y; ++l) {
-            const int64_t i = sl.x + l, g = first_row + i;
-            const int64_t cs = std::max<int64_t>(first_row, g / B * B);
-            const int64_t ce = std::min(first_row + n_rows, (g / B + 1) * B);
-            double l1 = 0.0, d = 0.0;
+            const int64_t i = sl.x + l;
             for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) {
-                const int64_t gc = host.col[k];
                 const size_t at = ((size_t)sl.z + (size_t)(k - host.rp[i])) * 64 + l;
-                sc[at] = local_col(gc);
+                sc[at] = local_col(host.col[k]);
                 sv[at] = host.val[k];
-                if (gc < cs || gc >= ce) l1 += std::fabs(host.val[k]);
-                if (gc == g) d = host.val[k];
             }
-            AMG_CHECK(d != 0.0 || l1 != 0.0, "hybrid GS: zero row");
-            di[i] = 1.0 / (d + l1);
         }
     }
     // value dictionary: <= 256 distinct values (bit patterns) in the local operator; each
@@ -786,7 +932,13 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
     gs_dinv.upload(di.data(), di.size());
     n_gs_slabs = (int)slabs.size();
     gs_block = B;
-    gs_bytes = (gs_ndict > 0 ? 5 : 12) * 64 * cells + 16 * (int64_t)slabs.size() + 32 * n_rows;
+    // bytes per sweep: ELL cells + slab headers + 32 B per ELL row (b, x, dinv, y)
+    int64_t ell_rows = 0;
+    for (const int4& sl : slabs) ell_rows += sl.y;
+    gs_bytes = (gs_ndict > 0 ? 5 : 12) * 64 * cells + 16 * (int64_t)slabs.size() + 32 * ell_rows;
+    // template rows: acc kernel 1 B id + b + x (window) + acc out; chain kernel acc + x + id + y
+    if (n_gs_tblk > 0)
+        gs_bytes += 50 * (n_rows - ell_rows) + 16 * (int64_t)n_tpl_ent + 12 * (int64_t)n_gs_tpl;
     gs_wide = !slabs.empty() && cells >= (int64_t)kGsWide * (int64_t)slabs.size();
 }
 
@@ -882,8 +1034,11 @@ void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, in
                    bool backward, double* partial) {
     A.ensure_gs_blocks(block);
     const bool comm = A.halo_begin(x);
+    hipStream_t s = A.ctx->stream;
+    // template blocks and interior slabs never read the halo: they run while it is in flight
+    launch_hybrid_gs(s, A, x, b, y, backward, partial, 0, A.n_gs_slabs_int, true);
     if (comm) A.halo_wait();
-    launch_hybrid_gs(A.ctx->stream, A, x, b, y, backward, partial);
+    launch_hybrid_gs(s, A, x, b, y, backward, partial, A.n_gs_slabs_int, A.n_gs_slabs, false);
 }
 
 void norm_finish(DevMatrix& A, const NormSink& ns, int nparts) {

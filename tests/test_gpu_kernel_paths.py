@@ -248,3 +248,64 @@ def test_full_size_27pt_256(ctx, oracle):
     assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs(x, b, 64))
     A.hybrid_gs(dx, db, out, 64, backward=True)
     assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs_backward(x, b, 64))
+
+
+# ---- hybrid GS on row templates -----------------------------------------
+GS_SHAPES = [("27pt", (260, 8, 8)), ("27pt", (40, 40, 40)), ("7pt", (37, 41, 29)), ("5pt", (200, 61))]
+
+
+@pytest.mark.parametrize("tpl_gs", [True, False], ids=["templates", "ell"])
+@pytest.mark.parametrize("kind,dims", GS_SHAPES, ids=[f"{k}-{'x'.join(map(str, d))}" for k, d in GS_SHAPES])
+def test_hybrid_gs_template_kernel(ctx, oracle, monkeypatch, kind, dims, tpl_gs):
+    """l1 hybrid GS, forward / backward, block sizes 64, 32, 8, 1 (the template kernel needs B
+    | 64) and 17, 48 (sliced ELL only): bit-identical to the oracle on templated stencils
+    (NPL 16, 8 and 4 windows; a last partial block), with the template kernel on and off."""
+    import raptor_amd as ra
+
+    O = oracle
+    if not tpl_gs:
+        monkeypatch.setenv("AMG_GS_TEMPLATES", "0")
+    Ao = {"7pt": O.gen_7pt, "27pt": O.gen_27pt, "5pt": O.gen_5pt}[kind](*dims)
+    A = _dev(ra, ctx, Ao)
+    n = Ao.shape[0]
+    x, b = O.vec_uniform(n, 3), O.vec_uniform(n, 4)
+    dx, db, out = to_dev(ctx, x), to_dev(ctx, b), ctx.empty(n)
+    for blk in (64, 32, 8, 1, 17, 48):
+        A.hybrid_gs(dx, db, out, blk)
+        assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs(x, b, blk)), ("fwd", blk)
+        A.hybrid_gs(dx, db, out, blk, backward=True)
+        assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs_backward(x, b, blk)), ("bwd", blk)
+    assert A._info()["gs_bytes"] > 0
+    # B = 8: every shape here has no in-chunk coupling but +-1 -> template kernels (50 B per
+    # row + table) when they are on, sliced ELL (>= 5 B per cell) when off
+    A.hybrid_gs(dx, db, out, 8)
+    per_row = A._info()["gs_bytes"] / n
+    assert (per_row < 60) if tpl_gs else (per_row > 60), per_row
+
+
+@pytest.mark.parametrize("tpl_gs", [True, False], ids=["templates", "ell"])
+def test_sa_gs_vcycle_template_kernel(ctx, oracle, monkeypatch, tpl_gs):
+    """SA + hybrid GS V-cycle and solve (fused forward-GS norm partials from both GS kernels)
+    against the oracle hierarchy, level-0 GS on the template kernel or on sliced ELL."""
+    import raptor_amd as ra
+
+    O = oracle
+    if not tpl_gs:
+        monkeypatch.setenv("AMG_GS_TEMPLATES", "0")
+    dims = (64, 40, 24)
+    Ao = O.gen_27pt(*dims)
+    A = ra.par_stencil_grid(ctx, "27pt", dims)
+    ml = ra.ParSmoothedAggregationSolver().setup(A)
+    Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS["sa"], smoother=O.SMOOTH_HYBRID_GS))
+    n = Ao.shape[0]
+    b = Ao.spmv(O.vec_uniform(n, 42))
+    db = to_dev(ctx, b)
+    dx = ctx.zeros(n)
+    xo = np.zeros(n)
+    for _ in range(2):
+        ml.cycle(dx, db)
+        xo = Ho.cycle(xo, b)
+        assert np.array_equal(to_host(ctx, dx), xo)
+    _, h = ml.solve(ctx.zeros(n), db, max_iter=5)
+    _, ho = Ho.solve(np.zeros(n), b, max_iter=5)
+    assert np.all(np.abs(h - ho) <= 1e-10 * ho)

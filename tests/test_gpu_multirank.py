@@ -253,3 +253,36 @@ def test_one_row_per_rank(oracle, values):
     for r, (got, _) in enumerate(res):
         for k in ("y", "r", "j"):
             assert np.array_equal(got[k], ref[k][r:r + 1]), (k, r)
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_multirank_gs_templates(oracle, monkeypatch, nranks):
+    """Hybrid GS per rank with the template kernel on interior blocks (size floor lowered so
+    the slabs' stencil rows template), interior ELL slabs before the halo wait, boundary slabs
+    after it: forward and backward sweeps bit-identical to the oracle with the rank cuts."""
+    import raptor_amd as ra
+
+    monkeypatch.setenv("AMG_TPL_MIN_ROWS", "0")
+    O = oracle
+    dims = (64, 16, 4 * nranks)  # 4 planes of 1024 rows per rank: first_row % 64 == 0
+    Ao = O.gen_27pt(*dims)
+    n = Ao.shape[0]
+    x, b = O.vec_uniform(n, 3), O.vec_uniform(n, 4)
+
+    def rank(r, nr, world):
+        ctx = ra.Context.loopback(r, nr, world)
+        A = ra.par_stencil_grid(ctx, "27pt", dims)
+        f, m = A.first_row, A.local_rows
+        dx, db, out = to_dev(ctx, x[f:f + m]), to_dev(ctx, b[f:f + m]), ctx.empty(m)
+        A.hybrid_gs(dx, db, out, 64)
+        fw = to_host(ctx, out)
+        A.hybrid_gs(dx, db, out, 64, backward=True)
+        return f, m, fw, to_host(ctx, out)
+
+    res = run_ranks(nranks, rank)
+    cuts = [f for f, *_ in res]
+    fo = Ao.hybrid_gs_cut(x, b, 64, False, cuts)
+    bo = Ao.hybrid_gs_cut(x, b, 64, True, cuts)
+    for f, m, fw, bw in res:
+        assert np.array_equal(fw, fo[f:f + m])
+        assert np.array_equal(bw, bo[f:f + m])
