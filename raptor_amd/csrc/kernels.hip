@@ -66,6 +66,22 @@ __device__ __forceinline__ double epilogue(const CsrArgs& a, int r, double s, do
     return a.x[r] + a.omega * (a.dinv[r] * t);
 }
 
+// s += stage[k] for k in [lo, hi), in order.  Eight LDS reads are issued before their eight
+// dependent adds, so a long row waits on LDS once per eight entries instead of once per
+// entry (the adds stay sequential: the oracle's summation order).
+__device__ __forceinline__ double lds_row_sum(const double* stage, int lo, int hi, double s) {
+    int k = lo;
+    for (; k + 8 <= hi; k += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = stage[k + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; k < hi; ++k) s += stage[k];
+    return s;
+}
+
 // XCD-aware bijection: consecutive row blocks land on the same XCD (blocks b and b+8 share
 // one under round-robin dispatch), so a row block's x neighbours (+-nx*ny rows) are in the
 // same L2.  Placement only changes speed, never results (MI355X_MICROARCH.md).
@@ -284,7 +300,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     __syncthreads();
     const int e0 = tid ? rends[tid - 1] : 0;
     double s = 0.0;
-    for (int k = e0; k < e1; ++k) s += stage[k];
+    s = lds_row_sum(stage, e0, e1, s);
     double out, sq = 0.0;
     if (MODE == KM_SPMV) {
         out = s;
@@ -323,7 +339,7 @@ __device__ __forceinline__ double block_long(const CsrArgs& a, int4 h0, double* 
             stage[k] = a.val[k0 + base + k] * xload(a, a.col[k0 + base + k]);
         __syncthreads();
         if (tid == 0)
-            for (int k = 0; k < cnt; ++k) s += stage[k];
+            s = lds_row_sum(stage, 0, cnt, s);
         __syncthreads();
     }
     const int r = r0 + tid;
@@ -464,7 +480,7 @@ __global__ __launch_bounds__(kTPB, 8) void csr_plain_kernel(PlainArgs a) {
                 v2d_t{vv[p].x * plain_x(a, cc[p].x), vv[p].y * plain_x(a, cc[p].y)};
         __syncthreads();
         const int lo = max(rs, base) - base, hi = min(re, base + kCAP) - base;
-        for (int k = lo; k < hi; ++k) s += stage[k];
+        s = lds_row_sum(stage, lo, hi, s);
         __syncthreads();  // the next chunk overwrites the stage
     }
     double out, sq = 0.0;
