@@ -32,7 +32,8 @@ constexpr int kCAP = 2048;  // nonzeros staged in LDS per workgroup (16 KiB of p
 constexpr int kPad = kCAP;  // col/val padding (entries): unconditional loads past a block's end
 constexpr int kTileLines = 256;  // x tile per workgroup: 256 lines x 64 B = 16 KiB of LDS
 constexpr int kNormParts = kTPB / 64;  // norm partials per CSR block (one per wave)
-constexpr int kGsWide = 128;     // sliced-ELL width from which hybrid GS uses the wide variant
+constexpr int kGsWide = 128;
+constexpr int kGatherRPB = 4;    // rows per lane of gather (rectangular-operator) row blocks     // sliced-ELL width from which hybrid GS uses the wide variant
 // row templates: 1-byte template id per row (kTplNone = row not templated)
 constexpr int kTplNone = 255;
 constexpr int kTplMax = 255;       // templates per operator
@@ -160,6 +161,9 @@ struct DevMatrix {
     // csr-stream variant bits (kernels.hip): 2 = XCD block order, 4 = gather (no x tile).
     // Set at build: x tile for square operators; gather + XCD order for rectangular ones.
     int default_variant = 0;
+    // rows per lane of gather blocks: kGatherRPB for short-row rectangular operators (avg <= 4
+    // entries per row: P of the classical hierarchy), whose blocks then hold up to 1024 rows
+    int gather_rpb = 1;
     // l1 hybrid GS (built on first use for a given block size B <= 64): GS chunks = global
     // multiples of B clipped to this rank, packed whole into slabs of <= 64 rows (one
     // wavefront each, lane = row).  Each slab's rows are stored sliced-ELL, column-major

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/raptor_amd.h"
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 namespace amg {
 
@@ -161,6 +162,15 @@ uint32_t hash32(int64_t gid, uint64_t seed);
 
 // Setup phase timing: with AMG_TIMING=1 in the environment, rank 0 prints
 // "[amg] <label> <ms>" to stderr for every phase (host wall clock).
+// roctx range for the lifetime of the object (rocprofv3 --marker-trace shows the setup phases,
+// solves and cycle replays on the host timeline)
+struct RoctxRange {
+    explicit RoctxRange(const char* name) { roctxRangePushA(name); }
+    ~RoctxRange() { roctxRangePop(); }
+    RoctxRange(const RoctxRange&) = delete;
+    RoctxRange& operator=(const RoctxRange&) = delete;
+};
+
 struct PhaseTimer {
     static bool enabled();
     explicit PhaseTimer(const HostComm& comm);

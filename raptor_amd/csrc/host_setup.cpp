@@ -614,6 +614,8 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
         const std::string L = "L" + std::to_string(l) + " ";
         const int64_t n = A.n_global_rows;
         if (l + 1 >= opt.max_levels || n <= opt.max_coarse) break;
+        const std::string rname = "setup level " + std::to_string(l);
+        RoctxRange range(rname.c_str());
         HostCSR P;
         std::vector<int32_t> split(A.nrows());
         if (opt.coarsen == AMG_COARSEN_SA) {

@@ -149,11 +149,15 @@ __device__ __forceinline__ void csr_pre_tile(const CsrArgs& a, int bid, CsrPre& 
 
 // PRE: 0 = load batch 1 here; 1 / 2 = batch 1 comes in *pre, which is then refilled with
 // block nxt's batch 1 (2: with VI indices) unless nxt < 0
-template <int MODE, bool NORM, bool TILE, bool VIB, int NU, int PRE = 0>
+// RPB: rows per lane (gather blocks of rectangular operators hold up to kTPB * kGatherRPB
+// rows; a short-row P block of 256 rows filled a quarter of its 2048-entry stage)
+template <int MODE, bool NORM, bool TILE, bool VIB, int NU, int PRE = 0, int RPB = 1>
 __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* stage, double* tabl,
                                              int* rends, CsrPre* pre = nullptr, int nxt = -1) {
     constexpr int U = kCAP / kTPB;  // 8 lane slots
     static_assert(NU >= 2 && NU % 2 == 0 && NU <= U && (TILE ? NU == U : true), "slot pairs");
+    static_assert(RPB == 1 || (!TILE && !NORM && (MODE == KM_SPMV || MODE == KM_SPMV_ADD)),
+                  "several rows per lane: gather SpMV / y += Ax only");
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     static_assert(!PRE || TILE, "prefetched batch 1: x-tile path only");
     int tid_line = 0;
@@ -190,6 +194,18 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     const int r0 = h0.x, r1 = h0.y, k0 = h0.z, nnz = h0.w;
     const int r = r0 + tid;
     const bool own = r < r1;
+    // rows r0 + tid + kTPB j, j >= 1 (RPB > 1): ends and y operands, loaded with batch 2
+    int e1m[RPB > 1 ? RPB : 1];
+    double pxm[RPB > 1 ? RPB : 1];
+    if constexpr (RPB > 1) {
+#pragma unroll
+        for (int j = 1; j < RPB; ++j) {
+            const int rj = r0 + tid + kTPB * j, rjj = rj < r1 ? rj : r0;
+            e1m[j] = a.rend[rjj];
+            rends[tid + kTPB * j] = e1m[j];
+            pxm[j] = MODE == KM_SPMV_ADD ? a.y[rjj] : 0.0;
+        }
+    }
     // Entry-to-lane map.  TILE: lane t holds entries 512 p + 2 t + {0, 1} (p < 4) of the
     // block-aligned val stream (k0 even): 16-byte value loads (profiles/r1o_libab.txt: A2
     // SpMV / Jacobi -8% / -9%).  Gather: lane t holds entries t + 256 u, so one wave-
@@ -298,6 +314,16 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
         for (int u = 0; u < NU; ++u) stage[tid + u * kTPB] = pr[u];
     }
     __syncthreads();
+    if constexpr (RPB > 1) {
+#pragma unroll
+        for (int j = 1; j < RPB; ++j) {
+            const int k = tid + kTPB * j, rj = r0 + k;
+            if (rj < r1) {
+                const double sj = lds_row_sum(stage, rends[k - 1], e1m[j], 0.0);
+                a.y[rj] = MODE == KM_SPMV ? sj : pxm[j] + sj;
+            }
+        }
+    }
     const int e0 = tid ? rends[tid - 1] : 0;
     double s = 0.0;
     s = lds_row_sum(stage, e0, e1, s);
@@ -315,15 +341,16 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     return sq;
 }
 
-template <int MODE, bool NORM, bool TILE, bool VIB>
+template <int MODE, bool NORM, bool TILE, bool VIB, int GRPB = 1>
 __device__ __forceinline__ double block_dispatch(const CsrArgs& a, int bid, int nnz, double* stage,
                                                  double* tabl, int* rends) {
     if constexpr (TILE) {
         return block_main<MODE, NORM, TILE, VIB, 8>(a, bid, stage, tabl, rends);
     } else {
-        if (nnz > 4 * kTPB) return block_main<MODE, NORM, TILE, VIB, 8>(a, bid, stage, tabl, rends);
-        if (nnz > 2 * kTPB) return block_main<MODE, NORM, TILE, VIB, 4>(a, bid, stage, tabl, rends);
-        return block_main<MODE, NORM, TILE, VIB, 2>(a, bid, stage, tabl, rends);
+        constexpr int RP = (MODE == KM_SPMV || MODE == KM_SPMV_ADD) && !NORM ? GRPB : 1;
+        if (nnz > 4 * kTPB) return block_main<MODE, NORM, TILE, VIB, 8, 0, RP>(a, bid, stage, tabl, rends);
+        if (nnz > 2 * kTPB) return block_main<MODE, NORM, TILE, VIB, 4, 0, RP>(a, bid, stage, tabl, rends);
+        return block_main<MODE, NORM, TILE, VIB, 2, 0, RP>(a, bid, stage, tabl, rends);
     }
 }
 
@@ -342,11 +369,12 @@ __device__ __forceinline__ double block_long(const CsrArgs& a, int4 h0, double* 
             s = lds_row_sum(stage, 0, cnt, s);
         __syncthreads();
     }
-    const int r = r0 + tid;
-    if (r < r1 && (tid == 0 || nnz == 0)) {  // nnz == 0: every row of the block is empty
-        double res = 0.0;
-        a.y[r] = epilogue<MODE>(a, r, s, &res);
-        if (NORM) sq = res * res;
+    for (int r = r0 + tid; r < r1; r += kTPB) {
+        if (r == r0 || nnz == 0) {  // nnz == 0: every row of the block is empty
+            double res = 0.0;
+            a.y[r] = epilogue<MODE>(a, r, s, &res);
+            if (NORM) sq += res * res;
+        }
     }
     return sq;
 }
@@ -361,20 +389,22 @@ __device__ __forceinline__ void block_partial(const CsrArgs& a, int bid, double 
     }
 }
 
-template <int MODE, bool NORM, bool XCD, bool TILE, bool VI>
-__global__ __launch_bounds__(kTPB, 8) void csr_block_kernel(CsrArgs a, int first_block) {
+// GRPB: rows per lane of gather blocks (1, or kGatherRPB for short-row rectangular operators
+// whose blocks hold up to kTPB * kGatherRPB rows; DevMatrix::gather_rpb)
+template <int MODE, bool NORM, bool XCD, bool TILE, bool VI, int GRPB = 1>
+__global__ __launch_bounds__(kTPB, GRPB > 1 ? 7 : 8) void csr_block_kernel(CsrArgs a, int first_block) {
     static_assert(kCAP / kTPB == 8 && kTileLines * 8 == kCAP && kTPB == 256,
                   "lane-major layouts assume 8 entries per lane, 4 waves");
     __shared__ __attribute__((aligned(16))) double stage[kCAP];  // x tile, then products
     __shared__ double tabl[VI ? 256 : 1];
-    __shared__ int rends[kTPB];
+    __shared__ int rends[kTPB * GRPB];
     const int bid = first_block + (XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x);
     const int4 h0 = a.hdr[2 * bid], h1 = a.hdr[2 * bid + 1];
     const int nnz = h0.w;
     double sq;
     if (nnz <= kCAP && (!TILE || (h1.y & 0xffff) <= kTileLines) && nnz > 0) {
-        if (VI && h1.z >= 0) sq = block_dispatch<MODE, NORM, TILE, true>(a, bid, nnz, stage, tabl, rends);
-        else sq = block_dispatch<MODE, NORM, TILE, false>(a, bid, nnz, stage, tabl, rends);
+        if (VI && h1.z >= 0) sq = block_dispatch<MODE, NORM, TILE, true, GRPB>(a, bid, nnz, stage, tabl, rends);
+        else sq = block_dispatch<MODE, NORM, TILE, false, GRPB>(a, bid, nnz, stage, tabl, rends);
     } else {
         sq = block_long<MODE, NORM>(a, h0, stage);
     }
@@ -1701,6 +1731,17 @@ static void launch_csr_persist(hipStream_t s, int mode, bool norm, const CsrArgs
     HIP_CHECK(hipGetLastError());
 }
 
+template <int M, bool N, bool X, bool T, bool V>
+static void launch_block(hipStream_t s, dim3 g, const CsrArgs& a, int first_block, bool rpb4) {
+    if constexpr (!T && !N && (M == KM_SPMV || M == KM_SPMV_ADD)) {
+        if (rpb4) {
+            hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, kGatherRPB>), g, dim3(kTPB), 0, s, a, first_block);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V>), g, dim3(kTPB), 0, s, a, first_block);
+}
+
 void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, int first_block,
                        int n_blocks, const double* x, const double* b, double* y, double omega,
                        double* partial, int part_off) {
@@ -1710,13 +1751,14 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
               A.rp.p, A.col.p, A.val.p,
               x, A.halo.p, ncl, nh, (ncl + 7) / 8, (ncl >= 2 && nh != 1) ? 1 : 0, A.square ? 0 : 1,
               b, A.dinv.p, y, omega, partial, part_off};
-    dim3 g(n_blocks), t(kTPB);
+    const dim3 g(n_blocks);
     const int var = kernel_variant(A);
     if ((var & 64) && !(var & 4)) {
         launch_csr_persist(s, mode, norm, a, first_block, n_blocks, (var & 8) != 0);
         return;
     }
-#define AMG_L1(M, N, X, T, V) hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V>), g, t, 0, s, a, first_block)
+    const bool rpb4 = A.gather_rpb > 1;
+#define AMG_L1(M, N, X, T, V) launch_block<M, N, X, T, V>(s, g, a, first_block, rpb4)
 #define AMG_L2(M, N, V)                                               \
     do {                                                              \
         const bool xo = var & 2, tl = !(var & 4);                     \

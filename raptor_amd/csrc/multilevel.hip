@@ -14,6 +14,7 @@ Solver::~Solver() {
 }
 
 void Solver::setup(DevMatrix& A, const amg_options& o) {
+    RoctxRange range("ParMultilevel::setup");
     AMG_CHECK(A.square, "AMG setup needs a square matrix");
     AMG_CHECK(o.pre_sweeps >= 0 && o.post_sweeps >= 0, "negative sweep count");
     AMG_CHECK(o.max_levels >= 1, "max_levels must be >= 1");
@@ -30,7 +31,10 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
             return spgemm_device(*ctx, comm, X, Y);
         };
     PhaseTimer tm(comm);
-    build_hierarchy(comm, A.host, opt, H, galerkin);
+    {
+        RoctxRange r("setup: hierarchy (strength, split / aggregates, P, R, Galerkin)");
+        build_hierarchy(comm, A.host, opt, H, galerkin);
+    }
     tm.lap("hierarchy (host + SpGEMM)");
     // replicated coarse levels (multi-rank): from the first level with <= replicate_below
     // global rows on, every rank holds the whole operators and cycles them locally
@@ -43,6 +47,7 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
             }
     levels.clear();
     levels.resize(H.levels.size());
+    RoctxRange rbuild("setup: device level formats");
     for (size_t l = 0; l < H.levels.size(); ++l) {
         HostLevel& hl = H.levels[l];
         const bool rep = rep_level >= 0 && (int)l >= rep_level;
@@ -226,6 +231,7 @@ bool Solver::can_fuse_norm() const {
 void Solver::cycle(double* x, const double* b, bool with_norm) {
     AMG_ASSERT(!with_norm || can_fuse_norm());
     if (!use_graph) {
+        RoctxRange r("cycle: eager");
         cycle_rec(0, x, b, false, with_norm);
         return;
     }
@@ -235,6 +241,7 @@ void Solver::cycle(double* x, const double* b, bool with_norm) {
         if (G.exec) HIP_CHECK(hipGraphExecDestroy(G.exec));
         G.exec = nullptr;
         hipGraph_t g = nullptr;
+        RoctxRange r("cycle: hipGraph capture");
         HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         try {
             cycle_rec(0, x, b, false, with_norm);
@@ -250,11 +257,13 @@ void Solver::cycle(double* x, const double* b, bool with_norm) {
         G.b = b;
         G.fmt_gen = DevMatrix::format_generation;
     }
+    RoctxRange r("cycle: hipGraph replay");
     HIP_CHECK(hipGraphLaunch(G.exec, s));
 }
 
 int32_t Solver::solve(double* x, const double* b, int32_t max_iter, double tol, double* hist_host) {
     AMG_CHECK(max_iter >= 0, "max_iter must be >= 0");
+    RoctxRange range("ParMultilevel::solve");
     hipStream_t s = ctx->stream;
     ensure_hist(max_iter + 1);
     HIP_CHECK(hipMemsetAsync(hist_counter.p, 0, sizeof(int), s));
@@ -316,6 +325,7 @@ void Solver::dot(const double* a, const double* b, double* dst, bool take_sqrt) 
 
 int32_t Solver::pcg(double* x, const double* b, int32_t max_iter, double tol, double* hist_host) {
     AMG_CHECK(max_iter >= 0, "max_iter must be >= 0");
+    RoctxRange range("ParMultilevel::pcg");
     DevMatrix& A = *A0;
     const int64_t n = A.n_rows;
     hipStream_t s = ctx->stream;

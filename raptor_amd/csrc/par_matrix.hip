@@ -44,7 +44,7 @@ struct BlockBuild {
 // changes, and all-templated interior blocks come first
 static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector<int>& col,
                                    const std::vector<uint8_t>& cls, int64_t ncl, int64_t nhalo,
-                                   const std::vector<uint8_t>* tplf = nullptr) {
+                                   const std::vector<uint8_t>* tplf = nullptr, int row_cap = kTPB) {
     const int n = (int)rp.size() - 1;
     const int64_t hl0 = (ncl + 7) / 8;
     auto line_of = [&](int c) -> int64_t { return c < ncl ? c >> 3 : hl0 + ((c - ncl) >> 3); };
@@ -92,7 +92,7 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
     for (int r = 0; r < n; ++r) {
         const long long len = rp[r + 1] - rp[r];
         collect(r, 2 * (int64_t)r);
-        if (r > r0 && (cls[r] != cls[r0] || acc + len > kCAP || r - r0 >= kTPB ||
+        if (r > r0 && (cls[r] != cls[r0] || acc + len > kCAP || r - r0 >= row_cap ||
                        nl + (int)cand.size() > kTileLines || (tplf && (*tplf)[r] != (*tplf)[r0]))) {
             emit(r0, r);  // closes [r0, r); blk advances
             r0 = r;
@@ -430,8 +430,12 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             tplf.resize(n_rows);
             for (int64_t i = 0; i < n_rows; ++i) tplf[i] = tb.id[i] != kTplNone && cls[i] == 0;
         }
+        // square operators: x tiles, one row per lane; short-row rectangular ones (gather
+        // path): up to kGatherRPB rows per lane (profiles/r2n: P0 x += P e 162 -> 95 us; R
+        // with 7+ entries per row was slower that way: R0 94 -> 106 us, sa27 R0 350 -> 415)
+        gather_rpb = !square && nnz <= 4 * n_rows ? kGatherRPB : 1;
         BlockBuild bb = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(),
-                                         tplf.empty() ? nullptr : &tplf);
+                                         tplf.empty() ? nullptr : &tplf, kTPB * gather_rpb);
         nb_int = bb.nb_int;
         nb_bnd = bb.nb_bnd;
         if (!tb.hdr.empty()) {
