@@ -222,8 +222,14 @@ int amg_solver_solve(amg_solver S, double* x, const double* b, int32_t max_iter,
  * caller of the cycle).  Same contract as amg_solver_solve; hist receives ||r_k||. */
 int amg_solver_pcg(amg_solver S, double* x, const double* b, int32_t max_iter, double tol,
                    double* hist, int32_t* iters);
-/* Capture each V-cycle in a hipGraph and replay it (1 = on, default on for 1 rank). */
+/* Capture each V-cycle in a hipGraph and replay it (1 = on; default on for 1 rank, off for
+ * several: loopback ranks meet at host barriers; with the RCCL transport capture is allowed
+ * (the send/recv groups and allgathers are captured with the kernels) but experimental --
+ * see DESIGN.md 5). */
 int amg_solver_set_graph(amg_solver S, int32_t enable);
+/* 1 while cycles replay a hipGraph (0 after set_graph(0), or if the runtime refused to
+ * instantiate a multi-rank graph and the solver fell back to eager launches). */
+int amg_solver_get_graph(amg_solver S, int32_t* enabled);
 int amg_solver_destroy(amg_solver S);
 
 /* ---- host-only hierarchy (no GPU needed) ------------------------------------------ */

@@ -407,6 +407,13 @@ class ParMultilevel:
                                            out.ctypes.data_as(C.POINTER(C.c_int32))))
         return out
 
+    @property
+    def graph_enabled(self) -> bool:
+        """True while cycles replay a captured hipGraph."""
+        v = C.c_int32()
+        check(lib().amg_solver_get_graph(self.h, C.byref(v)))
+        return bool(v.value)
+
     def bytes_per_cycle(self) -> int:
         """Algorithmic HBM bytes of one V-cycle on this rank."""
         return sum(self.level_info(l)["bytes_per_cycle_local"] for l in range(self.num_levels))

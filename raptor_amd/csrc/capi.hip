@@ -526,13 +526,22 @@ int amg_solver_pcg(amg_solver S, double* x, const double* b, int32_t max_iter, d
 int amg_solver_set_graph(amg_solver S, int32_t enable) {
     return guard([&] {
         AMG_CHECK(S, "null solver");
-        AMG_CHECK(!enable || S->s.ctx->host.nranks == 1, "hipGraph capture is single-rank only");
+        AMG_CHECK(!enable || S->s.ctx->host.nranks == 1 || S->s.ctx->transport == TR_RCCL,
+                  "hipGraph capture needs one rank or the RCCL transport (loopback ranks "
+                  "synchronise on the host)");
         S->s.use_graph = enable != 0;
         for (auto& g : S->s.graphs)
             if (g.exec) {
                 HIP_CHECK(hipGraphExecDestroy(g.exec));
                 g.exec = nullptr;
             }
+    });
+}
+
+int amg_solver_get_graph(amg_solver S, int32_t* enabled) {
+    return guard([&] {
+        AMG_CHECK(S && enabled, "null argument");
+        *enabled = S->s.use_graph ? 1 : 0;
     });
 }
 

@@ -10,6 +10,9 @@
 #include <map>
 #include <mutex>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "device.hpp"
 
 namespace amg {
@@ -176,7 +179,10 @@ void loopback_before_pack(Context& c, const std::vector<int>& send_procs) {
 
 void Context::allgather(const double* send, double* recv, size_t count) {
     if (transport == TR_RCCL) {
+        static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
+        if (trace) std::fprintf(stderr, "[amg] rank %d allgather %zu\n", host.rank, count);
         NCCL_CHECK(ncclAllGather(send, recv, count, ncclDouble, nccl, stream));
+        if (trace) std::fprintf(stderr, "[amg] rank %d allgather enqueued\n", host.rank);
         return;
     }
     if (transport != TR_LOOPBACK) {

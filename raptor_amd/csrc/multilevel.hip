@@ -2,6 +2,7 @@
 // SURVEY.md 8a rows a6-a10.  The cycle mirrors oracle/amg_oracle.c cycle_rec() operation
 // for operation, so the iterates are bit-identical to the oracle's.
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 
 #include "device.hpp"
@@ -128,6 +129,10 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         bfull.alloc((size_t)npad + (size_t)cmax);  // gathered + local padded send slot
         HIP_CHECK(hipMemset(bfull.p, 0, bfull.n * sizeof(double)));
     }
+    // multi-rank cycles run eagerly by default: loopback ranks meet at host barriers, which a
+    // graph cannot replay, and capturing the RCCL groups (amg_solver_set_graph(1) allows it)
+    // crashed in hipStreamEndCapture on the 1-GPU socket-transport test setup (torch's RCCL
+    // 2.26.6 in the process) -- not validated over xGMI
     use_graph = comm.nranks == 1;
 }
 
@@ -242,6 +247,8 @@ void Solver::cycle(double* x, const double* b, bool with_norm) {
         G.exec = nullptr;
         hipGraph_t g = nullptr;
         RoctxRange r("cycle: hipGraph capture");
+        static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
+        if (trace) std::fprintf(stderr, "[amg] rank %d capture begin\n", ctx->host.rank);
         HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         try {
             cycle_rec(0, x, b, false, with_norm);
@@ -251,14 +258,27 @@ void Solver::cycle(double* x, const double* b, bool with_norm) {
             throw;
         }
         HIP_CHECK(hipStreamEndCapture(s, &g));
-        HIP_CHECK(hipGraphInstantiate(&G.exec, g, nullptr, nullptr, 0));
+        if (trace) std::fprintf(stderr, "[amg] rank %d capture end\n", ctx->host.rank);
+        const hipError_t ie = hipGraphInstantiate(&G.exec, g, nullptr, nullptr, 0);
         HIP_CHECK(hipGraphDestroy(g));
+        if (ie != hipSuccess) {
+            // a multi-rank graph the runtime cannot instantiate: replay nothing, run eagerly
+            // from now on (identical results; only the launch overhead differs)
+            AMG_CHECK(ctx->host.nranks > 1, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+            (void)hipGetLastError();
+            G.exec = nullptr;
+            use_graph = false;
+            cycle_rec(0, x, b, false, with_norm);
+            return;
+        }
         G.x = x;
         G.b = b;
         G.fmt_gen = DevMatrix::format_generation;
     }
     RoctxRange r("cycle: hipGraph replay");
     HIP_CHECK(hipGraphLaunch(G.exec, s));
+    static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
+    if (trace) std::fprintf(stderr, "[amg] rank %d graph launched\n", ctx->host.rank);
 }
 
 int32_t Solver::solve(double* x, const double* b, int32_t max_iter, double tol, double* hist_host) {

@@ -11,6 +11,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <unordered_map>
 
@@ -995,6 +996,9 @@ bool DevMatrix::halo_begin(const double* x) {
         return true;
     }
     if (plan.send_idx.empty() && plan.halo_gid.empty()) return false;
+    static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
+    if (trace) std::fprintf(stderr, "[amg] rank %d halo_begin seq %lld send %zu recv %lld\n", comm.rank,
+                            (long long)seq, plan.send_idx.size(), (long long)plan.n_halo());
     launch_pack(s, (int64_t)plan.send_idx.size(), send_idx.p, x, send_buf.p);
     HIP_CHECK(hipEventRecord(ctx->ev_pack, s));
     HIP_CHECK(hipStreamWaitEvent(cs, ctx->ev_pack, 0));
@@ -1006,6 +1010,7 @@ bool DevMatrix::halo_begin(const double* x) {
         NCCL_CHECK(ncclRecv(halo.p + plan.recv_ptr[p], (size_t)(plan.recv_ptr[p + 1] - plan.recv_ptr[p]),
                             ncclDouble, plan.recv_procs[p], ctx->nccl, cs));
     NCCL_CHECK(ncclGroupEnd());
+    if (trace) std::fprintf(stderr, "[amg] rank %d halo group enqueued\n", comm.rank);
     HIP_CHECK(hipEventRecord(ctx->ev_halo, cs));
     return true;
 }

@@ -72,6 +72,7 @@ def main():
     dx = ctx.zeros(m)
     _, hp = ml.pcg(dx, bb, max_iter=5)
     res["pcg"] = hp
+    res["graph_used"] = ml.graph_enabled
     np.savez(f"{out}.{rank}.npz", **res)
     dist.barrier()
     del ml, A

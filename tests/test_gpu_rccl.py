@@ -107,3 +107,4 @@ def test_rccl_vcycle_bit_exact(oracle, tmp_path, nranks, spec, graph):
         assert np.all(np.abs(r["hist"] - hist_o) <= 1e-10 * hist_o)
         assert np.all(np.abs(r["pcg"] - pcg_o) <= 1e-9 * pcg_o[0])
         assert np.array_equal(r["hist"], res[0]["hist"])  # every rank reports the same
+        assert bool(r["graph_used"]) == graph  # captured and replayed, no eager fallback
