@@ -182,7 +182,10 @@ typedef struct amg_options {
     int64_t max_coarse;       /* stop when the global size is <= this; dense solve there */
     int64_t gs_block;         /* hybrid GS block (global row multiples)                 */
     uint64_t seed;            /* PMIS / MIS(2) hash seed                                 */
-    int32_t setup_device;     /* 1: Galerkin SpGEMM R(AP) on the GPU (default), 0: host  */
+    int32_t setup_device;     /* 1 (default): setup on the GPU -- strength, PMIS / MIS(2),
+                                 P, R = P^T (one rank; several ranks: host) and the
+                                 Galerkin SpGEMM R(AP); 2: Galerkin SpGEMM only; 0: host.
+                                 Results are identical in every mode.                     */
     int64_t replicate_below;  /* multi-rank: levels with <= this many global rows are held
                                  whole by every rank and cycled without communication (one
                                  allgather of b per cycle); 0 = never.  Default 65536.      */

@@ -368,7 +368,7 @@ class ParMultilevel:
         self.options = Options(self._COARSEN[coarsen], self._SMOOTH[smoother],
                                float(strong_threshold), float(jacobi_omega), int(pre_sweeps),
                                int(post_sweeps), int(max_levels), int(max_coarse), int(gs_block),
-                               int(seed), 1 if setup_device else 0, int(replicate_below))
+                               int(seed), int(setup_device), int(replicate_below))
         self.use_graph = use_graph
         self.h = None
         self.A = None

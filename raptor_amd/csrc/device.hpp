@@ -114,6 +114,11 @@ struct Context {
 
 // Galerkin SpGEMM on the device (spgemm.hip); result downloaded as a host image
 HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, const HostCSR& B);
+// device setup of one level (setup_device.hip, single rank): strength, PMIS or MIS(2)
+// aggregation, classical or smoothed-aggregation P; false where it does not apply
+bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, const amg_options& opt,
+                        int level, HostCSR& P, std::vector<int32_t>& split);
+bool transpose_device(Context& ctx, const HostComm& comm, const HostCSR& P, HostCSR& R);
 
 void loopback_join(Context& c, int rank, int nranks, const std::string& world);
 void loopback_leave(Context& c);

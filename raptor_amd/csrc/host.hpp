@@ -154,8 +154,14 @@ struct HostHierarchy {
 // Galerkin SpGEMM hook: C = A * B for the local rows (the device SpGEMM of spgemm.hip when
 // the hierarchy is built for a GPU solver; the host spgemm() otherwise).  Same results.
 using SpgemmFn = std::function<HostCSR(const HostCSR&, const HostCSR&)>;
+// Device hooks for the rest of a level's setup (setup_device.hip, single rank): P and the
+// integer split of level l, and R = P^T.  Each returns false where it does not apply (the
+// host algorithms below run instead); results are identical either way.
+using LevelSetupFn = std::function<bool(int level, const HostCSR& A, HostCSR& P, std::vector<int32_t>& split)>;
+using TransposeFn = std::function<bool(const HostCSR& P, HostCSR& R)>;
 void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options& opt,
-                     HostHierarchy& H, const SpgemmFn& galerkin = nullptr);
+                     HostHierarchy& H, const SpgemmFn& galerkin = nullptr,
+                     const LevelSetupFn& level_fn = nullptr, const TransposeFn& transpose_fn = nullptr);
 
 uint64_t mix64(uint64_t z);
 uint32_t hash32(int64_t gid, uint64_t seed);

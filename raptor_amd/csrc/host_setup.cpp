@@ -600,7 +600,8 @@ std::vector<double> dense_inverse_gathered(const HostComm& comm, const HostCSR& 
 }
 
 void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options& opt,
-                     HostHierarchy& H, const SpgemmFn& galerkin) {
+                     HostHierarchy& H, const SpgemmFn& galerkin, const LevelSetupFn& level_fn,
+                     const TransposeFn& transpose_fn) {
     AMG_CHECK(opt.max_levels >= 1, "max_levels must be >= 1");
     auto mm = [&](const HostCSR& X, const HostCSR& Y) {
         return galerkin ? galerkin(X, Y) : spgemm(comm, X, Y);
@@ -618,7 +619,9 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
         RoctxRange range(rname.c_str());
         HostCSR P;
         std::vector<int32_t> split(A.nrows());
-        if (opt.coarsen == AMG_COARSEN_SA) {
+        if (level_fn && level_fn(l, A, P, split)) {
+            tm.lap(L + "device strength + split / aggregates + P");
+        } else if (opt.coarsen == AMG_COARSEN_SA) {
             HostCSR S = strength_symmetric(comm, A, std::ldexp(opt.strong_threshold, -l));
             tm.lap(L + "strength");
             int64_t na = 0;
@@ -643,7 +646,8 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
         // coarsening stalled (same rule as the oracle): no coarse points, no reduction, or
         // less than 20% reduction on a level small enough to be the dense-solved coarsest
         if (nc == 0 || nc >= n || (n <= 8192 && 5 * nc > 4 * n)) break;
-        HostCSR R = transpose(comm, P);
+        HostCSR R;
+        if (!(transpose_fn && transpose_fn(P, R))) R = transpose(comm, P);
         tm.lap(L + "transpose");
         HostCSR AP = mm(A, P);
         tm.lap(L + "A*P");

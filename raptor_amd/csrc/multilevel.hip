@@ -27,14 +27,27 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     const HostComm& comm = ctx->host;
     HostHierarchy H;
     SpgemmFn galerkin = nullptr;
-    if (opt.setup_device)
+    LevelSetupFn level_fn = nullptr;
+    TransposeFn transpose_fn = nullptr;
+    if (opt.setup_device) {
         galerkin = [this, &comm](const HostCSR& X, const HostCSR& Y) {
             return spgemm_device(*ctx, comm, X, Y);
         };
+        // setup_device == 1: the whole level setup on the GPU where it applies (one rank);
+        // 2: Galerkin products only (the round-1 split, for A/B and tests)
+        if (opt.setup_device == 1) {
+            level_fn = [this, &comm](int l, const HostCSR& A, HostCSR& P, std::vector<int32_t>& split) {
+                return level_setup_device(*ctx, comm, A, opt, l, P, split);
+            };
+            transpose_fn = [this, &comm](const HostCSR& P, HostCSR& R) {
+                return transpose_device(*ctx, comm, P, R);
+            };
+        }
+    }
     PhaseTimer tm(comm);
     {
         RoctxRange r("setup: hierarchy (strength, split / aggregates, P, R, Galerkin)");
-        build_hierarchy(comm, A.host, opt, H, galerkin);
+        build_hierarchy(comm, A.host, opt, H, galerkin, level_fn, transpose_fn);
     }
     tm.lap("hierarchy (host + SpGEMM)");
     // replicated coarse levels (multi-rank): from the first level with <= replicate_below

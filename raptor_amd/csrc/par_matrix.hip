@@ -147,6 +147,7 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
                               std::vector<uint8_t>& dvi, std::vector<char>& dvi_ok,
                               std::vector<int64_t>& vofs) {
     const size_t nbk = bb.blocks.size();
+    PhaseTimer tm(M.ctx->host);
     std::vector<std::vector<uint64_t>> tabs(nbk);
 #pragma omp parallel for schedule(dynamic, 64)
     for (size_t q = 0; q < nbk; ++q) {
@@ -158,6 +159,7 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
         t.erase(std::unique(t.begin(), t.end()), t.end());
         if (t.size() <= 256) tabs[q] = std::move(t);
     }
+    tm.lap("      vi: per-block sort / unique");
     std::vector<int> ptr(std::max<size_t>(nbk, 1), -1);
     int64_t total = 0, vin = 0;
     int nvi = 0;
@@ -190,6 +192,7 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
     }
     AMG_CHECK(vofs[nbk] < INT_MAX, "value index stream too large");
     std::vector<uint8_t> idx((size_t)vofs[nbk] + 16, 0);
+    tm.lap("      vi: offsets");
 #pragma omp parallel for schedule(dynamic, 64)
     for (size_t q = 0; q < nbk; ++q) {
         if (tabs[q].empty()) continue;
@@ -222,8 +225,10 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
         }
         dvi_ok[q] = ok;
     }
+    tm.lap("      vi: indices + diagonal table slots");
     M.vtab.upload(tab.data(), tab.size());
     M.vidx.upload(idx.data(), idx.size());
+    tm.lap("      vi: upload");
 }
 
 
@@ -279,6 +284,19 @@ static TplBuild build_templates(const std::vector<int>& rp, const std::vector<in
                 return false;
         return true;
     };
+    // quick rejection (Galerkin coarse operators: nearly every row is its own shape): when
+    // 4096 rows spread over the operator already show more than 2 kTplMax distinct keys,
+    // the templates could not cover half the rows -- skip the full scan
+    if (n > 65536) {
+        std::vector<uint64_t> sk;
+        for (int t = 0; t < 4096; ++t) {
+            const int r = (int)((int64_t)n * t / 4096);
+            if (qualifies(r)) sk.push_back(key_hash(r));
+        }
+        std::sort(sk.begin(), sk.end());
+        sk.erase(std::unique(sk.begin(), sk.end()), sk.end());
+        if ((int)sk.size() > 2 * kTplMax) return T;
+    }
     const int nch = std::max(1, std::min(256, n / 16384));
     std::vector<std::vector<int>> reps(nch);       // representative row per local template
     std::vector<std::vector<uint64_t>> hashes(nch);
@@ -374,6 +392,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
     replicated = replicated_view;
     static const HostComm serial;  // rank 0 of 1: replicated matrices have no halo
     const HostComm& comm = replicated ? serial : ctx->host;
+    PhaseTimer tm(comm);
     AMG_CHECK((int)host.row_starts.size() == comm.nranks + 1, "matrix row partition size");
     AMG_CHECK((int)host.col_starts.size() == comm.nranks + 1, "matrix column partition size");
     first_row = host.row_starts[comm.rank];
@@ -386,6 +405,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
     square = host.n_global_rows == host.n_global_cols && host.row_starts == host.col_starts;
     plan = halo_plan_for_cols(comm, host);
     AMG_CHECK(n_cols_local + plan.n_halo() < INT_MAX, "too many columns for int32");
+    tm.lap("    build: halo plan");
 
     std::vector<int> hrp(n_rows + 1), hcol(nnz);
     std::vector<uint8_t> cls(n_rows, 0);
@@ -424,6 +444,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         const bool use = tb.rows == n_rows || (n_rows >= min_rows && 2 * tb.rows >= n_rows);
         if (!use) tb = TplBuild();
     }
+    tm.lap("    build: local columns, dinv, templates");
     hcol.resize(nnz + kPad, 0);
     {
         std::vector<uint8_t> tplf;
@@ -439,6 +460,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                                          tplf.empty() ? nullptr : &tplf, kTPB * gather_rpb);
         nb_int = bb.nb_int;
         nb_bnd = bb.nb_bnd;
+        tm.lap("    build: row blocks + x tiles");
         if (!tb.hdr.empty()) {
             // rows of blocks the CSR kernel still runs are not the template kernel's
             std::vector<char> keep(n_rows, 0);
@@ -552,6 +574,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             tpl_val.reset();
             tpl_pd.reset();
         }
+        tm.lap("    build: template window / march");
         blocks.upload(bb.blocks.data(), bb.blocks.size());
         const size_t nbk = bb.blocks.size();
         // device col / val: block-aligned copies -- block q's entries at an even offset
@@ -576,6 +599,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             // x-tile line ids at a fixed stride (kTileLines per block, padded with the block's
             // last line), so the kernel loads them without waiting for the block header
             std::vector<int> fx(std::max<size_t>(nbk, 1) * kTileLines, 0);
+#pragma omp parallel for schedule(static)
             for (size_t q = 0; q < nbk; ++q) {
                 const int t0 = bb.tile_ptr[q], nt = bb.tile_ptr[q + 1] - t0;
                 if (nt <= 0 || nt > kTileLines) continue;
@@ -586,6 +610,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             // lane-major per block (lane_pos): lane t's 8 indices are 16 contiguous bytes,
             // one 16-byte load per lane
             std::vector<uint16_t> perm(std::max<size_t>(nbk, 1) * kCAP, 0);
+#pragma omp parallel for schedule(static)
             for (size_t q = 0; q < nbk; ++q) {
                 const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
                 if (nz > kCAP) continue;
@@ -597,6 +622,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             tile_fixed.reset();
             lcol.reset();
         }
+        tm.lap("    build: col / val / tile layouts");
         std::vector<int> vt_off, vt_len;
         std::vector<uint8_t> hdvi;
         std::vector<char> dvi_ok;
@@ -604,6 +630,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         build_value_index(*this, hrp, bb, vt_off, vt_len, hdvi, dvi_ok, vofs);
         if (n_vi_blocks > 0 && square) dvi.upload(hdvi.data(), hdvi.size());
         else dvi.reset();
+        tm.lap("    build: value index");
         {
             // per row: end of its nonzeros relative to its block's first (<= kCAP: 16 bits)
             std::vector<uint16_t> re((size_t)n_rows + 1, 0);
@@ -677,6 +704,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         }
         csr_fmt_bytes = fb;
         spmv_fmt_bytes = n_tpl > 0 ? fb_tpl : fb;
+        tm.lap("    build: row ends, headers");
     }
     std::vector<int> sidx(plan.send_idx.begin(), plan.send_idx.end());
     send_idx.upload(sidx.data(), sidx.size());

@@ -226,19 +226,29 @@ def test_spgemm_bit_exact(ctx, oracle, problems, name):
     assert same_csr(C.to_scipy_local(), Co)
 
 
-def test_galerkin_device_equals_host(ctx, oracle):
-    """R (A P) on the device == host setup, level by level, and R A P via matmat."""
+@pytest.mark.parametrize("kind,dims,coarsen", [("7pt", (22, 21, 20), "pmis"), ("27pt", (30, 28, 26), "sa"),
+                                               ("5pt", (70, 61), "pmis"), ("7pt", (19, 18, 17), "sa")])
+def test_device_setup_equals_host(ctx, oracle, kind, dims, coarsen):
+    """setup_device = 1 (strength, PMIS / MIS(2), P and R = P^T on the GPU, SURVEY 8f row
+    f1), 2 (Galerkin SpGEMM only) and 0 (host): identical hierarchies -- every level's A,
+    P, R and integer split bit for bit -- and R A P via matmat reproduces A_1."""
     import raptor_amd as ra
 
-    A = ra.par_stencil_grid(ctx, "7pt", (22, 21, 20))
-    mg = ra.ParRugeStubenSolver(setup_device=True).setup(A)
-    mh = ra.ParRugeStubenSolver(setup_device=False).setup(A)
-    assert mg.num_levels == mh.num_levels
-    for l in range(mg.num_levels):
-        assert same_csr(mg.level_matrix(l, "A").to_scipy_local(), mh.level_matrix(l, "A").to_scipy_local())
-    R, P = mg.level_matrix(0, "R"), mg.level_matrix(0, "P")
+    A = ra.par_stencil_grid(ctx, kind, dims)
+    ms = [ra.ParMultilevel(coarsen=coarsen, setup_device=m).setup(A) for m in (1, 2, 0)]
+    nl = ms[0].num_levels
+    assert all(m.num_levels == nl for m in ms) and nl >= 2
+    for l in range(nl):
+        for w in ("APR" if l + 1 < nl else "A"):
+            ref = ms[2].level_matrix(l, w).to_scipy_local()
+            for m in ms[:2]:
+                assert same_csr(m.level_matrix(l, w).to_scipy_local(), ref), (l, w)
+        if l + 1 < nl:
+            for m in ms[:2]:
+                assert np.array_equal(m.level_split(l), ms[2].level_split(l)), l
+    R, P = ms[0].level_matrix(0, "R"), ms[0].level_matrix(0, "P")
     Ac = R.matmat(A.matmat(P))
-    assert same_csr(Ac.to_scipy_local(), mg.level_matrix(1, "A").to_scipy_local())
+    assert same_csr(Ac.to_scipy_local(), ms[0].level_matrix(1, "A").to_scipy_local())
 
 
 def test_empty_and_tiny(ctx, oracle):
