@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 GRIDS = {1: (256, 256, 256), 2: (256, 256, 512), 4: (256, 512, 512), 8: (512, 512, 512)}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MALL_BYTES = 256 << 20  # Infinity Cache (MALL) capacity
 
 
 def log(rank, *a):
@@ -215,9 +216,14 @@ def main():
     # algorithmic bytes 12 nnz + 4 (n+1) + 8 (cols + halo) + 8 n
     A.set_format("csr")
     csr_bytes = int(A.info["csr_bytes"])
-    csr_ms = timed(lambda: A.mult(x, y), args.spmv_reps)
+    csr_warm_ms = timed(lambda: A.mult(x, y), args.spmv_reps)
     csr_cold_ms = timed(lambda: A.mult(x, y), 10, flush)
     A.set_format("auto")
+    # an operator whose plain-CSR stream fits the 256 MiB Infinity Cache (the G3 substitute)
+    # is scored on cache-cold launches (a 1 GiB copy between them), so the HBM roofline is
+    # not credited with MALL hits; larger ones on back-to-back launches
+    mall = csr_bytes < MALL_BYTES
+    csr_ms = csr_cold_ms if mall else csr_warm_ms
     # the product's default format on the same operator (row templates / CSR-VI blocks),
     # scored on the bytes that format streams
     spmv_bytes = int(A.info["spmv_bytes"])
@@ -260,6 +266,7 @@ def main():
         for name, fn, nbytes in ops:
             ms = timed(fn, 10)
             table.append({"level": l, "op": name, "us": round(ms * 1e3, 1), "stored_bytes": int(nbytes),
+                          "mall_resident": int(nbytes) < MALL_BYTES,
                           "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
                           "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
         del xl, bl, tl, xc, bc
@@ -343,6 +350,9 @@ def main():
                 "bytes_per_launch": csr_bytes,
                 "bytes_definition": "SURVEY.md 8(d): 12 nnz + 4 (n+1) + 8 (local + halo cols) + 8 n",
                 "avg_launch_ms": round(csr_ms, 5),
+                "timing": ("cache-cold launches (operator fits the 256 MiB Infinity Cache)" if mall
+                           else "back-to-back launches"),
+                "warm_avg_launch_ms": round(csr_warm_ms, 5),
                 "cold_avg_launch_ms": round(csr_cold_ms, 5),
                 "cold_GBps": round(csr_bytes / (csr_cold_ms * 1e-3) / 1e9, 1),
                 "stream_copy_GBps": round(copy_gbs, 1),

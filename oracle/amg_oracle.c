@@ -951,17 +951,31 @@ static void smooth(orc_hier* H, int32_t l, double* x, const double* b, double* t
     memcpy(x, tmp, sizeof(double) * (size_t)A->n_rows);
 }
 
+/* Coarsest level: x_i = sum_j inv_ij b_j as 64 interleaved partial sums --
+ * p_l = sum over j = l, l + 64, l + 128, ... in ascending order, each from 0.0 -- combined by
+ * the butterfly p_l <- p_l + p_{l xor m} for m = 32, 16, ..., 1 (every l at once); x_i = p_0.
+ * The GPU runs one wavefront per row, lane l = p_l, the butterfly as shuffles. */
+static double coarse_row(const double* inv_row, const double* b, int64_t n) {
+    double p[64], q[64];
+    for (int l = 0; l < 64; ++l) {
+        double s = 0.0;
+        for (int64_t j = l; j < n; j += 64) s += inv_row[j] * b[j];
+        p[l] = s;
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+        for (int l = 0; l < 64; ++l) q[l] = p[l] + p[l ^ m];
+        memcpy(p, q, sizeof(p));
+    }
+    return p[0];
+}
+
 /* cycle(l): nu1 smooths; r = b - A x; b_{l+1} = R r; x_{l+1} = 0; cycle(l+1);
- * x = x + P x_{l+1}; nu2 smooths.  Coarsest: x_i = sum_j inv_ij b_j (sequential j). */
+ * x = x + P x_{l+1}; nu2 smooths.  Coarsest: x = inv b (coarse_row). */
 static void cycle_rec(orc_hier* H, int32_t l, double* x, const double* b) {
     const orc_csr* A = H->A[l];
     int64_t n = A->n_rows;
     if (l == H->nlev - 1) {
-        for (int64_t i = 0; i < n; ++i) {
-            double s = 0.0;
-            for (int64_t j = 0; j < n; ++j) s += H->inv[i * n + j] * b[j];
-            x[i] = s;
-        }
+        for (int64_t i = 0; i < n; ++i) x[i] = coarse_row(H->inv + i * n, b, n);
         return;
     }
     for (int32_t s = 0; s < H->opt.pre_sweeps; ++s) smooth(H, l, x, b, H->t[l], 0);

@@ -305,8 +305,9 @@ void launch_pcg_xr(hipStream_t s, int64_t n, const double* rz, const double* pq,
 void launch_pcg_p(hipStream_t s, int64_t n, const double* rz_new, const double* rz_old,
                   const double* z, double* p);
 void launch_append(hipStream_t s, const double* v, double* hist, int* counter);
-void launch_dense_gemv(hipStream_t s, int64_t n_local, int64_t n, const double* invT,
-                       const double* bfull, double* x);
+// x_i = inv_i . b, one wavefront per row, lane-interleaved partial sums + xor butterfly
+void launch_dense_gemv(hipStream_t s, int64_t n_local, int64_t n, const double* inv,
+                       const double* b, double* x);
 void launch_uniform(hipStream_t s, int64_t n, int64_t first_gid, uint64_t seed, double* out);
 void launch_zero(hipStream_t s, int64_t n, double* y);
 
@@ -343,8 +344,10 @@ struct Solver {
     amg_options opt{};
     std::vector<Level> levels;
     DevMatrix* A0 = nullptr;  // borrowed fine matrix (levels[0].A is null)
-    // coarsest level: dense inverse rows of this rank, transposed: invT[j * n_local + i]
+    // coarsest level: dense inverse rows of this rank, row-major (invT[i * n + j]); b gathered
+    // padded, then unpadded into global order (bfull)
     DevBuf<double> invT, bfull;
+    std::vector<int64_t> coarse_starts;
     int64_t coarse_n = 0;
     std::vector<int> coarse_counts, coarse_displs;
     // replicated coarse levels: levels >= rep_level are whole on every rank (-1: none)

@@ -1399,24 +1399,31 @@ __global__ void finish_norm_kernel(int n, const double* in, double* hist, int* c
     }
 }
 
-// coarsest level: x_i = sum_j inv_ij * b_j, sequential j per lane (bit-identical to the
-// oracle); invT is stored column-major for coalesced lanes
-__global__ void dense_gemv_kernel(long long nl, long long n, const double* invT,
-                                  const double* bfull, double* x) {
-    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nl) return;
+// coarsest level: x_i = sum_j inv_ij b_j, one wavefront per row: lane l sums
+// j = l, l + 64, ... in order from 0.0 (coalesced reads of the row-major inverse row), then a
+// fixed xor butterfly -- the oracle's coarse_row() exactly.  (The round-1 kernel walked each row
+// sequentially in one lane: 27 waves for the 1,709-row G3 substitute, 110 us on a 23 MB inverse.)
+__global__ __launch_bounds__(256) void dense_gemv_kernel(long long nl, long long n, const double* inv,
+                                                         const double* b, double* x) {
+    const long long i = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (i >= nl) return;  // wave-uniform
+    const double* row = inv + i * n;
     double s = 0.0;
-    long long j = 0;
-    // 8 products' loads in flight per step; the sum stays sequential in j
-    for (; j + 8 <= n; j += 8) {
-        double p[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) p[u] = invT[(j + u) * nl + i] * bfull[j + u];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s += p[u];
+    long long j = lane;
+    // four products' loads in flight per step; the lane's sum stays sequential in j
+    for (; j + 192 < n; j += 256) {
+        const double p0 = row[j] * b[j], p1 = row[j + 64] * b[j + 64];
+        const double p2 = row[j + 128] * b[j + 128], p3 = row[j + 192] * b[j + 192];
+        s += p0;
+        s += p1;
+        s += p2;
+        s += p3;
     }
-    for (; j < n; ++j) s += invT[j * nl + i] * bfull[j];
-    x[i] = s;
+    for (; j < n; j += 64) s += row[j] * b[j];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s = s + __shfl_xor(s, m, 64);
+    if (lane == 0) x[i] = s;
 }
 
 __device__ __forceinline__ unsigned long long dmix64(unsigned long long z) {
@@ -1963,11 +1970,11 @@ void launch_finish_norm(hipStream_t s, int n, const double* in, double* hist, in
     HIP_CHECK(hipGetLastError());
 }
 
-void launch_dense_gemv(hipStream_t s, int64_t n_local, int64_t n, const double* invT,
+void launch_dense_gemv(hipStream_t s, int64_t n_local, int64_t n, const double* inv,
                        const double* bfull, double* x) {
     if (n_local <= 0) return;
-    hipLaunchKernelGGL(dense_gemv_kernel, dim3((unsigned)((n_local + 63) / 64)), dim3(64), 0, s,
-                       (long long)n_local, (long long)n, invT, bfull, x);
+    hipLaunchKernelGGL(dense_gemv_kernel, dim3((unsigned)((n_local + 3) / 4)), dim3(256), 0, s,
+                       (long long)n_local, (long long)n, inv, bfull, x);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -116,9 +116,10 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     hist_counter.alloc(1);
     sink.counter = hist_counter.p;
     ensure_hist(1024);
-    // coarsest level: gathered dense inverse, this rank's rows, column-major.  With several
-    // ranks b is allgathered into a padded [nranks x cmax] layout; invT has zero rows at the
-    // padding so the sum order over real entries is the global order j = 0..n-1.
+    // coarsest level: this rank's rows of the gathered dense inverse, row-major (one
+    // wavefront per row reads its row coalesced).  With several ranks b is
+    // allgathered into a padded [nranks x cmax] layout and unpadded into the global order
+    // before the solve (the lanes' interleaving is defined on the global index j).
     DevMatrix& Ac = Amat(levels.size() - 1);
     coarse_n = Ac.host.n_global_rows;
     const std::vector<double>& inv = H.coarse_inv;
@@ -126,20 +127,16 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     const bool serial_coarse = comm.nranks == 1 || Ac.replicated;
     const int nparts = serial_coarse ? 1 : comm.nranks;
     int64_t cmax = 0;
+    coarse_starts.assign(Ac.host.row_starts.begin(), Ac.host.row_starts.end());
     for (int r = 0; r < nparts; ++r)
         cmax = std::max(cmax, Ac.host.row_starts[r + 1] - Ac.host.row_starts[r]);
-    const int64_t npad = serial_coarse ? coarse_n : cmax * comm.nranks;
-    std::vector<double> invT((size_t)std::max<int64_t>(npad * nl, 1), 0.0);
-    for (int r = 0; r < nparts; ++r)
-        for (int64_t j = Ac.host.row_starts[r]; j < Ac.host.row_starts[r + 1]; ++j) {
-            const int64_t jp = serial_coarse ? j : r * cmax + (j - Ac.host.row_starts[r]);
-            for (int64_t i = 0; i < nl; ++i) invT[jp * nl + i] = inv[(f + i) * coarse_n + j];
-        }
-    this->invT.upload(invT.data(), invT.size());
+    this->invT.upload(inv.data() + (size_t)(f * coarse_n), (size_t)std::max<int64_t>(nl * coarse_n, 0));
+    if (nl * coarse_n == 0) this->invT.alloc(1);
     tm.lap("coarse inverse upload");
     coarse_counts.assign(1, (int)cmax);
     if (!serial_coarse) {
-        bfull.alloc((size_t)npad + (size_t)cmax);  // gathered + local padded send slot
+        // gathered (nranks x cmax) + local padded send slot + the unpadded global vector
+        bfull.alloc((size_t)cmax * comm.nranks + (size_t)cmax + (size_t)coarse_n);
         HIP_CHECK(hipMemset(bfull.p, 0, bfull.n * sizeof(double)));
     }
     // multi-rank cycles run eagerly by default: loopback ranks meet at host barriers, which a
@@ -197,8 +194,14 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
             if (A.n_rows > 0)
                 HIP_CHECK(hipMemcpyAsync(slot, b, A.n_rows * sizeof(double), hipMemcpyDeviceToDevice, s));
             ctx->allgather(slot, bfull.p, (size_t)cmax);
-            bf = bfull.p;
-            launch_dense_gemv(s, A.n_rows, cmax * comm.nranks, invT.p, bf, x);
+            double* glob = bfull.p + cmax * (comm.nranks + 1);
+            for (int q = 0; q < comm.nranks; ++q) {
+                const int64_t c = coarse_starts[q + 1] - coarse_starts[q];
+                if (c)
+                    HIP_CHECK(hipMemcpyAsync(glob + coarse_starts[q], bfull.p + q * cmax, c * sizeof(double),
+                                             hipMemcpyDeviceToDevice, s));
+            }
+            launch_dense_gemv(s, A.n_rows, coarse_n, invT.p, glob, x);
         } else {
             launch_dense_gemv(s, A.n_rows, coarse_n, invT.p, bf, x);
         }
