@@ -32,8 +32,8 @@ constexpr int kCAP = 2048;  // nonzeros staged in LDS per workgroup (16 KiB of p
 constexpr int kPad = kCAP;  // col/val padding (entries): unconditional loads past a block's end
 constexpr int kTileLines = 256;  // x tile per workgroup: 256 lines x 64 B = 16 KiB of LDS
 constexpr int kNormParts = kTPB / 64;  // norm partials per CSR block (one per wave)
-constexpr int kGsWide = 128;
-constexpr int kGatherRPB = 4;    // rows per lane of gather (rectangular-operator) row blocks     // sliced-ELL width from which hybrid GS uses the wide variant
+constexpr int kGsWide = 128;     // sliced-ELL width from which hybrid GS uses the wide variant
+constexpr int kGatherRPB = 4;    // rows per lane of gather (rectangular-operator) row blocks
 // row templates: 1-byte template id per row (kTplNone = row not templated)
 constexpr int kTplNone = 255;
 constexpr int kTplMax = 255;       // templates per operator
@@ -50,6 +50,7 @@ constexpr int kTplMaxLen = 64;     // entries per template
 #endif
 constexpr int kTplRPL = AMG_TPL_RPL;  // rows per lane of the template kernel
 constexpr int kTplBands = 8;       // x-window bands
+constexpr int kTplChunks = 16;     // window chunks of kTPB slots (kTplWin / kTPB)
 constexpr int kTplWin = 16 * 256;  // x-window doubles per workgroup (32 KiB of LDS)
 constexpr int kTplRows = kTPB * kTplRPL;  // rows per template-kernel workgroup
 

@@ -574,6 +574,10 @@ struct TplArgs {
     int wend;                  // window end relative to r0 (last band's end)
     int blo[kTplBands];        // band b covers x[r0 + blo[b] + i], i < bbase[b+1] - bbase[b]
     int bbase[kTplBands + 1];  // first window slot of band b
+    // per chunk u of kTPB * S window slots (S = 2: slot pairs, S = 1: single slots): slot
+    // i = S tid + kTPB S u holds x[r0 + i + (S tid >= thr ? dhi : dlo)] -- bands are at least
+    // kTplRows slots long, so at most one band starts inside a chunk (tpl_chunk_tables)
+    int wdlo[2][kTplChunks], wdhi[2][kTplChunks], wthr[2][kTplChunks];
     const double* x;
     const double* b;
     double* y;
@@ -588,6 +592,26 @@ struct TplArgs {
 // profiles/r1t_lds_ab.txt; kept because it costs nothing.)
 // (A 1/a_ii table of ntpl instead of 256 entries -- 8 instead of 7 Jacobi workgroups per CU
 // -- made the 7-pt Jacobi slower, 102 -> 120 us, profiles/r1u_pdtrim_ab.txt.)
+// host: the per-chunk band tables of TplArgs (wdlo / wdhi / wthr) from blo / bbase / nband
+inline void tpl_chunk_tables(TplArgs& a) {
+    for (int S = 1; S <= 2; ++S)
+        for (int u = 0; u < kTplChunks; ++u) {
+            const int c0 = kTPB * S * u, c1 = c0 + kTPB * S;
+            int q = 0;
+            while (q + 1 < a.nband && a.bbase[q + 1] <= c0) ++q;
+            const int dlo = a.nband ? a.blo[q] - a.bbase[q] : 0;
+            int thr = 1 << 30, dhi = dlo;
+            if (q + 1 < a.nband && a.bbase[q + 1] < c1) {
+                thr = a.bbase[q + 1] - c0;
+                dhi = a.blo[q + 1] - a.bbase[q + 1];
+                AMG_ASSERT(q + 2 >= a.nband || a.bbase[q + 2] >= c1);  // one band start per chunk
+            }
+            a.wdlo[S - 1][u] = dlo;
+            a.wdhi[S - 1][u] = dhi;
+            a.wthr[S - 1][u] = thr;
+        }
+}
+
 inline size_t tpl_lds_bytes(int win, int nent, bool jacobi) {
     return 8 * ((size_t)win + (size_t)nent + (jacobi ? kTplMax + 1 : 0)) + 4 * ((size_t)nent + kTplMax + 1);
 }
@@ -602,7 +626,7 @@ struct TplLds {
 
 template <int MODE>
 __device__ __forceinline__ TplLds tpl_lds_layout(const TplArgs& a) {
-    extern __shared__ double tpl_lds[];
+    extern __shared__ __attribute__((aligned(16))) double tpl_lds[];
     TplLds L;
     L.win = tpl_lds;
     L.val = L.win + a.win;
@@ -631,6 +655,19 @@ __device__ __forceinline__ void tpl_stage_table(const TplArgs& a, const TplLds& 
         if (MODE == KM_JACOBI) L.pd[tid] = a.pd[tid];
     }
     if (tid == kTplNone) L.hdr[kTplNone] = (int)(255u << 24);  // length 0, no diagonal
+}
+
+// x offsets (relative to the block's first row) of the lane's window slots i_u = S (tid +
+// kTPB u), S = 2 for slot pairs: one compare and select per slot against the chunk's
+// workgroup-uniform band start (an unrolled select over all kTplBands bands cost more VALU
+// than the 27-pt rows themselves, profiles/r2w_tpl_sq_instr.txt)
+template <int S, int NS>
+__device__ __forceinline__ void tpl_slot_offsets(const TplArgs& a, int (&go)[NS]) {
+    static_assert(NS <= kTplChunks, "window chunks");
+    const int t = S * (int)threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < NS; ++u)
+        go[u] = t + kTPB * S * u + (t >= a.wthr[S - 1][u] ? a.wdhi[S - 1][u] : a.wdlo[S - 1][u]);
 }
 
 // the row operands and x window of the rows block starting at r0, into registers
@@ -675,33 +712,21 @@ struct TplFetch {
         // the others load single slots, out-of-range ones returning 0.
         pairs = r0 + a.blo[0] >= 0 && r0 + a.wend <= a.n;  // workgroup-uniform
         if (NPL > 0 && pairs) {
+            int go[NP / 2 > 0 ? NP / 2 : 1];
+            tpl_slot_offsets<2>(a, go);
 #pragma unroll
             for (int u = 0; u < NP / 2; ++u) {
-                const int i = 2 * (tid + kTPB * u);
-                int lo = a.blo[0], bb = a.bbase[0];
-#pragma unroll
-                for (int q = 1; q < kTplBands; ++q) {  // band of slot i: selects, no branch
-                    const bool in = i >= a.bbase[q];
-                    lo = in ? a.blo[q] : lo;
-                    bb = in ? a.bbase[q] : bb;
-                }
-                const int vo = i < a.win ? (r0 + lo + (i - bb)) * 8 : -16;
+                const int vo = 2 * (tid + kTPB * u) < a.win ? (r0 + go[u]) * 8 : -16;
                 const v2d_t p2 = __builtin_bit_cast(v2d_t, __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, 0, 0));
                 wv[2 * u] = p2.x;
                 wv[2 * u + 1] = p2.y;
             }
         } else if (NPL > 0) {
+            int go[NP];
+            tpl_slot_offsets<1>(a, go);
 #pragma unroll
             for (int u = 0; u < NP; ++u) {
-                const int i = tid + kTPB * u;
-                int lo = a.blo[0], bb = a.bbase[0];
-#pragma unroll
-                for (int q = 1; q < kTplBands; ++q) {
-                    const bool in = i >= a.bbase[q];
-                    lo = in ? a.blo[q] : lo;
-                    bb = in ? a.bbase[q] : bb;
-                }
-                const int vo = i < a.win ? (r0 + lo + (i - bb)) * 8 : -8;  // negative: returns 0
+                const int vo = tid + kTPB * u < a.win ? (r0 + go[u]) * 8 : -8;  // negative: returns 0
                 wv[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xrs, vo, 0, 0));
             }
         }
@@ -775,15 +800,33 @@ __device__ __forceinline__ double tpl_rows(const TplArgs& a, const TplLds& L, __
                 }
         }
     } else if constexpr (NPL > 0) {
-        // window: one entry at a time per row (measured faster than 4-entry batches,
-        // profiles/r1t_tpl.txt)
+        // window: 4 entries per step -- runs start at multiples of 4 entries (padded,
+        // build_templates), so one ds_read_b128 of slots and two of values serve 4 entries:
+        // 5 LDS cycles per entry instead of 8 with per-entry reads (the template kernels are
+        // LDS-bound on the 27-pt operator, profiles/r2w_tpl_sq_*.txt); entries past the row's
+        // length are masked, the sum keeps CSR order
+        // (the lane's two rows advancing together measured slower: 27-pt SpMV 159 vs 147 us,
+        // profiles/r2w_wide_forms.txt)
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int base = kTPB * j + tid;
+            for (int k = 0; k < ln[j]; k += 4) {
+                const int e = st[j] + k;
+                const int4 o = *(const int4*)(L.off + e);
+                const v2d_t v0 = *(const v2d_t*)(L.val + e), v1 = *(const v2d_t*)(L.val + e + 2);
+                const double x0 = L.win[o.x + base], x1 = L.win[o.y + base];
+                const double x2 = L.win[o.z + base], x3 = L.win[o.w + base];
+                s[j] = s[j] + v0.x * x0;
+                s[j] = k + 1 < ln[j] ? s[j] + v0.y * x1 : s[j];
+                s[j] = k + 2 < ln[j] ? s[j] + v1.x * x2 : s[j];
+                s[j] = k + 3 < ln[j] ? s[j] + v1.y * x3 : s[j];
+            }
+        }
+        // Jacobi: x_r from the window at the diagonal entry (fewer registers than a select
+        // per entry)
 #pragma unroll
         for (int j = 0; j < R; ++j)
-            for (int k = 0; k < ln[j]; ++k) {
-                const double xv = L.win[L.off[st[j] + k] + kTPB * j + tid];
-                s[j] = s[j] + L.val[st[j] + k] * xv;
-                if (MODE == KM_JACOBI) xr[j] = k == dk[j] ? xv : xr[j];
-            }
+            if (MODE == KM_JACOBI && dk[j] != 255) xr[j] = L.win[L.off[st[j] + dk[j]] + kTPB * j + tid];
     } else {
         // global x: both rows of the lane advance together, C entries per batch, every load
         // of a batch issued before its first product
@@ -838,6 +881,12 @@ __device__ __forceinline__ void tpl_partial(const TplArgs& a, int blk, double sq
     }
 }
 
+// waves per SIMD the persistent and marching forms are compiled for: windows of more than
+// 8 slots per lane (27-pt: 3084 doubles, ~34 KiB of LDS with the table) fit 4 workgroups per
+// CU, i.e. 4 waves per SIMD, so those forms may use 128 VGPRs (at 6 they spilled their
+// register-prefetched window to scratch)
+constexpr int tpl_waves(int npl) { return npl > 8 ? 4 : 6; }
+
 // one workgroup per block of kTplRows rows
 template <int MODE, bool NORM, int NPL>
 __global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
@@ -860,7 +909,7 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
 // fetched into registers while the current block is computed from LDS (double buffering
 // through registers), so the load latency overlaps the arithmetic.
 template <int MODE, bool NORM, int NPL>
-__global__ __launch_bounds__(kTPB, 6) void tpl_persist_kernel(TplArgs a, int nblk) {
+__global__ __launch_bounds__(kTPB, tpl_waves(NPL)) void tpl_persist_kernel(TplArgs a, int nblk) {
     static_assert(NPL > 0, "window path only");
     const TplLds L = tpl_lds_layout<MODE>(a);
     const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
@@ -899,7 +948,7 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_persist_kernel(TplArgs a, int nbl
 // only the rest is loaded -- 1024 instead of 2048 doubles per 7-pt block.  The next block's
 // loaded slots and row ids are prefetched into registers during the current block.
 template <int MODE, bool NORM, int NPL>
-__global__ __launch_bounds__(kTPB, 6) void tpl_march_kernel(TplArgs a, int nblk, int S, int nchunk) {
+__global__ __launch_bounds__(kTPB, tpl_waves(NPL)) void tpl_march_kernel(TplArgs a, int nblk, int S, int nchunk) {
     static_assert(NPL > 0 && NPL % 2 == 0, "window path, slot pairs");
     constexpr int NP = NPL / 2;  // slot pairs per lane (16-byte loads and LDS copies)
     const TplLds L = tpl_lds_layout<MODE>(a);
@@ -908,17 +957,10 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_march_kernel(TplArgs a, int nblk,
     // pair u of this lane: slots i, i + 1 with i = 2 (tid + kTPB u); bands have even starts
     // and lengths and the shift is even, so both slots of a pair share their source
     int gof[NP], src[NP];
+    tpl_slot_offsets<2>(a, gof);
 #pragma unroll
     for (int u = 0; u < NP; ++u) {
         const int i = 2 * (tid + kTPB * u);
-        int lo = a.blo[0], bb = a.bbase[0];
-#pragma unroll
-        for (int q = 1; q < kTplBands; ++q) {
-            const bool in = i >= a.bbase[q];
-            lo = in ? a.blo[q] : lo;
-            bb = in ? a.bbase[q] : bb;
-        }
-        gof[u] = lo + (i - bb);
         src[u] = i < a.win ? a.wsrc[i] : -2;  // -2: pair past the window
     }
     tpl_stage_table<MODE>(a, L);
@@ -1217,11 +1259,18 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
         const bool chain = BACK ? (pos != g.B - 1 && i + 1 < a.n) : pos != 0;
         const int ke = chain ? loffr[f.id[j]] : -1;  // template entry of the chain coupling
         double acc = f.pb[j], sold = 0.0;
-        for (int k = 0; k < ln; ++k) {
+        for (int k = 0; k < ln; k += 4) {  // 4 entries per step, as in tpl_rows
             const int e = st + k;
-            const double p = L.val[e] * L.win[L.off[e] + lr];
-            if (NORM) sold += p;
-            acc = k == ke ? acc : acc - p;
+            const int4 o = *(const int4*)(L.off + e);
+            const v2d_t v0 = *(const v2d_t*)(L.val + e), v1 = *(const v2d_t*)(L.val + e + 2);
+            const double p[4] = {v0.x * L.win[o.x + lr], v0.y * L.win[o.y + lr], v1.x * L.win[o.z + lr],
+                                 v1.y * L.win[o.w + lr]};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const bool in = k + u < ln;
+                if (NORM) sold = in ? sold + p[u] : sold;
+                acc = in && k + u != ke ? acc - p[u] : acc;
+            }
         }
         if (f.id[j] != kTplNone) {
             a.y[i] = acc;
@@ -1539,6 +1588,15 @@ void launch_append(hipStream_t s, const double* v, double* hist, int* counter) {
     HIP_CHECK(hipGetLastError());
 }
 
+// AMG_TPL_MARCH_WIDE=1: z-marching also for windows of more than 8 slots per lane (A/B)
+static bool tpl_march_wide() {
+    static const bool on = [] {
+        const char* e = std::getenv("AMG_TPL_MARCH_WIDE");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+
 int kernel_variant(const DevMatrix& A) {
     // variant bits: 2 = XCD-ordered blocks, 4 = gather path (no x tile), 8 = value-indexed
     // blocks (when any block qualifies), 32 = row templates (when built), 64 = persistent
@@ -1552,7 +1610,7 @@ int kernel_variant(const DevMatrix& A) {
     // scripts/spmv_variants.py; results are identical).
     const char* ev = getenv("AMG_KERNEL_VARIANT");
     int var = ev ? atoi(ev) : (A.default_variant | (A.n_vi_blocks > 0 ? 8 : 0) | (A.n_tpl > 0 ? 32 : 0) |
-                                (A.tpl_march_s > 0 && A.tpl_win <= 8 * kTPB ? 128 : 0));
+                                (A.tpl_march_s > 0 && (A.tpl_win <= 8 * kTPB || tpl_march_wide()) ? 128 : 0));
     if (A.n_vi_blocks == 0) var &= ~8;
     if (A.n_tpl == 0) var &= ~32;
     // AMG_FORMAT_BLOCKS: the CSR block kernel on every row (no templates)
@@ -1580,7 +1638,8 @@ static void launch_tpl_window(hipStream_t s, const TplArgs& a, int g, size_t lds
         const char* e = std::getenv("AMG_TPL_PERSIST");
         return !(e && std::atoi(e) == 0);
     }();
-    if constexpr (P > 8) {  // larger windows: the persistent form exceeds the VGPR budget
+    if constexpr (P > 8) {  // larger windows: the one-block kernel (27-pt SpMV 146 us; the
+                            // persistent form 164, marching 153: profiles/r2w_wide_forms.txt)
         hipLaunchKernelGGL((tpl_kernel<M, N, P>), dim3(g), dim3(kTPB), lds, s, a);
         return;
     }
@@ -1660,6 +1719,7 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
     for (int q = 0; q < a.nband; ++q) a.blo[q] = A.tpl_blo[q], a.bbase[q] = A.tpl_bbase[q];
     a.bbase[a.nband] = a.win;
     for (int q = a.nband; q < kTplBands; ++q) a.blo[q] = 0, a.bbase[q + 1] = a.win;
+    tpl_chunk_tables(a);
     a.x = x;
     a.b = b;
     a.y = y;
@@ -1859,6 +1919,7 @@ static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, co
     for (int q = 0; q < a.nband; ++q) a.blo[q] = A.tpl_blo[q], a.bbase[q] = A.tpl_bbase[q];
     a.bbase[a.nband] = a.win;
     for (int q = a.nband; q < kTplBands; ++q) a.blo[q] = 0, a.bbase[q + 1] = a.win;
+    tpl_chunk_tables(a);
     a.x = x;
     a.b = b;
     a.y = A.gs_racc.p;

@@ -351,12 +351,12 @@ static TplBuild build_templates(const std::vector<int>& rp, const std::vector<in
                         g = q;
                         break;
                     }
-            const int len = rp[r + 1] - rp[r];
-            if (g < 0 && (int)grep.size() < kTplMax && ent + len <= kTplEntries) {
+            const int len4 = (rp[r + 1] - rp[r] + 3) & ~3;  // padded run (below)
+            if (g < 0 && (int)grep.size() < kTplMax && ent + len4 <= kTplEntries) {
                 g = (int)grep.size();
                 grep.push_back(r);
                 gm[h].push_back(g);
-                ent += len;
+                ent += len4;
             }
             gmap[c][t] = g;
         }
@@ -379,6 +379,13 @@ static TplBuild build_templates(const std::vector<int>& rp, const std::vector<in
             T.off.push_back(col[rp[r] + k] - r);
             T.val.push_back(val[rp[r] + k]);
             if (col[rp[r] + k] == r && dk == 255) dk = k;
+        }
+        // runs start at multiples of 4 entries: the window kernels read 4 slots (16 bytes) and
+        // 2 x 2 values per LDS instruction; padding repeats the run's first slot with value 0
+        // and is never summed (entries >= len are masked)
+        for (int k = len; k & 3; ++k) {
+            T.off.push_back(col[rp[r]] - r);
+            T.val.push_back(0.0);
         }
         T.hdr.push_back(start | len << 16 | (int)((unsigned)dk << 24));
         T.pd.push_back(dinv[r]);
