@@ -10,6 +10,8 @@
 // the upper bound sum_k |B_k| into table sizes 256 .. 8192; the rare larger rows are
 // computed on the host with the same order.  Two passes: symbolic (count), numeric (fill
 // sorted by column: rank = number of smaller keys).
+#include <omp.h>
+
 #include <algorithm>
 #include <numeric>
 
@@ -26,7 +28,9 @@ __device__ __forceinline__ unsigned hslot(long long j, unsigned mask) {
     return (unsigned)(z >> 40) & mask;
 }
 
-// one 64-lane workgroup per row of `rows`; T table entries (power of two)
+// one 64-lane workgroup per row of `rows`; T table entries (power of two).  A row whose
+// distinct columns do not fit (a probe sequence longer than the table) is abandoned: the
+// symbolic pass marks it with count -1 and the host computes it.
 template <int T, bool NUMERIC>
 __global__ __launch_bounds__(kWave) void spgemm_rows_kernel(
     const int* __restrict__ rows, int nrows, const long long* __restrict__ arp,
@@ -36,7 +40,7 @@ __global__ __launch_bounds__(kWave) void spgemm_rows_kernel(
     const long long* __restrict__ crp, long long* __restrict__ ccol, double* __restrict__ cval) {
     __shared__ long long keys[T];
     __shared__ double vals[NUMERIC ? T : 1];
-    __shared__ int nocc;
+    __shared__ int nocc, ovf;
     const int lane = threadIdx.x;
     const int w = blockIdx.x;
     if (w >= nrows) return;
@@ -45,6 +49,7 @@ __global__ __launch_bounds__(kWave) void spgemm_rows_kernel(
         keys[t] = -1;
         if (NUMERIC) vals[t] = 0.0;
     }
+    if (lane == 0) ovf = 0;
     __syncthreads();
     const unsigned mask = T - 1;
     for (long long ka = arp[i]; ka < arp[i + 1]; ++ka) {
@@ -53,15 +58,22 @@ __global__ __launch_bounds__(kWave) void spgemm_rows_kernel(
         for (long long q = brp[k] + lane; q < brp[k + 1]; q += kWave) {
             const long long j = bcol[q];
             unsigned h = hslot(j, mask);
+            int probes = 0;
             for (;;) {
                 const long long prev = atomicCAS((unsigned long long*)&keys[h], (unsigned long long)-1LL,
                                                  (unsigned long long)j);
                 if (prev == -1 || prev == j) break;
                 h = (h + 1) & mask;
+                if (++probes >= T) break;  // table full
+            }
+            if (probes >= T) {
+                ovf = 1;
+                break;
             }
             if (NUMERIC) vals[h] += a * bval[q];
         }
         __syncthreads();  // next k step sees every update of this one
+        if (ovf) break;   // workgroup-uniform after the barrier
     }
     if (!NUMERIC) {
         if (lane == 0) nocc = 0;
@@ -70,11 +82,11 @@ __global__ __launch_bounds__(kWave) void spgemm_rows_kernel(
         for (int t = lane; t < T; t += kWave) c += keys[t] != -1;
         atomicAdd(&nocc, c);
         __syncthreads();
-        if (lane == 0) counts[i] = nocc;
+        if (lane == 0) counts[i] = ovf ? -1 : nocc;
         return;
     }
-    // compact the occupied slots in place (targets never pass the chunk being read), then
-    // emit sorted by column: rank = number of smaller keys among the m occupied ones
+    // compact the occupied slots in place (targets never pass the chunk being read), pad to
+    // a power of two with +inf keys and sort by column (bitonic network in LDS)
     int m = 0;
     for (int b = 0; b < T; b += kWave) {
         const long long j = keys[b + lane];
@@ -90,13 +102,31 @@ __global__ __launch_bounds__(kWave) void spgemm_rows_kernel(
         m += __popcll(bal);
         __syncthreads();
     }
+    int P = 1;
+    while (P < m) P <<= 1;
+    for (int t = m + lane; t < P; t += kWave) keys[t] = 0x7fffffffffffffffLL;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1)
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int t = lane; t < P; t += kWave) {
+                const int u = t ^ jj;
+                if (u > t) {
+                    const long long kt = keys[t], ku = keys[u];
+                    if (((t & k) == 0) == (kt > ku)) {
+                        keys[t] = ku;
+                        keys[u] = kt;
+                        const double vt = vals[t];
+                        vals[t] = vals[u];
+                        vals[u] = vt;
+                    }
+                }
+            }
+            __syncthreads();
+        }
     const long long base = crp[i];
     for (int e = lane; e < m; e += kWave) {
-        const long long j = keys[e];
-        int rank = 0;
-        for (int u = 0; u < m; ++u) rank += keys[u] < j;
-        ccol[base + rank] = j;
-        cval[base + rank] = vals[e];
+        ccol[base + e] = keys[e];
+        cval[base + e] = vals[e];
     }
 }
 
@@ -117,6 +147,7 @@ void launch_bin(hipStream_t s, const std::vector<int>& rows, DevBuf<int>& drows,
 
 HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, const HostCSR& B) {
     AMG_CHECK(A.col_starts == B.row_starts, "spgemm: A columns and B rows partitioned differently");
+    PhaseTimer tm(comm);
     HaloPlan plan = halo_plan_for_cols(comm, A);
     GhostRows G = fetch_rows(comm, plan, B);
     const int64_t n = A.nrows(), nbl = B.nrows(), lo = B.row_starts[comm.rank],
@@ -145,16 +176,17 @@ HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, cons
     std::copy(B.val.begin(), B.val.end(), bval.begin());
     std::copy(G.col.begin(), G.col.end(), bcol.begin() + B.nnz());
     std::copy(G.val.begin(), G.val.end(), bval.begin() + B.nnz());
-    // bins by table size (load factor <= 1/2)
+    // bins by table size (load factor <= 1/2 on the upper bound); rows beyond the largest
+    // table try it anyway (their distinct columns are usually far fewer than the bound) and
+    // fall back to the host only when it overflows
     static constexpr int kBins[] = {256, 1024, 4096, 8192};
     std::vector<int> bins[4];
-    std::vector<int64_t> host_rows;
     for (int64_t i = 0; i < n; ++i) {
         int b = 0;
-        while (b < 4 && 2 * ub[i] > kBins[b]) ++b;
-        if (b < 4) bins[b].push_back((int)i);
-        else host_rows.push_back(i);
+        while (b < 3 && 2 * ub[i] > kBins[b]) ++b;
+        bins[b].push_back((int)i);
     }
+    tm.lap("    spgemm: column map, B image, bins");
     hipStream_t s = ctx.stream;
     DevBuf<long long> d_arp, d_brp, d_bcol, d_counts, d_crp, d_ccol;
     DevBuf<int> d_acol, d_rows[4];
@@ -168,6 +200,7 @@ HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, cons
     d_bval.upload(bval.data(), bval.size());
     d_counts.alloc((size_t)std::max<int64_t>(n, 1));
     HIP_CHECK(hipMemsetAsync(d_counts.p, 0, sizeof(long long) * d_counts.n, s));
+    tm.lap("    spgemm: uploads");
 #define AMG_BIN(T, NUM, b)                                                                          \
     launch_bin<T, NUM>(s, bins[b], d_rows[b], d_arp.p, d_acol.p, d_aval.p, d_brp.p, d_bcol.p,      \
                        d_bval.p, d_counts.p, d_crp.p, d_ccol.p, d_cval.p)
@@ -178,31 +211,54 @@ HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, cons
     std::vector<long long> counts((size_t)n);
     if (n) HIP_CHECK(hipMemcpyAsync(counts.data(), d_counts.p, sizeof(long long) * n, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    // the few oversized rows: host, same canonical order
+    tm.lap("    spgemm: symbolic");
+    // rows that overflowed the largest table: host, same canonical order, a dense
+    // accumulator per thread (acc_j in k order, then the touched columns sorted)
+    std::vector<int64_t> host_rows;
+    {
+        std::vector<int> keep;
+        for (int i : bins[3])
+            if (counts[i] < 0) host_rows.push_back(i);
+            else keep.push_back(i);
+        bins[3].swap(keep);
+    }
     std::vector<std::vector<std::pair<int64_t, double>>> hostout(host_rows.size());
-    for (size_t t = 0; t < host_rows.size(); ++t) {
-        const int64_t i = host_rows[t];
-        std::vector<int64_t> order;
-        std::vector<double> acc;
-        std::vector<std::pair<int64_t, size_t>> idx;  // (col, slot), kept sorted
-        for (int64_t ka = A.rp[i]; ka < A.rp[i + 1]; ++ka) {
-            const int64_t r = acol[ka];
-            for (long long q = brp[r]; q < brp[r + 1]; ++q) {
-                auto it = std::lower_bound(idx.begin(), idx.end(), std::make_pair((int64_t)bcol[q], (size_t)0));
-                size_t slot;
-                if (it == idx.end() || it->first != bcol[q]) {
-                    slot = acc.size();
-                    acc.push_back(0.0);
-                    idx.insert(it, {bcol[q], slot});
-                } else {
-                    slot = it->second;
+    if (!host_rows.empty()) {
+        const int64_t ncol = B.n_global_cols;
+        // dense accumulators: at most ~2 GB of them across threads
+        const int nth = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)host_rows.size(), (int64_t)omp_get_max_threads(),
+                                                                     (int64_t)2000000000 / (9 * std::max<int64_t>(ncol, 1))}));
+        (void)nth;
+#pragma omp parallel num_threads(nth)
+        {
+            std::vector<double> acc((size_t)ncol, 0.0);
+            std::vector<char> seen((size_t)ncol, 0);
+            std::vector<int64_t> touched;
+#pragma omp for schedule(dynamic, 1)
+            for (size_t t = 0; t < host_rows.size(); ++t) {
+                const int64_t i = host_rows[t];
+                touched.clear();
+                for (int64_t ka = A.rp[i]; ka < A.rp[i + 1]; ++ka) {
+                    const int64_t r = acol[ka];
+                    for (long long q = brp[r]; q < brp[r + 1]; ++q) {
+                        const int64_t j = bcol[q];
+                        if (!seen[j]) seen[j] = 1, touched.push_back(j);
+                        acc[j] += A.val[ka] * bval[q];
+                    }
                 }
-                acc[slot] += A.val[ka] * bval[q];
+                std::sort(touched.begin(), touched.end());
+                auto& out = hostout[t];
+                out.reserve(touched.size());
+                for (int64_t j : touched) {
+                    out.push_back({j, acc[j]});
+                    acc[j] = 0.0;
+                    seen[j] = 0;
+                }
+                counts[i] = (long long)out.size();
             }
         }
-        for (auto& e : idx) hostout[t].push_back({e.first, acc[e.second]});
-        counts[i] = (long long)hostout[t].size();
     }
+    tm.lap("    spgemm: host rows (" + std::to_string(host_rows.size()) + ")");
     HostCSR C;
     C.n_global_rows = A.n_global_rows;
     C.n_global_cols = B.n_global_cols;
@@ -227,6 +283,7 @@ HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, cons
         HIP_CHECK(hipMemcpyAsync(C.val.data(), d_cval.p, sizeof(double) * cnnz, hipMemcpyDeviceToHost, s));
     }
     HIP_CHECK(hipStreamSynchronize(s));
+    tm.lap("    spgemm: numeric + download");
     for (size_t t = 0; t < host_rows.size(); ++t) {
         int64_t p = C.rp[host_rows[t]];
         for (auto& e : hostout[t]) C.col[p] = e.first, C.val[p++] = e.second;

@@ -226,6 +226,29 @@ def test_spgemm_bit_exact(ctx, oracle, problems, name):
     assert same_csr(C.to_scipy_local(), Co)
 
 
+def test_spgemm_large_rows(ctx, oracle):
+    """Rows whose upper bound exceeds the largest LDS table: a dense row's product (12000
+    distinct columns) overflows it and takes the host path; rows with a large bound but few
+    distinct columns (long rows of a narrow band) stay on the GPU's largest table.  Both
+    bit-identical to the oracle's canonical order."""
+    import raptor_amd as ra
+
+    O = oracle
+    n = 12000
+    M = sp.random(n, n, density=0.0008, random_state=3, format="lil")
+    M.setdiag(4.0)
+    M[3, :] = np.linspace(-1.0, 1.0, n)                 # dense row: > 8192 distinct outputs
+    band = sp.diags([np.full(n - abs(d), 1.0 + 0.01 * d) for d in range(-60, 61)],
+                    list(range(-60, 61)), format="lil")
+    M[100:300, :] = band[100:300, :]                    # 121 x 121 entries: bound > 8192, ~250 distinct
+    M = M.tocsr()
+    M.sort_indices()
+    Ao = O.Csr.from_scipy(M)
+    A = _dev_matrix(ra, ctx, Ao)
+    C = A.matmat(A)
+    assert same_csr(C.to_scipy_local(), (Ao @ Ao).to_scipy())
+
+
 @pytest.mark.parametrize("kind,dims,coarsen", [("7pt", (22, 21, 20), "pmis"), ("27pt", (30, 28, 26), "sa"),
                                                ("5pt", (70, 61), "pmis"), ("7pt", (19, 18, 17), "sa")])
 def test_device_setup_equals_host(ctx, oracle, kind, dims, coarsen):
