@@ -42,6 +42,9 @@ constexpr int kTplMaxLen = 64;     // entries per template
 #ifndef AMG_CSR_PERSIST_WAVES  // build-time knob: waves/SIMD bound of the persistent x-tile kernel
 #define AMG_CSR_PERSIST_WAVES 6
 #endif
+#ifndef AMG_CSR_PRE_TILE  // build-time knob: x-tile blocks issue batch 1 with the header
+#define AMG_CSR_PRE_TILE 1
+#endif
 #ifndef AMG_TPL_BATCH  // build-time knob: window entries per batch in the template kernel (0: one)
 #define AMG_TPL_BATCH 0
 #endif
@@ -296,6 +299,8 @@ void launch_pack(hipStream_t s, int64_t n, const int* idx, const double* x, doub
 // deterministic sum of n per-block partials into *out (tmp: >= n/4096 + 16 doubles)
 void launch_reduce_partials(hipStream_t s, int n, const double* partial, double* tmp, double* out);
 // hist[*counter] = sqrt(sum_{i<n} in[i]) (rank order); ++*counter
+bool launch_reduce_norm(hipStream_t s, int n, const double* partial, double* tmp, unsigned* done,
+                        double* out, double* hist, int* counter);
 void launch_finish_norm(hipStream_t s, int n, const double* in, double* hist, int* counter);
 // PCG helpers: deterministic dot partials (fixed block span), scalar finish, fused updates
 int dot_partial_count(int64_t n);
@@ -327,6 +332,7 @@ struct NormSink {
     double* gathered = nullptr; // nranks + 1
     double* hist = nullptr;
     int* counter = nullptr;
+    unsigned* done = nullptr;   // zeroed arrival counter of reduce_norm_kernel (null: two launches)
 };
 // reduce `nparts` partials (default: one per CSR-stream block) and append the norm
 void norm_finish(DevMatrix& A, const NormSink& ns, int nparts = -1);
@@ -359,6 +365,7 @@ struct Solver {
     // solve state: residual history kept on the device, appended by finish_norm_kernel
     DevBuf<double> hist, norm_scratch;
     DevBuf<int> hist_counter;
+    DevBuf<unsigned> norm_done;
     NormSink sink;
     bool use_graph = true;
     struct Graph {

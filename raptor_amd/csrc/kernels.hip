@@ -399,6 +399,24 @@ __global__ __launch_bounds__(kTPB, GRPB > 1 ? 7 : 8) void csr_block_kernel(CsrAr
     __shared__ double tabl[VI ? 256 : 1];
     __shared__ int rends[kTPB * GRPB];
     const int bid = first_block + (XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x);
+    if constexpr (TILE && AMG_CSR_PRE_TILE) {
+        // square operators: batch 1 (tile line ids, tile / VI indices: fixed offsets from the
+        // block id) issued together with the header instead of after it -- one dependent
+        // round of loads less per block
+        constexpr int PV = VI ? 2 : 1;
+        CsrPre f;
+        csr_pre_tile<VI>(a, bid, f);
+        const int4 h0 = f.h0, h1 = f.h1;
+        double sq;
+        if (h0.w <= kCAP && (h1.y & 0xffff) <= kTileLines && h0.w > 0) {
+            if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV>(a, bid, stage, tabl, rends, &f, -1);
+            else sq = block_main<MODE, NORM, true, false, 8, PV>(a, bid, stage, tabl, rends, &f, -1);
+        } else {
+            sq = block_long<MODE, NORM>(a, h0, stage);
+        }
+        block_partial<NORM>(a, bid, sq);
+        return;
+    }
     const int4 h0 = a.hdr[2 * bid], h1 = a.hdr[2 * bid + 1];
     const int nnz = h0.w;
     double sq;
@@ -886,6 +904,9 @@ __device__ __forceinline__ void tpl_partial(const TplArgs& a, int blk, double sq
 // CU, i.e. 4 waves per SIMD, so those forms may use 128 VGPRs (at 6 they spilled their
 // register-prefetched window to scratch)
 constexpr int tpl_waves(int npl) { return npl > 8 ? 4 : 6; }
+// the 7-pt marching form at 7 waves (72 VGPRs): its Jacobi + norm variant took 74 at 6 waves
+// (a wave per SIMD fewer than the plain Jacobi: 101 vs 83 us per launch)
+constexpr int tpl_march_waves(int npl) { return npl == 8 ? 7 : tpl_waves(npl); }
 
 // one workgroup per block of kTplRows rows
 template <int MODE, bool NORM, int NPL>
@@ -948,7 +969,7 @@ __global__ __launch_bounds__(kTPB, tpl_waves(NPL)) void tpl_persist_kernel(TplAr
 // only the rest is loaded -- 1024 instead of 2048 doubles per 7-pt block.  The next block's
 // loaded slots and row ids are prefetched into registers during the current block.
 template <int MODE, bool NORM, int NPL>
-__global__ __launch_bounds__(kTPB, tpl_waves(NPL)) void tpl_march_kernel(TplArgs a, int nblk, int S, int nchunk) {
+__global__ __launch_bounds__(kTPB, tpl_march_waves(NPL)) void tpl_march_kernel(TplArgs a, int nblk, int S, int nchunk) {
     static_assert(NPL > 0 && NPL % 2 == 0, "window path, slot pairs");
     constexpr int NP = NPL / 2;  // slot pairs per lane (16-byte loads and LDS copies)
     const TplLds L = tpl_lds_layout<MODE>(a);
@@ -1420,9 +1441,8 @@ __global__ void zero_kernel(long long n, double* y) {
 // deterministic two-stage sum of n partials: block g sums [g*4096, (g+1)*4096) with 16
 // fixed loads per lane, a fixed shuffle tree and 4 wave sums in order
 constexpr int kRedSpan = kTPB * 16;
-__global__ __launch_bounds__(kTPB) void sum_partials_kernel(int n, const double* p, double* out) {
-    __shared__ double red[kTPB / 64];
-    const int base = blockIdx.x * kRedSpan + threadIdx.x;
+__device__ __forceinline__ double block_sum_span(int n, const double* p, int g, double* red) {
+    const int base = g * kRedSpan + threadIdx.x;
     double v[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -1435,7 +1455,45 @@ __global__ __launch_bounds__(kTPB) void sum_partials_kernel(int n, const double*
     for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (threadIdx.x == 0) out[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    return (red[0] + red[1]) + (red[2] + red[3]);  // meaningful in thread 0
+}
+
+__global__ __launch_bounds__(kTPB) void sum_partials_kernel(int n, const double* p, double* out) {
+    __shared__ double red[kTPB / 64];
+    const double s = block_sum_span(n, p, blockIdx.x, red);
+    if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
+// The same two stages (n <= kRedSpan^2) and the single-rank finish in ONE launch: each block
+// writes its span's sum, then an agent-scope acq_rel counter picks the last block to arrive,
+// which sums the block sums exactly as the second sum_partials_kernel would, appends sqrt to
+// hist and resets the counter (bit-identical to reduce + finish, two launches fewer per norm).
+// Visibility (MI355X_MICROARCH.md, inter-workgroup): the writer's release orders its store of
+// tmp[g]; the last block's acquire (one lane) and barrier precede its plain loads.
+__global__ __launch_bounds__(kTPB) void reduce_norm_kernel(int n, const double* p, double* tmp,
+                                                           unsigned* done, double* out, double* hist,
+                                                           int* counter) {
+    __shared__ double red[kTPB / 64];
+    __shared__ int last;
+    const int g = gridDim.x;
+    const double s = block_sum_span(n, p, blockIdx.x, red);
+    if (threadIdx.x == 0) {
+        tmp[blockIdx.x] = s;
+        const unsigned prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev == (unsigned)(g - 1);
+    }
+    __syncthreads();
+    if (!last) return;  // workgroup-uniform
+    __syncthreads();    // red[] is reused below
+    const double t = block_sum_span(g, tmp, 0, red);
+    if (threadIdx.x == 0) {
+        *done = 0u;
+        out[0] = t;
+        double f = 0.0;
+        f += t;  // finish_norm_kernel's sum over one rank
+        hist[*counter] = sqrt(f);
+        *counter += 1;
+    }
 }
 
 // sum of per-rank sums in rank order (identical on every rank), sqrt, append to hist
@@ -2024,6 +2082,15 @@ void launch_reduce_partials(hipStream_t s, int n, const double* partial, double*
         launch_reduce_partials(s, g, tmp, tmp + g, out);
     }
     HIP_CHECK(hipGetLastError());
+}
+
+bool launch_reduce_norm(hipStream_t s, int n, const double* partial, double* tmp, unsigned* done,
+                        double* out, double* hist, int* counter) {
+    if (n <= 0 || n > kRedSpan * kRedSpan || !done) return false;
+    const int g = (n + kRedSpan - 1) / kRedSpan;
+    hipLaunchKernelGGL(reduce_norm_kernel, dim3(g), dim3(kTPB), 0, s, n, partial, tmp, done, out, hist, counter);
+    HIP_CHECK(hipGetLastError());
+    return true;
 }
 
 void launch_finish_norm(hipStream_t s, int n, const double* in, double* hist, int* counter) {

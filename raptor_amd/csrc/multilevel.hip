@@ -115,6 +115,9 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     sink.gathered = sink.tmp + tmpn;
     hist_counter.alloc(1);
     sink.counter = hist_counter.p;
+    norm_done.alloc(1);
+    HIP_CHECK(hipMemset(norm_done.p, 0, sizeof(unsigned)));
+    sink.done = norm_done.p;
     ensure_hist(1024);
     // coarsest level: this rank's rows of the gathered dense inverse, row-major (one
     // wavefront per row reads its row coalesced).  With several ranks b is

@@ -1090,6 +1090,9 @@ void norm_finish(DevMatrix& A, const NormSink& ns, int nparts) {
     const int nb = nparts >= 0 ? nparts : A.norm_parts();
     const int nr = c->host.nranks;
     double* local = ns.gathered + nr;
+    // one rank: the reduction and the finish in one launch
+    if (nr == 1 && launch_reduce_norm(c->stream, nb, ns.partial, ns.tmp, ns.done, local, ns.hist, ns.counter))
+        return;
     if (nb > 0) launch_reduce_partials(c->stream, nb, ns.partial, ns.tmp, local);
     else launch_zero(c->stream, 1, local);
     if (nr > 1) {
