@@ -279,7 +279,8 @@ int kernel_variant(const DevMatrix& A);
 // partial slot of block bid's wave w: part_off + bid * kNormParts + w
 void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, int first_block,
                        int n_blocks, const double* x, const double* b, double* y, double omega,
-                       double* partial, int part_off = 0);
+                       double* partial, int part_off = 0,
+                       double* y2 = nullptr, const double* d2 = nullptr);
 // template rows of A (all of them, one launch); partials at [0, tpl_blocks() * kNormParts)
 void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const double* x,
                 const double* b, double* y, double omega, double* partial);
@@ -334,6 +335,10 @@ struct NormSink {
     int* counter = nullptr;
     unsigned* done = nullptr;   // zeroed arrival counter of reduce_norm_kernel (null: two launches)
 };
+// b_c = R r and, fused, x0_c = omega * (dinv_c * b_c) (the coarse level's first Jacobi sweep
+// from x = 0); false (nothing launched) where R is not on the CSR block path
+bool par_restrict_j0(DevMatrix& R, const double* r, double* bc, double* x0c, const double* dinvc,
+                     double omega);
 // reduce `nparts` partials (default: one per CSR-stream block) and append the norm
 void norm_finish(DevMatrix& A, const NormSink& ns, int nparts = -1);
 // r = b - A x and append ||r|| (device-side) through ns
@@ -380,7 +385,9 @@ struct Solver {
     // one V-cycle; with_norm: the first level-0 Jacobi sweep also appends ||b - A x_in||
     // to the device history (falls back to a separate residual when it cannot)
     void cycle(double* x, const double* b, bool with_norm = false);
-    void cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool with_norm);
+    // x0_in_t: level l's first pre-sweep from x = 0 already sits in levels[l].t (fused into
+    // the restriction above, par_restrict_j0)
+    void cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool with_norm, bool x0_in_t = false);
     void smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_zero, bool with_norm,
                 bool post = false);
     void ensure_hist(int32_t n);

@@ -47,7 +47,17 @@ struct CsrArgs {
     double omega;
     double* partial;
     int part_off;      // partial slot of block bid's wave w: part_off + bid * kNormParts + w
+    double* y2;        // SPMV only, non-null: y2[r] = omega * (dinv[r] * y[r]) as well (the next
+                       // level's first Jacobi sweep from x = 0, fused into the restriction)
 };
+
+// the fused second output of a restriction (CsrArgs::y2): jacobi_zero_kernel's expression;
+// d = dinv[r], loaded with the row operands (a load after the sum cost a memory round trip
+// per block)
+template <int MODE>
+__device__ __forceinline__ void store_y2(const CsrArgs& a, int r, double out, double d) {
+    if (MODE == KM_SPMV && a.y2) a.y2[r] = a.omega * (d * out);
+}
 
 __device__ __forceinline__ double xload(const CsrArgs& a, int c) {
     const double* p = c < a.ncl ? a.x + c : a.xh + (c - a.ncl);
@@ -203,7 +213,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
             const int rj = r0 + tid + kTPB * j, rjj = rj < r1 ? rj : r0;
             e1m[j] = a.rend[rjj];
             rends[tid + kTPB * j] = e1m[j];
-            pxm[j] = MODE == KM_SPMV_ADD ? a.y[rjj] : 0.0;
+            pxm[j] = MODE == KM_SPMV_ADD ? a.y[rjj] : MODE == KM_SPMV && a.y2 ? a.dinv[rjj] : 0.0;
         }
     }
     // Entry-to-lane map.  TILE: lane t holds entries 512 p + 2 t + {0, 1} (p < 4) of the
@@ -243,6 +253,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     double pb = 0.0, pd = 0.0, px = 0.0;
     int dv = 0;
     if (MODE == KM_SPMV_ADD) px = a.y[rr];
+    if (MODE == KM_SPMV && a.y2) pd = a.dinv[rr];  // store_y2
     if (MODE == KM_RESID || MODE == KM_JACOBI) pb = a.b[rr];
     if (MODE == KM_JACOBI) {
         if (pd_tab) dv = a.dvi[rr];
@@ -321,6 +332,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
             if (rj < r1) {
                 const double sj = lds_row_sum(stage, rends[k - 1], e1m[j], 0.0);
                 a.y[rj] = MODE == KM_SPMV ? sj : pxm[j] + sj;
+                store_y2<MODE>(a, rj, sj, pxm[j]);
             }
         }
     }
@@ -337,7 +349,10 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
         if (NORM) sq = own ? t * t : 0.0;
         out = MODE == KM_RESID ? t : px + a.omega * (pd * t);
     }
-    if (own) a.y[r] = out;
+    if (own) {
+        a.y[r] = out;
+        store_y2<MODE>(a, r, out, pd);
+    }
     return sq;
 }
 
@@ -372,7 +387,9 @@ __device__ __forceinline__ double block_long(const CsrArgs& a, int4 h0, double* 
     for (int r = r0 + tid; r < r1; r += kTPB) {
         if (r == r0 || nnz == 0) {  // nnz == 0: every row of the block is empty
             double res = 0.0;
-            a.y[r] = epilogue<MODE>(a, r, s, &res);
+            const double o = epilogue<MODE>(a, r, s, &res);
+            a.y[r] = o;
+            if (MODE == KM_SPMV && a.y2) store_y2<MODE>(a, r, o, a.dinv[r]);
             if (NORM) sq += res * res;
         }
     }
@@ -1261,7 +1278,7 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
     const int tid = threadIdx.x, lane = tid & 63;
     const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
     const int q = xcd_remap(blockIdx.x, gridDim.x);
-    const int r0 = g.blocks[q] * kTplRows;
+    const int r0 = (g.blocks ? g.blocks[q] : q) * kTplRows;  // null list: every block (no dependent load)
     TplFetch<KM_RESID, NPL> f;  // ids, b, window
     f.issue(a, xrs, r0);
     tpl_stage_table<KM_RESID>(a, L);
@@ -1331,8 +1348,12 @@ struct TplGsChainArgs {
 template <bool BACK>
 __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
     constexpr int U = 8;
-    __shared__ double sdl[kTplMax + 1], scv[kTplMax + 1];
-    __shared__ int scf[kTplMax + 1];
+    // per-GS-template tables sized by the launch (ntpl entries; 27-pt: 27): a wave-sized
+    // workgroup with 5 KiB of fixed 256-entry tables fit 11 per CU, 3.7 TB/s on the 27-pt sweep
+    extern __shared__ __attribute__((aligned(16))) double chain_lds[];
+    double* sdl = chain_lds;
+    double* scv = sdl + a.ntpl;
+    int* scf = (int*)(scv + a.ntpl);
     __shared__ __attribute__((aligned(16))) double sacc[64 * U], sx[64 * U];
     __shared__ unsigned sid[64 * 2];
     const int lane = threadIdx.x;
@@ -1345,7 +1366,9 @@ __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
     const int cpb = kTplRows / a.B;  // chunks per block
     const long long nq = (long long)a.nblk * cpb;
     const long long q0 = (long long)blockIdx.x * 64;
-    auto cstart = [&](long long qc) { return a.blocks[qc / cpb] * kTplRows + (int)(qc % cpb) * a.B; };
+    auto cstart = [&](long long qc) {
+        return (a.blocks ? a.blocks[qc / cpb] : (int)(qc / cpb)) * kTplRows + (int)(qc % cpb) * a.B;
+    };
     // my chunk
     const long long qc = q0 + lane;
     const bool live = qc < nq;
@@ -1869,13 +1892,14 @@ static void launch_block(hipStream_t s, dim3 g, const CsrArgs& a, int first_bloc
 
 void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, int first_block,
                        int n_blocks, const double* x, const double* b, double* y, double omega,
-                       double* partial, int part_off) {
+                       double* partial, int part_off, double* y2, const double* d2) {
     if (n_blocks <= 0) return;
     const int ncl = (int)A.n_cols_local, nh = (int)A.n_halo();
+    AMG_ASSERT(!y2 || (mode == KM_SPMV && d2));
     CsrArgs a{A.hdr.p, A.tile_fixed.p, A.lcol.p, A.vidx.p, A.vtab.p, A.rend.p, A.dvi.p,
               A.rp.p, A.col.p, A.val.p,
               x, A.halo.p, ncl, nh, (ncl + 7) / 8, (ncl >= 2 && nh != 1) ? 1 : 0, A.square ? 0 : 1,
-              b, A.dinv.p, y, omega, partial, part_off};
+              b, y2 ? d2 : A.dinv.p, y, omega, partial, part_off, y2};
     const dim3 g(n_blocks);
     const int var = kernel_variant(A);
     if ((var & 64) && !(var & 4)) {
@@ -1983,7 +2007,9 @@ static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, co
     a.y = A.gs_racc.p;
     a.partial = partial;
     g.ke = backward ? A.gs_tkep.p : A.gs_tkem.p;
-    g.blocks = A.gs_tblocks.p;
+    // every block on the template path (27-pt): no block list to load before the window
+    const bool all_blocks = A.n_gs_tblk == A.tpl_blocks();
+    g.blocks = all_blocks ? nullptr : A.gs_tblocks.p;
     g.nblk = A.n_gs_tblk;
     g.first_row = A.first_row;
     g.B = (int)A.gs_block;
@@ -2010,12 +2036,13 @@ static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, co
 #undef AMG_G2
     HIP_CHECK(hipGetLastError());
     TplGsChainArgs c{A.gs_racc.p, x, A.gs_tid.p, A.gs_tdl.p, backward ? A.gs_tcvp.p : A.gs_tcvm.p,
-                     A.gs_tcf.p, A.n_gs_tpl, A.gs_tblocks.p, A.n_gs_tblk, (int)A.gs_block, (int)A.n_rows,
+                     A.gs_tcf.p, A.n_gs_tpl, g.blocks, A.n_gs_tblk, (int)A.gs_block, (int)A.n_rows,
                      (long long)A.first_row, y};
     const long long nch = (long long)A.n_gs_tblk * (kTplRows / A.gs_block);
     const dim3 cg((unsigned)((nch + 63) / 64)), cb(64);
-    if (backward) hipLaunchKernelGGL((tpl_gs_chain_kernel<true>), cg, cb, 0, s, c);
-    else hipLaunchKernelGGL((tpl_gs_chain_kernel<false>), cg, cb, 0, s, c);
+    const size_t clds = (size_t)c.ntpl * (8 + 8 + 4);
+    if (backward) hipLaunchKernelGGL((tpl_gs_chain_kernel<true>), cg, cb, clds, s, c);
+    else hipLaunchKernelGGL((tpl_gs_chain_kernel<false>), cg, cb, clds, s, c);
     HIP_CHECK(hipGetLastError());
 }
 

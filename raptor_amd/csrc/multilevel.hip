@@ -185,7 +185,16 @@ void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_
     std::swap(x, tmp);
 }
 
-void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool with_norm) {
+// AMG_FUSE_RESTRICT_J0=0: separate jacobi_zero launches (A/B)
+static bool fuse_restrict_j0() {
+    static const bool on = [] {
+        const char* e = std::getenv("AMG_FUSE_RESTRICT_J0");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
+void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool with_norm, bool x0_in_t) {
     DevMatrix& A = Amat(l);
     hipStream_t s = ctx->stream;
     const HostComm& comm = ctx->host;
@@ -215,7 +224,8 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
     double* tmp = L.t.p;
     bool zero = x_zero;
     for (int k = 0; k < opt.pre_sweeps; ++k) {
-        smooth(l, cur, b, tmp, zero, with_norm && k == 0);
+        if (k == 0 && x0_in_t) std::swap(cur, tmp);  // the sweep from zero is in tmp already
+        else smooth(l, cur, b, tmp, zero, with_norm && k == 0);
         zero = false;
     }
     if (zero) launch_zero(s, A.n_rows, cur);
@@ -238,8 +248,13 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
         // this rank's slice of the whole correction feeds the distributed interpolation
         par_apply(*L.P, KM_SPMV_ADD, C.x.p + L.P->first_col, nullptr, cur, 0.0, nullptr);
     } else {
-        par_apply(*L.R, KM_SPMV, L.r.p, nullptr, C.b.p, 0.0, nullptr);
-        cycle_rec(l + 1, C.x.p, C.b.p, true, false);
+        // Jacobi: the coarse level's first sweep from x = 0 (omega dinv b) rides along with
+        // the restriction that produces b (one pass over b and a launch fewer per level)
+        const bool j0 = opt.smoother == AMG_SMOOTH_JACOBI && opt.pre_sweeps >= 1 && l + 2 < levels.size() &&
+                        fuse_restrict_j0() &&
+                        par_restrict_j0(*L.R, L.r.p, C.b.p, C.t.p, Amat(l + 1).dinv.p, opt.jacobi_omega);
+        if (!j0) par_apply(*L.R, KM_SPMV, L.r.p, nullptr, C.b.p, 0.0, nullptr);
+        cycle_rec(l + 1, C.x.p, C.b.p, true, false, j0);
         par_apply(*L.P, KM_SPMV_ADD, C.x.p, nullptr, cur, 0.0, nullptr);
     }
     for (int k = 0; k < opt.post_sweeps; ++k) smooth(l, cur, b, tmp, false, false, true);
@@ -465,8 +480,12 @@ int64_t Solver::stored_bytes_per_cycle(size_t l) const {
     int64_t b = 0;
     bool zero = l > 0;
     int64_t sweeps = 0;
+    // the sweep from zero fused into the restriction above (cycle_rec): dinv read + x write
+    const DevMatrix* Rup = l > 0 ? levels[l - 1].R.get() : nullptr;
+    const bool j0 = !gs && Rup && (int)l != rep_level && fuse_restrict_j0() && Rup->format != AMG_FORMAT_CSR &&
+                    !Rup->tpl_on();
     for (int k = 0; k < opt.pre_sweeps; ++k, ++sweeps) {
-        if (zero && !gs) b += 24 * n;              // omega * dinv * b
+        if (zero && !gs) b += (j0 ? 16 : 24) * n;  // omega * dinv * b
         else b += sweep + (zero ? 8 * n : 0);      // (zero fill of x first)
         zero = false;
     }

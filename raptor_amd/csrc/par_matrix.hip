@@ -1074,6 +1074,17 @@ void par_apply(DevMatrix& A, int mode, const double* x, const double* b, double*
     launch_csr_stream(s, mode, norm, A, A.nb_int, A.nb_bnd, x, b, y, omega, partial, poff);
 }
 
+bool par_restrict_j0(DevMatrix& R, const double* r, double* bc, double* x0c, const double* dinvc,
+                     double omega) {
+    if (R.format == AMG_FORMAT_CSR || R.tpl_on()) return false;
+    const bool comm = R.halo_begin(r);
+    hipStream_t s = R.ctx->stream;
+    launch_csr_stream(s, KM_SPMV, false, R, 0, R.nb_int, r, nullptr, bc, omega, nullptr, 0, x0c, dinvc);
+    if (comm) R.halo_wait();
+    launch_csr_stream(s, KM_SPMV, false, R, R.nb_int, R.nb_bnd, r, nullptr, bc, omega, nullptr, 0, x0c, dinvc);
+    return true;
+}
+
 void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block,
                    bool backward, double* partial) {
     A.ensure_gs_blocks(block);
