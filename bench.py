@@ -62,7 +62,7 @@ def main():
     ap.add_argument("--traffic-json", type=str,
                     default=os.path.join(ROOT, "profiles", "pmc_level0_spmv.json"),
                     help="PMC-measured per-launch HBM traffic of the level-0 SpMV "
-                         "(scripts/gpu_round_profile.sh); reported as roofline.traffic")
+                         "(scripts/gpu_profile.sh); reported as roofline.traffic")
     args = ap.parse_args()
 
     import numpy as np

@@ -19,6 +19,8 @@ for st in ("27pt", "7pt"):
         A.mult(x, y)
     for _ in range(3):
         A.residual(x, b, y)
+    for _ in range(3):
+        A.residual_norm(x, b)
     if st == "7pt":
         for _ in range(3):
             A.jacobi(x, b, y)
