@@ -22,6 +22,34 @@ namespace amg {
 
 namespace {
 
+// Sum over the 64 lanes of a wave, the same value in every lane: DPP row_shr steps 1, 2, 4, 8
+// build each 16-lane row's prefix sum (VALU; lanes before the row start read 0), then the four
+// row totals are added in order (readlane).  The norm partials used a shuffle tree instead:
+// 6 ds_bpermute round trips at the end of every block (27-pt residual + norm 195 vs 168 us).
+// Fixed order: deterministic, and the same in every kernel family.
+template <int S>
+__device__ __forceinline__ double row_shr_f64(double v) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, 0x110 + S, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), 0x110 + S, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ double lane_f64(double v, int l) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+    v += row_shr_f64<1>(v);
+    v += row_shr_f64<2>(v);
+    v += row_shr_f64<4>(v);
+    v += row_shr_f64<8>(v);
+    return (lane_f64(v, 15) + lane_f64(v, 31)) + (lane_f64(v, 47) + lane_f64(v, 63));
+}
+
 struct CsrArgs {
     const int4* hdr;         // 2 x int4 per block (par_matrix.hip): {r0, r1, k0, nnz},
                              // {diag slot, tile lines, value-table offset (-1), table size}
@@ -401,7 +429,7 @@ __device__ __forceinline__ double block_long(const CsrArgs& a, int4 h0, double* 
 template <bool NORM>
 __device__ __forceinline__ void block_partial(const CsrArgs& a, int bid, double sq) {
     if (NORM) {
-        for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
+        sq = wave_sum(sq);
         if ((threadIdx.x & 63) == 0) a.partial[a.part_off + bid * kNormParts + (threadIdx.x >> 6)] = sq;
     }
 }
@@ -560,7 +588,7 @@ __global__ __launch_bounds__(kTPB, 8) void csr_plain_kernel(PlainArgs a) {
     }
     if (own) a.y[r] = out;
     if (NORM) {
-        for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
+        sq = wave_sum(sq);
         if ((tid & 63) == 0) a.partial[bid * kNormParts + (tid >> 6)] = sq;
     }
 }
@@ -911,7 +939,7 @@ __device__ __forceinline__ double tpl_rows(const TplArgs& a, const TplLds& L, __
 template <bool NORM>
 __device__ __forceinline__ void tpl_partial(const TplArgs& a, int blk, double sq) {
     if (NORM) {
-        for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
+        sq = wave_sum(sq);
         if ((threadIdx.x & 63) == 0) a.partial[blk * kNormParts + (threadIdx.x >> 6)] = sq;
     }
 }
@@ -1233,11 +1261,10 @@ __global__ __launch_bounds__(WIDE ? 64 : 256) void hybrid_gs_kernel(GsArgs a) {
         }
     }
     if (live) a.y[r] = xi + acc * dinv;
-    if (NORM) {  // ||b - A x_old||^2 partial of this slab; butterfly order is fixed
+    if (NORM) {  // ||b - A x_old||^2 partial of this slab (wave_sum: fixed order)
         const double rr = live ? a.b[r] - s_old : 0.0;
         double q = rr * rr;
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m);
+        q = wave_sum(q);
         if (lane == 0) a.partial[wave] = q;
     }
 }
@@ -1319,7 +1346,7 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
         }
     }
     if (NORM) {
-        for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
+        sq = wave_sum(sq);
         if (lane == 0) a.partial[g.part_off + 4 * q + (tid >> 6)] = sq;
     }
 }
