@@ -78,9 +78,17 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        device = local_rank
+        if os.environ.get("AMG_BENCH_SHARED_GPU") == "1":
+            # rehearsal of the N-GPU path on a 1-GPU box: every rank on device 0, each its own
+            # RCCL "host" (RCCL refuses two ranks of one host on one device; it then connects
+            # them over its socket transport, as tests/test_gpu_rccl.py does).  Timings of such
+            # a run are not a scaling measurement.
+            device = 0
+            os.environ["NCCL_HOSTID"] = f"amg-bench-rank{rank}"
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        torch.cuda.set_device(local_rank)
-        ctx = ra.Context.distributed(local_rank)
+        torch.cuda.set_device(device)
+        ctx = ra.Context.distributed(device)
     else:
         torch.cuda.set_device(0)
         ctx = ra.Context(0)

@@ -28,7 +28,8 @@ namespace amg {
 
 // kernel geometry shared by host-side block building and the kernels
 constexpr int kTPB = 256;   // threads per workgroup (4 waves of 64)
-constexpr int kCAP = 2048;  // nonzeros staged in LDS per workgroup (16 KiB of products)
+constexpr int kCAP = 2048;
+constexpr int kGatherBand = 1 << 14;  // gather column-code band width (col16)  // nonzeros staged in LDS per workgroup (16 KiB of products)
 constexpr int kPad = kCAP;  // col/val padding (entries): unconditional loads past a block's end
 constexpr int kTileLines = 256;  // x tile per workgroup: 256 lines x 64 B = 16 KiB of LDS
 constexpr int kNormParts = kTPB / 64;  // norm partials per CSR block (one per wave)
@@ -157,6 +158,11 @@ struct DevMatrix {
     DevBuf<uint16_t> rend;
     DevBuf<uint8_t> dvi;
     DevBuf<uint16_t> lcol;
+    // gather operators (P, R): 16-bit column codes band << 14 | (col - band base) when every
+    // block's columns fit in <= 4 bands of kGatherBand (gband: the block's 4 band bases);
+    // null otherwise (int32 col).  Blocks of more than kCAP entries read col either way.
+    DevBuf<uint16_t> col16;
+    DevBuf<int4> gband;
     // HBM bytes of one SpMV launch in the stored format with the default kernel variant
     // (headers, tile ids, 16-bit tile indices, VI indices + tables or values, columns for the
     // gather path, row_ptr, x once, y): the roofline numerator, DESIGN.md section 4

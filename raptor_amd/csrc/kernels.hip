@@ -77,6 +77,8 @@ struct CsrArgs {
     int part_off;      // partial slot of block bid's wave w: part_off + bid * kNormParts + w
     double* y2;        // SPMV only, non-null: y2[r] = omega * (dinv[r] * y[r]) as well (the next
                        // level's first Jacobi sweep from x = 0, fused into the restriction)
+    const uint16_t* col16;  // gather operators: 16-bit column codes (C16 kernels), with
+    const int4* gband;      // the block's 4 band bases: col = base[code >> 14] + (code & 0x3fff)
 };
 
 // the fused second output of a restriction (CsrArgs::y2): jacobi_zero_kernel's expression;
@@ -189,7 +191,7 @@ __device__ __forceinline__ void csr_pre_tile(const CsrArgs& a, int bid, CsrPre& 
 // block nxt's batch 1 (2: with VI indices) unless nxt < 0
 // RPB: rows per lane (gather blocks of rectangular operators hold up to kTPB * kGatherRPB
 // rows; a short-row P block of 256 rows filled a quarter of its 2048-entry stage)
-template <int MODE, bool NORM, bool TILE, bool VIB, int NU, int PRE = 0, int RPB = 1>
+template <int MODE, bool NORM, bool TILE, bool VIB, int NU, int PRE = 0, int RPB = 1, bool C16 = false>
 __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* stage, double* tabl,
                                              int* rends, CsrPre* pre = nullptr, int nxt = -1) {
     constexpr int U = kCAP / kTPB;  // 8 lane slots
@@ -198,10 +200,11 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
                   "several rows per lane: gather SpMV / y += Ax only");
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     static_assert(!PRE || TILE, "prefetched batch 1: x-tile path only");
+    static_assert(!C16 || !TILE, "column codes: gather path only");
     int tid_line = 0;
     v4u_t lq = {0u, 0u, 0u, 0u};
     v2u_t vq = {0u, 0u};
-    int4 h0, h1;
+    int4 h0, h1, gb = {0, 0, 0, 0};
     if constexpr (PRE > 0) {
         tid_line = pre->tid_line;
         lq = pre->lq;
@@ -218,6 +221,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     if (TILE) lq = __builtin_nontemporal_load((const v4u_t*)(a.lcol + (size_t)bid * kCAP + (size_t)tid * U));
     h0 = a.hdr[2 * bid];
     h1 = a.hdr[2 * bid + 1];
+    if (C16) gb = a.gband[bid];  // with the header: no extra round
     if (VIB) {
         if (!a.vi_packed) {
             vq = __builtin_nontemporal_load((const v2u_t*)(a.vidx + (size_t)bid * kCAP + (size_t)tid * U));
@@ -250,10 +254,18 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     // instruction's x gathers cover consecutive nonzeros (pairs measured 5-7% slower on P/R).
     // Lanes past the block re-read its last entry / pair.
     int c[U];
-    if (!TILE) {
+    if (!TILE && !C16) {
 #pragma unroll
         for (int u = 0; u < NU; ++u)
             c[u] = __builtin_nontemporal_load(a.col + k0 + min(tid + u * kTPB, nnz - 1));
+    } else if (C16) {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const unsigned code = __builtin_nontemporal_load(a.col16 + k0 + min(tid + u * kTPB, nnz - 1));
+            const unsigned t = code >> 14;
+            const int base = t == 0 ? gb.x : t == 1 ? gb.y : t == 2 ? gb.z : gb.w;
+            c[u] = base + (int)(code & 0x3fffu);
+        }
     }
     double v[U], tv = 0.0;
     if (VIB) {
@@ -384,16 +396,16 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     return sq;
 }
 
-template <int MODE, bool NORM, bool TILE, bool VIB, int GRPB = 1>
+template <int MODE, bool NORM, bool TILE, bool VIB, int GRPB = 1, bool C16 = false>
 __device__ __forceinline__ double block_dispatch(const CsrArgs& a, int bid, int nnz, double* stage,
                                                  double* tabl, int* rends) {
     if constexpr (TILE) {
         return block_main<MODE, NORM, TILE, VIB, 8>(a, bid, stage, tabl, rends);
     } else {
         constexpr int RP = (MODE == KM_SPMV || MODE == KM_SPMV_ADD) && !NORM ? GRPB : 1;
-        if (nnz > 4 * kTPB) return block_main<MODE, NORM, TILE, VIB, 8, 0, RP>(a, bid, stage, tabl, rends);
-        if (nnz > 2 * kTPB) return block_main<MODE, NORM, TILE, VIB, 4, 0, RP>(a, bid, stage, tabl, rends);
-        return block_main<MODE, NORM, TILE, VIB, 2, 0, RP>(a, bid, stage, tabl, rends);
+        if (nnz > 4 * kTPB) return block_main<MODE, NORM, TILE, VIB, 8, 0, RP, C16>(a, bid, stage, tabl, rends);
+        if (nnz > 2 * kTPB) return block_main<MODE, NORM, TILE, VIB, 4, 0, RP, C16>(a, bid, stage, tabl, rends);
+        return block_main<MODE, NORM, TILE, VIB, 2, 0, RP, C16>(a, bid, stage, tabl, rends);
     }
 }
 
@@ -436,7 +448,8 @@ __device__ __forceinline__ void block_partial(const CsrArgs& a, int bid, double 
 
 // GRPB: rows per lane of gather blocks (1, or kGatherRPB for short-row rectangular operators
 // whose blocks hold up to kTPB * kGatherRPB rows; DevMatrix::gather_rpb)
-template <int MODE, bool NORM, bool XCD, bool TILE, bool VI, int GRPB = 1>
+// C16: gather path with 16-bit column codes (DevMatrix::col16)
+template <int MODE, bool NORM, bool XCD, bool TILE, bool VI, int GRPB = 1, bool C16 = false>
 __global__ __launch_bounds__(kTPB, GRPB > 1 ? 7 : 8) void csr_block_kernel(CsrArgs a, int first_block) {
     static_assert(kCAP / kTPB == 8 && kTileLines * 8 == kCAP && kTPB == 256,
                   "lane-major layouts assume 8 entries per lane, 4 waves");
@@ -466,8 +479,8 @@ __global__ __launch_bounds__(kTPB, GRPB > 1 ? 7 : 8) void csr_block_kernel(CsrAr
     const int nnz = h0.w;
     double sq;
     if (nnz <= kCAP && (!TILE || (h1.y & 0xffff) <= kTileLines) && nnz > 0) {
-        if (VI && h1.z >= 0) sq = block_dispatch<MODE, NORM, TILE, true, GRPB>(a, bid, nnz, stage, tabl, rends);
-        else sq = block_dispatch<MODE, NORM, TILE, false, GRPB>(a, bid, nnz, stage, tabl, rends);
+        if (VI && h1.z >= 0) sq = block_dispatch<MODE, NORM, TILE, true, GRPB, C16>(a, bid, nnz, stage, tabl, rends);
+        else sq = block_dispatch<MODE, NORM, TILE, false, GRPB, C16>(a, bid, nnz, stage, tabl, rends);
     } else {
         sq = block_long<MODE, NORM>(a, h0, stage);
     }
@@ -1726,6 +1739,13 @@ int kernel_variant(const DevMatrix& A) {
     // each operator is stored for one kernel: square -> x tile, rectangular -> gather
     if (A.square) var &= ~4;
     else var |= 4;
+    // 256: gather path with 16-bit column codes, where built (DevMatrix::col16; default on,
+    // AMG_GATHER_C16=0 turns it off for A/B runs)
+    if (!ev && !A.square && A.col16.p) {
+        const char* e = std::getenv("AMG_GATHER_C16");
+        if (!(e && std::atoi(e) == 0)) var |= 256;
+    }
+    if (!A.col16.p) var &= ~256;
     return var;
 }
 
@@ -1909,6 +1929,11 @@ static void launch_csr_persist(hipStream_t s, int mode, bool norm, const CsrArgs
 template <int M, bool N, bool X, bool T, bool V>
 static void launch_block(hipStream_t s, dim3 g, const CsrArgs& a, int first_block, bool rpb4) {
     if constexpr (!T && !N && (M == KM_SPMV || M == KM_SPMV_ADD)) {
+        if (a.col16) {
+            if (rpb4) hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, kGatherRPB, true>), g, dim3(kTPB), 0, s, a, first_block);
+            else hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, 1, true>), g, dim3(kTPB), 0, s, a, first_block);
+            return;
+        }
         if (rpb4) {
             hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, kGatherRPB>), g, dim3(kTPB), 0, s, a, first_block);
             return;
@@ -1926,9 +1951,10 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
     CsrArgs a{A.hdr.p, A.tile_fixed.p, A.lcol.p, A.vidx.p, A.vtab.p, A.rend.p, A.dvi.p,
               A.rp.p, A.col.p, A.val.p,
               x, A.halo.p, ncl, nh, (ncl + 7) / 8, (ncl >= 2 && nh != 1) ? 1 : 0, A.square ? 0 : 1,
-              b, y2 ? d2 : A.dinv.p, y, omega, partial, part_off, y2};
+              b, y2 ? d2 : A.dinv.p, y, omega, partial, part_off, y2, nullptr, A.gband.p};
     const dim3 g(n_blocks);
     const int var = kernel_variant(A);
+    if (var & 256) a.col16 = A.col16.p;
     if ((var & 64) && !(var & 4)) {
         launch_csr_persist(s, mode, norm, a, first_block, n_blocks, (var & 8) != 0);
         return;

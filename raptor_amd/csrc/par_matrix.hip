@@ -601,6 +601,50 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             }
             col.upload(cb.data(), cb.size());
             val.upload(vb.data(), vb.size());
+            // gather operators: 16-bit column codes when every block's columns fit in <= 4
+            // bands of kGatherBand: a structured P / R block reads three
+            // planes' worth of columns, each a narrow band.  Lossless: the kernel decodes
+            // base[code >> 14] + (code & 0x3fff), the same column.
+            col16.reset();
+            gband.reset();
+            if (!square && nbk > 0) {
+                std::vector<uint16_t> c16(cb.size(), 0);
+                std::vector<int4> gb(nbk, make_int4(0, 0, 0, 0));
+                int bad = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : bad)
+                for (size_t q = 0; q < nbk; ++q) {
+                    const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
+                    if (nz == 0 || nz > kCAP) continue;  // chunked path: int32 columns
+                    std::vector<int> u(cb.begin() + koff[q], cb.begin() + koff[q] + nz);
+                    std::sort(u.begin(), u.end());
+                    int base[4] = {0, 0, 0, 0}, nbnd = 0;
+                    for (int c : u) {
+                        if (nbnd == 0 || c - base[nbnd - 1] >= kGatherBand) {
+                            if (nbnd == 4) {
+                                nbnd = 5;
+                                break;
+                            }
+                            base[nbnd++] = c;
+                        }
+                    }
+                    if (nbnd > 4) {
+                        ++bad;
+                        continue;
+                    }
+                    for (int t = nbnd; t < 4; ++t) base[t] = base[nbnd - 1];
+                    gb[q] = make_int4(base[0], base[1], base[2], base[3]);
+                    for (int j = 0; j < nz; ++j) {
+                        const int c = cb[koff[q] + j];
+                        int t = nbnd - 1;
+                        while (c < base[t]) --t;
+                        c16[koff[q] + j] = (uint16_t)((t << 14) | (c - base[t]));
+                    }
+                }
+                if (bad == 0) {
+                    col16.upload(c16.data(), c16.size());
+                    gband.upload(gb.data(), gb.size());
+                }
+            }
         }
         if (square) {  // x tiles: the square-operator kernel only
             // x-tile line ids at a fixed stride (kTileLines per block, padded with the block's
@@ -702,6 +746,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 continue;
             }
             if (square) fb += 4 * kTileLines + 2 * kCAP;    // tile ids, tile indices
+            else if (col16.p) fb += 2 * (int64_t)nz + 16;  // column codes, band bases
             else fb += 4 * (int64_t)nz;                     // columns
             if (hh[2 * q + 1].z >= 0)
                 fb += (square ? kCAP : gather_slots(nz) * kTPB) + 8 * (int64_t)hh[2 * q + 1].w;
