@@ -140,6 +140,9 @@ struct DevMatrix {
     HostCSR host;              // host image (global column ids), kept for export / setup
     int64_t first_row = 0, n_rows = 0, first_col = 0, n_cols_local = 0, nnz = 0;
     bool square = false;
+    // stored for the x-tile kernel (tile ids, 16-bit tile indices, kCAP-stride VI indices):
+    // square operators, and restrictions (rectangular, one row per lane) under AMG_RECT_TILE=1
+    bool tiled = false;
     DevBuf<int> rp, col;
     DevBuf<double> val, dinv;
     // CSR-stream row blocks: [0, nb_int) interior rows, [nb_int, nb_int+nb_bnd) rows that

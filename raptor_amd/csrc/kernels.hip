@@ -1737,11 +1737,11 @@ int kernel_variant(const DevMatrix& A) {
     // AMG_FORMAT_BLOCKS: the CSR block kernel on every row (no templates)
     if (A.format == AMG_FORMAT_BLOCKS) var &= ~(32 | 128);
     // each operator is stored for one kernel: square -> x tile, rectangular -> gather
-    if (A.square) var &= ~4;
+    if (A.tiled) var &= ~4;
     else var |= 4;
     // 256: gather path with 16-bit column codes, where built (DevMatrix::col16; default on,
     // AMG_GATHER_C16=0 turns it off for A/B runs)
-    if (!ev && !A.square && A.col16.p) {
+    if (!ev && !A.tiled && A.col16.p) {
         const char* e = std::getenv("AMG_GATHER_C16");
         if (!(e && std::atoi(e) == 0)) var |= 256;
     }
@@ -1950,7 +1950,7 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
     AMG_ASSERT(!y2 || (mode == KM_SPMV && d2));
     CsrArgs a{A.hdr.p, A.tile_fixed.p, A.lcol.p, A.vidx.p, A.vtab.p, A.rend.p, A.dvi.p,
               A.rp.p, A.col.p, A.val.p,
-              x, A.halo.p, ncl, nh, (ncl + 7) / 8, (ncl >= 2 && nh != 1) ? 1 : 0, A.square ? 0 : 1,
+              x, A.halo.p, ncl, nh, (ncl + 7) / 8, (ncl >= 2 && nh != 1) ? 1 : 0, A.tiled ? 0 : 1,
               b, y2 ? d2 : A.dinv.p, y, omega, partial, part_off, y2, nullptr, A.gband.p};
     const dim3 g(n_blocks);
     const int var = kernel_variant(A);

@@ -188,7 +188,7 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
     vofs.assign(nbk + 1, 0);
     for (size_t q = 0; q < nbk; ++q) {
         const int nz = hrp[bb.blocks[q].y] - hrp[bb.blocks[q].x];
-        vofs[q + 1] = vofs[q] + (M.square ? kCAP : tabs[q].empty() ? 0 : gather_slots(nz) * kTPB);
+        vofs[q + 1] = vofs[q] + (M.tiled ? kCAP : tabs[q].empty() ? 0 : gather_slots(nz) * kTPB);
     }
     AMG_CHECK(vofs[nbk] < INT_MAX, "value index stream too large");
     std::vector<uint8_t> idx((size_t)vofs[nbk] + 16, 0);
@@ -205,7 +205,7 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
             const size_t at = std::lower_bound(t.begin(), t.end(), bits) - t.begin();
             // square (x-tile kernel): entry pairs; rectangular (gather kernel): entry j at
             // lane j % kTPB, slot j / kTPB, NU slots per lane
-            const size_t pos = M.square ? lane_pos(j, kCAP / kTPB)
+            const size_t pos = M.tiled ? lane_pos(j, kCAP / kTPB)
                                         : (size_t)(j % kTPB) * gather_slots(nz) + (size_t)(j / kTPB);
             idx[(size_t)vofs[q] + pos] = (uint8_t)at;
         }
@@ -468,6 +468,30 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         nb_int = bb.nb_int;
         nb_bnd = bb.nb_bnd;
         tm.lap("    build: row blocks + x tiles");
+        // rectangular operators with one row per lane (R; P of SA) take the x-tile kernel when
+        // their blocks reuse x lines: at most 0.5 tile lines per nonzero.  Same-box A/B
+        // (profiles/r2y_rtile_*): 7-pt R0 106 -> 79 us (0.23 lines / nnz), R1 66 -> 53 (0.34),
+        // sa27 P0 299 -> 234 (0.04), P1 33 -> 26, g3sub R0 24 -> 20 (0.33); sa27 R1 122 -> 158
+        // at 0.70 (a 297-entry block loading 210 lines) stays on the gather kernel.
+        // AMG_RECT_TILE=0 / 1: never / always (A/B runs)
+        int64_t tile_lines_total = 0, tile_full = 0;
+        for (size_t q = 0; q + 1 < bb.tile_ptr.size(); ++q) {
+            const int nt = bb.tile_ptr[q + 1] - bb.tile_ptr[q];
+            tile_lines_total += nt;
+            tile_full += nt >= kTileLines;
+        }
+        {
+            const char* e = std::getenv("AMG_RECT_TILE");
+            const int mode = e ? std::atoi(e) : -1;
+            tiled = square || (gather_rpb == 1 && mode != 0 &&
+                               (mode == 1 || 2 * tile_lines_total <= (int64_t)nnz));
+        }
+        if (std::getenv("AMG_TRACE_BLOCKS")) {
+            const int64_t lines = tile_lines_total, full = tile_full;
+            std::fprintf(stderr, "[amg-blocks] %s rows %lld cols %lld nnz %lld blocks %zu lines %lld full %lld rpb %d\n",
+                         square ? "square" : tiled ? "rect-tiled" : "rect-gather", (long long)n_rows, (long long)n_cols_local, (long long)nnz,
+                         bb.blocks.size(), (long long)lines, (long long)full, gather_rpb);
+        }
         if (!tb.hdr.empty()) {
             // rows of blocks the CSR kernel still runs are not the template kernel's
             std::vector<char> keep(n_rows, 0);
@@ -607,7 +631,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             // base[code >> 14] + (code & 0x3fff), the same column.
             col16.reset();
             gband.reset();
-            if (!square && nbk > 0) {
+            if (!tiled && nbk > 0) {
                 std::vector<uint16_t> c16(cb.size(), 0);
                 std::vector<int4> gb(nbk, make_int4(0, 0, 0, 0));
                 int bad = 0;
@@ -646,7 +670,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 }
             }
         }
-        if (square) {  // x tiles: the square-operator kernel only
+        if (tiled) {  // x tiles: the x-tile kernel only
             // x-tile line ids at a fixed stride (kTileLines per block, padded with the block's
             // last line), so the kernel loads them without waiting for the block header
             std::vector<int> fx(std::max<size_t>(nbk, 1) * kTileLines, 0);
@@ -719,14 +743,14 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
                 if ((int)q >= bb.nb_skip) jac_extra_csr += e;
             }
             // rectangular (gather) operators: field 0 = the block's offset in the VI index stream
-            const int f0 = square ? dslot : (vofs.empty() ? 0 : (int)vofs[q]);
+            const int f0 = square ? dslot : tiled ? -1 : (vofs.empty() ? 0 : (int)vofs[q]);
             hh[2 * q + 1] = make_int4(f0, nt | (dvi_ok[q] ? 1 << 16 : 0), vt_off[q], vt_len[q]);
         }
         hdr.upload(hh.data(), hh.size());
         // measured (profiles/r1m_variants.txt): x tiles in XCD order on square operators (A0
         // -6..8%, A1 -6..8%, A2 +1% vs plain order; gathers are 1.3-1.9x slower); gathers in
         // XCD order on the rectangular P / R (R0 -10% vs plain order)
-        default_variant = square ? 2 : (4 | 2);
+        default_variant = tiled ? 2 : (4 | 2);
         // format bytes of one default-variant SpMV (the kernel reads every lane slot of the
         // fixed-stride streams, so their padding counts)
         // with templates: the skipped blocks cost nothing; template rows cost 1 byte (id); the
@@ -741,15 +765,15 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             const int64_t fb0 = fb;
             fb += 32;
             if (nz == 0) continue;
-            if (nz > kCAP || (square && nt > kTileLines)) {  // long row: CSR stream
+            if (nz > kCAP || (tiled && nt > kTileLines)) {  // long row: CSR stream
                 fb += 12 * (int64_t)nz;
                 continue;
             }
-            if (square) fb += 4 * kTileLines + 2 * kCAP;    // tile ids, tile indices
+            if (tiled) fb += 4 * kTileLines + 2 * kCAP;     // tile ids, tile indices
             else if (col16.p) fb += 2 * (int64_t)nz + 16;  // column codes, band bases
             else fb += 4 * (int64_t)nz;                     // columns
             if (hh[2 * q + 1].z >= 0)
-                fb += (square ? kCAP : gather_slots(nz) * kTPB) + 8 * (int64_t)hh[2 * q + 1].w;
+                fb += (tiled ? kCAP : gather_slots(nz) * kTPB) + 8 * (int64_t)hh[2 * q + 1].w;
             else
                 fb += 8 * (int64_t)nz;
             if ((int)q >= nb_skip) fb_tpl += fb - fb0 + 2 * (int64_t)(bb.blocks[q].y - bb.blocks[q].x);

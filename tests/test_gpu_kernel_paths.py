@@ -170,6 +170,8 @@ def test_march_reuse_shapes(ctx, oracle, monkeypatch, kind, dims):
 VPATHS = {"persist_csr": {"AMG_KERNEL_VARIANT": "106"},
           "march_chained": {"AMG_KERNEL_VARIANT": "170", "AMG_TPL_MARCH_CHUNKS": "1"},
           "blocks_only": {"AMG_KERNEL_VARIANT": "10"},
+          "gather_int32": {"AMG_GATHER_C16": "0"},
+          "rect_tile": {"AMG_RECT_TILE": "1"},
           "eager": {}}
 
 
@@ -198,6 +200,31 @@ def test_vcycle_paths_vs_oracle(ctx, oracle, monkeypatch, path):
     _, h = ml.solve(ctx.zeros(n), db, max_iter=4)
     _, ho = H.solve(np.zeros(n), b, max_iter=4)
     assert np.all(np.abs(h - ho) <= 1e-10 * ho)
+
+
+@pytest.mark.parametrize("rect_tile", ["0", "1"])
+def test_sa_restriction_paths_vs_oracle(ctx, oracle, monkeypatch, rect_tile):
+    """Smoothed aggregation + hybrid GS with the restrictions on the gather kernel (16-bit
+    column codes) or on the x-tile kernel (AMG_RECT_TILE=1): iterates bit-identical to the
+    oracle's cycle on the product's own operators."""
+    import raptor_amd as ra
+
+    O = oracle
+    monkeypatch.setenv("AMG_RECT_TILE", rect_tile)
+    A = ra.par_stencil_grid(ctx, "27pt", (40, 32, 24))
+    ml = ra.ParSmoothedAggregationSolver().setup(A)
+    R0 = ml.level_matrix(0, "R")
+    assert bool(R0.info["kernel_variant"] & 4) == (rect_tile == "0")  # 4 = gather path
+    H = O.Hierarchy(None, levels=oracle_levels(O, ml), smoother=O.SMOOTH_HYBRID_GS)
+    n = A.local_rows
+    b = O.vec_uniform(n, 19)
+    db = to_dev(ctx, b)
+    dx = ctx.zeros(n)
+    xo = np.zeros(n)
+    for _ in range(2):
+        ml.cycle(dx, db)
+        xo = H.cycle(xo, b)
+        assert np.array_equal(to_host(ctx, dx), xo)
 
 
 def test_sa27_npl16_vcycle_vs_oracle(ctx, oracle):

@@ -335,10 +335,12 @@ def test_vcycle_bit_exact(ctx, oracle, kind, dims, coarsen, smoother):
             assert same_csr(ml.level_matrix(l, "P").to_scipy_local(), Ho.matrix(l, "P"))
             assert same_csr(ml.level_matrix(l, "R").to_scipy_local(), Ho.matrix(l, "R"))
             assert np.array_equal(ml.level_split(l), Ho.split(l))
-            # P and R run the gather kernel with 16-bit column codes (variant bit 256): every
-            # block's columns fit in <= 4 bands of 16384 at these sizes
+            # P and R run the x-tile kernel (variant bit 4 clear: blocks that reuse x lines)
+            # or the gather kernel with 16-bit column codes (bit 256): every block's columns
+            # fit in <= 4 bands of 16384 at these sizes
             for w in "PR":
-                assert ml.level_matrix(l, w).info["kernel_variant"] & 256, (l, w)
+                v = ml.level_matrix(l, w).info["kernel_variant"]
+                assert (v & 256) or not (v & 4), (l, w, v)
     n = Ao.shape[0]
     b = Ao.spmv(O.vec_uniform(n, 42))
     db = to_dev(ctx, b)
