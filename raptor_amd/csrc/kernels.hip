@@ -196,8 +196,8 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
                                              int* rends, CsrPre* pre = nullptr, int nxt = -1) {
     constexpr int U = kCAP / kTPB;  // 8 lane slots
     static_assert(NU >= 2 && NU % 2 == 0 && NU <= U && (TILE ? NU == U : true), "slot pairs");
-    static_assert(RPB == 1 || (!TILE && !NORM && (MODE == KM_SPMV || MODE == KM_SPMV_ADD)),
-                  "several rows per lane: gather SpMV / y += Ax only");
+    static_assert(RPB == 1 || (!NORM && (MODE == KM_SPMV || MODE == KM_SPMV_ADD)),
+                  "several rows per lane: SpMV / y += Ax only");
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     static_assert(!PRE || TILE, "prefetched batch 1: x-tile path only");
     static_assert(!C16 || !TILE, "column codes: gather path only");
@@ -467,8 +467,8 @@ __global__ __launch_bounds__(kTPB, GRPB > 1 ? 7 : 8) void csr_block_kernel(CsrAr
         const int4 h0 = f.h0, h1 = f.h1;
         double sq;
         if (h0.w <= kCAP && (h1.y & 0xffff) <= kTileLines && h0.w > 0) {
-            if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV>(a, bid, stage, tabl, rends, &f, -1);
-            else sq = block_main<MODE, NORM, true, false, 8, PV>(a, bid, stage, tabl, rends, &f, -1);
+            if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV, GRPB>(a, bid, stage, tabl, rends, &f, -1);
+            else sq = block_main<MODE, NORM, true, false, 8, PV, GRPB>(a, bid, stage, tabl, rends, &f, -1);
         } else {
             sq = block_long<MODE, NORM>(a, h0, stage);
         }
@@ -1928,10 +1928,10 @@ static void launch_csr_persist(hipStream_t s, int mode, bool norm, const CsrArgs
 
 template <int M, bool N, bool X, bool T, bool V>
 static void launch_block(hipStream_t s, dim3 g, const CsrArgs& a, int first_block, bool rpb4) {
-    if constexpr (!T && !N && (M == KM_SPMV || M == KM_SPMV_ADD)) {
-        if (a.col16) {
-            if (rpb4) hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, kGatherRPB, true>), g, dim3(kTPB), 0, s, a, first_block);
-            else hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, 1, true>), g, dim3(kTPB), 0, s, a, first_block);
+    if constexpr (!N && (M == KM_SPMV || M == KM_SPMV_ADD)) {
+        if (!T && a.col16) {
+            if (rpb4) hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, kGatherRPB, !T>), g, dim3(kTPB), 0, s, a, first_block);
+            else hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, 1, !T>), g, dim3(kTPB), 0, s, a, first_block);
             return;
         }
         if (rpb4) {

@@ -468,11 +468,12 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         nb_int = bb.nb_int;
         nb_bnd = bb.nb_bnd;
         tm.lap("    build: row blocks + x tiles");
-        // rectangular operators with one row per lane (R; P of SA) take the x-tile kernel when
-        // their blocks reuse x lines: at most 0.5 tile lines per nonzero.  Same-box A/B
-        // (profiles/r2y_rtile_*): 7-pt R0 106 -> 79 us (0.23 lines / nnz), R1 66 -> 53 (0.34),
-        // sa27 P0 299 -> 234 (0.04), P1 33 -> 26, g3sub R0 24 -> 20 (0.33); sa27 R1 122 -> 158
-        // at 0.70 (a 297-entry block loading 210 lines) stays on the gather kernel.
+        // rectangular operators take the x-tile kernel when their blocks reuse x lines: at most
+        // 0.5 tile lines per nonzero.  Same-box A/B (profiles/r2y_rtile_*, r2z_rpb_*): 7-pt R0
+        // 106 -> 79 us (0.23 lines / nnz), R1 66 -> 53 (0.34), P0 (4 rows per lane, 0.06)
+        // 97 -> 80, P1 49 -> 39; sa27 P0 299 -> 234 (0.04), P1 33 -> 26; g3sub R0 24 -> 20
+        // (0.33), P0 19 -> 15; sa27 R1 122 -> 158 at 0.70 (a 297-entry block loading 210
+        // lines) stays on the gather kernel.
         // AMG_RECT_TILE=0 / 1: never / always (A/B runs)
         int64_t tile_lines_total = 0, tile_full = 0;
         for (size_t q = 0; q + 1 < bb.tile_ptr.size(); ++q) {
@@ -483,8 +484,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         {
             const char* e = std::getenv("AMG_RECT_TILE");
             const int mode = e ? std::atoi(e) : -1;
-            tiled = square || (gather_rpb == 1 && mode != 0 &&
-                               (mode == 1 || 2 * tile_lines_total <= (int64_t)nnz));
+            tiled = square || (mode != 0 && (mode == 1 || 2 * tile_lines_total <= (int64_t)nnz));
         }
         if (std::getenv("AMG_TRACE_BLOCKS")) {
             const int64_t lines = tile_lines_total, full = tile_full;
