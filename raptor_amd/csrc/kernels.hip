@@ -1955,7 +1955,7 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
     const dim3 g(n_blocks);
     const int var = kernel_variant(A);
     if (var & 256) a.col16 = A.col16.p;
-    if ((var & 64) && !(var & 4)) {
+    if ((var & 64) && !(var & 4) && A.square) {  // persistent x-tile kernel: square operators
         launch_csr_persist(s, mode, norm, a, first_block, n_blocks, (var & 8) != 0);
         return;
     }

@@ -45,7 +45,8 @@ struct BlockBuild {
 // changes, and all-templated interior blocks come first
 static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector<int>& col,
                                    const std::vector<uint8_t>& cls, int64_t ncl, int64_t nhalo,
-                                   const std::vector<uint8_t>* tplf = nullptr, int row_cap = kTPB) {
+                                   const std::vector<uint8_t>* tplf = nullptr, int row_cap = kTPB,
+                                   bool line_cap = true) {
     const int n = (int)rp.size() - 1;
     const int64_t hl0 = (ncl + 7) / 8;
     auto line_of = [&](int c) -> int64_t { return c < ncl ? c >> 3 : hl0 + ((c - ncl) >> 3); };
@@ -94,7 +95,8 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
         const long long len = rp[r + 1] - rp[r];
         collect(r, 2 * (int64_t)r);
         if (r > r0 && (cls[r] != cls[r0] || acc + len > kCAP || r - r0 >= row_cap ||
-                       nl + (int)cand.size() > kTileLines || (tplf && (*tplf)[r] != (*tplf)[r0]))) {
+                       (line_cap && nl + (int)cand.size() > kTileLines) ||
+                       (tplf && (*tplf)[r] != (*tplf)[r0]))) {
             emit(r0, r);  // closes [r0, r); blk advances
             r0 = r;
             acc = 0;
@@ -491,6 +493,20 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             std::fprintf(stderr, "[amg-blocks] %s rows %lld cols %lld nnz %lld blocks %zu lines %lld full %lld rpb %d\n",
                          square ? "square" : tiled ? "rect-tiled" : "rect-gather", (long long)n_rows, (long long)n_cols_local, (long long)nnz,
                          bb.blocks.size(), (long long)lines, (long long)full, gather_rpb);
+        }
+        // the gather kernel reads x from global memory: its blocks need only the kCAP-entry
+        // and row caps, not the 256-line tile cap.  sa27's R1 (270 entries per row over ~200
+        // lines each) was cut into blocks of ~1 row by that cap: one lane summing while 255
+        // idled.  AMG_GATHER_LINECAP=1 keeps the cap (A/B)
+        if (!tiled) {
+            const char* e = std::getenv("AMG_GATHER_LINECAP");
+            if (!(e && std::atoi(e) != 0)) {
+                bb = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(), nullptr, kTPB * gather_rpb, false);
+                nb_int = bb.nb_int;
+                nb_bnd = bb.nb_bnd;
+                if (std::getenv("AMG_TRACE_BLOCKS"))
+                    std::fprintf(stderr, "[amg-blocks]   gather blocks without the line cap: %zu\n", bb.blocks.size());
+            }
         }
         if (!tb.hdr.empty()) {
             // rows of blocks the CSR kernel still runs are not the template kernel's
