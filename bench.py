@@ -65,6 +65,13 @@ def main():
                          "(scripts/gpu_profile.sh); reported as roofline.traffic")
     args = ap.parse_args()
 
+    # the bench line is the only thing on stdout: native libraries (RCCL's version banner at
+    # communicator init) write to fd 1 directly, so fd 1 is pointed at stderr for the run and
+    # the JSON line goes to a duplicate of the original stdout
+    out_stream = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -387,7 +394,7 @@ def main():
             "vcycle_dominant_kernel": dominant,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=out_stream, flush=True)
     if world > 1:
         dist.destroy_process_group()
 
