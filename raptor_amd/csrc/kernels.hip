@@ -1335,7 +1335,8 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
         // start is a multiple of 64 and B | 64, so pos = i mod B and only the rank end clips)
         const int pos = i & (g.B - 1);
         const bool chain = BACK ? (pos != g.B - 1 && i + 1 < a.n) : pos != 0;
-        const int ke = chain ? loffr[f.id[j]] : -1;  // template entry of the chain coupling
+        // template entry of the chain coupling (loffr holds the ntpl GS templates only)
+        const int ke = chain && f.id[j] != kTplNone ? loffr[f.id[j]] : -1;
         double acc = f.pb[j], sold = 0.0;
         for (int k = 0; k < ln; k += 4) {  // 4 entries per step, as in tpl_rows
             const int e = st + k;
@@ -2032,7 +2033,12 @@ void launch_copy(hipStream_t s, int64_t n, const double* src, double* dst) {
 }
 
 // acc kernel LDS: the template kernel's RESID layout + the entries' column offsets
-inline size_t tpl_gs_lds_bytes(int win, int nent) { return tpl_lds_bytes(win, nent, false) + 4 * (kTplMax + 1); }
+// + the per-GS-template chain-entry table, sized by the templates in use: at kTplMax + 1 ints
+// the 27-pt acc kernel needed 32.7 KiB and fit 4 workgroups per CU against the residual's 5
+// (its LDS is 31.6 KiB): 205-211 vs 165-170 us per launch
+inline size_t tpl_gs_lds_bytes(int win, int nent, int ntpl) {
+    return tpl_lds_bytes(win, nent, false) + 4 * (((size_t)ntpl + 4) & ~(size_t)3);
+}
 
 static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
                           double* y, bool backward, double* partial) {
@@ -2069,7 +2075,7 @@ static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, co
     g.part_off = A.n_gs_slabs;
     const int npl = a.win <= 4 * kTPB ? 4 : a.win <= 8 * kTPB ? 8 : a.win <= 12 * kTPB ? 12 : 16;
     AMG_ASSERT(a.win <= npl * kTPB && a.win <= kTplWin);
-    const size_t lds = tpl_gs_lds_bytes(a.win, a.nent);
+    const size_t lds = tpl_gs_lds_bytes(a.win, a.nent, a.ntpl);
     const bool norm = partial != nullptr;
     const dim3 grid(g.nblk), blk(kTPB);
 #define AMG_G2(BK, NM, P) hipLaunchKernelGGL((tpl_gs_acc_kernel<BK, NM, P>), grid, blk, lds, s, g)

@@ -49,78 +49,96 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
                                    bool line_cap = true) {
     const int n = (int)rp.size() - 1;
     const int64_t hl0 = (ncl + 7) / 8;
+    const size_t nlines = (size_t)(hl0 + (nhalo + 7) / 8) + 1;
     auto line_of = [&](int c) -> int64_t { return c < ncl ? c >> 3 : hl0 + ((c - ncl) >> 3); };
-    std::vector<int> stamp((size_t)(hl0 + (nhalo + 7) / 8) + 1, -1), slot(stamp.size(), 0);
     struct Rec {
         int r0, r1;
         std::vector<int> lines;
         bool bnd, tpl;
     };
-    std::vector<Rec> recs;
     BlockBuild out;
     out.lcol.assign(col.size() + kPad, 0);
-    int r0 = 0, nl = 0, blk = 0;
-    long long acc = 0;
-    std::vector<int> lines;
-    auto emit = [&](int a, int b) {
-        if (b <= a) return;
-        std::sort(lines.begin(), lines.end());
-        for (size_t s = 0; s < lines.size(); ++s) slot[lines[s]] = (int)s;
-        const bool tiled = (int)lines.size() <= kTileLines;
-        for (int k = rp[a]; k < rp[b]; ++k) {
-            const int c = col[k];
-            const int e = c < ncl ? (c & 7) : (int)((c - ncl) & 7);  // element within its line
-            out.lcol[k] = tiled ? (uint16_t)(slot[line_of(c)] * 8 + e) : (uint16_t)0;
-        }
-        recs.push_back({a, b, tiled ? lines : std::vector<int>(), cls[a] != 0,
-                        tplf != nullptr && (*tplf)[a] != 0});
-        if (!tiled) recs.back().lines.assign(kTileLines + 1, 0);  // marker: untiled
-        lines.clear();
-        ++blk;
-    };
-    std::vector<int64_t> tstamp(stamp.size(), -1);
-    std::vector<int> cand;
-    // distinct lines of row r not yet in the open block (marker keeps them distinct per call)
-    auto collect = [&](int r, int64_t marker) {
-        cand.clear();
-        for (int k = rp[r]; k < rp[r + 1]; ++k) {
-            const int64_t L = line_of(col[k]);
-            if (stamp[L] != blk && tstamp[L] != marker) {
-                tstamp[L] = marker;
-                cand.push_back((int)L);
+    // The greedy cut runs independently on a fixed number of row chunks (each chunk starts a
+    // block at its first row), in parallel: blocks never change the arithmetic (rows never
+    // straddle a block), and a fixed chunk count keeps the cut independent of the thread count.
+    // Sequential, the cut took 0.4-0.7 s per 256^3-level operator.
+    const int nch = n >= (1 << 16) ? 64 : 1;
+    std::vector<std::vector<Rec>> recs((size_t)nch);
+#pragma omp parallel if (nch > 1)
+    {
+        std::vector<int> stamp(nlines, -1), slot(nlines, 0);
+        std::vector<int64_t> tstamp(nlines, -1);
+        std::vector<int> lines, cand;
+        int blk = 0;  // per thread, never reset: stamp markers stay unique across chunks
+#pragma omp for schedule(dynamic, 1)
+        for (int ch = 0; ch < nch; ++ch) {
+            const int ra = (int)((int64_t)n * ch / nch), rb = (int)((int64_t)n * (ch + 1) / nch);
+            std::vector<Rec>& rc = recs[(size_t)ch];
+            int r0 = ra, nl = 0;
+            long long acc = 0;
+            lines.clear();
+            ++blk;
+            auto emit = [&](int a, int b) {
+                if (b <= a) return;
+                std::sort(lines.begin(), lines.end());
+                for (size_t q = 0; q < lines.size(); ++q) slot[lines[q]] = (int)q;
+                const bool tiled = (int)lines.size() <= kTileLines;
+                for (int k = rp[a]; k < rp[b]; ++k) {
+                    const int c = col[k];
+                    const int e = c < ncl ? (c & 7) : (int)((c - ncl) & 7);  // element within its line
+                    out.lcol[k] = tiled ? (uint16_t)(slot[line_of(c)] * 8 + e) : (uint16_t)0;
+                }
+                rc.push_back({a, b, tiled ? lines : std::vector<int>(), cls[a] != 0,
+                              tplf != nullptr && (*tplf)[a] != 0});
+                if (!tiled) rc.back().lines.assign(kTileLines + 1, 0);  // marker: untiled
+                lines.clear();
+                ++blk;
+            };
+            // distinct lines of row r not yet in the open block (marker keeps them distinct
+            // per call)
+            auto collect = [&](int r, int64_t marker) {
+                cand.clear();
+                for (int k = rp[r]; k < rp[r + 1]; ++k) {
+                    const int64_t L = line_of(col[k]);
+                    if (stamp[L] != blk && tstamp[L] != marker) {
+                        tstamp[L] = marker;
+                        cand.push_back((int)L);
+                    }
+                }
+            };
+            for (int r = ra; r < rb; ++r) {
+                const long long len = rp[r + 1] - rp[r];
+                collect(r, 2 * (int64_t)r);
+                if (r > r0 && (cls[r] != cls[r0] || acc + len > kCAP || r - r0 >= row_cap ||
+                               (line_cap && nl + (int)cand.size() > kTileLines) ||
+                               (tplf && (*tplf)[r] != (*tplf)[r0]))) {
+                    emit(r0, r);  // closes [r0, r); blk advances
+                    r0 = r;
+                    acc = 0;
+                    nl = 0;
+                    collect(r, 2 * (int64_t)r + 1);  // all of row r's lines are new to the new block
+                }
+                for (int L : cand) {
+                    stamp[L] = blk;
+                    lines.push_back(L);
+                }
+                nl += (int)cand.size();
+                acc += len;
             }
+            emit(r0, rb);
         }
-    };
-    for (int r = 0; r < n; ++r) {
-        const long long len = rp[r + 1] - rp[r];
-        collect(r, 2 * (int64_t)r);
-        if (r > r0 && (cls[r] != cls[r0] || acc + len > kCAP || r - r0 >= row_cap ||
-                       (line_cap && nl + (int)cand.size() > kTileLines) ||
-                       (tplf && (*tplf)[r] != (*tplf)[r0]))) {
-            emit(r0, r);  // closes [r0, r); blk advances
-            r0 = r;
-            acc = 0;
-            nl = 0;
-            collect(r, 2 * (int64_t)r + 1);  // all of row r's lines are new to the new block
-        }
-        for (int L : cand) {
-            stamp[L] = blk;
-            lines.push_back(L);
-        }
-        nl += (int)cand.size();
-        acc += len;
     }
-    emit(r0, n);
     for (int pass = 0; pass < 3; ++pass)
-        for (const Rec& R : recs) {
-            const int p = R.bnd ? 2 : R.tpl ? 0 : 1;
-            if (p != pass) continue;
-            out.blocks.push_back(make_int2(R.r0, R.r1));
-            out.tile_ptr.push_back((int)out.tile_lines.size());
-            out.tile_lines.insert(out.tile_lines.end(), R.lines.begin(), R.lines.end());
-            (pass == 2 ? out.nb_bnd : out.nb_int)++;
-            if (pass == 0) out.nb_skip++;
-        }
+        for (const std::vector<Rec>& rc : recs)
+            for (const Rec& R : rc) {
+                const int p = R.bnd ? 2 : R.tpl ? 0 : 1;
+                if (p != pass) continue;
+                out.blocks.push_back(make_int2(R.r0, R.r1));
+                out.tile_ptr.push_back((int)out.tile_lines.size());
+                out.tile_lines.insert(out.tile_lines.end(), R.lines.begin(), R.lines.end());
+                (pass == 2 ? out.nb_bnd : out.nb_int)++;
+                if (pass == 0) out.nb_skip++;
+            }
     out.tile_ptr.push_back((int)out.tile_lines.size());
     return out;
 }
