@@ -964,7 +964,10 @@ __device__ __forceinline__ void tpl_partial(const TplArgs& a, int blk, double sq
 constexpr int tpl_waves(int npl) { return npl > 8 ? 4 : 6; }
 // the 7-pt marching form at 7 waves (72 VGPRs): its Jacobi + norm variant took 74 at 6 waves
 // (a wave per SIMD fewer than the plain Jacobi: 101 vs 83 us per launch)
-constexpr int tpl_march_waves(int npl) { return npl == 8 ? 7 : tpl_waves(npl); }
+#ifndef AMG_MARCH_NORM_WAVES  // build-time A/B knob: waves per SIMD of the 7-pt Jacobi + norm form
+#define AMG_MARCH_NORM_WAVES 7
+#endif
+constexpr int tpl_march_waves(int npl, bool norm) { return npl == 8 ? (norm ? AMG_MARCH_NORM_WAVES : 7) : tpl_waves(npl); }
 
 // one workgroup per block of kTplRows rows
 template <int MODE, bool NORM, int NPL>
@@ -1027,7 +1030,7 @@ __global__ __launch_bounds__(kTPB, tpl_waves(NPL)) void tpl_persist_kernel(TplAr
 // only the rest is loaded -- 1024 instead of 2048 doubles per 7-pt block.  The next block's
 // loaded slots and row ids are prefetched into registers during the current block.
 template <int MODE, bool NORM, int NPL>
-__global__ __launch_bounds__(kTPB, tpl_march_waves(NPL)) void tpl_march_kernel(TplArgs a, int nblk, int S, int nchunk) {
+__global__ __launch_bounds__(kTPB, tpl_march_waves(NPL, NORM)) void tpl_march_kernel(TplArgs a, int nblk, int S, int nchunk) {
     static_assert(NPL > 0 && NPL % 2 == 0, "window path, slot pairs");
     constexpr int NP = NPL / 2;  // slot pairs per lane (16-byte loads and LDS copies)
     const TplLds L = tpl_lds_layout<MODE>(a);
