@@ -170,12 +170,12 @@ HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, cons
         ub[i] = u;
     }
     const int64_t bnnz = brp.back();
-    std::vector<long long> bcol(bnnz);
-    std::vector<double> bval(bnnz);
-    std::copy(B.col.begin(), B.col.end(), bcol.begin());
-    std::copy(B.val.begin(), B.val.end(), bval.begin());
-    std::copy(G.col.begin(), G.col.end(), bcol.begin() + B.nnz());
-    std::copy(G.val.begin(), G.val.end(), bval.begin() + B.nnz());
+    // the B image [local rows | ghost rows] is assembled on the device (two uploads each),
+    // not in a host copy of B; the host fallback reads B or G through bcol_at / bval_at
+    static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
+    const int64_t bl = B.nnz();
+    auto bcol_at = [&](long long q) -> int64_t { return q < bl ? B.col[q] : G.col[q - bl]; };
+    auto bval_at = [&](long long q) -> double { return q < bl ? B.val[q] : G.val[q - bl]; };
     // bins by table size (load factor <= 1/2 on the upper bound); rows beyond the largest
     // table try it anyway (their distinct columns are usually far fewer than the bound) and
     // fall back to the host only when it overflows
@@ -191,13 +191,20 @@ HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, cons
     DevBuf<long long> d_arp, d_brp, d_bcol, d_counts, d_crp, d_ccol;
     DevBuf<int> d_acol, d_rows[4];
     DevBuf<double> d_aval, d_bval, d_cval;
-    std::vector<long long> arp(A.rp.begin(), A.rp.end());
-    d_arp.upload(arp.data(), arp.size());
+    d_arp.upload(reinterpret_cast<const long long*>(A.rp.data()), A.rp.size());
     d_acol.upload(acol.data(), acol.size());
     d_aval.upload(A.val.data(), A.val.size());
     d_brp.upload(brp.data(), brp.size());
-    d_bcol.upload(bcol.data(), bcol.size());
-    d_bval.upload(bval.data(), bval.size());
+    d_bcol.alloc((size_t)bnnz);
+    d_bval.alloc((size_t)bnnz);
+    if (bl) {
+        HIP_CHECK(hipMemcpy(d_bcol.p, B.col.data(), sizeof(long long) * bl, hipMemcpyHostToDevice));
+        HIP_CHECK(hipMemcpy(d_bval.p, B.val.data(), sizeof(double) * bl, hipMemcpyHostToDevice));
+    }
+    if (bnnz > bl) {
+        HIP_CHECK(hipMemcpy(d_bcol.p + bl, G.col.data(), sizeof(long long) * (bnnz - bl), hipMemcpyHostToDevice));
+        HIP_CHECK(hipMemcpy(d_bval.p + bl, G.val.data(), sizeof(double) * (bnnz - bl), hipMemcpyHostToDevice));
+    }
     d_counts.alloc((size_t)std::max<int64_t>(n, 1));
     HIP_CHECK(hipMemsetAsync(d_counts.p, 0, sizeof(long long) * d_counts.n, s));
     tm.lap("    spgemm: uploads");
@@ -241,9 +248,9 @@ HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, cons
                 for (int64_t ka = A.rp[i]; ka < A.rp[i + 1]; ++ka) {
                     const int64_t r = acol[ka];
                     for (long long q = brp[r]; q < brp[r + 1]; ++q) {
-                        const int64_t j = bcol[q];
+                        const int64_t j = bcol_at(q);
                         if (!seen[j]) seen[j] = 1, touched.push_back(j);
-                        acc[j] += A.val[ka] * bval[q];
+                        acc[j] += A.val[ka] * bval_at(q);
                     }
                 }
                 std::sort(touched.begin(), touched.end());
@@ -267,8 +274,7 @@ HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, cons
     C.rp.assign(n + 1, 0);
     for (int64_t i = 0; i < n; ++i) C.rp[i + 1] = C.rp[i] + counts[i];
     const int64_t cnnz = C.rp[n];
-    std::vector<long long> crp(C.rp.begin(), C.rp.end());
-    d_crp.upload(crp.data(), crp.size());
+    d_crp.upload(reinterpret_cast<const long long*>(C.rp.data()), C.rp.size());
     d_ccol.alloc((size_t)std::max<int64_t>(cnnz, 1));
     d_cval.alloc((size_t)std::max<int64_t>(cnnz, 1));
     AMG_BIN(256, true, 0);
