@@ -247,33 +247,43 @@ __global__ void interp_kernel(DCsr A, DCsr S, const int* cf, const int* cmap, in
         }
         if (s == 0.0) d += A.val[k];
     }
-    int q = prp[i];
+    // num_j accumulates in this row's own P slots (pval), k outer: s_k is formed once per
+    // strong F neighbour instead of once per (j, k) pair, and every num_j still receives its
+    // terms in A-row order of k -- the host loop's order, so the weights are bit-identical
+    const int q0 = prp[i];
+    int q = q0;
     for (int kj = A.rp[i]; kj < A.rp[i + 1]; ++kj) {
         const int j = A.col[kj];
         if (j == i || cf[j] != ST_C || !strong(S, i, j)) continue;
-        double num = A.val[kj];
-        for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) {
-            const int kk = A.col[k];
-            if (kk == i || cf[kk] == ST_C || !strong(S, i, kk)) continue;
-            const int uj = dfind(A.col, A.rp[kk], A.rp[kk + 1], j);
-            double akk = 0.0;
-            for (int u = A.rp[kk]; u < A.rp[kk + 1]; ++u)
-                if (A.col[u] == kk) {
-                    akk = A.val[u];
-                    break;
-                }
-            const bool pos = akk > 0.0;
-            if (uj < 0 || !(pos ? A.val[uj] < 0.0 : A.val[uj] > 0.0)) continue;
-            double s = 0.0;
-            for (int u = A.rp[kk]; u < A.rp[kk + 1]; ++u) {
-                const double v = A.val[u];
-                if ((pos ? v < 0.0 : v > 0.0) && in_ci(A.col[u])) s += v;
-            }
-            if (s != 0.0) num += (A.val[k] * A.val[uj]) / s;
-        }
         pcol[q] = cmap[j];
-        pval[q++] = -num / d;
+        pval[q++] = A.val[kj];
     }
+    for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+        const int kk = A.col[k];
+        if (kk == i || cf[kk] == ST_C || !strong(S, i, kk)) continue;
+        double akk = 0.0;
+        for (int u = A.rp[kk]; u < A.rp[kk + 1]; ++u)
+            if (A.col[u] == kk) {
+                akk = A.val[u];
+                break;
+            }
+        const bool pos = akk > 0.0;
+        double s = 0.0;
+        for (int u = A.rp[kk]; u < A.rp[kk + 1]; ++u) {
+            const double v = A.val[u];
+            if ((pos ? v < 0.0 : v > 0.0) && in_ci(A.col[u])) s += v;
+        }
+        if (s == 0.0) continue;
+        q = q0;
+        for (int kj = A.rp[i]; kj < A.rp[i + 1]; ++kj) {
+            const int j = A.col[kj];
+            if (j == i || cf[j] != ST_C || !strong(S, i, j)) continue;
+            const int uj = dfind(A.col, A.rp[kk], A.rp[kk + 1], j);
+            if (uj >= 0 && (pos ? A.val[uj] < 0.0 : A.val[uj] > 0.0)) pval[q] += (A.val[k] * A.val[uj]) / s;
+            ++q;
+        }
+    }
+    for (q = q0; q < q0 + nci; ++q) pval[q] = -pval[q] / d;
 }
 
 // ---- MIS(2) aggregation -----------------------------------------------------------------
