@@ -462,7 +462,9 @@ int amg_solver_level_info(amg_solver S, int32_t l, amg_level_info* info) {
         info->n_global = A.host.n_global_rows;
         info->n_local = A.n_rows;
         info->nnz_local = A.nnz;
-        info->nnz_global = comm.allreduce_sum(A.nnz);
+        // a replicated coarse level is whole on every rank: its nnz is not summed over ranks
+        const int64_t nz = comm.allreduce_sum(A.nnz);
+        info->nnz_global = A.replicated ? A.nnz : nz;
         const Level& L = S->s.levels[l];
         info->p_nnz_local = L.P ? L.P->nnz : 0;
         info->r_nnz_local = L.R ? L.R->nnz : 0;

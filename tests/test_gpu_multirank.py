@@ -140,6 +140,9 @@ def test_multirank_vcycle_bit_exact(oracle, nranks, kind, dims, coarsen, smoothe
             if not (np.array_equal(loc.indptr, G.indptr) and np.array_equal(loc.indices, G.indices)
                     and np.array_equal(loc.data, G.data)):
                 bad.append(("A", l))
+            # global nonzeros, replicated levels included (held whole by every rank)
+            if ml.level_info(l)["nnz_global"] != levels[l].nnz:
+                bad.append(("nnz_global", l, ml.level_info(l)["nnz_global"], levels[l].nnz))
         db = to_dev(ctx, b[f:f + m])
         dx = ctx.zeros(m)
         xs = []
