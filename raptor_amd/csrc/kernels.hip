@@ -109,8 +109,22 @@ __device__ __forceinline__ double epilogue(const CsrArgs& a, int r, double s, do
 // s += stage[k] for k in [lo, hi), in order.  Eight LDS reads are issued before their eight
 // dependent adds, so a long row waits on LDS once per eight entries instead of once per
 // entry (the adds stay sequential: the oracle's summation order).
+#ifndef AMG_ROWSUM_AHEAD  // build-time A/B knob: LDS reads issued ahead of a long row's adds
+#define AMG_ROWSUM_AHEAD 16
+#endif
 __device__ __forceinline__ double lds_row_sum(const double* stage, int lo, int hi, double s) {
     int k = lo;
+    if constexpr (AMG_ROWSUM_AHEAD >= 16) {
+        // long rows (restrictions of SA hierarchies: 100-700 entries): one LDS round trip per
+        // 16 entries
+        for (; k + 16 <= hi; k += 16) {
+            double v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = stage[k + u];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) s += v[u];
+        }
+    }
     for (; k + 8 <= hi; k += 8) {
         double v[8];
 #pragma unroll
