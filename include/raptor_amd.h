@@ -48,6 +48,10 @@ typedef int (*amg_alltoallv_fn)(void* user, const void* sendbuf, const int64_t* 
 /* ---- error / version ----------------------------------------------------------- */
 const char* amg_last_error(void);
 int amg_version(void); /* 100 * major + minor */
+/* Versions of the runtimes this process actually bound (the loader may have mapped copies
+ * other than the ones the library was built against, e.g. a framework's bundled HIP / RCCL):
+ * hipRuntimeGetVersion() and ncclGetVersion() (e.g. 22706 = RCCL 2.27.6).               */
+int amg_runtime_versions(int32_t* hip_runtime, int32_t* rccl);
 
 /* ---- context (one per GPU / rank) ----------------------------------------------- */
 /* hip_stream: a hipStream_t owned by the caller (NULL: the context creates one).      */

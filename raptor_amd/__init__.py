@@ -335,6 +335,15 @@ def read_par_matrix(ctx: Context, path) -> ParCSRMatrix:
     return ParCSRMatrix(ctx, h)
 
 
+def runtime_versions() -> dict:
+    """The HIP runtime and RCCL versions this process actually bound (hipRuntimeGetVersion,
+    ncclGetVersion): a process that imported torch first runs the library on torch's bundled
+    copies, which need not be the ROCm release the library was built against."""
+    hv, nv = C.c_int32(), C.c_int32()
+    check(lib().amg_runtime_versions(C.byref(hv), C.byref(nv)))
+    return {"hip_runtime": hv.value, "rccl": nv.value}
+
+
 def vector_copy(ctx: Context, src, dst):
     """dst = src with the 16-byte nontemporal copy kernel (the bench's copy ceiling)."""
     if src.numel() != dst.numel():

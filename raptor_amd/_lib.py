@@ -99,6 +99,7 @@ _pf64 = C.POINTER(C.c_double)
 SIGNATURES = {
     "amg_last_error": (C.c_char_p, []),
     "amg_version": (C.c_int, []),
+    "amg_runtime_versions": (C.c_int, [C.POINTER(_i32), C.POINTER(_i32)]),
     "amg_context_create": (C.c_int, [C.c_int, _vp, C.POINTER(_vp)]),
     "amg_context_set_comm": (C.c_int, [_vp, C.c_int, C.c_int, _vp, ALLTOALLV_FN, _vp]),
     "amg_rccl_unique_id": (C.c_int, [_vp]),

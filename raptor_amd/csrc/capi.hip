@@ -1,6 +1,11 @@
 // capi.hip -- extern "C" boundary (include/raptor_amd.h).  Every entry point catches
 // exceptions and turns them into an error code + thread-local message.
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 
@@ -81,14 +86,47 @@ static HostCSR make_host_csr(const HostComm& comm, int64_t n_global, int64_t fir
     return h;
 }
 
+// AMG_SEGV_BACKTRACE=1 (debugging a host crash inside a runtime call, e.g. RCCL graph
+// capture): print the native stack to stderr on SIGSEGV / SIGABRT, then re-raise
+static void amg_crash_handler(int sig) {
+    void* fr[64];
+    const int n = backtrace(fr, 64);
+    const char msg[] = "[amg] fatal signal, native backtrace:\n";
+    (void)!write(2, msg, sizeof(msg) - 1);
+    backtrace_symbols_fd(fr, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
+// (re)installed at context creation and again right before a hipGraph capture: runtimes
+// loaded later (RCCL, a framework) may have replaced the handler in between
+void amg::install_crash_handler() {
+    const char* e = std::getenv("AMG_SEGV_BACKTRACE");
+    if (!(e && std::atoi(e) != 0)) return;
+    signal(SIGSEGV, amg_crash_handler);
+    signal(SIGABRT, amg_crash_handler);
+}
+
 extern "C" {
 
 const char* amg_last_error(void) { return g_err.c_str(); }
 int amg_version(void) { return 100; }
 
+int amg_runtime_versions(int32_t* hip_runtime, int32_t* rccl) {
+    return guard([&] {
+        AMG_CHECK(hip_runtime && rccl, "null output");
+        int hv = 0, nv = 0;
+        HIP_CHECK(hipRuntimeGetVersion(&hv));
+        NCCL_CHECK(ncclGetVersion(&nv));
+        *hip_runtime = hv;
+        *rccl = nv;
+    });
+}
+
 int amg_context_create(int device, void* hip_stream, amg_context* out) {
     return guard([&] {
         AMG_CHECK(out, "null output");
+        install_crash_handler();
         int ndev = 0;
         HIP_CHECK(hipGetDeviceCount(&ndev));
         AMG_CHECK(device >= 0 && device < ndev, "device index out of range");
@@ -531,6 +569,13 @@ int amg_solver_set_graph(amg_solver S, int32_t enable) {
         AMG_CHECK(!enable || S->s.ctx->host.nranks == 1 || S->s.ctx->transport == TR_RCCL,
                   "hipGraph capture needs one rank or the RCCL transport (loopback ranks "
                   "synchronise on the host)");
+        // capturing the RCCL groups of a multi-rank cycle is validated only where the capture
+        // tests run; elsewhere it stays behind an explicit opt-in
+        if (enable && S->s.ctx->host.nranks > 1) {
+            const char* e = std::getenv("AMG_RCCL_GRAPH");
+            AMG_CHECK(e && std::atoi(e) != 0,
+                      "multi-rank hipGraph capture of RCCL cycles is experimental: set AMG_RCCL_GRAPH=1");
+        }
         S->s.use_graph = enable != 0;
         for (auto& g : S->s.graphs)
             if (g.exec) {

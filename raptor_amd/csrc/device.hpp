@@ -35,6 +35,9 @@ constexpr int kTileLines = 256;  // x tile per workgroup: 256 lines x 64 B = 16 
 constexpr int kNormParts = kTPB / 64;  // norm partials per CSR block (one per wave)
 constexpr int kGsWide = 128;     // sliced-ELL width from which hybrid GS uses the wide variant
 constexpr int kGatherRPB = 4;    // rows per lane of gather (rectangular-operator) row blocks
+// CSR block header h1.y: tile lines (low 16 bits); bit kHdrDvi = a value-indexed square
+// block whose Jacobi takes 1/a_ii from its value table
+constexpr int kHdrDvi = 1 << 16;
 // row templates: 1-byte template id per row (kTplNone = row not templated)
 constexpr int kTplNone = 255;
 constexpr int kTplMax = 255;       // templates per operator
@@ -90,6 +93,10 @@ struct DevBuf {
         if (count) HIP_CHECK(hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice));
     }
 };
+
+// AMG_SEGV_BACKTRACE=1: print the native stack on SIGSEGV / SIGABRT (debugging host crashes
+// inside runtime calls); a no-op otherwise
+void install_crash_handler();
 
 struct LoopbackWorld;
 

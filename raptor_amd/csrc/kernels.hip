@@ -303,7 +303,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     const int e1 = a.rend[rr];
     rends[tid] = e1;
     const bool px_tile = TILE && MODE == KM_JACOBI && h1.x >= 0;       // block-uniform
-    const bool pd_tab = VIB && MODE == KM_JACOBI && (h1.y >> 16) != 0;  // block-uniform
+    const bool pd_tab = VIB && MODE == KM_JACOBI && (h1.y & kHdrDvi) != 0;  // block-uniform
     double pb = 0.0, pd = 0.0, px = 0.0;
     int dv = 0;
     if (MODE == KM_SPMV_ADD) px = a.y[rr];
@@ -413,10 +413,12 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
 template <int MODE, bool NORM, bool TILE, bool VIB, int GRPB = 1, bool C16 = false>
 __device__ __forceinline__ double block_dispatch(const CsrArgs& a, int bid, int nnz, double* stage,
                                                  double* tabl, int* rends) {
+    constexpr int RP = (MODE == KM_SPMV || MODE == KM_SPMV_ADD) && !NORM ? GRPB : 1;
     if constexpr (TILE) {
-        return block_main<MODE, NORM, TILE, VIB, 8>(a, bid, stage, tabl, rends);
+        // a tiled short-row P holds up to kTPB * GRPB rows per block: every row is summed
+        // (AMG_CSR_PRE_TILE=0 builds reach this branch)
+        return block_main<MODE, NORM, TILE, VIB, 8, 0, RP>(a, bid, stage, tabl, rends);
     } else {
-        constexpr int RP = (MODE == KM_SPMV || MODE == KM_SPMV_ADD) && !NORM ? GRPB : 1;
         if (nnz > 4 * kTPB) return block_main<MODE, NORM, TILE, VIB, 8, 0, RP, C16>(a, bid, stage, tabl, rends);
         if (nnz > 2 * kTPB) return block_main<MODE, NORM, TILE, VIB, 4, 0, RP, C16>(a, bid, stage, tabl, rends);
         return block_main<MODE, NORM, TILE, VIB, 2, 0, RP, C16>(a, bid, stage, tabl, rends);

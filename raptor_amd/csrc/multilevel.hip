@@ -283,7 +283,15 @@ void Solver::cycle(double* x, const double* b, bool with_norm) {
         RoctxRange r("cycle: hipGraph capture");
         static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
         if (trace) std::fprintf(stderr, "[amg] rank %d capture begin\n", ctx->host.rank);
-        HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        install_crash_handler();
+        // AMG_CAPTURE_MODE=global|relaxed: other capture modes (experiments; default thread-local)
+        static const hipStreamCaptureMode mode = [] {
+            const char* e = std::getenv("AMG_CAPTURE_MODE");
+            if (e && std::string(e) == "global") return hipStreamCaptureModeGlobal;
+            if (e && std::string(e) == "relaxed") return hipStreamCaptureModeRelaxed;
+            return hipStreamCaptureModeThreadLocal;
+        }();
+        HIP_CHECK(hipStreamBeginCapture(s, mode));
         try {
             cycle_rec(0, x, b, false, with_norm);
         } catch (...) {
@@ -295,11 +303,18 @@ void Solver::cycle(double* x, const double* b, bool with_norm) {
         if (trace) std::fprintf(stderr, "[amg] rank %d capture end\n", ctx->host.rank);
         const hipError_t ie = hipGraphInstantiate(&G.exec, g, nullptr, nullptr, 0);
         HIP_CHECK(hipGraphDestroy(g));
-        if (ie != hipSuccess) {
-            // a multi-rank graph the runtime cannot instantiate: replay nothing, run eagerly
-            // from now on (identical results; only the launch overhead differs)
-            AMG_CHECK(ctx->host.nranks > 1, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
-            (void)hipGetLastError();
+        if (ie != hipSuccess) (void)hipGetLastError();
+        AMG_CHECK(ie == hipSuccess || ctx->host.nranks > 1,
+                  std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+        // multi-rank: the ranks decide together (host exchange), so no rank replays a graph
+        // whose RCCL groups a peer runs eagerly
+        bool all_ok = ie == hipSuccess;
+        if (ctx->host.nranks > 1)
+            for (int64_t v : ctx->host.allgather((int64_t)(ie == hipSuccess ? 1 : 0))) all_ok = all_ok && v == 1;
+        if (!all_ok) {
+            // a multi-rank graph some rank's runtime cannot instantiate: replay nothing, run
+            // eagerly from now on (identical results; only the launch overhead differs)
+            if (G.exec) (void)hipGraphExecDestroy(G.exec);
             G.exec = nullptr;
             use_graph = false;
             cycle_rec(0, x, b, false, with_norm);

@@ -796,7 +796,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
             }
             // rectangular (gather) operators: field 0 = the block's offset in the VI index stream
             const int f0 = square ? dslot : tiled ? -1 : (vofs.empty() ? 0 : (int)vofs[q]);
-            hh[2 * q + 1] = make_int4(f0, nt | (dvi_ok[q] ? 1 << 16 : 0), vt_off[q], vt_len[q]);
+            hh[2 * q + 1] = make_int4(f0, nt | (dvi_ok[q] ? kHdrDvi : 0), vt_off[q], vt_len[q]);
         }
         hdr.upload(hh.data(), hh.size());
         // measured (profiles/r1m_variants.txt): x tiles in XCD order on square operators (A0
@@ -1135,6 +1135,12 @@ void DevMatrix::set_format(int f) {
         }
         pcol.upload(pc.data(), pc.size());
         pval.upload(pv.data(), pv.size());
+    }
+    if (f != AMG_FORMAT_CSR) {
+        // the plain arrays (12 B per nonzero) are rebuilt when CSR is selected again; hipFree
+        // waits for the kernels that may still read them
+        pcol.reset();
+        pval.reset();
     }
     if (format != f) ++format_generation;
     format = f;

@@ -1,0 +1,338 @@
+// cxx_driver.cpp -- a compiled C++ caller of the boundary (include/raptor_amd.hpp over
+// include/raptor_amd.h): what a RAPtor-style C++ host code links against.  No Python and no
+// torch in the process, so the library runs on the HIP runtime and RCCL it was built against.
+//
+//   cxx_driver solve  <golden.txt>          7-pt 24^3, PMIS + Jacobi, 1 rank: ParMultilevel::
+//                                           solve history vs the committed oracle history
+//   cxx_driver errors                       C-ABI error codes surface as amg::Error
+//   cxx_driver ranks N [graph] <golden.txt> the same solve on N processes (fork), RCCL halo
+//                                           exchange; "graph": hipGraph-captured cycles
+//
+// Exit status 0 = every check passed.  Multi-rank: the parent forks N children before any HIP
+// call; the setup-time all-to-all-v runs over socketpairs made before the fork (a sender
+// thread per call, so large messages never deadlock); rank 0's RCCL id travels the same way.
+// All ranks share device 0 with their own NCCL_HOSTID (RCCL's socket transport), as in
+// tests/test_gpu_rccl.py; on a multi-GPU node ranks would use devices 0..N-1 and xGMI.
+#include <hip/hip_runtime.h>
+#include <sys/socket.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "raptor_amd.hpp"
+
+namespace {
+
+#define HIPOK(e)                                                                              \
+    do {                                                                                      \
+        hipError_t r_ = (e);                                                                  \
+        if (r_ != hipSuccess) {                                                               \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #e, hipGetErrorString(r_)); \
+            std::exit(3);                                                                     \
+        }                                                                                     \
+    } while (0)
+
+std::vector<double> read_golden(const char* path) {
+    std::vector<double> v;
+    FILE* f = std::fopen(path, "r");
+    if (!f) {
+        std::fprintf(stderr, "cannot open %s\n", path);
+        std::exit(2);
+    }
+    char line[256];
+    while (std::fgets(line, sizeof line, f))
+        if (line[0] != '#' && line[0] != '\n') v.push_back(std::strtod(line, nullptr));
+    std::fclose(f);
+    return v;
+}
+
+// history vs golden: relative 1e-10 per entry (BASELINE.json:5 residual match)
+bool compare(const std::vector<double>& h, const std::vector<double>& g, const char* who) {
+    if (h.size() != g.size()) {
+        std::fprintf(stderr, "%s: %zu norms, golden has %zu\n", who, h.size(), g.size());
+        return false;
+    }
+    bool ok = true;
+    for (size_t k = 0; k < h.size(); ++k) {
+        const double rel = std::fabs(h[k] - g[k]) / g[k];
+        if (!(rel <= 1e-10)) {
+            std::fprintf(stderr, "%s: norm %zu = %.17g, golden %.17g (rel %.3g)\n", who, k, h[k], g[k], rel);
+            ok = false;
+        }
+    }
+    return ok;
+}
+
+// one rank: 7-pt 24^3 slab, b = A x*, x0 = 0, 10 V-cycles; returns the history
+std::vector<double> solve_7pt(amg::Context& ctx, bool graph, int* levels, bool* graph_used) {
+    amg::ParCSRMatrix A = amg::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 24, 24, 24);
+    const int64_t n = A.local_rows(), f = A.first_row();
+    amg::ParMultilevel ml(A, amg::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
+    if (graph) ml.set_graph(true);
+    const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
+    if (trace) std::fprintf(stderr, "[cxx] rows %lld setup done (%d levels)\n", (long long)n, ml.num_levels());
+    double *xs = nullptr, *b = nullptr, *x = nullptr;
+    HIPOK(hipMalloc(&xs, n * sizeof(double)));
+    HIPOK(hipMalloc(&b, n * sizeof(double)));
+    HIPOK(hipMalloc(&x, n * sizeof(double)));
+    ctx.uniform(n, f, 42, xs);  // x* on the global ids of this rank's rows
+    A.mult(xs, b);
+    HIPOK(hipMemsetAsync(x, 0, n * sizeof(double), (hipStream_t)ctx.stream()));
+    if (trace) std::fprintf(stderr, "[cxx] b = A x* done\n");
+    std::vector<double> hist = ml.solve(x, b, 10);
+    if (trace) std::fprintf(stderr, "[cxx] solve done\n");
+    *levels = ml.num_levels();
+    *graph_used = ml.graph();
+    ctx.synchronize();
+    HIPOK(hipFree(xs));
+    HIPOK(hipFree(b));
+    HIPOK(hipFree(x));
+    return hist;
+}
+
+int run_solve(const char* golden) {
+    const std::vector<double> g = read_golden(golden);
+    amg::Context ctx(0);
+    int levels = 0;
+    bool used = false;
+    const std::vector<double> h = solve_7pt(ctx, false, &levels, &used);
+    for (size_t k = 0; k < h.size(); ++k) std::printf("%zu %.17g\n", k, h[k]);
+    if (!used) {  // one rank: cycles replay a hipGraph by default
+        std::fprintf(stderr, "expected hipGraph replay on one rank\n");
+        return 1;
+    }
+    return compare(h, g, "1 rank") && h.back() < 0.01 * h.front() ? 0 : 1;
+}
+
+int run_errors() {
+    amg::Context ctx(0);
+    int fails = 0;
+    // row_ptr[0] != 0 is rejected with AMG_ERR_INVALID, the message naming the problem
+    const int64_t rp[3] = {1, 2, 3}, col[3] = {0, 1, 0};
+    const double val[3] = {1.0, 1.0, 1.0};
+    try {
+        amg::ParCSRMatrix bad(ctx, 2, 0, 2, rp, col, val);
+        std::fprintf(stderr, "bad row_ptr accepted\n");
+        ++fails;
+    } catch (const amg::Error& e) {
+        if (e.code() != AMG_ERR_INVALID || std::string(e.what()).find("row_ptr") == std::string::npos) {
+            std::fprintf(stderr, "unexpected error %d: %s\n", e.code(), e.what());
+            ++fails;
+        }
+    }
+    // duplicate column in a row
+    const int64_t rp2[3] = {0, 2, 3}, col2[3] = {1, 1, 1};
+    try {
+        amg::ParCSRMatrix bad(ctx, 2, 0, 2, rp2, col2, val);
+        std::fprintf(stderr, "duplicate column accepted\n");
+        ++fails;
+    } catch (const amg::Error& e) {
+        if (e.code() != AMG_ERR_INVALID) ++fails;
+    }
+    // a valid 2x2 matrix: y = A x
+    const int64_t rp3[3] = {0, 2, 4}, col3[4] = {0, 1, 0, 1};
+    const double val3[4] = {2.0, -1.0, -1.0, 2.0};
+    amg::ParCSRMatrix A(ctx, 2, 0, 2, rp3, col3, val3);
+    double hx[2] = {1.0, 3.0}, hy[2] = {0.0, 0.0};
+    double *dx = nullptr, *dy = nullptr;
+    HIPOK(hipMalloc(&dx, sizeof hx));
+    HIPOK(hipMalloc(&dy, sizeof hy));
+    HIPOK(hipMemcpy(dx, hx, sizeof hx, hipMemcpyHostToDevice));
+    A.mult(dx, dy);
+    ctx.synchronize();
+    HIPOK(hipMemcpy(hy, dy, sizeof hy, hipMemcpyDeviceToHost));
+    if (hy[0] != -1.0 || hy[1] != 5.0) {
+        std::fprintf(stderr, "y = (%g, %g), expected (-1, 5)\n", hy[0], hy[1]);
+        ++fails;
+    }
+    HIPOK(hipFree(dx));
+    HIPOK(hipFree(dy));
+    std::printf("errors: %d failures\n", fails);
+    return fails ? 1 : 0;
+}
+
+// ---- multi-rank over socketpairs -------------------------------------------------------
+
+struct Mesh {
+    int rank = 0, nranks = 1;
+    std::vector<int> fd;  // fd[q]: this rank's end of the socketpair to rank q (-1 for self)
+};
+
+bool write_all(int fd, const char* p, int64_t n) {
+    while (n > 0) {
+        const ssize_t w = ::write(fd, p, (size_t)std::min<int64_t>(n, 1 << 20));
+        if (w <= 0) return false;
+        p += w, n -= w;
+    }
+    return true;
+}
+
+bool read_all(int fd, char* p, int64_t n) {
+    while (n > 0) {
+        const ssize_t r = ::read(fd, p, (size_t)std::min<int64_t>(n, 1 << 20));
+        if (r <= 0) return false;
+        p += r, n -= r;
+    }
+    return true;
+}
+
+// amg_alltoallv_fn: a sender thread writes every outgoing block while this thread reads the
+// incoming ones, so no pair of ranks blocks on full socket buffers
+int mesh_alltoallv(void* user, const void* sendbuf, const int64_t* send_bytes, void* recvbuf,
+                   const int64_t* recv_bytes) {
+    Mesh& m = *(Mesh*)user;
+    const char* s = (const char*)sendbuf;
+    char* r = (char*)recvbuf;
+    std::vector<int64_t> so(m.nranks + 1, 0), ro(m.nranks + 1, 0);
+    for (int q = 0; q < m.nranks; ++q) so[q + 1] = so[q] + send_bytes[q], ro[q + 1] = ro[q] + recv_bytes[q];
+    bool sent = true;
+    std::thread tx([&] {
+        for (int q = 0; q < m.nranks; ++q)
+            if (q != m.rank && send_bytes[q] > 0) sent = sent && write_all(m.fd[q], s + so[q], send_bytes[q]);
+    });
+    bool got = true;
+    for (int q = 0; q < m.nranks; ++q) {
+        if (q == m.rank) {
+            if (send_bytes[q] != recv_bytes[q]) got = false;
+            else if (recv_bytes[q] > 0) std::memcpy(r + ro[q], s + so[q], (size_t)recv_bytes[q]);
+        } else if (recv_bytes[q] > 0) {
+            got = got && read_all(m.fd[q], r + ro[q], recv_bytes[q]);
+        }
+    }
+    tx.join();
+    return sent && got ? 0 : 1;
+}
+
+int rank_main(Mesh& m, bool graph, const char* golden, int result_fd) {
+    // RCCL refuses two ranks of one host on one device: each rank is its own "host" (socket
+    // transport), as in tests/test_gpu_rccl.py
+    const std::string hostid = "raptor-amd-cxx-" + std::to_string(m.rank);
+    setenv("NCCL_HOSTID", hostid.c_str(), 1);
+    amg::Context ctx(0);
+    std::vector<char> id(128);
+    if (m.rank == 0) {
+        id = amg::Context::rccl_unique_id();
+        for (int q = 1; q < m.nranks; ++q)
+            if (!write_all(m.fd[q], id.data(), 128)) return 4;
+    } else if (!read_all(m.fd[0], id.data(), 128)) {
+        return 4;
+    }
+    ctx.set_comm(m.rank, m.nranks, id.data(), mesh_alltoallv, &m);
+    int levels = 0;
+    bool used = false;
+    const std::vector<double> h = solve_7pt(ctx, graph, &levels, &used);
+    const int64_t cnt = (int64_t)h.size();
+    const char flag = used ? 1 : 0;
+    if (!write_all(result_fd, (const char*)&cnt, sizeof cnt) ||
+        !write_all(result_fd, (const char*)h.data(), cnt * (int64_t)sizeof(double)) ||
+        !write_all(result_fd, &flag, 1))
+        return 5;
+    (void)golden;
+    return 0;
+}
+
+int run_ranks(int nranks, bool graph, const char* golden) {
+    const std::vector<double> g = read_golden(golden);
+    // full mesh of socketpairs, plus one result pipe per rank, all before any HIP call
+    std::vector<std::vector<int>> fds(nranks, std::vector<int>(nranks, -1));
+    for (int a = 0; a < nranks; ++a)
+        for (int b = a + 1; b < nranks; ++b) {
+            int sv[2];
+            if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) return 2;
+            fds[a][b] = sv[0];
+            fds[b][a] = sv[1];
+        }
+    std::vector<int> res_rd(nranks), pids(nranks);
+    for (int r = 0; r < nranks; ++r) {
+        int p[2];
+        if (pipe(p) != 0) return 2;
+        const pid_t pid = fork();
+        if (pid < 0) return 2;
+        if (pid == 0) {
+            close(p[0]);
+            Mesh m;
+            m.rank = r;
+            m.nranks = nranks;
+            m.fd = fds[r];
+            for (int a = 0; a < nranks; ++a)  // keep only this rank's ends
+                for (int b = 0; b < nranks; ++b)
+                    if (a != r && fds[a][b] >= 0) close(fds[a][b]);
+            int rc = 6;
+            try {
+                rc = rank_main(m, graph, golden, p[1]);
+            } catch (const amg::Error& e) {
+                std::fprintf(stderr, "rank %d: %s\n", r, e.what());
+            }
+            close(p[1]);
+            std::fflush(stdout);
+            _exit(rc);
+        }
+        close(p[1]);
+        res_rd[r] = p[0];
+        pids[r] = pid;
+    }
+    for (auto& row : fds)
+        for (int f : row)
+            if (f >= 0) close(f);
+    bool ok = true;
+    std::vector<std::vector<double>> hs(nranks);
+    for (int r = 0; r < nranks; ++r) {
+        int64_t cnt = 0;
+        char flag = 0;
+        if (!read_all(res_rd[r], (char*)&cnt, sizeof cnt) || cnt <= 0 || cnt > 1024) {
+            ok = false;
+        } else {
+            hs[r].resize((size_t)cnt);
+            ok = read_all(res_rd[r], (char*)hs[r].data(), cnt * (int64_t)sizeof(double)) &&
+                 read_all(res_rd[r], &flag, 1) && ok;
+            if (graph && !flag) {
+                std::fprintf(stderr, "rank %d fell back to eager cycles\n", r);
+                ok = false;
+            }
+        }
+        close(res_rd[r]);
+    }
+    for (int r = 0; r < nranks; ++r) {
+        int st = 0;
+        waitpid(pids[r], &st, 0);
+        if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+            std::fprintf(stderr, "rank %d: exit status %d (signal %d)\n", r, WIFEXITED(st) ? WEXITSTATUS(st) : -1,
+                         WIFSIGNALED(st) ? WTERMSIG(st) : 0);
+            ok = false;
+        }
+    }
+    if (!ok) return 1;
+    for (int r = 0; r < nranks; ++r) {
+        if (hs[r] != hs[0]) {  // every rank reports the same history, bit for bit
+            std::fprintf(stderr, "rank %d history differs from rank 0\n", r);
+            ok = false;
+        }
+    }
+    // PMIS + Jacobi is partition independent: the N-rank history is the 1-rank one (norms
+    // reduced in rank order: 1e-10)
+    ok = ok && compare(hs[0], g, "N ranks");
+    for (size_t k = 0; k < hs[0].size(); ++k) std::printf("%zu %.17g\n", k, hs[0][k]);
+    return ok ? 0 : 1;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc >= 3 && std::string(argv[1]) == "solve") return run_solve(argv[2]);
+    if (argc >= 2 && std::string(argv[1]) == "errors") return run_errors();
+    if (argc >= 4 && std::string(argv[1]) == "ranks") {
+        const int n = std::atoi(argv[2]);
+        const bool graph = argc >= 5 && std::string(argv[3]) == "graph";
+        if (n < 1 || n > 16) return 2;
+        return run_ranks(n, graph, argv[argc - 1]);
+    }
+    std::fprintf(stderr, "usage: %s solve <golden> | errors | ranks N [graph] <golden>\n", argv[0]);
+    return 2;
+}
