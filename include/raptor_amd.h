@@ -282,6 +282,10 @@ int amg_vector_uniform(amg_context ctx, int64_t n, int64_t first_gid, uint64_t s
 /* dst = src on the context stream (16-byte nontemporal copy kernel; 16-byte aligned device
  * pointers).  bench.py times it as the box's STREAM-copy ceiling. */
 int amg_vector_copy(amg_context ctx, int64_t n, const double* src, double* dst);
+/* One read pass over src (16-byte loads, as amg_vector_copy without the stores), per-wave
+ * partial sums into partials[n_partials] (n_partials >= 4 * ceil(n / 2048)).  bench.py times
+ * it as the box's read-bandwidth ceiling: most level kernels read far more than they write. */
+int amg_vector_read(amg_context ctx, int64_t n, const double* src, double* partials, int64_t n_partials);
 
 #ifdef __cplusplus
 }

@@ -1067,3 +1067,11 @@ int32_t orc_num_threads(void) {
     return 1;
 #endif
 }
+
+void orc_set_num_threads(int32_t n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads((int)n);
+#else
+    (void)n;
+#endif
+}

@@ -112,6 +112,7 @@ const orc_csr* orc_hier_matrix(const orc_hier* H, int32_t level, int32_t which);
 void orc_hier_split(const orc_hier* H, int32_t level, int32_t* out);
 void orc_hier_cycle(orc_hier* H, double* x, const double* b);
 int32_t orc_num_threads(void); /* OpenMP threads the level kernels use */
+void orc_set_num_threads(int32_t n); /* OpenMP team size of later parallel regions (n > 0) */
 int32_t orc_hier_solve(orc_hier* H, double* x, const double* b, int32_t max_iter, double tol,
                        double* hist);
 /* CG preconditioned by one V-cycle (z = 0; cycle(z, r)) per iteration (row f3). */

@@ -94,6 +94,7 @@ def lib():
                                           C.POINTER(vp), C.POINTER(_Opt)]),
             "orc_hier_levels": (C.c_int32, [vp]),
             "orc_num_threads": (C.c_int32, []),
+            "orc_set_num_threads": (None, [C.c_int32]),
             "orc_hier_pcg": (C.c_int32, [vp, _f64p, _f64p, C.c_int32, C.c_double, _f64p]),
             "orc_hier_matrix": (vp, [vp, C.c_int32, C.c_int32]),
             "orc_hier_split": (None, [vp, C.c_int32, _i32p]),

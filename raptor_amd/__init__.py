@@ -352,6 +352,13 @@ def vector_copy(ctx: Context, src, dst):
     return dst
 
 
+def vector_read(ctx: Context, src, partials):
+    """One read pass over src (16-byte loads) leaving per-wave partial sums in `partials`
+    (>= 4 * ceil(n / 2048) entries): the bench's read-bandwidth ceiling."""
+    check(lib().amg_vector_read(ctx.h, int(src.numel()), _ptr(src), _ptr(partials), int(partials.numel())))
+    return partials
+
+
 def vector_uniform(ctx: Context, n: int, first_gid: int = 0, seed: int = 42):
     """Device vector u_i = uniform(-1, 1) of splitmix64(seed, first_gid + i)."""
     out = ctx.empty(n)

@@ -139,6 +139,7 @@ SIGNATURES = {
     "amg_solver_destroy": (C.c_int, [_vp]),
     "amg_vector_uniform": (C.c_int, [_vp, _i64, _i64, C.c_uint64, _vp]),
     "amg_vector_copy": (C.c_int, [_vp, _i64, _vp, _vp]),
+    "amg_vector_read": (C.c_int, [_vp, _i64, _vp, _vp, _i64]),
     "amg_host_hierarchy_build": (C.c_int, [C.c_int, C.c_int, ALLTOALLV_FN, _vp, _i64, _i64, _i64,
                                            _pi64, _pi64, _pf64, C.POINTER(Options),
                                            C.POINTER(_vp)]),

@@ -773,6 +773,16 @@ int amg_vector_copy(amg_context ctx, int64_t n, const double* src, double* dst) 
     });
 }
 
+int amg_vector_read(amg_context ctx, int64_t n, const double* src, double* partials, int64_t n_partials) {
+    return guard([&] {
+        AMG_CHECK(ctx && n >= 0, "bad argument");
+        AMG_CHECK(n == 0 || (src && partials), "null vector");
+        AMG_CHECK(n_partials >= read_partials(n), "read: too few partial slots");
+        set_device(ctx->c);
+        launch_read(ctx->c.stream, n, src, partials);
+    });
+}
+
 int amg_vector_uniform(amg_context ctx, int64_t n, int64_t first_gid, uint64_t seed, double* out) {
     return guard([&] {
         AMG_CHECK(ctx && (out || n == 0), "null argument");

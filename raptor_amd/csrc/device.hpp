@@ -309,6 +309,10 @@ void launch_csr_plain(hipStream_t s, int mode, bool norm, const DevMatrix& A, co
                       const double* b, double* y, double omega, double* partial);
 // dst = src (16-byte nontemporal copy kernel; the bench's STREAM-copy ceiling)
 void launch_copy(hipStream_t s, int64_t n, const double* src, double* dst);
+// one read pass over src (16-byte loads), per-wave partial sums into part[read_partials(n)]
+// (the bench's read-bandwidth ceiling)
+int64_t read_partials(int64_t n);
+void launch_read(hipStream_t s, int64_t n, const double* src, double* part);
 int tpl_march_chunk_cap();
 void launch_jacobi_zero(hipStream_t s, int64_t n, const double* b, const double* dinv, double* y,
                         double omega);

@@ -640,6 +640,27 @@ __global__ __launch_bounds__(kTPB) void copy_kernel(long long npair, const v2d_t
     }
 }
 
+// READ ceiling (bench.py): the copy kernel's access pattern with the stores dropped -- one pass
+// of 16-byte loads, 4 pairs per lane, one partial sum per workgroup (so the loads are live).
+// Most level kernels read 5-20x what they write, so the read rate, not the copy rate, is the
+// ceiling they approach.
+__global__ __launch_bounds__(kTPB) void read_kernel(long long npair, const v2d_t* __restrict__ src,
+                                                     double* __restrict__ part) {
+    const long long i = (long long)blockIdx.x * 4 * kTPB + threadIdx.x;
+    double s = 0.0;
+    if (i + 3 * kTPB < npair) {
+        v2d_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + i + u * kTPB);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s += v[u].x + v[u].y;
+    } else {
+        for (long long k = i; k < npair; k += kTPB) s += src[k].x + src[k].y;
+    }
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) part[(long long)blockIdx.x * 4 + (threadIdx.x >> 6)] = s;
+}
+
 // Row-template kernel.  A templated row is (column - row) offsets, values and
 // 1/a_ii shared with every row of the same shape -- for a constant-coefficient stencil a few
 // dozen templates cover the operator -- so the kernel streams 1 byte per row (its template
@@ -2035,6 +2056,18 @@ void launch_csr_plain(hipStream_t s, int mode, bool norm, const DevMatrix& A, co
         default: throw Error(AMG_ERR_INTERNAL, "bad kernel mode");
     }
 #undef AMG_PL
+    HIP_CHECK(hipGetLastError());
+}
+
+int64_t read_partials(int64_t n) { return std::max<int64_t>(1, (n / 2 + 4 * kTPB - 1) / (4 * kTPB)) * 4; }
+
+void launch_read(hipStream_t s, int64_t n, const double* src, double* part) {
+    AMG_CHECK(((uintptr_t)src & 15) == 0, "read: 16-byte aligned vector");
+    const long long np = n / 2;
+    if (np <= 0) return;
+    const long long g = (np + 4 * kTPB - 1) / (4 * kTPB);
+    AMG_CHECK(g < INT_MAX, "read: vector too long");
+    hipLaunchKernelGGL(read_kernel, dim3((unsigned)g), dim3(kTPB), 0, s, np, (const v2d_t*)src, part);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -43,7 +43,11 @@ struct LoopbackWorld {
             cv.notify_all();
             return;
         }
-        if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g; }))
+        // AMG_LOOPBACK_TIMEOUT (seconds, default 120): full-size runs (512^3 over 8 ranks)
+        // spend minutes in the host setup between two collectives
+        const char* e = std::getenv("AMG_LOOPBACK_TIMEOUT");
+        const int secs = e && std::atoi(e) > 0 ? std::atoi(e) : 120;
+        if (!cv.wait_for(lk, std::chrono::seconds(secs), [&] { return gen != g; }))
             throw Error(AMG_ERR_COMM, "loopback barrier timed out (a peer rank failed?)");
     }
 };

@@ -51,11 +51,41 @@ __device__ __forceinline__ int dfind(const int* cols, int lo, int hi, int c) {
     return -1;
 }
 
+// rows of this rank: local row i is global row lo + i; columns are GLOBAL ids (int32: the
+// global size is checked < 2^31), ascending per row -- the host image's order, so every
+// loop below visits entries exactly as host_setup.cpp does
 struct DCsr {
     const int* rp;
     const int* col;
     const double* val;
     int n;
+    int lo;
+};
+
+// where the state of global point g lives: local rows [lo, lo + n) or the sorted halo ids
+// gid[0, nh) (several ranks: states forwarded from their owners each round)
+struct Dist {
+    int lo, n;
+    const int* gid;
+    int nh;
+    // >= 0: local index; < 0: halo index -(t + 1); INT_MIN: neither
+    __device__ __forceinline__ int loc(int g) const {
+        if (g >= lo && g < lo + n) return g - lo;
+        int a = 0, b = nh;
+        while (a < b) {
+            const int m = (a + b) >> 1;
+            const int v = gid[m];
+            if (v == g) return -m - 1;
+            if (v < g) a = m + 1;
+            else b = m;
+        }
+        return INT_MIN;
+    }
+    template <class T>
+    __device__ __forceinline__ T get(const T* local, const T* halo, int g) const {
+        const int l = loc(g);
+        return l >= 0 ? local[l] : halo[-l - 1];
+    }
 };
 
 // ---- strength ------------------------------------------------------------------------
@@ -68,8 +98,9 @@ __global__ void strength_classical_kernel(DCsr A, double theta, int* cnt, const 
     if (i >= A.n) return;
     double mx = 0.0;
     bool any = false;
+    const int gi = A.lo + i;
     for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) {
-        if (A.col[k] == i) continue;
+        if (A.col[k] == gi) continue;
         const double v = -A.val[k];
         if (!any || v > mx) mx = v;
         any = true;
@@ -78,7 +109,7 @@ __global__ void strength_classical_kernel(DCsr A, double theta, int* cnt, const 
     const double thr = theta * mx;
     int q = FILL ? srp[i] : 0, c = 0;
     for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) {
-        if (!(has && A.col[k] != i && -A.val[k] >= thr)) continue;
+        if (!(has && A.col[k] != gi && -A.val[k] >= thr)) continue;
         if (FILL) {
             scol[q] = A.col[k];
             sval[q++] = A.val[k];
@@ -94,7 +125,7 @@ __global__ void diagonal_kernel(DCsr A, double* d) {
     if (i >= A.n) return;
     double v = 0.0;
     for (int k = A.rp[i]; k < A.rp[i + 1]; ++k)
-        if (A.col[k] == i) {
+        if (A.col[k] == A.lo + i) {
             v = A.val[k];
             break;
         }
@@ -122,49 +153,79 @@ __global__ void strength_symmetric_kernel(DCsr A, const double* d, double theta,
 }
 
 // ---- PMIS ------------------------------------------------------------------------------
+// |S^T_i| over this rank's rows: local columns only (off-rank dependents arrive as pairs)
 __global__ void col_count_kernel(DCsr S, int* tcnt) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= S.n) return;
-    for (int k = S.rp[i]; k < S.rp[i + 1]; ++k) atomicAdd(&tcnt[S.col[k]], 1);
+    for (int k = S.rp[i]; k < S.rp[i + 1]; ++k) {
+        const int c = S.col[k] - S.lo;
+        if (c >= 0 && c < S.n) atomicAdd(&tcnt[c], 1);
+    }
 }
 
-// S^T adjacency (row j of S^T = the rows i with j in S_i; order within a row arbitrary --
-// PMIS only takes maxima over the set)
+// S^T adjacency of the local-local part (row j of S^T = the global ids of local rows i with
+// j in S_i; order within a row arbitrary -- PMIS only takes maxima over the set)
 __global__ void transpose_fill_kernel(DCsr S, int* cursor, int* tcol) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= S.n) return;
-    for (int k = S.rp[i]; k < S.rp[i + 1]; ++k) tcol[atomicAdd(&cursor[S.col[k]], 1)] = i;
+    for (int k = S.rp[i]; k < S.rp[i + 1]; ++k) {
+        const int c = S.col[k] - S.lo;
+        if (c >= 0 && c < S.n) tcol[atomicAdd(&cursor[c], 1)] = S.lo + i;
+    }
 }
 
-__global__ void pmis_init_kernel(int n, const int* tcnt, unsigned long long seed,
+// entries of S whose column lives on another rank: (column, dependent row) pairs, row order
+template <bool FILL>
+__global__ void offrank_kernel(DCsr S, int* cnt, const int* orp, int* pc, int* pj) {
+    const int i = blockIdx.x * kT + threadIdx.x;
+    if (i >= S.n) return;
+    int q = FILL ? orp[i] : 0, c = 0;
+    for (int k = S.rp[i]; k < S.rp[i + 1]; ++k) {
+        const int g = S.col[k];
+        if (g >= S.lo && g < S.lo + S.n) continue;
+        if (FILL) {
+            pc[q] = g;
+            pj[q++] = S.lo + i;
+        }
+        ++c;
+    }
+    if (!FILL) cnt[i] = c;
+}
+
+// key = |S^T_i| << 32 | hash32(global id): tcnt = local dependents, ecnt = off-rank ones
+__global__ void pmis_init_kernel(int n, int lo, const int* tcnt, const int* erp, unsigned long long seed,
                                  unsigned long long* key, int* cf) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= n) return;
-    key[i] = ((unsigned long long)tcnt[i] << 32) | (unsigned long long)dhash32(i, seed);
-    cf[i] = tcnt[i] == 0 ? ST_F : ST_U;
+    const int c = tcnt[i] + (erp ? erp[i + 1] - erp[i] : 0);
+    key[i] = ((unsigned long long)c << 32) | (unsigned long long)dhash32(lo + i, seed);
+    cf[i] = c == 0 ? ST_F : ST_U;
 }
 
-// undecided i -> C iff its (key, id) beats every undecided j in S_i u S^T_i
-__global__ void pmis_select_kernel(DCsr S, const int* trp, const int* tcol,
-                                   const unsigned long long* key, const int* cf, unsigned char* newc) {
+// undecided i -> C iff its (key, global id) beats every undecided j in S_i u S^T_i (local
+// dependents tcol, off-rank dependents ecol); halo states / keys through D
+__global__ void pmis_select_kernel(DCsr S, Dist D, const int* trp, const int* tcol, const int* erp,
+                                   const int* ecol, const unsigned long long* key,
+                                   const unsigned long long* hkey, const int* cf, const int* hcf,
+                                   unsigned char* newc) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= S.n) return;
     newc[i] = 0;
     if (cf[i] != ST_U) return;
     const unsigned long long ki = key[i];
+    const int gi = S.lo + i;
     bool best = true;
-    for (int k = S.rp[i]; k < S.rp[i + 1] && best; ++k) {
-        const int j = S.col[k];
-        if (cf[j] != ST_U) continue;
-        const unsigned long long kj = key[j];
-        if (kj > ki || (kj == ki && j > i)) best = false;
-    }
-    for (int t = trp[i]; t < trp[i + 1] && best; ++t) {
-        const int j = tcol[t];
-        if (cf[j] != ST_U) continue;
-        const unsigned long long kj = key[j];
-        if (kj > ki || (kj == ki && j > i)) best = false;
-    }
+    auto beats = [&](int g) {  // false when undecided neighbour g outranks i
+        const int l = D.loc(g);
+        const int sj = l >= 0 ? cf[l] : hcf[-l - 1];
+        if (sj != ST_U) return true;
+        const unsigned long long kj = l >= 0 ? key[l] : hkey[-l - 1];
+        return !(kj > ki || (kj == ki && g > gi));
+    };
+    for (int k = S.rp[i]; k < S.rp[i + 1] && best; ++k) best = beats(S.col[k]);
+    for (int t = trp[i]; t < trp[i + 1] && best; ++t) best = beats(tcol[t]);
+    if (erp)
+        for (int t = erp[i]; t < erp[i + 1] && best; ++t) best = beats(ecol[t]);
     newc[i] = best;
 }
 
@@ -174,30 +235,58 @@ __global__ void pmis_apply_kernel(int n, const unsigned char* newc, int* cf) {
 }
 
 // undecided i with a C point in S_i -> F; count the undecided that remain
-__global__ void pmis_fpass_kernel(DCsr S, int* cf, unsigned long long* nu) {
+__global__ void pmis_fpass_kernel(DCsr S, Dist D, int* cf, const int* hcf, unsigned long long* nu) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= S.n || cf[i] != ST_U) return;
     for (int k = S.rp[i]; k < S.rp[i + 1]; ++k)
-        if (cf[S.col[k]] == ST_C) {
+        if (D.get(cf, hcf, S.col[k]) == ST_C) {
             cf[i] = ST_F;
             return;
         }
     atomicAdd(nu, 1ull);
 }
 
+// halo forwarding: packed[t] = local[send_idx[t]]
+template <class T>
+__global__ void pack_kernel_t(int n, const int* idx, const T* local, T* packed) {
+    const int t = blockIdx.x * kT + threadIdx.x;
+    if (t < n) packed[t] = local[idx[t]];
+}
+
 // ---- classical interpolation ------------------------------------------------------------
-// is j a strong neighbour of i (S rows ascending)
+// is global j a strong neighbour of local row i (S rows ascending)
 __device__ __forceinline__ bool strong(const DCsr& S, int i, int j) {
     return dfind(S.col, S.rp[i], S.rp[i + 1], j) >= 0;
 }
+
+// rows of A reachable from this rank: local rows, and the ghost rows of the halo points
+// (D's halo = A's off-rank columns; ghost row t of halo point D.gid[t], global column ids)
+struct ARows {
+    DCsr A;
+    Dist D;
+    const int* grp;
+    const int* gcol;
+    const double* gval;
+    __device__ __forceinline__ void row(int g, int& b, int& e, const int*& c, const double*& v) const {
+        const int l = D.loc(g);
+        if (l >= 0) {
+            b = A.rp[l], e = A.rp[l + 1], c = A.col, v = A.val;
+        } else {
+            const int t = -l - 1;
+            b = grp[t], e = grp[t + 1], c = gcol, v = gval;
+        }
+    }
+};
 
 // F row i: d = a_ii + weak couplings + couplings to strong F neighbours whose s_k is 0;
 // w_ij = -num_j / d for j in C_i (strong C neighbours), num_j = a_ij + sum over strong F
 // neighbours k (A-row order) of (a_ik a_kj) / s_k, s_k = sum of row k's couplings to C_i of
 // sign opposite to a_kk.  Same loops and order as host_setup.cpp interp_classical().
+// cf / cmap of halo points through R.D (hcf, hcmap); P columns are global coarse ids.
 template <bool FILL>
-__global__ void interp_kernel(DCsr A, DCsr S, const int* cf, const int* cmap, int* cnt, const int* prp,
-                              int* pcol, double* pval) {
+__global__ void interp_kernel(ARows R, DCsr S, const int* cf, const int* hcf, const int* cmap,
+                              const int* hcmap, int* cnt, const int* prp, int* pcol, double* pval) {
+    const DCsr& A = R.A;
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= A.n) return;
     if (cf[i] == ST_C) {
@@ -209,19 +298,22 @@ __global__ void interp_kernel(DCsr A, DCsr S, const int* cf, const int* cmap, in
         }
         return;
     }
-    auto in_ci = [&](int m) { return m != i && cf[m] == ST_C && strong(S, i, m); };
+    const int gi = A.lo + i;
+    // strong first: a strong neighbour is a column of row i, so its state is local or halo
+    auto is_c = [&](int g) { return R.D.get(cf, hcf, g) == ST_C; };
+    auto in_ci = [&](int m) { return m != gi && strong(S, i, m) && is_c(m); };
     double d = 0.0;
     for (int k = A.rp[i]; k < A.rp[i + 1]; ++k)
-        if (A.col[k] == i) {
+        if (A.col[k] == gi) {
             d = A.val[k];
             break;
         }
     int nci = 0;
     for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) {
         const int j = A.col[k];
-        if (j == i) continue;
+        if (j == gi) continue;
         const bool st = strong(S, i, j);
-        if (st && cf[j] == ST_C) ++nci;
+        if (st && is_c(j)) ++nci;
         else if (!st) d += A.val[k];
     }
     if (!FILL) {
@@ -229,23 +321,32 @@ __global__ void interp_kernel(DCsr A, DCsr S, const int* cf, const int* cmap, in
         return;
     }
     if (nci == 0) return;
+    // s_k of strong F neighbour kk over its row (local or ghost)
+    auto s_of = [&](int kk, bool& pos) {
+        int b, e;
+        const int* rc;
+        const double* rv;
+        R.row(kk, b, e, rc, rv);
+        double akk = 0.0;
+        for (int u = b; u < e; ++u)
+            if (rc[u] == kk) {
+                akk = rv[u];
+                break;
+            }
+        pos = akk > 0.0;
+        double s = 0.0;
+        for (int u = b; u < e; ++u) {
+            const double v = rv[u];
+            if ((pos ? v < 0.0 : v > 0.0) && in_ci(rc[u])) s += v;
+        }
+        return s;
+    };
     // s_k == 0 neighbours add a_ik to d, in A-row order (second pass of the host loop)
     for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) {
         const int kk = A.col[k];
-        if (kk == i || cf[kk] == ST_C || !strong(S, i, kk)) continue;
-        double akk = 0.0;
-        for (int u = A.rp[kk]; u < A.rp[kk + 1]; ++u)
-            if (A.col[u] == kk) {
-                akk = A.val[u];
-                break;
-            }
-        const bool pos = akk > 0.0;
-        double s = 0.0;
-        for (int u = A.rp[kk]; u < A.rp[kk + 1]; ++u) {
-            const double v = A.val[u];
-            if ((pos ? v < 0.0 : v > 0.0) && in_ci(A.col[u])) s += v;
-        }
-        if (s == 0.0) d += A.val[k];
+        if (kk == gi || !strong(S, i, kk) || is_c(kk)) continue;
+        bool pos;
+        if (s_of(kk, pos) == 0.0) d += A.val[k];
     }
     // num_j accumulates in this row's own P slots (pval), k outer: s_k is formed once per
     // strong F neighbour instead of once per (j, k) pair, and every num_j still receives its
@@ -254,32 +355,26 @@ __global__ void interp_kernel(DCsr A, DCsr S, const int* cf, const int* cmap, in
     int q = q0;
     for (int kj = A.rp[i]; kj < A.rp[i + 1]; ++kj) {
         const int j = A.col[kj];
-        if (j == i || cf[j] != ST_C || !strong(S, i, j)) continue;
-        pcol[q] = cmap[j];
+        if (j == gi || !strong(S, i, j) || !is_c(j)) continue;
+        pcol[q] = R.D.get(cmap, hcmap, j);
         pval[q++] = A.val[kj];
     }
     for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) {
         const int kk = A.col[k];
-        if (kk == i || cf[kk] == ST_C || !strong(S, i, kk)) continue;
-        double akk = 0.0;
-        for (int u = A.rp[kk]; u < A.rp[kk + 1]; ++u)
-            if (A.col[u] == kk) {
-                akk = A.val[u];
-                break;
-            }
-        const bool pos = akk > 0.0;
-        double s = 0.0;
-        for (int u = A.rp[kk]; u < A.rp[kk + 1]; ++u) {
-            const double v = A.val[u];
-            if ((pos ? v < 0.0 : v > 0.0) && in_ci(A.col[u])) s += v;
-        }
+        if (kk == gi || !strong(S, i, kk) || is_c(kk)) continue;
+        bool pos;
+        const double s = s_of(kk, pos);
         if (s == 0.0) continue;
+        int b, e;
+        const int* rc;
+        const double* rv;
+        R.row(kk, b, e, rc, rv);
         q = q0;
         for (int kj = A.rp[i]; kj < A.rp[i + 1]; ++kj) {
             const int j = A.col[kj];
-            if (j == i || cf[j] != ST_C || !strong(S, i, j)) continue;
-            const int uj = dfind(A.col, A.rp[kk], A.rp[kk + 1], j);
-            if (uj >= 0 && (pos ? A.val[uj] < 0.0 : A.val[uj] > 0.0)) pval[q] += (A.val[k] * A.val[uj]) / s;
+            if (j == gi || !strong(S, i, j) || !is_c(j)) continue;
+            const int uj = dfind(rc, b, e, j);
+            if (uj >= 0 && (pos ? rv[uj] < 0.0 : rv[uj] > 0.0)) pval[q] += (A.val[k] * rv[uj]) / s;
             ++q;
         }
     }
@@ -417,38 +512,40 @@ int64_t exclusive_scan(hipStream_t s, const int* in, int* out, int n, DevBuf<cha
     return total;
 }
 
-// the level operator on the device (single rank: global column ids are local)
+// the level operator on the device: this rank's rows, global column ids (int32)
 struct DevLevel {
     DevBuf<int> rp, col;
     DevBuf<double> val;
-    int n = 0;
-    DCsr view() const { return DCsr{rp.p, col.p, val.p, n}; }
+    int n = 0, lo = 0;
+    DCsr view() const { return DCsr{rp.p, col.p, val.p, n, lo}; }
 };
 
-void upload_level(const HostCSR& A, DevLevel& D) {
+void upload_level(const HostComm& comm, const HostCSR& A, DevLevel& D) {
     const int64_t n = A.nrows(), nnz = A.nnz();
-    AMG_CHECK(n < INT_MAX && nnz < INT_MAX, "device setup: level exceeds int32 indexing");
+    AMG_CHECK(n < INT_MAX && nnz < INT_MAX && A.n_global_cols < INT_MAX,
+              "device setup: level exceeds int32 indexing");
     std::vector<int> rp(n + 1), col((size_t)std::max<int64_t>(nnz, 1));
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i <= n; ++i) rp[i] = (int)A.rp[i];
 #pragma omp parallel for schedule(static)
     for (int64_t k = 0; k < nnz; ++k) col[k] = (int)A.col[k];
     D.n = (int)n;
+    D.lo = (int)A.row_starts[comm.rank];
     D.rp.upload(rp.data(), rp.size());
     D.col.upload(col.data(), col.size());
     if (nnz) D.val.upload(A.val.data(), (size_t)nnz);
     else D.val.alloc(1);
 }
 
-struct DevS {  // strength graph
+struct DevS {  // strength graph (this rank's rows, global column ids)
     DevBuf<int> rp, col;
     DevBuf<double> val;
-    int n = 0;
-    DCsr view() const { return DCsr{rp.p, col.p, val.p, n}; }
+    int n = 0, lo = 0;
+    DCsr view() const { return DCsr{rp.p, col.p, val.p, n, lo}; }
 };
 
 template <class CountK, class FillK>
-void build_strength(hipStream_t s, int n, DevS& S, DevBuf<char>& tmp, CountK count, FillK fill) {
+void build_strength(hipStream_t s, int n, int lo, DevS& S, DevBuf<char>& tmp, CountK count, FillK fill) {
     DevBuf<int> cnt;
     cnt.alloc((size_t)n + 1);
     HIP_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int) * cnt.n, s));
@@ -458,6 +555,7 @@ void build_strength(hipStream_t s, int n, DevS& S, DevBuf<char>& tmp, CountK cou
     S.col.alloc((size_t)std::max<int64_t>(nnz, 1));
     S.val.alloc((size_t)std::max<int64_t>(nnz, 1));
     S.n = n;
+    S.lo = lo;
     fill(S.rp.p, S.col.p, S.val.p);
     HIP_CHECK(hipGetLastError());
 }
@@ -469,100 +567,242 @@ std::vector<int32_t> download_ints(hipStream_t s, const int* p, int64_t n) {
     return h;
 }
 
+// A halo on the device: the sorted global ids (Dist lookups), the local send indices, and
+// forward(): pack on the device, the setup exchange on the host, the halo values uploaded
+struct DevHalo {
+    const HaloPlan* plan = nullptr;
+    DevBuf<int> gid, sidx;
+    void build(const HaloPlan& p) {
+        plan = &p;
+        std::vector<int> g(p.halo_gid.begin(), p.halo_gid.end()), si(p.send_idx.begin(), p.send_idx.end());
+        gid.upload(g.data(), g.size());
+        sidx.upload(si.data(), si.size());
+    }
+    Dist dist(int lo, int n) const { return Dist{lo, n, gid.p, (int)plan->n_halo()}; }
+    template <class T>
+    void forward(hipStream_t s, const HostComm& comm, const T* local, DevBuf<T>& halo) const {
+        const HaloPlan& p = *plan;
+        const int ns = (int)p.send_idx.size();
+        DevBuf<T> packed;
+        packed.alloc((size_t)std::max(ns, 1));
+        if (ns) hipLaunchKernelGGL(pack_kernel_t<T>, dim3(grid1(ns)), dim3(kT), 0, s, ns, sidx.p, local, packed.p);
+        std::vector<T> sbuf((size_t)ns), rbuf((size_t)p.n_halo());
+        if (ns) HIP_CHECK(hipMemcpyAsync(sbuf.data(), packed.p, sizeof(T) * ns, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        std::vector<int64_t> sb(comm.nranks, 0), rb(comm.nranks, 0);
+        for (size_t q = 0; q < p.send_procs.size(); ++q)
+            sb[p.send_procs[q]] = (p.send_ptr[q + 1] - p.send_ptr[q]) * (int64_t)sizeof(T);
+        for (size_t q = 0; q < p.recv_procs.size(); ++q)
+            rb[p.recv_procs[q]] = (p.recv_ptr[q + 1] - p.recv_ptr[q]) * (int64_t)sizeof(T);
+        comm.alltoallv(sbuf.data(), sb, rbuf.data(), rb);
+        if (halo.n < rbuf.size() || halo.n == 0) halo.alloc(std::max<size_t>(rbuf.size(), 1));
+        if (!rbuf.empty())
+            HIP_CHECK(hipMemcpyAsync(halo.p, rbuf.data(), sizeof(T) * rbuf.size(), hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+    }
+};
+
 }  // namespace
 
-// One level of the setup on the device (single rank): P and the integer split (C/F marker
-// for RS-family coarsening, aggregate id for SA).  Returns false when the device path does
-// not apply (several ranks, RS coarsening -- the serial Ruge-Stueben pass stays on the host).
+// One level of the setup on the device: P and the integer split (C/F marker for RS-family
+// coarsening, aggregate id for SA).  PMIS + classical interpolation run on any number of
+// ranks: each rank works on its rows with global column ids, the states of other ranks'
+// points arrive through halo forwards (pack on the device, the setup exchange on the host),
+// exactly the synchronous rounds of host_setup.cpp pmis_split / interp_classical.  Returns
+// false where the device path does not apply: Ruge-Stueben (the serial first pass stays on
+// the host) and smoothed aggregation on several ranks.
 bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, const amg_options& opt,
                         int level, HostCSR& P, std::vector<int32_t>& split) {
-    if (comm.nranks != 1 || opt.coarsen == AMG_COARSEN_RS) return false;
+    if (opt.coarsen == AMG_COARSEN_RS) return false;
+    if (opt.coarsen == AMG_COARSEN_SA && comm.nranks != 1) return false;
     hipStream_t s = ctx.stream;
     const int n = (int)A.nrows();
-    if (n == 0) return false;
+    if (comm.nranks == 1 && n == 0) return false;
     PhaseTimer tm(comm);
     DevLevel D;
-    upload_level(A, D);
+    upload_level(comm, A, D);
+    const int lo = D.lo;
     DevBuf<char> tmp;
     DevS S;
     const DCsr Av = D.view();
     if (opt.coarsen == AMG_COARSEN_PMIS) {
         const double theta = opt.strong_threshold;
         build_strength(
-            s, n, S, tmp,
+            s, n, lo, S, tmp,
             [&](int* cnt) {
-                hipLaunchKernelGGL(strength_classical_kernel<false>, dim3(grid1(n)), dim3(kT), 0, s, Av, theta, cnt,
-                                   nullptr, nullptr, nullptr);
+                if (n)
+                    hipLaunchKernelGGL(strength_classical_kernel<false>, dim3(grid1(n)), dim3(kT), 0, s, Av, theta,
+                                       cnt, nullptr, nullptr, nullptr);
             },
             [&](const int* srp, int* scol, double* sval) {
-                hipLaunchKernelGGL(strength_classical_kernel<true>, dim3(grid1(n)), dim3(kT), 0, s, Av, theta,
-                                   nullptr, srp, scol, sval);
+                if (n)
+                    hipLaunchKernelGGL(strength_classical_kernel<true>, dim3(grid1(n)), dim3(kT), 0, s, Av, theta,
+                                       nullptr, srp, scol, sval);
             });
         tm.lap("  device strength");
         const DCsr Sv = S.view();
-        // |S^T_i| and the S^T adjacency
+        // |S^T_i| and the S^T adjacency of the local-local part
         DevBuf<int> tcnt, trp, tcol, cursor;
         tcnt.alloc((size_t)n + 1);
         HIP_CHECK(hipMemsetAsync(tcnt.p, 0, sizeof(int) * tcnt.n, s));
-        hipLaunchKernelGGL(col_count_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, tcnt.p);
+        if (n) hipLaunchKernelGGL(col_count_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, tcnt.p);
         trp.alloc((size_t)n + 1);
-        const int64_t snnz = exclusive_scan(s, tcnt.p, trp.p, n, tmp);
-        tcol.alloc((size_t)std::max<int64_t>(snnz, 1));
+        const int64_t tnnz = exclusive_scan(s, tcnt.p, trp.p, n, tmp);
+        tcol.alloc((size_t)std::max<int64_t>(tnnz, 1));
         cursor.alloc((size_t)n + 1);
         HIP_CHECK(hipMemcpyAsync(cursor.p, trp.p, sizeof(int) * (n + 1), hipMemcpyDeviceToDevice, s));
-        hipLaunchKernelGGL(transpose_fill_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, cursor.p, tcol.p);
-        DevBuf<unsigned long long> key, nu;
-        DevBuf<int> cf;
+        if (n) hipLaunchKernelGGL(transpose_fill_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, cursor.p, tcol.p);
+        // several ranks: off-rank dependents (pairs (i, j), j on another rank depends on local
+        // i) and the halo of the neighbourhoods S_i u S^T_i, as pmis_split builds them
+        HaloPlan hplan;
+        DevHalo H;
+        DevBuf<int> erp, ecol;
+        if (comm.nranks > 1) {
+            DevBuf<int> ocnt, orp, opc, opj;
+            ocnt.alloc((size_t)n + 1);
+            HIP_CHECK(hipMemsetAsync(ocnt.p, 0, sizeof(int) * ocnt.n, s));
+            if (n)
+                hipLaunchKernelGGL(offrank_kernel<false>, dim3(grid1(n)), dim3(kT), 0, s, Sv, ocnt.p, nullptr,
+                                   nullptr, nullptr);
+            orp.alloc((size_t)n + 1);
+            const int64_t no = exclusive_scan(s, ocnt.p, orp.p, n, tmp);
+            opc.alloc((size_t)std::max<int64_t>(no, 1));
+            opj.alloc((size_t)std::max<int64_t>(no, 1));
+            if (n)
+                hipLaunchKernelGGL(offrank_kernel<true>, dim3(grid1(n)), dim3(kT), 0, s, Sv, nullptr, orp.p, opc.p,
+                                   opj.p);
+            const std::vector<int32_t> pc = download_ints(s, opc.p, no), pj = download_ints(s, opj.p, no);
+            std::vector<std::vector<int64_t>> sendp(comm.nranks);
+            std::vector<int64_t> need;
+            for (int64_t t = 0; t < no; ++t) {
+                const int o = owner_of(A.col_starts, pc[t]);
+                sendp[o].push_back(pc[t]);
+                sendp[o].push_back(pj[t]);
+                need.push_back(pc[t]);
+            }
+            const auto gotp = comm.exchange(sendp);
+            std::vector<int> ec((size_t)n + 1, 0);
+            for (int r = 0; r < comm.nranks; ++r)
+                for (size_t t = 0; t < gotp[r].size(); t += 2) ++ec[gotp[r][t] - lo + 1];
+            for (int i = 0; i < n; ++i) ec[i + 1] += ec[i];
+            std::vector<int> el((size_t)std::max(ec[n], 1)), pos(ec.begin(), ec.end() - 1);
+            for (int r = 0; r < comm.nranks; ++r)
+                for (size_t t = 0; t < gotp[r].size(); t += 2) {
+                    el[pos[gotp[r][t] - lo]++] = (int)gotp[r][t + 1];
+                    need.push_back(gotp[r][t + 1]);
+                }
+            erp.upload(ec.data(), ec.size());
+            ecol.upload(el.data(), el.size());
+            hplan = build_halo_plan(comm, A.col_starts, std::move(need));
+        }
+        H.build(hplan);
+        const Dist Dn = H.dist(lo, n);
+        DevBuf<unsigned long long> key, hkey, nu;
+        DevBuf<int> cf, hcf;
         DevBuf<unsigned char> newc;
-        key.alloc(n);
-        cf.alloc(n);
-        newc.alloc(n);
+        key.alloc((size_t)std::max(n, 1));
+        cf.alloc((size_t)std::max(n, 1));
+        newc.alloc((size_t)std::max(n, 1));
         nu.alloc(1);
-        hipLaunchKernelGGL(pmis_init_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, tcnt.p,
-                           (unsigned long long)(opt.seed + (uint64_t)level), key.p, cf.p);
+        hkey.alloc(1);
+        hcf.alloc(1);
+        if (n)
+            hipLaunchKernelGGL(pmis_init_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, lo, tcnt.p,
+                               comm.nranks > 1 ? erp.p : nullptr, (unsigned long long)(opt.seed + (uint64_t)level),
+                               key.p, cf.p);
         HIP_CHECK(hipGetLastError());
+        const bool dist = comm.nranks > 1;
+        if (dist) H.forward(s, comm, key.p, hkey);
         for (int round = 0;; ++round) {
-            AMG_CHECK(round <= n, "PMIS did not terminate");
-            hipLaunchKernelGGL(pmis_select_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, trp.p, tcol.p, key.p, cf.p,
-                               newc.p);
-            hipLaunchKernelGGL(pmis_apply_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, newc.p, cf.p);
+            AMG_CHECK(round <= A.n_global_rows, "PMIS did not terminate");
+            if (dist) H.forward(s, comm, cf.p, hcf);
+            if (n) {
+                hipLaunchKernelGGL(pmis_select_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, Dn, trp.p, tcol.p,
+                                   dist ? erp.p : nullptr, dist ? ecol.p : nullptr, key.p, hkey.p, cf.p, hcf.p,
+                                   newc.p);
+                hipLaunchKernelGGL(pmis_apply_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, newc.p, cf.p);
+            }
+            if (dist) H.forward(s, comm, cf.p, hcf);
             HIP_CHECK(hipMemsetAsync(nu.p, 0, sizeof(unsigned long long), s));
-            hipLaunchKernelGGL(pmis_fpass_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, cf.p, nu.p);
+            if (n) hipLaunchKernelGGL(pmis_fpass_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, Dn, cf.p, hcf.p, nu.p);
             HIP_CHECK(hipGetLastError());
             unsigned long long left = 0;
             HIP_CHECK(hipMemcpyAsync(&left, nu.p, sizeof(left), hipMemcpyDeviceToHost, s));
             HIP_CHECK(hipStreamSynchronize(s));
-            if (left == 0) break;
+            const int64_t all = dist ? comm.allreduce_sum((int64_t)left) : (int64_t)left;
+            if (all == 0) break;
         }
         tm.lap("  device PMIS");
-        // coarse numbering: C points in row order
-        DevBuf<int> cflag, cmap;
-        cflag.alloc((size_t)n + 1);
-        cmap.alloc((size_t)n + 1);
-        HIP_CHECK(hipMemsetAsync(cflag.p, 0, sizeof(int) * cflag.n, s));
-        hipLaunchKernelGGL(flag_eq_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, cf.p, (int)ST_C, cflag.p);
-        const int64_t nc = exclusive_scan(s, cflag.p, cmap.p, n, tmp);
+        // coarse numbering: C points in row order, ranks in order
         split = download_ints(s, cf.p, n);
+        int64_t ncl = 0;
+        for (int32_t v : split) ncl += v == ST_C;
+        std::vector<int64_t> cstarts(comm.nranks + 1, 0);
+        {
+            const std::vector<int64_t> counts = comm.allgather(ncl);
+            for (int r = 0; r < comm.nranks; ++r) cstarts[r + 1] = cstarts[r] + counts[r];
+        }
+        AMG_CHECK(cstarts[comm.nranks] < INT_MAX, "device setup: coarse level exceeds int32 indexing");
+        std::vector<int> hcmap((size_t)std::max(n, 1), -1);
+        for (int i = 0, c = (int)cstarts[comm.rank]; i < n; ++i)
+            if (split[i] == ST_C) hcmap[i] = c++;
+        DevBuf<int> cmap;
+        cmap.upload(hcmap.data(), hcmap.size());
+        // A's halo: states and coarse ids of the off-rank columns, and their ghost rows
+        HaloPlan aplan;
+        GhostRows G;
+        if (dist) {
+            aplan = halo_plan_for_cols(comm, A);
+            G = fetch_rows(comm, aplan, A);
+        }
+        DevHalo AH;
+        AH.build(aplan);
+        DevBuf<int> acf, acmap, grp, gcol;
+        DevBuf<double> gval;
+        acf.alloc(1);
+        acmap.alloc(1);
+        if (dist) {
+            std::vector<int32_t> hcfa(aplan.n_halo());
+            std::vector<int64_t> cm64(hcmap.begin(), hcmap.begin() + n), hcm64(aplan.n_halo());
+            aplan.forward(comm, split.data(), hcfa.data());
+            aplan.forward(comm, cm64.data(), hcm64.data());
+            std::vector<int> hcma(hcm64.begin(), hcm64.end());
+            acf.upload(hcfa.data(), hcfa.size());
+            acmap.upload(hcma.data(), hcma.size());
+            AMG_CHECK(G.rp.back() < INT_MAX, "device setup: ghost rows exceed int32 indexing");
+            std::vector<int> gr(G.rp.begin(), G.rp.end()), gc(G.col.begin(), G.col.end());
+            grp.upload(gr.data(), gr.size());
+            gcol.upload(gc.data(), std::max<size_t>(gc.size(), 1));
+            gval.upload(G.val.data(), std::max<size_t>(G.val.size(), 1));
+        } else {
+            grp.alloc(1);
+            gcol.alloc(1);
+            gval.alloc(1);
+        }
+        const ARows Ar{Av, AH.dist(lo, n), grp.p, gcol.p, gval.p};
+        tm.lap("  device coarse ids + ghost rows");
         // P: count, scan, fill
         DevBuf<int> pcnt, prp, pcol;
         DevBuf<double> pval;
         pcnt.alloc((size_t)n + 1);
         HIP_CHECK(hipMemsetAsync(pcnt.p, 0, sizeof(int) * pcnt.n, s));
-        hipLaunchKernelGGL(interp_kernel<false>, dim3(grid1(n)), dim3(kT), 0, s, Av, Sv, cf.p, cmap.p, pcnt.p,
-                           nullptr, nullptr, nullptr);
+        if (n)
+            hipLaunchKernelGGL(interp_kernel<false>, dim3(grid1(n)), dim3(kT), 0, s, Ar, Sv, cf.p, acf.p, cmap.p,
+                               acmap.p, pcnt.p, nullptr, nullptr, nullptr);
         prp.alloc((size_t)n + 1);
         const int64_t pnnz = exclusive_scan(s, pcnt.p, prp.p, n, tmp);
         pcol.alloc((size_t)std::max<int64_t>(pnnz, 1));
         pval.alloc((size_t)std::max<int64_t>(pnnz, 1));
-        hipLaunchKernelGGL(interp_kernel<true>, dim3(grid1(n)), dim3(kT), 0, s, Av, Sv, cf.p, cmap.p, nullptr,
-                           prp.p, pcol.p, pval.p);
+        if (n)
+            hipLaunchKernelGGL(interp_kernel<true>, dim3(grid1(n)), dim3(kT), 0, s, Ar, Sv, cf.p, acf.p, cmap.p,
+                               acmap.p, nullptr, prp.p, pcol.p, pval.p);
         HIP_CHECK(hipGetLastError());
         std::vector<int> hrp = download_ints(s, prp.p, (int64_t)n + 1), hcol = download_ints(s, pcol.p, pnnz);
         P = HostCSR();
         P.n_global_rows = A.n_global_rows;
-        P.n_global_cols = nc;
+        P.n_global_cols = cstarts[comm.nranks];
         P.row_starts = A.row_starts;
-        P.col_starts = {0, nc};
+        P.col_starts = cstarts;
         P.rp.assign(hrp.begin(), hrp.end());
         P.col.assign(hcol.begin(), hcol.end());
         P.val.resize((size_t)pnnz);
@@ -578,7 +818,7 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
     d.alloc(n);
     hipLaunchKernelGGL(diagonal_kernel, dim3(grid1(n)), dim3(kT), 0, s, Av, d.p);
     build_strength(
-        s, n, S, tmp,
+        s, n, lo, S, tmp,
         [&](int* cnt) {
             hipLaunchKernelGGL(strength_symmetric_kernel<false>, dim3(grid1(n)), dim3(kT), 0, s, Av, d.p, theta,
                                cnt, nullptr, nullptr, nullptr);

@@ -1,0 +1,54 @@
+"""Driver for the per-cycle-kernel PMC passes: the exact operations of
+bench.py's `vcycle_kernels` table (7-pt 256^3 PMIS hierarchy, levels with >= 1e5 rows: Jacobi,
+residual, R r, x += P e), each launched 3 times, with a marker kernel between operations
+(uniform_kernel on (1000 + op index) workgroups) so scripts/pmc_vcycle_traffic.py can cut the
+per-dispatch counter stream into operations.  Run under one rocprofv3 --pmc pass per counter
+(FETCH_SIZE, WRITE_SIZE); see scripts/gpu_pmc_vcycle.sh."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import raptor_amd as ra  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+ctx = ra.Context(0)
+A = ra.par_stencil_grid(ctx, "7pt", (N, N, N))
+ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
+ops = []
+
+
+def marker(idx):
+    ra.vector_uniform(ctx, (1000 + idx) * 256, 0, 1)
+
+
+for l in range(ml.num_levels - 1):
+    if ml.level_info(l)["n_global"] < 100000:
+        break
+    Al = A if l == 0 else ml.level_matrix(l, "A")
+    P, R = ml.level_matrix(l, "P"), ml.level_matrix(l, "R")
+    nl, nc = Al.local_rows, P.local_cols
+    with torch.cuda.stream(ctx.stream):
+        xl, bl, tl = ra.vector_uniform(ctx, nl, 0, 5), ra.vector_uniform(ctx, nl, 0, 6), ctx.empty(nl)
+        xc, bc = ra.vector_uniform(ctx, nc, 0, 7), ctx.empty(R.local_rows)
+    table = [("Jacobi", lambda: Al.jacobi(xl, bl, tl), Al.info["jacobi_bytes"]),
+             ("residual", lambda: Al.residual(xl, bl, tl), Al.info["residual_bytes"]),
+             ("restrict R r", lambda: R.mult(tl, bc), R.info["spmv_bytes"]),
+             ("interp x += P e", lambda: P.mult_add(xc, xl), P.info["mult_add_bytes"])]
+    for name, fn, nbytes in table:
+        fn()  # warm (first-use builds, caches)
+        ctx.synchronize()
+        marker(len(ops))
+        for _ in range(3):
+            fn()
+        ctx.synchronize()
+        ops.append({"level": l, "op": name, "stored_bytes": int(nbytes)})
+    del xl, bl, tl, xc, bc
+marker(len(ops))  # closes the last segment
+ctx.synchronize()
+out = os.environ.get("AMG_PMC_OPS", os.path.join(ROOT, "gpurun_out", "pmc_vcycle_ops.json"))
+json.dump({"grid": [N, N, N], "launches_per_op": 3, "ops": ops}, open(out, "w"), indent=1)
+print(json.dumps(ops))

@@ -210,6 +210,46 @@ int mesh_alltoallv(void* user, const void* sendbuf, const int64_t* send_bytes, v
     return sent && got ? 0 : 1;
 }
 
+// "graphmult": the smallest RCCL-in-a-graph case -- one ParCSRMatrix::mult (pack + one
+// ncclSend/ncclRecv group on the comm stream + interior / boundary kernels) captured on the
+// context stream and replayed, compared with the eager result
+std::vector<double> graph_mult(amg::Context& ctx) {
+    amg::ParCSRMatrix A = amg::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 24, 24, 24);
+    const int64_t n = A.local_rows(), f = A.first_row();
+    hipStream_t s = (hipStream_t)ctx.stream();
+    double *x = nullptr, *y0 = nullptr, *y1 = nullptr;
+    HIPOK(hipMalloc(&x, n * sizeof(double)));
+    HIPOK(hipMalloc(&y0, n * sizeof(double)));
+    HIPOK(hipMalloc(&y1, n * sizeof(double)));
+    ctx.uniform(n, f, 3, x);
+    A.mult(x, y0);  // eager: connects the peers
+    ctx.synchronize();
+    std::fprintf(stderr, "[cxx] eager mult done\n");
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    HIPOK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    A.mult(x, y1);
+    HIPOK(hipStreamEndCapture(s, &g));
+    std::fprintf(stderr, "[cxx] capture done\n");
+    HIPOK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    std::fprintf(stderr, "[cxx] instantiate done\n");
+    for (int k = 0; k < 3; ++k) {
+        HIPOK(hipMemsetAsync(y1, 0, n * sizeof(double), s));
+        HIPOK(hipGraphLaunch(ge, s));
+        HIPOK(hipStreamSynchronize(s));
+        std::fprintf(stderr, "[cxx] replay %d done\n", k);
+    }
+    std::vector<double> h0(n), h1(n);
+    HIPOK(hipMemcpy(h0.data(), y0, n * sizeof(double), hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(h1.data(), y1, n * sizeof(double), hipMemcpyDeviceToHost));
+    HIPOK(hipGraphExecDestroy(ge));
+    HIPOK(hipGraphDestroy(g));
+    HIPOK(hipFree(x));
+    HIPOK(hipFree(y0));
+    HIPOK(hipFree(y1));
+    return {h0 == h1 ? 1.0 : 0.0};
+}
+
 int rank_main(Mesh& m, bool graph, const char* golden, int result_fd) {
     // RCCL refuses two ranks of one host on one device: each rank is its own "host" (socket
     // transport), as in tests/test_gpu_rccl.py
@@ -227,7 +267,9 @@ int rank_main(Mesh& m, bool graph, const char* golden, int result_fd) {
     ctx.set_comm(m.rank, m.nranks, id.data(), mesh_alltoallv, &m);
     int levels = 0;
     bool used = false;
-    const std::vector<double> h = solve_7pt(ctx, graph, &levels, &used);
+    const bool gm = std::getenv("AMG_CXX_GRAPH_MULT") != nullptr;
+    const std::vector<double> h = gm ? graph_mult(ctx) : solve_7pt(ctx, graph, &levels, &used);
+    if (gm) used = graph;
     const int64_t cnt = (int64_t)h.size();
     const char flag = used ? 1 : 0;
     if (!write_all(result_fd, (const char*)&cnt, sizeof cnt) ||
@@ -314,6 +356,11 @@ int run_ranks(int nranks, bool graph, const char* golden) {
             std::fprintf(stderr, "rank %d history differs from rank 0\n", r);
             ok = false;
         }
+    }
+    if (std::getenv("AMG_CXX_GRAPH_MULT")) {  // graph_mult: 1.0 = replay equals eager
+        for (int r = 0; r < nranks; ++r) ok = ok && hs[r].size() == 1 && hs[r][0] == 1.0;
+        std::printf("graph mult: %s\n", ok ? "replay == eager on every rank" : "MISMATCH");
+        return ok ? 0 : 1;
     }
     // PMIS + Jacobi is partition independent: the N-rank history is the 1-rank one (norms
     // reduced in rank order: 1e-10)

@@ -289,3 +289,39 @@ def test_multirank_gs_templates(oracle, monkeypatch, nranks):
     for f, m, fw, bw in res:
         assert np.array_equal(fw, fo[f:f + m])
         assert np.array_equal(bw, bo[f:f + m])
+
+
+@pytest.mark.parametrize("nranks,kind,dims", [(2, "7pt", (16, 15, 18)), (3, "7pt", (14, 14, 21)),
+                                              (8, "7pt", (24, 24, 64)), (4, "5pt", (40, 34))])
+def test_device_setup_equals_host_multirank(nranks, kind, dims):
+    """SURVEY 8f row f1 on several ranks: the device PMIS + classical interpolation (rank rows
+    with global column ids, halo states forwarded each round, ghost rows of A for the strong F
+    neighbours) builds the same hierarchy as the host path, level by level and bit for bit --
+    A, P, R and the C/F split of every rank."""
+    import raptor_amd as ra
+
+    def rank(r, nr, world):
+        ctx = ra.Context.loopback(r, nr, world)
+        A = ra.par_stencil_grid(ctx, kind, dims)
+        out = []
+        for m in (1, 0):
+            ml = ra.ParRugeStubenSolver(coarsen="pmis", setup_device=m, replicate_below=0).setup(A)
+            lev = []
+            for l in range(ml.num_levels):
+                mats = {w: ml.level_matrix(l, w).to_scipy_local() for w in ("APR" if l + 1 < ml.num_levels else "A")}
+                split = ml.level_split(l) if l + 1 < ml.num_levels else None
+                lev.append((mats, split))
+            out.append(lev)
+            del ml
+        return out
+
+    from tests.util import same_csr
+
+    res = run_ranks(nranks, rank)
+    for dev, host in res:
+        assert len(dev) == len(host) >= 2
+        for (md, sd), (mh, sh) in zip(dev, host):
+            assert md.keys() == mh.keys()
+            for w in md:
+                assert same_csr(md[w], mh[w]), w
+            assert (sd is None and sh is None) or np.array_equal(sd, sh)
