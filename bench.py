@@ -3,6 +3,8 @@
 
 Workload (BASELINE.json configs[1], weak-scaled for --gpus N):
   N=1: 256^3   N=2: 256x256x512   N=4: 256x512x512   N=8: 512^3   (16.8M rows per GPU)
+  partitioned into one 256^3 box per rank (N=8: 2 x 2 x 2 cubes, the grid numbered box by box;
+  --partition slabs: z-slabs of the natural numbering)
   PMIS coarsening + classical interpolation, 1 pre / 1 post Jacobi sweep (omega 2/3),
   dense solve at <= 256 rows; b = A x*, x* ~ U(-1,1) (splitmix64, seed 42), x0 = 0.
 One "step" = one ParMultilevel::solve iteration (V-cycle + residual norm) of the global
@@ -32,6 +34,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 GRIDS = {1: (256, 256, 256), 2: (256, 256, 512), 4: (256, 512, 512), 8: (512, 512, 512)}
+# box decomposition per rank count: every rank holds one 256^3 cube; the
+# z-slab alternative (--partition slabs) gives 512 x 512 x 64 slabs at N = 8
+BOXES = {1: (1, 1, 1), 2: (1, 1, 2), 4: (1, 2, 2), 8: (2, 2, 2)}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MALL_BYTES = 256 << 20  # Infinity Cache (MALL) capacity
 
@@ -59,6 +64,9 @@ def main():
     ap.add_argument("--lattice", type=int, default=1225,
                     help="g3sub: lattice side (1225^2 = 1.5M rows, G3_circuit size)")
     ap.add_argument("--no-reorder", action="store_true", help="g3sub: keep the random numbering")
+    ap.add_argument("--partition", choices=["boxes", "slabs"], default="boxes",
+                    help="7pt/sa27 over N ranks: boxes (default; 2 x 2 x 2 cubes of 256^3 at N = 8, "
+                         "the grid numbered box by box) or z-slabs of the natural numbering")
     ap.add_argument("--traffic-json", type=str,
                     default=os.path.join(ROOT, "profiles", "pmc_level0_spmv.json"),
                     help="PMC-measured per-launch HBM traffic of the level-0 SpMV "
@@ -126,7 +134,12 @@ def main():
             A, _ = A.reorder("rcm")
             reorder_s = time.perf_counter() - tr
     else:
-        A = ra.par_stencil_grid(ctx, "27pt" if sa27 else "7pt", grid)
+        boxes = None
+        if args.partition == "boxes" and world > 1:
+            boxes = BOXES.get(world) if not args.grid else None
+            if boxes is None:  # other rank counts / grids: boxes along z (= slabs)
+                boxes = (1, 1, world)
+        A = ra.par_stencil_grid(ctx, "27pt" if sa27 else "7pt", grid, boxes=boxes)
     log(rank, f"matrix {grid} built in {time.perf_counter() - t0:.1f}s; local rows {A.local_rows}")
     t1 = time.perf_counter()
     graph = False if args.no_graph else None
@@ -171,6 +184,9 @@ def main():
     iters_per_s = args.steps / dt
     value = iters_per_s * scale
     conv = float((hist[-1] / hist[0]) ** (1.0 / max(1, len(hist) - 1))) if hist[0] > 0 else None
+    # the geometric mean over all steps depends on the step count (the first cycles reduce
+    # the residual faster): the factor over the last 5 cycles is the asymptotic one
+    conv_last5 = (float((hist[-1] / hist[-6]) ** 0.2) if len(hist) >= 6 and hist[-6] > 0 else None)
     log(rank, f"{args.steps} V-cycles in {dt * 1e3:.2f} ms -> {iters_per_s:.1f} it/s, conv {conv}")
 
     # bytes of one V-cycle on all ranks: plain-CSR and stored-format (what
@@ -360,12 +376,17 @@ def main():
                 "level_nnz": [i["nnz_global"] for i in infos],
                 "operator_complexity": round(sum(i["nnz_global"] for i in infos) / infos[0]["nnz_global"], 3),
                 "parallelism": f"row-partition x{world}, RCCL halo",
+                "partition": ("one rank" if world == 1 else
+                              "boxes " + "x".join(str(v) for v in BOXES.get(world, (1, 1, world)))
+                              if args.partition == "boxes" and not g3 and not args.grid else
+                              "even rows" if g3 else "z-slabs"),
                 "setup_s": round(setup_s, 2),
                 "reorder_s": None if reorder_s is None else round(reorder_s, 2),
                 "hipgraph": world == 1 and not args.no_graph,
             },
             "iters_per_s": round(iters_per_s, 3),
             "convergence_factor": conv,
+            "convergence_factor_last5": conv_last5,
             # bytes one cycle streams in the stored formats (<= peak x time) and the plain-CSR
             # count of SURVEY.md 8(d) (what a CSR implementation of the same cycle would move)
             "vcycle_stored_bytes": cyc_stored,

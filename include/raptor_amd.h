@@ -86,6 +86,15 @@ int amg_par_csr_create(amg_context ctx, int64_t n_global, int64_t first_row, int
  * the rank and uploads it: par_stencil_grid analogue.  Collective.                       */
 int amg_par_stencil_create(amg_context ctx, int kind, int64_t nx, int64_t ny, int64_t nz,
                            const double* eps3, amg_matrix* out);
+/* The same problem numbered box by box: the grid is cut into bx x by x bz boxes (box
+ * (ix, iy, iz) covers x in [nx ix / bx, nx (ix + 1) / bx), ...; boxes numbered x fastest),
+ * each box's points get consecutive global ids (lexicographic inside the box), and rank r
+ * holds boxes [nb r / P, nb (r + 1) / P) -- e.g. 512^3 over 8 GPUs as 2 x 2 x 2 cubes of 256^3
+ * instead of z-slabs of 512 x 512 x 64.  The matrix is P A P^T of the natural-order stencil;
+ * boxes (1, 1, P) (2D: (1, P, 1)) give exactly amg_par_stencil_create's rows.  Collective. */
+int amg_par_stencil_create_boxes(amg_context ctx, int kind, int64_t nx, int64_t ny, int64_t nz,
+                                 int64_t bx, int64_t by, int64_t bz, const double* eps3,
+                                 amg_matrix* out);
 
 /* ---- unstructured inputs ------------------------------------ */
 /* All of these use the even row partition: rank r holds rows [n r / P, n (r+1) / P).
@@ -266,6 +275,8 @@ int amg_host_hierarchy_destroy(amg_host_hierarchy H);
 typedef struct amg_host_csr_s* amg_host_csr;
 int amg_host_csr_graph_laplacian(int rank, int nranks, int64_t nx, int64_t ny, uint64_t seed,
                                  amg_host_csr* out);
+int amg_host_csr_stencil(int rank, int nranks, int kind, int64_t nx, int64_t ny, int64_t nz,
+                         int64_t bx, int64_t by, int64_t bz, const double* eps3, amg_host_csr* out);
 int amg_host_csr_read(int rank, int nranks, const char* path, amg_host_csr* out);
 int amg_host_csr_write(int rank, int nranks, amg_alltoallv_fn exchange, void* user,
                        amg_host_csr A, const char* path);

@@ -303,21 +303,48 @@ class ParCSRMatrix:
 _STENCILS = {"5pt": AMG_STENCIL_5PT, "7pt": AMG_STENCIL_7PT, "27pt": AMG_STENCIL_27PT}
 
 
-def par_stencil_grid(ctx: Context, kind: str, dims, eps=(1.0, 1.0, 1e-3)) -> ParCSRMatrix:
-    """Model problem of SURVEY.md 8d; this rank's z-slab (2D: y-slab).  Collective."""
+def _grid3(kind, dims):
     dims = tuple(int(d) for d in dims)
     if kind == "5pt":
         if len(dims) != 2:
             raise ValueError("5pt takes (nx, ny)")
-        nx, ny, nz = dims[0], dims[1], 1
-    else:
-        if len(dims) != 3:
-            raise ValueError(f"{kind} takes (nx, ny, nz)")
-        nx, ny, nz = dims
+        return dims[0], dims[1], 1
+    if len(dims) != 3:
+        raise ValueError(f"{kind} takes (nx, ny, nz)")
+    return dims
+
+
+def par_stencil_grid(ctx: Context, kind: str, dims, eps=(1.0, 1.0, 1e-3), boxes=None) -> ParCSRMatrix:
+    """Model problem of SURVEY.md 8d.  Default: this rank's z-slab (2D: y-slab) of the
+    natural ordering.  boxes=(bx, by, bz): the grid numbered box by box, ranks holding
+    contiguous box ranges (e.g. (2, 2, 2) cubes for 8 ranks).  Collective."""
+    nx, ny, nz = _grid3(kind, dims)
     e = (C.c_double * 3)(*eps)
     h = C.c_void_p()
-    check(lib().amg_par_stencil_create(ctx.h, _STENCILS[kind], nx, ny, nz, e, C.byref(h)))
+    if boxes is None:
+        check(lib().amg_par_stencil_create(ctx.h, _STENCILS[kind], nx, ny, nz, e, C.byref(h)))
+    else:
+        bx, by, bz = (int(v) for v in boxes)
+        check(lib().amg_par_stencil_create_boxes(ctx.h, _STENCILS[kind], nx, ny, nz, bx, by, bz, e, C.byref(h)))
     return ParCSRMatrix(ctx, h)
+
+
+def box_order(dims, boxes):
+    """new_to_old of the box numbering of par_stencil_grid(boxes=...) relative to the natural
+    lexicographic order (numpy; for oracle comparisons: B = P A P^T = permute(A, new_to_old))."""
+    dims = tuple(int(d) for d in dims) + (1,) * (3 - len(dims))
+    boxes = tuple(int(b) for b in boxes) + (1,) * (3 - len(boxes))
+    nx, ny, nz = dims
+    out = []
+    for iz in range(boxes[2]):
+        for iy in range(boxes[1]):
+            for ix in range(boxes[0]):
+                x0, x1 = nx * ix // boxes[0], nx * (ix + 1) // boxes[0]
+                y0, y1 = ny * iy // boxes[1], ny * (iy + 1) // boxes[1]
+                z0, z1 = nz * iz // boxes[2], nz * (iz + 1) // boxes[2]
+                k, j, i = np.meshgrid(np.arange(z0, z1), np.arange(y0, y1), np.arange(x0, x1), indexing="ij")
+                out.append((i + nx * (j + ny * k)).ravel())
+    return np.concatenate(out).astype(np.int64)
 
 
 def par_graph_laplacian(ctx: Context, nx: int, ny: int, seed: int = 1) -> ParCSRMatrix:

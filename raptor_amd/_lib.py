@@ -109,6 +109,10 @@ SIGNATURES = {
     "amg_context_destroy": (C.c_int, [_vp]),
     "amg_par_csr_create": (C.c_int, [_vp, _i64, _i64, _i64, _pi64, _pi64, _pf64, C.POINTER(_vp)]),
     "amg_par_stencil_create": (C.c_int, [_vp, C.c_int, _i64, _i64, _i64, _pf64, C.POINTER(_vp)]),
+    "amg_par_stencil_create_boxes": (C.c_int, [_vp, C.c_int, _i64, _i64, _i64, _i64, _i64, _i64, _pf64,
+                                               C.POINTER(_vp)]),
+    "amg_host_csr_stencil": (C.c_int, [C.c_int, C.c_int, C.c_int, _i64, _i64, _i64, _i64, _i64, _i64, _pf64,
+                                       C.POINTER(_vp)]),
     "amg_par_csr_info": (C.c_int, [_vp, C.POINTER(MatrixInfo)]),
     "amg_par_csr_export": (C.c_int, [_vp, _pi64, _pi64, _pf64]),
     "amg_par_csr_set_format": (C.c_int, [_vp, _i32]),

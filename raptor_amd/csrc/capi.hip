@@ -253,6 +253,23 @@ int amg_par_stencil_create(amg_context ctx, int kind, int64_t nx, int64_t ny, in
     });
 }
 
+int amg_par_stencil_create_boxes(amg_context ctx, int kind, int64_t nx, int64_t ny, int64_t nz, int64_t bx,
+                                 int64_t by, int64_t bz, const double* eps3, amg_matrix* out) {
+    return guard([&] {
+        AMG_CHECK(ctx && out, "null argument");
+        AMG_CHECK(kind == AMG_STENCIL_5PT || kind == AMG_STENCIL_7PT || kind == AMG_STENCIL_27PT,
+                  "unknown stencil");
+        Context& c = ctx->c;
+        set_device(c);
+        HostCSR h = stencil_boxes(c.host, kind, nx, ny, nz, bx, by, bz, eps3);
+        std::unique_ptr<amg_matrix_s> m(new amg_matrix_s());
+        m->own.reset(new DevMatrix());
+        m->m = m->own.get();
+        m->m->build(&c, std::move(h));
+        *out = m.release();
+    });
+}
+
 static void upload(Context& c, HostCSR&& h, amg_matrix* out) {
     std::unique_ptr<amg_matrix_s> m(new amg_matrix_s());
     m->own.reset(new DevMatrix());
@@ -710,6 +727,18 @@ int amg_host_csr_graph_laplacian(int rank, int nranks, int64_t nx, int64_t ny, u
     return guard([&] {
         AMG_CHECK(out, "null argument");
         host_out(graph_laplacian_slab(host_comm(rank, nranks, nullptr, nullptr, false), nx, ny, seed), rank, out);
+    });
+}
+
+// the stencil generators need no communication either
+int amg_host_csr_stencil(int rank, int nranks, int kind, int64_t nx, int64_t ny, int64_t nz, int64_t bx,
+                         int64_t by, int64_t bz, const double* eps3, amg_host_csr* out) {
+    return guard([&] {
+        AMG_CHECK(out, "null argument");
+        AMG_CHECK(kind == AMG_STENCIL_5PT || kind == AMG_STENCIL_7PT || kind == AMG_STENCIL_27PT,
+                  "unknown stencil");
+        host_out(stencil_boxes(host_comm(rank, nranks, nullptr, nullptr, false), kind, nx, ny, nz, bx, by, bz, eps3),
+                 rank, out);
     });
 }
 

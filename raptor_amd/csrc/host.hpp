@@ -136,6 +136,9 @@ std::vector<double> dense_inverse_gathered(const HostComm& comm, const HostCSR& 
 // model problems: this rank's slab (rows split evenly by planes)
 HostCSR stencil_slab(const HostComm& comm, int kind, int64_t nx, int64_t ny, int64_t nz,
                      const double* eps3);
+// the same problem numbered box by box (bx x by x bz boxes, ranks own contiguous box ranges)
+HostCSR stencil_boxes(const HostComm& comm, int kind, int64_t nx, int64_t ny, int64_t nz, int64_t bx,
+                      int64_t by, int64_t bz, const double* eps3);
 
 // Whole hierarchy on the host (rows a7-a10): level l holds A_l (l >= 1), P_l, R_l and the
 // integer splitting; the coarsest level's gathered dense inverse.  Same stopping rule and

@@ -449,6 +449,120 @@ HostCSR stencil_slab(const HostComm& comm, int kind, int64_t nx, int64_t ny, int
     return A;
 }
 
+// Box-ordered model problem (bench.py --gpus 8: 2 x 2 x 2 cubes of 256^3 instead of z-slabs
+// of 512 x 512 x 64).  The grid is cut into bx x by x bz boxes (box (ix, iy, iz) covers
+// x in [nx ix / bx, nx (ix + 1) / bx), ...), boxes are numbered x fastest, and each box's
+// points get consecutive global ids in lexicographic order inside the box; rank r owns boxes
+// [nb r / P, nb (r + 1) / P).  The matrix is P A P^T of the natural-order stencil (same
+// values, rows with their columns sorted); boxes (1, 1, P) give exactly stencil_slab's rows.
+HostCSR stencil_boxes(const HostComm& comm, int kind, int64_t nx, int64_t ny, int64_t nz, int64_t bx,
+                      int64_t by, int64_t bz, const double* eps3) {
+    AMG_CHECK(nx > 0 && ny > 0 && nz > 0, "stencil: grid dims must be positive");
+    AMG_CHECK(kind != AMG_STENCIL_5PT || nz == 1, "5-pt stencil is 2D: nz must be 1");
+    AMG_CHECK(bx >= 1 && by >= 1 && bz >= 1 && bx <= nx && by <= ny && bz <= nz, "stencil: bad box grid");
+    const int64_t nb = bx * by * bz;
+    AMG_CHECK(nb >= comm.nranks, "stencil: fewer boxes than ranks");
+    // per axis: box of each coordinate and the coordinate inside it; box starts and widths
+    auto axis = [](int64_t n, int64_t b, std::vector<int64_t>& box, std::vector<int64_t>& loc,
+                   std::vector<int64_t>& start) {
+        start.resize(b + 1);
+        for (int64_t q = 0; q <= b; ++q) start[q] = n * q / b;
+        box.resize(n);
+        loc.resize(n);
+        for (int64_t q = 0; q < b; ++q)
+            for (int64_t i = start[q]; i < start[q + 1]; ++i) box[i] = q, loc[i] = i - start[q];
+    };
+    std::vector<int64_t> xb, xl, xs, yb, yl, ys, zb, zl, zs;
+    axis(nx, bx, xb, xl, xs);
+    axis(ny, by, yb, yl, ys);
+    axis(nz, bz, zb, zl, zs);
+    std::vector<int64_t> off(nb + 1, 0);
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t ix = b % bx, iy = (b / bx) % by, iz = b / (bx * by);
+        off[b + 1] = off[b] + (xs[ix + 1] - xs[ix]) * (ys[iy + 1] - ys[iy]) * (zs[iz + 1] - zs[iz]);
+    }
+    auto gid = [&](int64_t i, int64_t j, int64_t k) {
+        const int64_t ix = xb[i], iy = yb[j], iz = zb[k], b = ix + bx * (iy + by * iz);
+        const int64_t wx = xs[ix + 1] - xs[ix], wy = ys[iy + 1] - ys[iy];
+        return off[b] + xl[i] + wx * (yl[j] + wy * zl[k]);
+    };
+    HostCSR A;
+    A.n_global_rows = A.n_global_cols = nx * ny * nz;
+    A.row_starts.resize(comm.nranks + 1);
+    for (int r = 0; r <= comm.nranks; ++r) A.row_starts[r] = off[nb * r / comm.nranks];
+    A.col_starts = A.row_starts;
+    const int64_t b0 = nb * comm.rank / comm.nranks, b1 = nb * (comm.rank + 1) / comm.nranks;
+    const int64_t nloc = off[b1] - off[b0];
+    // local row t -> (i, j, k): walk this rank's boxes
+    std::vector<int64_t> pt((size_t)nloc);
+    for (int64_t b = b0; b < b1; ++b) {
+        const int64_t ix = b % bx, iy = (b / bx) % by, iz = b / (bx * by);
+        const int64_t wx = xs[ix + 1] - xs[ix], wy = ys[iy + 1] - ys[iy], wz = zs[iz + 1] - zs[iz];
+#pragma omp parallel for schedule(static)
+        for (int64_t t = 0; t < wx * wy * wz; ++t) {
+            const int64_t i = xs[ix] + t % wx, j = ys[iy] + (t / wx) % wy, k = zs[iz] + t / (wx * wy);
+            pt[off[b] - off[b0] + t] = i + nx * (j + ny * k);  // natural id: decoded below
+        }
+    }
+    auto inside = [&](int64_t i, int64_t j, int64_t k) {
+        return i >= 0 && i < nx && j >= 0 && j < ny && k >= 0 && k < nz;
+    };
+    const double ex = eps3 ? eps3[0] : 1.0, ey = eps3 ? eps3[1] : 1.0, ez = eps3 ? eps3[2] : 1e-3;
+    std::vector<int64_t> len((size_t)nloc);
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < nloc; ++t) {
+        const int64_t g = pt[t], i = g % nx, j = (g / nx) % ny, k = g / (nx * ny);
+        int64_t c = 0;
+        if (kind == AMG_STENCIL_27PT) {
+            for (int dz = -1; dz <= 1; ++dz)
+                for (int dy = -1; dy <= 1; ++dy)
+                    for (int dx = -1; dx <= 1; ++dx) c += inside(i + dx, j + dy, k + dz);
+        } else {
+            c = 1 + (i > 0) + (i < nx - 1) + (j > 0) + (j < ny - 1);
+            if (kind == AMG_STENCIL_7PT) c += (k > 0) + (k < nz - 1);
+        }
+        len[t] = c;
+    }
+    A.rp.assign(nloc + 1, 0);
+    for (int64_t t = 0; t < nloc; ++t) A.rp[t + 1] = A.rp[t] + len[t];
+    A.col.resize(A.rp[nloc]);
+    A.val.resize(A.rp[nloc]);
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < nloc; ++t) {
+        const int64_t g = pt[t], i = g % nx, j = (g / nx) % ny, k = g / (nx * ny);
+        int64_t q = A.rp[t];
+        auto put = [&](int64_t ii, int64_t jj, int64_t kk, double v) { A.col[q] = gid(ii, jj, kk), A.val[q] = v, ++q; };
+        if (kind == AMG_STENCIL_27PT) {
+            for (int dz = -1; dz <= 1; ++dz)
+                for (int dy = -1; dy <= 1; ++dy)
+                    for (int dx = -1; dx <= 1; ++dx)
+                        if (inside(i + dx, j + dy, k + dz)) put(i + dx, j + dy, k + dz, stencil27(dx, dy, dz, ex, ey, ez));
+        } else if (kind == AMG_STENCIL_7PT) {
+            if (k > 0) put(i, j, k - 1, -1.0);
+            if (j > 0) put(i, j - 1, k, -1.0);
+            if (i > 0) put(i - 1, j, k, -1.0);
+            put(i, j, k, 6.0);
+            if (i < nx - 1) put(i + 1, j, k, -1.0);
+            if (j < ny - 1) put(i, j + 1, k, -1.0);
+            if (k < nz - 1) put(i, j, k + 1, -1.0);
+        } else {
+            if (j > 0) put(i, j - 1, k, -1.0);
+            if (i > 0) put(i - 1, j, k, -1.0);
+            put(i, j, k, 4.0);
+            if (i < nx - 1) put(i + 1, j, k, -1.0);
+            if (j < ny - 1) put(i, j + 1, k, -1.0);
+        }
+        // columns ascending (a neighbour in another box may sit anywhere in the numbering)
+        const int64_t b = A.rp[t], e = A.rp[t + 1];
+        for (int64_t u = b + 1; u < e; ++u)
+            for (int64_t w = u; w > b && A.col[w - 1] > A.col[w]; --w) {
+                std::swap(A.col[w - 1], A.col[w]);
+                std::swap(A.val[w - 1], A.val[w]);
+            }
+    }
+    return A;
+}
+
 // ----------------------------------------------------------------------------------
 // Replicated coarse levels: every rank gets all rows (rank order = global row order).
 // ----------------------------------------------------------------------------------

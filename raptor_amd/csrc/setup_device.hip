@@ -1,15 +1,15 @@
 // setup_device.hip -- AMG setup on the GPU: strength of connection,
-// PMIS splitting, classical interpolation, MIS(2) aggregation, the smoothed-aggregation
-// prolongator and the transpose R = P^T, for one rank.  Every integer decision and every
-// floating-point sum follows host_setup.cpp / oracle/amg_oracle.c exactly, so
-// the hierarchy is bit-identical to the host path's; the Galerkin products stay on the
-// device SpGEMM (spgemm.hip).  Several ranks keep the host path (host_setup.cpp), whose
-// rounds exchange halo states between ranks.
+// PMIS splitting, classical interpolation, MIS(2) aggregation and the smoothed-aggregation
+// prolongator on any number of ranks, the transpose R = P^T on one rank.  Every integer
+// decision and every floating-point sum follows host_setup.cpp / oracle/amg_oracle.c exactly
+// (DESIGN.md 3), so the hierarchy is bit-identical to the host path's at every rank count;
+// the Galerkin products stay on the device SpGEMM (spgemm.hip).
 //
-// Layout: one upload of A per level -- int32 row_ptr, int32 columns (single rank: global =
-// local ids), fp64 values; the strength graph S stays on the device; per-row kernels are one
-// thread per row (rows are short and independent); rounds (PMIS, MIS(2)) are synchronous:
-// each round reads the previous round's states only.
+// Layout: one upload of this rank's rows of A per level -- int32 row_ptr, int32 GLOBAL column
+// ids, fp64 values; the strength graph S stays on the device; per-row kernels are one thread
+// per row (rows are short and independent); rounds (PMIS, MIS(2)) are synchronous: each round
+// reads the previous round's states only, other ranks' states through a halo (Dist) that is
+// forwarded between rounds (device pack, host setup exchange, upload).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -133,16 +133,17 @@ __global__ void diagonal_kernel(DCsr A, double* d) {
 }
 
 // symmetric: |a_ij| >= theta sqrt(|a_ii a_jj|), j != i
+// (a_jj of another rank's column through D: the forwarded diagonal hd)
 template <bool FILL>
-__global__ void strength_symmetric_kernel(DCsr A, const double* d, double theta, int* cnt, const int* srp,
-                                          int* scol, double* sval) {
+__global__ void strength_symmetric_kernel(DCsr A, Dist D, const double* d, const double* hd, double theta,
+                                          int* cnt, const int* srp, int* scol, double* sval) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= A.n) return;
     int q = FILL ? srp[i] : 0, c = 0;
     for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) {
         const int j = A.col[k];
-        if (j == i) continue;
-        if (!(fabs(A.val[k]) >= theta * sqrt(fabs(d[i] * d[j])))) continue;
+        if (j == A.lo + i) continue;
+        if (!(fabs(A.val[k]) >= theta * sqrt(fabs(d[i] * D.get(d, hd, j))))) continue;
         if (FILL) {
             scol[q] = j;
             sval[q++] = A.val[k];
@@ -382,63 +383,60 @@ __global__ void interp_kernel(ARows R, DCsr S, const int* cf, const int* hcf, co
 }
 
 // ---- MIS(2) aggregation -----------------------------------------------------------------
-__global__ void mis2_tuple_kernel(int n, const int* st, const unsigned* hs, unsigned long long* h,
+// tuple (state, hash, global id) of every local point, packed hi = state << 32 | hash, lo = id
+__global__ void mis2_tuple_kernel(int n, int lo, const int* st, const unsigned* hs, unsigned long long* h,
                                   unsigned long long* l) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= n) return;
     h[i] = ((unsigned long long)(unsigned)st[i] << 32) | hs[i];
-    l[i] = (unsigned long long)i;
+    l[i] = (unsigned long long)(lo + i);
 }
 
-__global__ void mis2_hop_kernel(DCsr S, const unsigned long long* h0, const unsigned long long* l0,
+// one hop of the lexicographic max over S_i (halo tuples through D: hh / hl)
+__global__ void mis2_hop_kernel(DCsr S, Dist D, const unsigned long long* h0, const unsigned long long* l0,
+                                const unsigned long long* hh, const unsigned long long* hl,
                                 unsigned long long* h1, unsigned long long* l1) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= S.n) return;
     unsigned long long mh = h0[i], ml = l0[i];
     for (int k = S.rp[i]; k < S.rp[i + 1]; ++k) {
-        const int j = S.col[k];
-        const unsigned long long xh = h0[j], xl = l0[j];
+        const int l = D.loc(S.col[k]);
+        const unsigned long long xh = l >= 0 ? h0[l] : hh[-l - 1], xl = l >= 0 ? l0[l] : hl[-l - 1];
         if (xh > mh || (xh == mh && xl > ml)) mh = xh, ml = xl;
     }
     h1[i] = mh;
     l1[i] = ml;
 }
 
-__global__ void mis2_update_kernel(int n, const unsigned long long* h, const unsigned long long* l,
+__global__ void mis2_update_kernel(int n, int lo, const unsigned long long* h, const unsigned long long* l,
                                    int* st, unsigned long long* nu) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= n || st[i] != M_U) return;
-    if (l[i] == (unsigned long long)i) st[i] = M_IN;
+    if (l[i] == (unsigned long long)(lo + i)) st[i] = M_IN;
     else if ((h[i] >> 32) == M_IN) st[i] = M_OUT;
     if (st[i] == M_U) atomicAdd(nu, 1ull);
 }
 
-__global__ void flag_eq_kernel(int n, const int* st, int value, int* flag) {
-    const int i = blockIdx.x * kT + threadIdx.x;
-    if (i < n) flag[i] = st[i] == value;
-}
-
-// pass 1: a root keeps its id; others join the first root neighbour in S-row order
-__global__ void mis2_pass1_kernel(DCsr S, const int* st, const int* rootid, int* a1) {
+// pass 1: a root keeps its aggregate id (aggr: the global id of a root, -1 otherwise); the
+// others join the first root neighbour in S-row order
+__global__ void mis2_pass1_kernel(DCsr S, Dist D, const int* aggr, const int* haggr, int* a1) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= S.n) return;
-    if (st[i] == M_IN) {
-        a1[i] = rootid[i];
-        return;
-    }
-    int a = -1;
-    for (int k = S.rp[i]; k < S.rp[i + 1]; ++k) {
-        const int j = S.col[k];
-        if (st[j] == M_IN) {
-            a = rootid[j];
-            break;
+    int a = aggr[i];
+    if (a < 0)
+        for (int k = S.rp[i]; k < S.rp[i + 1]; ++k) {
+            const int aj = D.get(aggr, haggr, S.col[k]);
+            if (aj >= 0) {
+                a = aj;
+                break;
+            }
         }
-    }
     a1[i] = a;
 }
 
 // pass 2: the rest join the pass-1 neighbour with max |s_ij| (ties: smaller aggregate id)
-__global__ void mis2_pass2_kernel(DCsr S, const int* a1, int* agg, unsigned long long* orphans) {
+__global__ void mis2_pass2_kernel(DCsr S, Dist D, const int* a1, const int* ha1, int* agg,
+                                  unsigned long long* orphans) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= S.n) return;
     if (a1[i] >= 0) {
@@ -448,7 +446,7 @@ __global__ void mis2_pass2_kernel(DCsr S, const int* a1, int* agg, unsigned long
     double best = -1.0;
     int ba = -1;
     for (int k = S.rp[i]; k < S.rp[i + 1]; ++k) {
-        const int aj = a1[S.col[k]];
+        const int aj = D.get(a1, ha1, S.col[k]);
         if (aj < 0) continue;
         const double w = fabs(S.val[k]);
         if (w > best || (w == best && aj < ba)) best = w, ba = aj;
@@ -457,20 +455,13 @@ __global__ void mis2_pass2_kernel(DCsr S, const int* a1, int* agg, unsigned long
     if (ba < 0) atomicAdd(orphans, 1ull);
 }
 
-__global__ void agg_size_kernel(int n, const int* agg, int* size) {
-    const int i = blockIdx.x * kT + threadIdx.x;
-    if (i < n) atomicAdd(&size[agg[i]], 1);
-}
-
-// rho_i = sum_k |a_ik| / |a_ii| (row order), and T_i = 1 / sqrt(|agg(i)|)
-__global__ void sa_rows_kernel(DCsr A, const double* d, const int* agg, const int* size, double* rho,
-                               double* tval) {
+// rho_i = sum_k |a_ik| / |a_ii| (row order)
+__global__ void sa_rho_kernel(DCsr A, const double* d, double* rho) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= A.n) return;
     double s = 0.0;
     for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) s += fabs(A.val[k]);
     rho[i] = s / fabs(d[i]);
-    tval[i] = 1.0 / sqrt((double)size[agg[i]]);
 }
 
 // ---- transpose: R = P^T, rows of R sorted by fine index (stable radix sort on columns) ---
@@ -605,16 +596,15 @@ struct DevHalo {
 }  // namespace
 
 // One level of the setup on the device: P and the integer split (C/F marker for RS-family
-// coarsening, aggregate id for SA).  PMIS + classical interpolation run on any number of
-// ranks: each rank works on its rows with global column ids, the states of other ranks'
-// points arrive through halo forwards (pack on the device, the setup exchange on the host),
-// exactly the synchronous rounds of host_setup.cpp pmis_split / interp_classical.  Returns
-// false where the device path does not apply: Ruge-Stueben (the serial first pass stays on
-// the host) and smoothed aggregation on several ranks.
+// coarsening, aggregate id for SA), on any number of ranks.  Each rank works on its rows
+// with global column ids; the states of other ranks' points arrive through halo forwards
+// (pack on the device, the setup exchange on the host) -- exactly the synchronous rounds of
+// host_setup.cpp pmis_split / interp_classical / mis2_aggregate / sa_prolongator, so the
+// hierarchy is bit-identical to the host path's at every rank count.  Returns false for
+// Ruge-Stueben (the serial first pass stays on the host).
 bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, const amg_options& opt,
                         int level, HostCSR& P, std::vector<int32_t>& split) {
     if (opt.coarsen == AMG_COARSEN_RS) return false;
-    if (opt.coarsen == AMG_COARSEN_SA && comm.nranks != 1) return false;
     hipStream_t s = ctx.stream;
     const int n = (int)A.nrows();
     if (comm.nranks == 1 && n == 0) return false;
@@ -811,98 +801,160 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
         tm.lap("  device interpolation");
         return true;
     }
-    // smoothed aggregation
+    // smoothed aggregation (host_setup.cpp strength_symmetric, mis2_aggregate, sa_prolongator)
     AMG_CHECK(opt.coarsen == AMG_COARSEN_SA, "unknown coarsening");
+    const bool dist = comm.nranks > 1;
     const double theta = std::ldexp(opt.strong_threshold, -level);
-    DevBuf<double> d;
-    d.alloc(n);
-    hipLaunchKernelGGL(diagonal_kernel, dim3(grid1(n)), dim3(kT), 0, s, Av, d.p);
+    // A's halo: a_jj of other ranks' columns, then the MIS(2) tuples and aggregate ids of the
+    // strong neighbours (S is a subset of A's pattern)
+    HaloPlan aplan;
+    if (dist) aplan = halo_plan_for_cols(comm, A);
+    DevHalo AH;
+    AH.build(aplan);
+    const Dist Da = AH.dist(lo, n);
+    DevBuf<double> d, hd;
+    d.alloc((size_t)std::max(n, 1));
+    hd.alloc(1);
+    if (n) hipLaunchKernelGGL(diagonal_kernel, dim3(grid1(n)), dim3(kT), 0, s, Av, d.p);
+    if (dist) AH.forward(s, comm, d.p, hd);
     build_strength(
         s, n, lo, S, tmp,
         [&](int* cnt) {
-            hipLaunchKernelGGL(strength_symmetric_kernel<false>, dim3(grid1(n)), dim3(kT), 0, s, Av, d.p, theta,
-                               cnt, nullptr, nullptr, nullptr);
+            if (n)
+                hipLaunchKernelGGL(strength_symmetric_kernel<false>, dim3(grid1(n)), dim3(kT), 0, s, Av, Da, d.p,
+                                   hd.p, theta, cnt, nullptr, nullptr, nullptr);
         },
         [&](const int* srp, int* scol, double* sval) {
-            hipLaunchKernelGGL(strength_symmetric_kernel<true>, dim3(grid1(n)), dim3(kT), 0, s, Av, d.p, theta,
-                               nullptr, srp, scol, sval);
+            if (n)
+                hipLaunchKernelGGL(strength_symmetric_kernel<true>, dim3(grid1(n)), dim3(kT), 0, s, Av, Da, d.p,
+                                   hd.p, theta, nullptr, srp, scol, sval);
         });
     tm.lap("  device strength");
     const DCsr Sv = S.view();
-    std::vector<unsigned> hs(n);
-    for (int i = 0; i < n; ++i) hs[i] = hash32(i, opt.seed + (uint64_t)level);
+    std::vector<unsigned> hs((size_t)std::max(n, 1));
+    for (int i = 0; i < n; ++i) hs[i] = hash32(lo + i, opt.seed + (uint64_t)level);
     DevBuf<unsigned> dhs;
     dhs.upload(hs.data(), hs.size());
     DevBuf<int> st;
-    DevBuf<unsigned long long> h0, l0, h1, l1, nu;
-    st.alloc(n);
-    h0.alloc(n), l0.alloc(n), h1.alloc(n), l1.alloc(n), nu.alloc(1);
+    DevBuf<unsigned long long> h0, l0, h1, l1, hh, hl, nu;
+    const size_t nn = (size_t)std::max(n, 1);
+    st.alloc(nn);
+    h0.alloc(nn), l0.alloc(nn), h1.alloc(nn), l1.alloc(nn), nu.alloc(1), hh.alloc(1), hl.alloc(1);
     {
-        std::vector<int> init(n, M_U);
+        std::vector<int> init(nn, M_U);
         st.upload(init.data(), init.size());
     }
     for (int round = 0;; ++round) {
-        AMG_CHECK(round <= n, "MIS(2) did not terminate");
-        hipLaunchKernelGGL(mis2_tuple_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, st.p, dhs.p, h0.p, l0.p);
+        AMG_CHECK(round <= A.n_global_rows, "MIS(2) did not terminate");
+        if (n) hipLaunchKernelGGL(mis2_tuple_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, lo, st.p, dhs.p, h0.p, l0.p);
         for (int hop = 0; hop < 2; ++hop) {
-            hipLaunchKernelGGL(mis2_hop_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, h0.p, l0.p, h1.p, l1.p);
+            if (dist) {
+                AH.forward(s, comm, h0.p, hh);
+                AH.forward(s, comm, l0.p, hl);
+            }
+            if (n)
+                hipLaunchKernelGGL(mis2_hop_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, Da, h0.p, l0.p, hh.p, hl.p,
+                                   h1.p, l1.p);
             std::swap(h0.p, h1.p);
             std::swap(l0.p, l1.p);
         }
         HIP_CHECK(hipMemsetAsync(nu.p, 0, sizeof(unsigned long long), s));
-        hipLaunchKernelGGL(mis2_update_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, h0.p, l0.p, st.p, nu.p);
+        if (n) hipLaunchKernelGGL(mis2_update_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, lo, h0.p, l0.p, st.p, nu.p);
         HIP_CHECK(hipGetLastError());
         unsigned long long left = 0;
         HIP_CHECK(hipMemcpyAsync(&left, nu.p, sizeof(left), hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipStreamSynchronize(s));
-        if (left == 0) break;
+        if ((dist ? comm.allreduce_sum((int64_t)left) : (int64_t)left) == 0) break;
     }
-    DevBuf<int> flag, rootid, a1, agg, size;
-    flag.alloc((size_t)n + 1);
-    rootid.alloc((size_t)n + 1);
-    HIP_CHECK(hipMemsetAsync(flag.p, 0, sizeof(int) * flag.n, s));
-    hipLaunchKernelGGL(flag_eq_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, st.p, (int)M_IN, flag.p);
-    const int64_t na = exclusive_scan(s, flag.p, rootid.p, n, tmp);
-    a1.alloc(n);
-    agg.alloc(n);
-    hipLaunchKernelGGL(mis2_pass1_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, st.p, rootid.p, a1.p);
+    // roots numbered in global row order (ranks in order); aggr = a root's aggregate id, -1
+    const std::vector<int32_t> hst = download_ints(s, st.p, n);
+    int64_t nroot = 0;
+    for (int32_t v : hst) nroot += v == M_IN;
+    std::vector<int64_t> astarts(comm.nranks + 1, 0);
+    {
+        const std::vector<int64_t> counts = comm.allgather(nroot);
+        for (int r = 0; r < comm.nranks; ++r) astarts[r + 1] = astarts[r] + counts[r];
+    }
+    const int64_t na = astarts[comm.nranks];
+    AMG_CHECK(na < INT_MAX, "device setup: coarse level exceeds int32 indexing");
+    std::vector<int> haggr(nn, -1);
+    for (int i = 0, c = (int)astarts[comm.rank]; i < n; ++i)
+        if (hst[i] == M_IN) haggr[i] = c++;
+    DevBuf<int> aggr, haggr_d, a1, ha1, agg;
+    aggr.upload(haggr.data(), haggr.size());
+    haggr_d.alloc(1);
+    ha1.alloc(1);
+    a1.alloc(nn);
+    agg.alloc(nn);
+    if (dist) AH.forward(s, comm, aggr.p, haggr_d);
+    if (n) hipLaunchKernelGGL(mis2_pass1_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, Da, aggr.p, haggr_d.p, a1.p);
+    if (dist) AH.forward(s, comm, a1.p, ha1);
     HIP_CHECK(hipMemsetAsync(nu.p, 0, sizeof(unsigned long long), s));
-    hipLaunchKernelGGL(mis2_pass2_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, a1.p, agg.p, nu.p);
+    if (n)
+        hipLaunchKernelGGL(mis2_pass2_kernel, dim3(grid1(n)), dim3(kT), 0, s, Sv, Da, a1.p, ha1.p, agg.p, nu.p);
     HIP_CHECK(hipGetLastError());
     unsigned long long orphans = 0;
     HIP_CHECK(hipMemcpyAsync(&orphans, nu.p, sizeof(orphans), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     if (orphans) throw Error(AMG_ERR_INTERNAL, "MIS(2): unaggregated node");
-    tm.lap("  device aggregation");
-    // tentative prolongator T (1 / sqrt(|aggregate|)), rho = max_i sum_k |a_ik| / |a_ii|
-    size.alloc((size_t)std::max<int64_t>(na, 1));
-    HIP_CHECK(hipMemsetAsync(size.p, 0, sizeof(int) * size.n, s));
-    hipLaunchKernelGGL(agg_size_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, agg.p, size.p);
-    DevBuf<double> rho, tv;
-    rho.alloc(n);
-    tv.alloc(n);
-    hipLaunchKernelGGL(sa_rows_kernel, dim3(grid1(n)), dim3(kT), 0, s, Av, d.p, agg.p, size.p, rho.p, tv.p);
-    HIP_CHECK(hipGetLastError());
     split = download_ints(s, agg.p, n);
-    std::vector<double> hrho(n), htv(n), hd(n);
-    HIP_CHECK(hipMemcpyAsync(hrho.data(), rho.p, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipMemcpyAsync(htv.data(), tv.p, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipMemcpyAsync(hd.data(), d.p, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    tm.lap("  device aggregation");
+    // aggregate sizes (owners count their members, members elsewhere report in), T = 1 /
+    // sqrt(|aggregate|), rho = max_i sum_k |a_ik| / |a_ii| over every rank
+    const int64_t alo = astarts[comm.rank], ahi = astarts[comm.rank + 1];
+    std::vector<int64_t> size((size_t)(ahi - alo), 0);
+    std::vector<std::vector<int64_t>> sendc(comm.nranks);
+    std::vector<int64_t> needa;
+    for (int i = 0; i < n; ++i) {
+        const int64_t a = split[i];
+        if (a >= alo && a < ahi) {
+            size[a - alo]++;
+        } else {
+            sendc[owner_of(astarts, a)].push_back(a);
+            needa.push_back(a);
+        }
+    }
+    if (dist) {
+        const auto got = comm.exchange(sendc);
+        for (int r = 0; r < comm.nranks; ++r)
+            for (int64_t a : got[r]) size[a - alo]++;
+    }
+    HaloPlan splan;
+    std::vector<int64_t> hsize;
+    if (dist) {
+        splan = build_halo_plan(comm, astarts, std::move(needa));
+        hsize.resize(splan.n_halo());
+        splan.forward(comm, size.data(), hsize.data());
+    }
+    DevBuf<double> rho;
+    rho.alloc(nn);
+    if (n) hipLaunchKernelGGL(sa_rho_kernel, dim3(grid1(n)), dim3(kT), 0, s, Av, d.p, rho.p);
+    HIP_CHECK(hipGetLastError());
+    std::vector<double> hrho(nn), hdiag(nn);
+    HIP_CHECK(hipMemcpyAsync(hrho.data(), rho.p, sizeof(double) * nn, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(hdiag.data(), d.p, sizeof(double) * nn, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     double r = 0.0;
     for (int i = 0; i < n; ++i)
         if (hrho[i] > r) r = hrho[i];
+    if (dist) r = comm.allreduce_max(r);
     const double omega = (4.0 / 3.0) / r;
+    const std::vector<double>& hd_loc = hdiag;
     HostCSR T;
     T.n_global_rows = A.n_global_rows;
     T.n_global_cols = na;
     T.row_starts = A.row_starts;
-    T.col_starts = {0, na};
+    T.col_starts = astarts;
     T.rp.resize((size_t)n + 1);
     T.col.resize(n);
-    T.val = htv;
+    T.val.resize(n);
     for (int i = 0; i <= n; ++i) T.rp[i] = i;
-    for (int i = 0; i < n; ++i) T.col[i] = split[i];
+    for (int i = 0; i < n; ++i) {
+        const int64_t a = split[i];
+        const int64_t sz = (a >= alo && a < ahi) ? size[a - alo] : hsize[splan.find(a)];
+        T.col[i] = a;
+        T.val[i] = 1.0 / std::sqrt((double)sz);
+    }
     tm.lap("  device tentative prolongator");
     HostCSR AT = spgemm_device(ctx, comm, A, T);
     tm.lap("  device A*T");
@@ -911,7 +963,7 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
     P.n_global_rows = A.n_global_rows;
     P.n_global_cols = na;
     P.row_starts = A.row_starts;
-    P.col_starts = {0, na};
+    P.col_starts = astarts;
     P.rp.assign((size_t)n + 1, 0);
     std::vector<int64_t> len(n);
 #pragma omp parallel for schedule(static)
@@ -926,7 +978,7 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
     P.val.resize(P.rp[n]);
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < n; ++i) {
-        const double c = omega * (1.0 / hd[i]);
+        const double c = omega * (1.0 / hd_loc[i]);
         int64_t ka = AT.rp[i], ea = AT.rp[i + 1], kt = T.rp[i], et = T.rp[i + 1], q = P.rp[i];
         while (ka < ea || kt < et) {
             const int64_t ja = ka < ea ? AT.col[ka] : INT64_MAX, jt = kt < et ? T.col[kt] : INT64_MAX;

@@ -115,6 +115,18 @@ class HostCSR:
         return cls(h, rank, nranks, group)
 
     @classmethod
+    def stencil(cls, kind, dims, boxes=(1, 1, 1), eps=(1.0, 1.0, 1e-3), rank=0, nranks=1, group=None):
+        """The box-ordered model problem of par_stencil_grid(boxes=...), host only."""
+        kinds = {"5pt": 0, "7pt": 1, "27pt": 2}
+        dims = tuple(int(d) for d in dims) + (1,) * (3 - len(dims))
+        b = tuple(int(v) for v in boxes) + (1,) * (3 - len(boxes))
+        e = (C.c_double * 3)(*eps)
+        h = C.c_void_p()
+        check(lib().amg_host_csr_stencil(rank, nranks, kinds[kind], dims[0], dims[1], dims[2], b[0], b[1], b[2],
+                                         e, C.byref(h)))
+        return cls(h, rank, nranks, group)
+
+    @classmethod
     def read(cls, path, rank=0, nranks=1, group=None):
         h = C.c_void_p()
         check(lib().amg_host_csr_read(rank, nranks, os.fsencode(path), C.byref(h)))

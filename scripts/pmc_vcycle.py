@@ -1,8 +1,9 @@
 """Driver for the per-cycle-kernel PMC passes: the exact operations of
 bench.py's `vcycle_kernels` table (7-pt 256^3 PMIS hierarchy, levels with >= 1e5 rows: Jacobi,
 residual, R r, x += P e), each launched 3 times, with a marker kernel between operations
-(uniform_kernel on (1000 + op index) workgroups) so scripts/pmc_vcycle_traffic.py can cut the
-per-dispatch counter stream into operations.  Run under one rocprofv3 --pmc pass per counter
+(uniform_kernel on 1000 + 2 op workgroups before an operation's 3 launches, 1000 + 2 op + 1
+after them) so scripts/pmc_vcycle_traffic.py can cut the per-dispatch counter stream into
+operations; the warm-up launch of each operation stays outside its segment.  Run under one rocprofv3 --pmc pass per counter
 (FETCH_SIZE, WRITE_SIZE); see scripts/gpu_pmc_vcycle.sh."""
 import json
 import os
@@ -39,15 +40,15 @@ for l in range(ml.num_levels - 1):
              ("restrict R r", lambda: R.mult(tl, bc), R.info["spmv_bytes"]),
              ("interp x += P e", lambda: P.mult_add(xc, xl), P.info["mult_add_bytes"])]
     for name, fn, nbytes in table:
-        fn()  # warm (first-use builds, caches)
+        fn()  # warm (first-use builds, caches): outside the segment
         ctx.synchronize()
-        marker(len(ops))
+        marker(2 * len(ops))  # segment start
         for _ in range(3):
             fn()
+        marker(2 * len(ops) + 1)  # segment end
         ctx.synchronize()
         ops.append({"level": l, "op": name, "stored_bytes": int(nbytes)})
     del xl, bl, tl, xc, bc
-marker(len(ops))  # closes the last segment
 ctx.synchronize()
 out = os.environ.get("AMG_PMC_OPS", os.path.join(ROOT, "gpurun_out", "pmc_vcycle_ops.json"))
 json.dump({"grid": [N, N, N], "launches_per_op": 3, "ops": ops}, open(out, "w"), indent=1)

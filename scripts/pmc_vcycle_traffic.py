@@ -4,7 +4,7 @@
 traffic = 2 x FETCH_SIZE + WRITE_SIZE (bytes; on gfx950 FETCH_SIZE counts half the bytes of
 wide coalesced reads, MI355X_MICROARCH.md "HBM") summed over the kernels one operation
 launches, averaged over its 3 launches.  The dispatch stream is cut at the marker kernels
-(uniform_kernel on 1000 + op workgroups).  FETCH_SIZE counts the L2's memory-side requests,
+(uniform_kernel on 1000 + 2 op / 1000 + 2 op + 1 workgroups: segment start / end).  FETCH_SIZE counts the L2's memory-side requests,
 Infinity-Cache hits included: for an operator that fits the 256 MiB cache the figure is
 L2-miss traffic, not HBM traffic.
 
@@ -27,12 +27,13 @@ def segments(path, counter, nops):
     cur = None
     for d in sorted(rows):
         r = rows[d]
-        if "uniform_kernel" in r["name"] and 1000 <= r["grid"] < 1000 + nops + 1:
-            cur = r["grid"] - 1000
-            if cur < nops:
+        if "uniform_kernel" in r["name"] and 1000 <= r["grid"] < 1000 + 2 * nops:
+            m = r["grid"] - 1000  # 2 op: segment start, 2 op + 1: segment end
+            cur = m // 2 if m % 2 == 0 else None
+            if cur is not None:
                 seg[cur] = defaultdict(float)
             continue
-        if cur is not None and cur < nops:
+        if cur is not None:
             k = r["name"].split("(amg::")[0].replace("void amg::(anonymous namespace)::", "")
             seg[cur][f"{k} [{r['grid']}]"] += r[counter]
     return seg

@@ -213,6 +213,41 @@ int mesh_alltoallv(void* user, const void* sendbuf, const int64_t* send_bytes, v
 // "graphmult": the smallest RCCL-in-a-graph case -- one ParCSRMatrix::mult (pack + one
 // ncclSend/ncclRecv group on the comm stream + interior / boundary kernels) captured on the
 // context stream and replayed, compared with the eager result
+// AMG_CXX_GRAPH_MULT=3: V-cycles replayed from a captured graph, synchronised after each,
+// against the same cycles run eagerly by a second solver on the same matrix
+std::vector<double> graph_cycles(amg::Context& ctx) {
+    amg::ParCSRMatrix A = amg::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 24, 24, 24);
+    const int64_t n = A.local_rows(), f = A.first_row();
+    amg::ParMultilevel mg(A, amg::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
+    amg::ParMultilevel me(A, amg::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
+    mg.set_graph(true);
+    double *xs = nullptr, *b = nullptr, *xg = nullptr, *xe = nullptr;
+    HIPOK(hipMalloc(&xs, n * sizeof(double)));
+    HIPOK(hipMalloc(&b, n * sizeof(double)));
+    HIPOK(hipMalloc(&xg, n * sizeof(double)));
+    HIPOK(hipMalloc(&xe, n * sizeof(double)));
+    ctx.uniform(n, f, 42, xs);
+    A.mult(xs, b);
+    HIPOK(hipMemsetAsync(xg, 0, n * sizeof(double), (hipStream_t)ctx.stream()));
+    HIPOK(hipMemsetAsync(xe, 0, n * sizeof(double), (hipStream_t)ctx.stream()));
+    for (int k = 0; k < 3; ++k) {
+        me.cycle(xe, b);
+        ctx.synchronize();
+        std::fprintf(stderr, "[cxx] eager cycle %d done\n", k);
+    }
+    for (int k = 0; k < 3; ++k) {
+        mg.cycle(xg, b);
+        std::fprintf(stderr, "[cxx] graph cycle %d enqueued (graph %d)\n", k, (int)mg.graph());
+        ctx.synchronize();
+        std::fprintf(stderr, "[cxx] graph cycle %d done\n", k);
+    }
+    std::vector<double> hg(n), he(n);
+    HIPOK(hipMemcpy(hg.data(), xg, n * sizeof(double), hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(he.data(), xe, n * sizeof(double), hipMemcpyDeviceToHost));
+    for (double* p : {xs, b, xg, xe}) HIPOK(hipFree(p));
+    return {hg == he && mg.graph() ? 1.0 : 0.0};
+}
+
 std::vector<double> graph_mult(amg::Context& ctx) {
     amg::ParCSRMatrix A = amg::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 24, 24, 24);
     const int64_t n = A.local_rows(), f = A.first_row();
@@ -267,8 +302,10 @@ int rank_main(Mesh& m, bool graph, const char* golden, int result_fd) {
     ctx.set_comm(m.rank, m.nranks, id.data(), mesh_alltoallv, &m);
     int levels = 0;
     bool used = false;
-    const bool gm = std::getenv("AMG_CXX_GRAPH_MULT") != nullptr;
-    const std::vector<double> h = gm ? graph_mult(ctx) : solve_7pt(ctx, graph, &levels, &used);
+    const char* gmode = std::getenv("AMG_CXX_GRAPH_MULT");
+    const bool gm = gmode != nullptr;
+    const std::vector<double> h = !gm ? solve_7pt(ctx, graph, &levels, &used)
+                                  : std::atoi(gmode) == 3 ? graph_cycles(ctx) : graph_mult(ctx);
     if (gm) used = graph;
     const int64_t cnt = (int64_t)h.size();
     const char flag = used ? 1 : 0;

@@ -115,10 +115,28 @@ CASES = [(2, "7pt", (16, 15, 18), "pmis", "jacobi"),
 def test_multirank_vcycle_bit_exact(oracle, nranks, kind, dims, coarsen, smoother, rep):
     """rep = replicate_below: 0 keeps every level distributed; 800 replicates the coarse
     tail; 1e9 replicates everything below the fine level."""
+    _vcycle_vs_oracle(oracle, nranks, kind, dims, coarsen, smoother, rep)
+
+
+@pytest.mark.parametrize("nranks,kind,dims,boxes,coarsen,smoother",
+                         [(8, "7pt", (24, 24, 24), (2, 2, 2), "pmis", "jacobi"),
+                          (4, "7pt", (20, 22, 24), (1, 2, 2), "pmis", "jacobi"),
+                          (8, "27pt", (12, 12, 12), (2, 2, 2), "sa", "hybrid_gs"),
+                          (3, "7pt", (18, 17, 16), (3, 1, 1), "pmis", "jacobi")])
+def test_multirank_boxes_vcycle_bit_exact(oracle, nranks, kind, dims, boxes, coarsen, smoother):
+    """The box decomposition (bench.py --gpus 8: 2 x 2 x 2 cubes of 256^3): every rank's slice
+    of every level operator and V-cycle iterate equals the oracle's hierarchy of P A P^T (the
+    box numbering of the same stencil), and the solve history agrees to 1e-10."""
+    _vcycle_vs_oracle(oracle, nranks, kind, dims, coarsen, smoother, 0, boxes)
+
+
+def _vcycle_vs_oracle(oracle, nranks, kind, dims, coarsen, smoother, rep, boxes=None):
     import raptor_amd as ra
 
     O = oracle
     Ao = {"7pt": O.gen_7pt, "5pt": O.gen_5pt, "27pt": O.gen_27pt}[kind](*dims)
+    if boxes is not None:
+        Ao = O.permute(Ao, ra.box_order(dims, boxes))
     Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS[coarsen], smoother=O.SMOOTH_JACOBI if smoother == "jacobi"
                                 else O.SMOOTH_HYBRID_GS))
     n = Ao.shape[0]
@@ -127,7 +145,7 @@ def test_multirank_vcycle_bit_exact(oracle, nranks, kind, dims, coarsen, smoothe
 
     def rank(r, nr, world):
         ctx = ra.Context.loopback(r, nr, world)
-        A = ra.par_stencil_grid(ctx, kind, dims)
+        A = ra.par_stencil_grid(ctx, kind, dims, boxes=boxes)
         ml = ra.ParMultilevel(coarsen=coarsen, smoother=smoother, replicate_below=rep).setup(A)
         f, m = A.first_row, A.local_rows
         bad = []
@@ -291,13 +309,14 @@ def test_multirank_gs_templates(oracle, monkeypatch, nranks):
         assert np.array_equal(bw, bo[f:f + m])
 
 
-@pytest.mark.parametrize("nranks,kind,dims", [(2, "7pt", (16, 15, 18)), (3, "7pt", (14, 14, 21)),
-                                              (8, "7pt", (24, 24, 64)), (4, "5pt", (40, 34))])
-def test_device_setup_equals_host_multirank(nranks, kind, dims):
-    """SURVEY 8f row f1 on several ranks: the device PMIS + classical interpolation (rank rows
-    with global column ids, halo states forwarded each round, ghost rows of A for the strong F
-    neighbours) builds the same hierarchy as the host path, level by level and bit for bit --
-    A, P, R and the C/F split of every rank."""
+@pytest.mark.parametrize("nranks,kind,dims,coarsen", [(2, "7pt", (16, 15, 18), "pmis"), (3, "7pt", (14, 14, 21), "pmis"),
+                                                      (8, "7pt", (24, 24, 64), "pmis"), (4, "5pt", (40, 34), "pmis"),
+                                                      (3, "27pt", (10, 11, 16), "sa"), (8, "7pt", (24, 24, 64), "sa")])
+def test_device_setup_equals_host_multirank(nranks, kind, dims, coarsen):
+    """SURVEY 8f row f1 on several ranks: the device PMIS + classical interpolation and MIS(2)
+    + smoothed prolongator (rank rows with global column ids, halo states forwarded each round,
+    ghost rows of A for the strong F neighbours) build the same hierarchy as the host path,
+    level by level and bit for bit -- A, P, R and the C/F split / aggregate ids of every rank."""
     import raptor_amd as ra
 
     def rank(r, nr, world):
@@ -305,7 +324,8 @@ def test_device_setup_equals_host_multirank(nranks, kind, dims):
         A = ra.par_stencil_grid(ctx, kind, dims)
         out = []
         for m in (1, 0):
-            ml = ra.ParRugeStubenSolver(coarsen="pmis", setup_device=m, replicate_below=0).setup(A)
+            ml = ra.ParMultilevel(coarsen=coarsen, smoother="jacobi" if coarsen == "pmis" else "hybrid_gs",
+                                  setup_device=m, replicate_below=0).setup(A)
             lev = []
             for l in range(ml.num_levels):
                 mats = {w: ml.level_matrix(l, w).to_scipy_local() for w in ("APR" if l + 1 < ml.num_levels else "A")}
