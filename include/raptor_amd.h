@@ -238,10 +238,13 @@ int amg_solver_solve(amg_solver S, double* x, const double* b, int32_t max_iter,
  * caller of the cycle).  Same contract as amg_solver_solve; hist receives ||r_k||. */
 int amg_solver_pcg(amg_solver S, double* x, const double* b, int32_t max_iter, double tol,
                    double* hist, int32_t* iters);
-/* Capture each V-cycle in a hipGraph and replay it (1 = on; default on for 1 rank, off for
- * several: loopback ranks meet at host barriers; with the RCCL transport capture is allowed
- * (the send/recv groups and allgathers are captured with the kernels) but experimental --
- * see DESIGN.md 5). */
+/* Capture each V-cycle in a hipGraph and replay it (1 = on).  Default: on for 1 rank; off
+ * for loopback ranks (they meet at host barriers); for RCCL ranks on where the process runs
+ * the runtime whole-cycle capture was validated on (HIP >= 7.2 with RCCL >= 2.27.7: the
+ * send/recv groups and allgathers are captured with the kernels, each replay waited for
+ * before the next enqueue).  On older runtimes (torch's bundled HIP 7.0 / RCCL 2.26.6)
+ * enable = 1 with several ranks returns AMG_ERR_INVALID naming the versions;
+ * AMG_RCCL_GRAPH=1 / 0 in the environment overrides the version check. */
 int amg_solver_set_graph(amg_solver S, int32_t enable);
 /* 1 while cycles replay a hipGraph (0 after set_graph(0), or if the runtime refused to
  * instantiate a multi-rank graph and the solver fell back to eager launches). */

@@ -586,13 +586,10 @@ int amg_solver_set_graph(amg_solver S, int32_t enable) {
         AMG_CHECK(!enable || S->s.ctx->host.nranks == 1 || S->s.ctx->transport == TR_RCCL,
                   "hipGraph capture needs one rank or the RCCL transport (loopback ranks "
                   "synchronise on the host)");
-        // capturing the RCCL groups of a multi-rank cycle is validated only where the capture
-        // tests run; elsewhere it stays behind an explicit opt-in
-        if (enable && S->s.ctx->host.nranks > 1) {
-            const char* e = std::getenv("AMG_RCCL_GRAPH");
-            AMG_CHECK(e && std::atoi(e) != 0,
-                      "multi-rank hipGraph capture of RCCL cycles is experimental: set AMG_RCCL_GRAPH=1");
-        }
+        // capturing the RCCL groups of a multi-rank cycle: only on the runtime it was
+        // validated on
+        std::string why;
+        if (enable && S->s.ctx->host.nranks > 1) AMG_CHECK(Solver::rccl_graph_allowed(&why), why);
         S->s.use_graph = enable != 0;
         for (auto& g : S->s.graphs)
             if (g.exec) {

@@ -126,6 +126,9 @@ struct Context {
 
 // Galerkin SpGEMM on the device (spgemm.hip); result downloaded as a host image
 HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, const HostCSR& B);
+// R (A P), A P kept on the device between the products where it can be (one rank)
+HostCSR galerkin_device(Context& ctx, const HostComm& comm, const HostCSR& R, const HostCSR& A,
+                        const HostCSR& P);
 // device setup of one level (setup_device.hip, single rank): strength, PMIS or MIS(2)
 // aggregation, classical or smoothed-aggregation P; false where it does not apply
 bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, const amg_options& opt,
@@ -278,6 +281,8 @@ struct DevMatrix {
     // replicated: a whole matrix held by every rank (one-rank view, no halo, no exchange)
     bool replicated = false;
     void build(Context* c, HostCSR&& h, bool replicated_view = false);
+    // the same formats from a CSR that stays the caller's (moved into `host` afterwards)
+    void build_view(Context* c, const HostCSR& h, bool replicated_view = false);
     void ensure_gs_blocks(int64_t block);
     // start the halo exchange of x (pack on the compute stream, RCCL on the comm stream);
     // returns true when a boundary phase is needed
@@ -393,6 +398,9 @@ struct Solver {
     DevBuf<unsigned> norm_done;
     NormSink sink;
     bool use_graph = true;
+    // multi-rank capture of whole cycles (RCCL groups inside the graph): allowed on the
+    // runtime it was validated on; *why gets the reason when it is not
+    static bool rccl_graph_allowed(std::string* why = nullptr);
     struct Graph {
         hipGraphExec_t exec = nullptr;
         const double* x = nullptr;

@@ -11,6 +11,7 @@
 // touches it (RCCL, see device.hpp).
 #pragma once
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <stdexcept>
 #include <string>
@@ -149,7 +150,9 @@ struct HostLevel {
     std::vector<int32_t> split;
 };
 struct HostHierarchy {
-    std::vector<HostLevel> levels;
+    // a deque: levels keep their addresses as the hierarchy grows (Solver::setup builds a
+    // level's device formats on a worker thread while the next level is coarsened)
+    std::deque<HostLevel> levels;
     std::vector<double> coarse_inv;  // row-major n_c x n_c
     const HostCSR* A0 = nullptr;
     const HostCSR& A(size_t l) const { return l == 0 ? *A0 : levels[l].A; }
@@ -162,9 +165,16 @@ using SpgemmFn = std::function<HostCSR(const HostCSR&, const HostCSR&)>;
 // host algorithms below run instead); results are identical either way.
 using LevelSetupFn = std::function<bool(int level, const HostCSR& A, HostCSR& P, std::vector<int32_t>& split)>;
 using TransposeFn = std::function<bool(const HostCSR& P, HostCSR& R)>;
+// called once level l is final (its P, R and the coarse operator A_{l+1}); none of the three
+// is written again by build_hierarchy
+using LevelDoneFn = std::function<void(int level)>;
+// the whole Galerkin product R (A P) in one hook (the device keeps A P between the two
+// products); when absent, two SpgemmFn / spgemm() calls
+using RapFn = std::function<HostCSR(const HostCSR& R, const HostCSR& A, const HostCSR& P)>;
 void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options& opt,
                      HostHierarchy& H, const SpgemmFn& galerkin = nullptr,
-                     const LevelSetupFn& level_fn = nullptr, const TransposeFn& transpose_fn = nullptr);
+                     const LevelSetupFn& level_fn = nullptr, const TransposeFn& transpose_fn = nullptr,
+                     const LevelDoneFn& level_done = nullptr, const RapFn& rap_fn = nullptr);
 
 uint64_t mix64(uint64_t z);
 uint32_t hash32(int64_t gid, uint64_t seed);

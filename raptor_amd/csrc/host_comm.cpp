@@ -172,9 +172,16 @@ HaloPlan build_halo_plan(const HostComm& comm, const std::vector<int64_t>& start
 
 HaloPlan halo_plan_for_cols(const HostComm& comm, const HostCSR& A) {
     int64_t lo = A.col_starts[comm.rank], hi = A.col_starts[comm.rank + 1];
+    // off-process columns, collected per chunk in parallel and concatenated in order
+    const int64_t nz = (int64_t)A.col.size();
+    const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(256, nz / (1 << 20)));
+    std::vector<std::vector<int64_t>> part((size_t)nch);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int c = 0; c < nch; ++c)
+        for (int64_t k = nz * c / nch; k < nz * (c + 1) / nch; ++k)
+            if (A.col[k] < lo || A.col[k] >= hi) part[(size_t)c].push_back(A.col[k]);
     std::vector<int64_t> need;
-    for (int64_t c : A.col)
-        if (c < lo || c >= hi) need.push_back(c);
+    for (auto& p : part) need.insert(need.end(), p.begin(), p.end());
     return build_halo_plan(comm, A.col_starts, std::move(need));
 }
 

@@ -601,7 +601,8 @@ std::vector<double> dense_inverse_gathered(const HostComm& comm, const HostCSR& 
 
 void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options& opt,
                      HostHierarchy& H, const SpgemmFn& galerkin, const LevelSetupFn& level_fn,
-                     const TransposeFn& transpose_fn) {
+                     const TransposeFn& transpose_fn, const LevelDoneFn& level_done,
+                     const RapFn& rap_fn) {
     AMG_CHECK(opt.max_levels >= 1, "max_levels must be >= 1");
     auto mm = [&](const HostCSR& X, const HostCSR& Y) {
         return galerkin ? galerkin(X, Y) : spgemm(comm, X, Y);
@@ -649,15 +650,22 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
         HostCSR R;
         if (!(transpose_fn && transpose_fn(P, R))) R = transpose(comm, P);
         tm.lap(L + "transpose");
-        HostCSR AP = mm(A, P);
-        tm.lap(L + "A*P");
-        HostCSR Ac = mm(R, AP);
-        tm.lap(L + "R*(AP)");
+        HostCSR Ac;
+        if (rap_fn) {
+            Ac = rap_fn(R, A, P);
+            tm.lap(L + "R*(AP)");
+        } else {
+            HostCSR AP = mm(A, P);
+            tm.lap(L + "A*P");
+            Ac = mm(R, AP);
+            tm.lap(L + "R*(AP)");
+        }
         H.levels[l].split = std::move(split);
         H.levels[l].P = std::move(P);
         H.levels[l].R = std::move(R);
         H.levels.emplace_back();
         H.levels[l + 1].A = std::move(Ac);
+        if (level_done) level_done(l);
     }
     const HostCSR& Ac = H.A(H.levels.size() - 1);
     AMG_CHECK(Ac.n_global_rows <= 20000,

@@ -2,12 +2,90 @@
 // SURVEY.md 8a rows a6-a10.  The cycle mirrors oracle/amg_oracle.c cycle_rec() operation
 // for operation, so the iterates are bit-identical to the oracle's.
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
+#include <exception>
+#include <mutex>
+#include <thread>
 
 #include "device.hpp"
 
 namespace amg {
+
+namespace {
+
+// AMG_SETUP_OVERLAP=0: build the device formats after the whole hierarchy (A/B)
+bool setup_overlap() {
+    static const bool on = [] {
+        const char* e = std::getenv("AMG_SETUP_OVERLAP");
+        return !(e && *e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
+// One worker thread that builds device formats (DevMatrix::build_view: host C++ format
+// builds + uploads) in FIFO order while the setup thread coarsens the next level: level l's
+// P and R and A_{l+1} are final once build_hierarchy reports level l done.  One rank only:
+// a multi-rank build_view runs host collectives (the halo plan), which must not interleave
+// with the hierarchy's.
+class FormatWorker {
+  public:
+    explicit FormatWorker(int device) : th_([this, device] { run(device); }) {}
+    ~FormatWorker() {
+        if (th_.joinable()) stop();
+    }
+    void push(std::function<void()> job) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(std::move(job));
+        }
+        cv_.notify_one();
+    }
+    // waits for every queued job; rethrows the first failure
+    void finish() {
+        stop();
+        if (err_) std::rethrow_exception(err_);
+    }
+
+  private:
+    void stop() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            done_ = true;
+        }
+        cv_.notify_one();
+        th_.join();
+    }
+    void run(int device) {
+        const hipError_t e = hipSetDevice(device);
+        for (;;) {
+            std::function<void()> job;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [this] { return done_ || !q_.empty(); });
+                if (q_.empty()) return;
+                job = std::move(q_.front());
+                q_.pop_front();
+            }
+            if (err_) continue;  // after a failure: drain, report the first one
+            try {
+                HIP_CHECK(e);
+                job();
+            } catch (...) {
+                err_ = std::current_exception();
+            }
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    bool done_ = false;
+    std::exception_ptr err_;
+    std::thread th_;
+};
+
+}  // namespace
 
 Solver::~Solver() {
     for (auto& g : graphs)
@@ -29,9 +107,13 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     SpgemmFn galerkin = nullptr;
     LevelSetupFn level_fn = nullptr;
     TransposeFn transpose_fn = nullptr;
+    RapFn rap_fn = nullptr;
     if (opt.setup_device) {
         galerkin = [this, &comm](const HostCSR& X, const HostCSR& Y) {
             return spgemm_device(*ctx, comm, X, Y);
+        };
+        rap_fn = [this, &comm](const HostCSR& R, const HostCSR& Am, const HostCSR& P) {
+            return galerkin_device(*ctx, comm, R, Am, P);
         };
         // setup_device == 1: the whole level setup on the GPU where it applies (one rank);
         // 2: Galerkin products only (the round-1 split, for A/B and tests)
@@ -45,11 +127,34 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         }
     }
     PhaseTimer tm(comm);
+    // device formats of finished levels, built on a worker thread during the hierarchy
+    const bool overlap = comm.nranks == 1 && setup_overlap();
+    const size_t maxl = (size_t)std::max(opt.max_levels, 1) + 1;
+    std::vector<std::unique_ptr<DevMatrix>> preA(maxl), preP(maxl), preR(maxl);
     {
         RoctxRange r("setup: hierarchy (strength, split / aggregates, P, R, Galerkin)");
-        build_hierarchy(comm, A.host, opt, H, galerkin, level_fn, transpose_fn);
+        std::unique_ptr<FormatWorker> worker;
+        LevelDoneFn done = nullptr;
+        if (overlap) {
+            worker.reset(new FormatWorker(ctx->device));
+            done = [&](int l) {
+                auto job = [this](std::unique_ptr<DevMatrix>& slot, const HostCSR& M) {
+                    return [this, &slot, &M] {
+                        std::unique_ptr<DevMatrix> d(new DevMatrix());
+                        d->build_view(ctx, M);
+                        slot = std::move(d);
+                    };
+                };
+                worker->push(job(preP[l], H.levels[l].P));
+                worker->push(job(preR[l], H.levels[l].R));
+                worker->push(job(preA[l + 1], H.levels[l + 1].A));
+            };
+        }
+        build_hierarchy(comm, A.host, opt, H, galerkin, level_fn, transpose_fn, done, rap_fn);
+        tm.lap("hierarchy (host + SpGEMM)");
+        if (worker) worker->finish();
+        if (overlap) tm.lap("format builds still running after the hierarchy");
     }
-    tm.lap("hierarchy (host + SpGEMM)");
     // replicated coarse levels (multi-rank): from the first level with <= replicate_below
     // global rows on, every rank holds the whole operators and cycles them locally
     rep_level = -1;
@@ -65,19 +170,24 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     for (size_t l = 0; l < H.levels.size(); ++l) {
         HostLevel& hl = H.levels[l];
         const bool rep = rep_level >= 0 && (int)l >= rep_level;
-        auto make = [&](HostCSR& M) {
-            std::unique_ptr<DevMatrix> d(new DevMatrix());
+        auto make = [&](HostCSR& M, std::unique_ptr<DevMatrix>& pre) {
+            std::unique_ptr<DevMatrix> d(std::move(pre));
+            if (d) {
+                d->host = std::move(M);  // built from M on the worker
+                return d;
+            }
+            d.reset(new DevMatrix());
             if (rep) d->build(ctx, gather_global(comm, M), true);
             else d->build(ctx, std::move(M));
             return d;
         };
-        if (l > 0) levels[l].A = make(hl.A);
-        tm.lap("L" + std::to_string(l) + " device A build");
+        if (l > 0) levels[l].A = make(hl.A, preA[l]);
+        if (!overlap) tm.lap("L" + std::to_string(l) + " device A build");
         if (l + 1 < H.levels.size()) {
             levels[l].split = std::move(hl.split);
-            levels[l].P = make(hl.P);
-            levels[l].R = make(hl.R);
-            tm.lap("L" + std::to_string(l) + " device P/R build");
+            levels[l].P = make(hl.P, preP[l]);
+            levels[l].R = make(hl.R, preR[l]);
+            if (!overlap) tm.lap("L" + std::to_string(l) + " device P/R build");
         }
     }
     if (rep_level > 0) {  // transition: distributed R output -> whole vector on every rank
@@ -142,11 +252,29 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         bfull.alloc((size_t)cmax * comm.nranks + (size_t)cmax + (size_t)coarse_n);
         HIP_CHECK(hipMemset(bfull.p, 0, bfull.n * sizeof(double)));
     }
-    // multi-rank cycles run eagerly by default: loopback ranks meet at host barriers, which a
-    // graph cannot replay, and capturing the RCCL groups (amg_solver_set_graph(1) allows it)
-    // crashed in hipStreamEndCapture on the 1-GPU socket-transport test setup (torch's RCCL
-    // 2.26.6 in the process) -- not validated over xGMI
-    use_graph = comm.nranks == 1;
+    // multi-rank cycles: loopback ranks meet at host barriers, which a graph cannot replay;
+    // RCCL ranks capture whole cycles where the runtime is the one capture was validated on
+    use_graph = comm.nranks == 1 || (ctx->transport == TR_RCCL && rccl_graph_allowed());
+}
+
+// Whole-cycle capture with RCCL groups inside: on HIP 7.0.51831 + RCCL 2.26.6
+// (the copies torch bundles, which a torch-first process binds) hipStreamEndCapture segfaults;
+// on ROCm 7.2's HIP 7.2.26015 + RCCL 2.27.7 (torch-free callers) captured cycles replay
+// bit-exact.  AMG_RCCL_GRAPH=0 / 1 overrides the version check either way.
+bool Solver::rccl_graph_allowed(std::string* why) {
+    static const int forced = [] {
+        const char* e = std::getenv("AMG_RCCL_GRAPH");
+        return e && *e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
+    }();
+    int hv = 0, nv = 0;
+    (void)hipRuntimeGetVersion(&hv);
+    (void)ncclGetVersion(&nv);
+    const bool ok = forced >= 0 ? forced == 1 : hv >= 70200000 && nv >= 22707;
+    if (!ok && why)
+        *why = "multi-rank hipGraph capture of RCCL cycles is validated on HIP >= 7.2 with RCCL >= "
+               "2.27.7; this process runs HIP " + std::to_string(hv) + " with RCCL " +
+               std::to_string(nv) + (forced == 0 ? " (AMG_RCCL_GRAPH=0)" : " (AMG_RCCL_GRAPH=1 overrides)");
+    return ok;
 }
 
 void Solver::ensure_hist(int32_t n) {
@@ -328,6 +456,14 @@ void Solver::cycle(double* x, const double* b, bool with_norm) {
     HIP_CHECK(hipGraphLaunch(G.exec, s));
     static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
     if (trace) std::fprintf(stderr, "[amg] rank %d graph launched\n", ctx->host.rank);
+    // a multi-rank replay completes before anything else is enqueued: replays queued back to
+    // back and followed by eager RCCL work never finished on the socket transport (the ROCm 7.2
+    // probes); one host wait per cycle.  AMG_RCCL_GRAPH_SYNC=0: no wait (probes)
+    static const bool sync_replay = [] {
+        const char* e = std::getenv("AMG_RCCL_GRAPH_SYNC");
+        return !(e && *e && std::atoi(e) == 0);
+    }();
+    if (sync_replay && ctx->host.nranks > 1) HIP_CHECK(hipStreamSynchronize(s));
 }
 
 int32_t Solver::solve(double* x, const double* b, int32_t max_iter, double tol, double* hist_host) {

@@ -180,7 +180,7 @@ static inline size_t lane_pos(int j, int nu) {
 // offset in vofs (header field 0, unused by the gather kernel otherwise).
 static int gather_slots(int nz) { return nz > 4 * kTPB ? 8 : nz > 2 * kTPB ? 4 : 2; }
 
-static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const BlockBuild& bb,
+static void build_value_index(DevMatrix& M, const HostCSR& H, const std::vector<int>& hrp, const BlockBuild& bb,
                               std::vector<int>& vt_off, std::vector<int>& vt_len,
                               std::vector<uint8_t>& dvi, std::vector<char>& dvi_ok,
                               std::vector<int64_t>& vofs) {
@@ -192,7 +192,7 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
         const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
         if (nz > kCAP || nz == 0) continue;
         std::vector<uint64_t> t(nz);
-        std::memcpy(t.data(), M.host.val.data() + kb, sizeof(double) * (size_t)nz);
+        std::memcpy(t.data(), H.val.data() + kb, sizeof(double) * (size_t)nz);
         std::sort(t.begin(), t.end());
         t.erase(std::unique(t.begin(), t.end()), t.end());
         if (t.size() <= 256) tabs[q] = std::move(t);
@@ -239,7 +239,7 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
         const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
         for (int j = 0; j < nz; ++j) {
             uint64_t bits;
-            std::memcpy(&bits, M.host.val.data() + kb + j, sizeof(bits));
+            std::memcpy(&bits, H.val.data() + kb + j, sizeof(bits));
             const size_t at = std::lower_bound(t.begin(), t.end(), bits) - t.begin();
             // square (x-tile kernel): entry pairs; rectangular (gather kernel): entry j at
             // lane j % kTPB, slot j / kTPB, NU slots per lane
@@ -250,15 +250,15 @@ static void build_value_index(DevMatrix& M, const std::vector<int>& hrp, const B
         if (!M.square) continue;
         bool ok = true;
         for (int r = bb.blocks[q].x; r < bb.blocks[q].y; ++r) {
-            int64_t k = M.host.rp[r], e = M.host.rp[r + 1];
+            int64_t k = H.rp[r], e = H.rp[r + 1];
             const int64_t g = M.first_row + r;
-            while (k < e && M.host.col[k] < g) ++k;
-            if (k == e || M.host.col[k] != g || M.host.val[k] == 0.0) {
+            while (k < e && H.col[k] < g) ++k;
+            if (k == e || H.col[k] != g || H.val[k] == 0.0) {
                 ok = false;
                 continue;
             }
             uint64_t bits;
-            std::memcpy(&bits, M.host.val.data() + k, sizeof(bits));
+            std::memcpy(&bits, H.val.data() + k, sizeof(bits));
             dvi[r] = (uint8_t)(std::lower_bound(t.begin(), t.end(), bits) - t.begin());
         }
         dvi_ok[q] = ok;
@@ -432,8 +432,15 @@ static TplBuild build_templates(const std::vector<int>& rp, const std::vector<in
 }
 
 void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
-    ctx = c;
+    build_view(c, h, replicated_view);
     host = std::move(h);
+}
+
+// Every device format from a CSR the caller keeps (the member `host` is shadowed by the
+// argument): Solver::setup runs this on a worker thread while the hierarchy thread still
+// reads the same CSR, and moves it into `host` after both are done.
+void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view) {
+    ctx = c;
     replicated = replicated_view;
     static const HostComm serial;  // rank 0 of 1: replicated matrices have no halo
     const HostComm& comm = replicated ? serial : ctx->host;
@@ -454,8 +461,10 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
 
     std::vector<int> hrp(n_rows + 1), hcol(nnz);
     std::vector<uint8_t> cls(n_rows, 0);
+#pragma omp parallel for schedule(static)
     for (int64_t i = 0; i <= n_rows; ++i) hrp[i] = (int)host.rp[i];
     const int64_t clo = first_col, chi = first_col + n_cols_local;
+#pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n_rows; ++i) {
         uint8_t b = 0;
         for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) {
@@ -474,6 +483,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
     if (square) {
         std::vector<double> d = diagonal(comm, host);
         di.resize(n_rows);
+#pragma omp parallel for schedule(static)
         for (int64_t i = 0; i < n_rows; ++i) di[i] = 1.0 / d[i];
         dinv.upload(di.data(), di.size());
     }
@@ -754,7 +764,7 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
         std::vector<uint8_t> hdvi;
         std::vector<char> dvi_ok;
         std::vector<int64_t> vofs;
-        build_value_index(*this, hrp, bb, vt_off, vt_len, hdvi, dvi_ok, vofs);
+        build_value_index(*this, host, hrp, bb, vt_off, vt_len, hdvi, dvi_ok, vofs);
         if (n_vi_blocks > 0 && square) dvi.upload(hdvi.data(), hdvi.size());
         else dvi.reset();
         tm.lap("    build: value index");

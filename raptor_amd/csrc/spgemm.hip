@@ -13,6 +13,8 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <array>
+#include <functional>
 #include <numeric>
 
 #include "device.hpp"
@@ -137,10 +139,185 @@ void launch_bin(hipStream_t s, const std::vector<int>& rows, DevBuf<int>& drows,
                 double* cval) {
     if (rows.empty()) return;
     drows.upload(rows.data(), rows.size());
-    hipLaunchKernelGGL((spgemm_rows_kernel<T, NUMERIC>), dim3((unsigned)rows.size()), dim3(kWave), 0, s,
-                       drows.p, (int)rows.size(), arp, acol, aval, brp, bcol, bval, counts, crp, ccol,
-                       cval);
-    HIP_CHECK(hipGetLastError());
+    // a launch covers at most 2^24 rows: HIP counts a grid in threads (uint32 per dimension),
+    // and one 64-lane workgroup per row of a 512^3 level (134M rows) would exceed it
+    constexpr size_t kMaxRows = size_t(1) << 24;
+    for (size_t off = 0; off < rows.size(); off += kMaxRows) {
+        const size_t cnt = std::min(kMaxRows, rows.size() - off);
+        hipLaunchKernelGGL((spgemm_rows_kernel<T, NUMERIC>), dim3((unsigned)cnt), dim3(kWave), 0, s,
+                           drows.p + off, (int)cnt, arp, acol, aval, brp, bcol, bval, counts, crp, ccol, cval);
+        HIP_CHECK(hipGetLastError());
+    }
+}
+
+}  // namespace
+
+namespace {
+
+// C = A * B with B's row image on the device: brp (host and device copies), bcol, bval.
+// acol: A's columns as rows of that image; ub: per row the bound sum_k |B_k|.  C stays on
+// the device (crp also on the host); rows that overflow the largest LDS table are computed on
+// the host (bhost() supplies B's host arrays for them) and uploaded into place.
+struct DevCSR64 {
+    std::vector<long long> rp;  // host copy
+    DevBuf<long long> d_rp, d_col;
+    DevBuf<double> d_val;
+    int64_t nnz() const { return rp.empty() ? 0 : rp.back(); }
+};
+
+struct BImage {
+    const long long* brp_host;  // nb + 1 entries
+    const long long *d_brp, *d_bcol;
+    const double* d_bval;
+    int64_t ncol;  // global column count (host fallback accumulators)
+    // host arrays of the image for the rare fallback rows: col / val of image entry q
+    std::function<void(std::function<int64_t(long long)>&, std::function<double(long long)>&)> bhost;
+};
+
+void spgemm_core(Context& ctx, PhaseTimer& tm, const HostCSR& A, const std::vector<int>& acol,
+                 const std::vector<int64_t>& ub, const BImage& B, DevCSR64& C) {
+    const int64_t n = A.nrows();
+    // bins by table size (load factor <= 1/2 on the upper bound); rows beyond the largest
+    // table try it anyway (their distinct columns are usually far fewer than the bound) and
+    // fall back to the host only when it overflows.  Chunks bin in parallel and concatenate
+    // in chunk order: each bin lists its rows ascending, as a serial pass would.
+    static constexpr int kBins[] = {256, 1024, 4096, 8192};
+    std::vector<int> bins[4];
+    {
+        const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(256, n / 65536));
+        std::vector<std::array<std::vector<int>, 4>> part((size_t)nch);
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int c = 0; c < nch; ++c) {
+            const int64_t r0 = n * c / nch, r1 = n * (c + 1) / nch;
+            for (int64_t i = r0; i < r1; ++i) {
+                int b = 0;
+                while (b < 3 && 2 * ub[i] > kBins[b]) ++b;
+                part[(size_t)c][b].push_back((int)i);
+            }
+        }
+        for (int b = 0; b < 4; ++b) {
+            size_t tot = 0;
+            for (auto& pc : part) tot += pc[b].size();
+            bins[b].reserve(tot);
+            for (auto& pc : part) bins[b].insert(bins[b].end(), pc[b].begin(), pc[b].end());
+        }
+    }
+    tm.lap("    spgemm: bins");
+    hipStream_t s = ctx.stream;
+    DevBuf<long long> d_arp, d_counts;
+    DevBuf<int> d_acol, d_rows[4];
+    DevBuf<double> d_aval;
+    d_arp.upload(reinterpret_cast<const long long*>(A.rp.data()), A.rp.size());
+    d_acol.upload(acol.data(), acol.size());
+    d_aval.upload(A.val.data(), A.val.size());
+    d_counts.alloc((size_t)std::max<int64_t>(n, 1));
+    HIP_CHECK(hipMemsetAsync(d_counts.p, 0, sizeof(long long) * d_counts.n, s));
+    tm.lap("    spgemm: uploads of A");
+#define AMG_BIN(T, NUM, b)                                                                          \
+    launch_bin<T, NUM>(s, bins[b], d_rows[b], d_arp.p, d_acol.p, d_aval.p, B.d_brp, B.d_bcol,      \
+                       B.d_bval, d_counts.p, C.d_rp.p, C.d_col.p, C.d_val.p)
+    AMG_BIN(256, false, 0);
+    AMG_BIN(1024, false, 1);
+    AMG_BIN(4096, false, 2);
+    AMG_BIN(8192, false, 3);
+    std::vector<long long> counts((size_t)n);
+    if (n) HIP_CHECK(hipMemcpyAsync(counts.data(), d_counts.p, sizeof(long long) * n, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    tm.lap("    spgemm: symbolic");
+    // rows that overflowed the largest table: host, same canonical order, a dense
+    // accumulator per thread (acc_j in k order, then the touched columns sorted)
+    std::vector<int64_t> host_rows;
+    {
+        std::vector<int> keep;
+        for (int i : bins[3])
+            if (counts[i] < 0) host_rows.push_back(i);
+            else keep.push_back(i);
+        bins[3].swap(keep);
+    }
+    std::vector<std::vector<std::pair<int64_t, double>>> hostout(host_rows.size());
+    if (!host_rows.empty()) {
+        std::function<int64_t(long long)> bcol_at;
+        std::function<double(long long)> bval_at;
+        B.bhost(bcol_at, bval_at);
+        const int64_t ncol = B.ncol;
+        // dense accumulators: at most ~2 GB of them across threads
+        const int nth = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)host_rows.size(), (int64_t)omp_get_max_threads(),
+                                                                     (int64_t)2000000000 / (9 * std::max<int64_t>(ncol, 1))}));
+        (void)nth;
+#pragma omp parallel num_threads(nth)
+        {
+            std::vector<double> acc((size_t)ncol, 0.0);
+            std::vector<char> seen((size_t)ncol, 0);
+            std::vector<int64_t> touched;
+#pragma omp for schedule(dynamic, 1)
+            for (size_t t = 0; t < host_rows.size(); ++t) {
+                const int64_t i = host_rows[t];
+                touched.clear();
+                for (int64_t ka = A.rp[i]; ka < A.rp[i + 1]; ++ka) {
+                    const int64_t r = acol[ka];
+                    for (long long q = B.brp_host[r]; q < B.brp_host[r + 1]; ++q) {
+                        const int64_t j = bcol_at(q);
+                        if (!seen[j]) seen[j] = 1, touched.push_back(j);
+                        acc[j] += A.val[ka] * bval_at(q);
+                    }
+                }
+                std::sort(touched.begin(), touched.end());
+                auto& out = hostout[t];
+                out.reserve(touched.size());
+                for (int64_t j : touched) {
+                    out.push_back({j, acc[j]});
+                    acc[j] = 0.0;
+                    seen[j] = 0;
+                }
+                counts[i] = (long long)out.size();
+            }
+        }
+    }
+    tm.lap("    spgemm: host rows (" + std::to_string(host_rows.size()) + ")");
+    C.rp.assign(n + 1, 0);
+    for (int64_t i = 0; i < n; ++i) C.rp[i + 1] = C.rp[i] + counts[i];
+    const int64_t cnnz = C.rp[n];
+    C.d_rp.upload(C.rp.data(), C.rp.size());
+    C.d_col.alloc((size_t)std::max<int64_t>(cnnz, 1));
+    C.d_val.alloc((size_t)std::max<int64_t>(cnnz, 1));
+    AMG_BIN(256, true, 0);
+    AMG_BIN(1024, true, 1);
+    AMG_BIN(4096, true, 2);
+    AMG_BIN(8192, true, 3);
+#undef AMG_BIN
+    for (size_t t = 0; t < host_rows.size(); ++t) {
+        const auto& out = hostout[t];
+        std::vector<long long> hc(out.size());
+        std::vector<double> hv(out.size());
+        for (size_t e = 0; e < out.size(); ++e) hc[e] = out[e].first, hv[e] = out[e].second;
+        const long long at = C.rp[host_rows[t]];
+        if (!out.empty()) {
+            HIP_CHECK(hipMemcpyAsync(C.d_col.p + at, hc.data(), sizeof(long long) * hc.size(), hipMemcpyHostToDevice, s));
+            HIP_CHECK(hipMemcpyAsync(C.d_val.p + at, hv.data(), sizeof(double) * hv.size(), hipMemcpyHostToDevice, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+        }
+    }
+    HIP_CHECK(hipStreamSynchronize(s));
+    tm.lap("    spgemm: numeric");
+}
+
+HostCSR download(Context& ctx, PhaseTimer& tm, const HostCSR& A, const HostCSR& B, DevCSR64& C) {
+    HostCSR out;
+    out.n_global_rows = A.n_global_rows;
+    out.n_global_cols = B.n_global_cols;
+    out.row_starts = A.row_starts;
+    out.col_starts = B.col_starts;
+    out.rp.assign(C.rp.begin(), C.rp.end());
+    const int64_t cnnz = C.nnz();
+    out.col.resize(cnnz);
+    out.val.resize(cnnz);
+    if (cnnz) {
+        HIP_CHECK(hipMemcpyAsync(out.col.data(), C.d_col.p, sizeof(long long) * cnnz, hipMemcpyDeviceToHost, ctx.stream));
+        HIP_CHECK(hipMemcpyAsync(out.val.data(), C.d_val.p, sizeof(double) * cnnz, hipMemcpyDeviceToHost, ctx.stream));
+    }
+    HIP_CHECK(hipStreamSynchronize(ctx.stream));
+    tm.lap("    spgemm: download");
+    return out;
 }
 
 }  // namespace
@@ -170,33 +347,16 @@ HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, cons
         ub[i] = u;
     }
     const int64_t bnnz = brp.back();
+    tm.lap("    spgemm: column map, B image");
     // the B image [local rows | ghost rows] is assembled on the device (two uploads each),
-    // not in a host copy of B; the host fallback reads B or G through bcol_at / bval_at
+    // not in a host copy of B; the host fallback reads B or G in place
     static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
     const int64_t bl = B.nnz();
-    auto bcol_at = [&](long long q) -> int64_t { return q < bl ? B.col[q] : G.col[q - bl]; };
-    auto bval_at = [&](long long q) -> double { return q < bl ? B.val[q] : G.val[q - bl]; };
-    // bins by table size (load factor <= 1/2 on the upper bound); rows beyond the largest
-    // table try it anyway (their distinct columns are usually far fewer than the bound) and
-    // fall back to the host only when it overflows
-    static constexpr int kBins[] = {256, 1024, 4096, 8192};
-    std::vector<int> bins[4];
-    for (int64_t i = 0; i < n; ++i) {
-        int b = 0;
-        while (b < 3 && 2 * ub[i] > kBins[b]) ++b;
-        bins[b].push_back((int)i);
-    }
-    tm.lap("    spgemm: column map, B image, bins");
-    hipStream_t s = ctx.stream;
-    DevBuf<long long> d_arp, d_brp, d_bcol, d_counts, d_crp, d_ccol;
-    DevBuf<int> d_acol, d_rows[4];
-    DevBuf<double> d_aval, d_bval, d_cval;
-    d_arp.upload(reinterpret_cast<const long long*>(A.rp.data()), A.rp.size());
-    d_acol.upload(acol.data(), acol.size());
-    d_aval.upload(A.val.data(), A.val.size());
+    DevBuf<long long> d_brp, d_bcol;
+    DevBuf<double> d_bval;
     d_brp.upload(brp.data(), brp.size());
-    d_bcol.alloc((size_t)bnnz);
-    d_bval.alloc((size_t)bnnz);
+    d_bcol.alloc((size_t)std::max<int64_t>(bnnz, 1));
+    d_bval.alloc((size_t)std::max<int64_t>(bnnz, 1));
     if (bl) {
         HIP_CHECK(hipMemcpy(d_bcol.p, B.col.data(), sizeof(long long) * bl, hipMemcpyHostToDevice));
         HIP_CHECK(hipMemcpy(d_bval.p, B.val.data(), sizeof(double) * bl, hipMemcpyHostToDevice));
@@ -205,96 +365,86 @@ HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, cons
         HIP_CHECK(hipMemcpy(d_bcol.p + bl, G.col.data(), sizeof(long long) * (bnnz - bl), hipMemcpyHostToDevice));
         HIP_CHECK(hipMemcpy(d_bval.p + bl, G.val.data(), sizeof(double) * (bnnz - bl), hipMemcpyHostToDevice));
     }
-    d_counts.alloc((size_t)std::max<int64_t>(n, 1));
-    HIP_CHECK(hipMemsetAsync(d_counts.p, 0, sizeof(long long) * d_counts.n, s));
-    tm.lap("    spgemm: uploads");
-#define AMG_BIN(T, NUM, b)                                                                          \
-    launch_bin<T, NUM>(s, bins[b], d_rows[b], d_arp.p, d_acol.p, d_aval.p, d_brp.p, d_bcol.p,      \
-                       d_bval.p, d_counts.p, d_crp.p, d_ccol.p, d_cval.p)
-    AMG_BIN(256, false, 0);
-    AMG_BIN(1024, false, 1);
-    AMG_BIN(4096, false, 2);
-    AMG_BIN(8192, false, 3);
-    std::vector<long long> counts((size_t)n);
-    if (n) HIP_CHECK(hipMemcpyAsync(counts.data(), d_counts.p, sizeof(long long) * n, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    tm.lap("    spgemm: symbolic");
-    // rows that overflowed the largest table: host, same canonical order, a dense
-    // accumulator per thread (acc_j in k order, then the touched columns sorted)
-    std::vector<int64_t> host_rows;
-    {
-        std::vector<int> keep;
-        for (int i : bins[3])
-            if (counts[i] < 0) host_rows.push_back(i);
-            else keep.push_back(i);
-        bins[3].swap(keep);
-    }
-    std::vector<std::vector<std::pair<int64_t, double>>> hostout(host_rows.size());
-    if (!host_rows.empty()) {
-        const int64_t ncol = B.n_global_cols;
-        // dense accumulators: at most ~2 GB of them across threads
-        const int nth = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)host_rows.size(), (int64_t)omp_get_max_threads(),
-                                                                     (int64_t)2000000000 / (9 * std::max<int64_t>(ncol, 1))}));
-        (void)nth;
-#pragma omp parallel num_threads(nth)
-        {
-            std::vector<double> acc((size_t)ncol, 0.0);
-            std::vector<char> seen((size_t)ncol, 0);
-            std::vector<int64_t> touched;
-#pragma omp for schedule(dynamic, 1)
-            for (size_t t = 0; t < host_rows.size(); ++t) {
-                const int64_t i = host_rows[t];
-                touched.clear();
-                for (int64_t ka = A.rp[i]; ka < A.rp[i + 1]; ++ka) {
-                    const int64_t r = acol[ka];
-                    for (long long q = brp[r]; q < brp[r + 1]; ++q) {
-                        const int64_t j = bcol_at(q);
-                        if (!seen[j]) seen[j] = 1, touched.push_back(j);
-                        acc[j] += A.val[ka] * bval_at(q);
-                    }
-                }
-                std::sort(touched.begin(), touched.end());
-                auto& out = hostout[t];
-                out.reserve(touched.size());
-                for (int64_t j : touched) {
-                    out.push_back({j, acc[j]});
-                    acc[j] = 0.0;
-                    seen[j] = 0;
-                }
-                counts[i] = (long long)out.size();
-            }
+    tm.lap("    spgemm: upload of B");
+    BImage img{brp.data(), d_brp.p, d_bcol.p, d_bval.p, B.n_global_cols,
+               [&](std::function<int64_t(long long)>& ca, std::function<double(long long)>& va) {
+                   ca = [&](long long q) -> int64_t { return q < bl ? B.col[q] : G.col[q - bl]; };
+                   va = [&](long long q) -> double { return q < bl ? B.val[q] : G.val[q - bl]; };
+               }};
+    DevCSR64 C;
+    spgemm_core(ctx, tm, A, acol, ub, img, C);
+    return download(ctx, tm, A, B, C);
+}
+
+// R (A P) with A P kept on the device between the two products (one rank: no ghost rows, so
+// A P's rows are the B image of the second product as they stand).  Several ranks: the two
+// spgemm_device calls (the ghost rows of A P come from other ranks).
+HostCSR galerkin_device(Context& ctx, const HostComm& comm, const HostCSR& R, const HostCSR& A,
+                        const HostCSR& P) {
+    if (comm.nranks > 1) return spgemm_device(ctx, comm, R, spgemm_device(ctx, comm, A, P));
+    AMG_CHECK(A.col_starts == P.row_starts && R.col_starts == A.row_starts, "galerkin: partitions differ");
+    PhaseTimer tm(comm);
+    const int64_t n = A.nrows();
+    // A P: B image = P's rows, A's (global = local) columns index it directly
+    std::vector<int> acol(A.nnz());
+    std::vector<int64_t> ub(n, 0);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t u = 0;
+        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+            acol[k] = (int)A.col[k];
+            u += P.rp[A.col[k] + 1] - P.rp[A.col[k]];
         }
+        ub[i] = u;
     }
-    tm.lap("    spgemm: host rows (" + std::to_string(host_rows.size()) + ")");
-    HostCSR C;
-    C.n_global_rows = A.n_global_rows;
-    C.n_global_cols = B.n_global_cols;
-    C.row_starts = A.row_starts;
-    C.col_starts = B.col_starts;
-    C.rp.assign(n + 1, 0);
-    for (int64_t i = 0; i < n; ++i) C.rp[i + 1] = C.rp[i] + counts[i];
-    const int64_t cnnz = C.rp[n];
-    d_crp.upload(reinterpret_cast<const long long*>(C.rp.data()), C.rp.size());
-    d_ccol.alloc((size_t)std::max<int64_t>(cnnz, 1));
-    d_cval.alloc((size_t)std::max<int64_t>(cnnz, 1));
-    AMG_BIN(256, true, 0);
-    AMG_BIN(1024, true, 1);
-    AMG_BIN(4096, true, 2);
-    AMG_BIN(8192, true, 3);
-#undef AMG_BIN
-    C.col.resize(cnnz);
-    C.val.resize(cnnz);
-    if (cnnz) {
-        HIP_CHECK(hipMemcpyAsync(C.col.data(), d_ccol.p, sizeof(long long) * cnnz, hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipMemcpyAsync(C.val.data(), d_cval.p, sizeof(double) * cnnz, hipMemcpyDeviceToHost, s));
+    static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
+    DevBuf<long long> d_prp, d_pcol;
+    DevBuf<double> d_pval;
+    d_prp.upload(reinterpret_cast<const long long*>(P.rp.data()), P.rp.size());
+    d_pcol.upload(reinterpret_cast<const long long*>(P.col.data()), P.col.size());
+    d_pval.upload(P.val.data(), P.val.size());
+    tm.lap("    galerkin: A column map, upload of P");
+    BImage pimg{reinterpret_cast<const long long*>(P.rp.data()), d_prp.p, d_pcol.p, d_pval.p, P.n_global_cols,
+                [&](std::function<int64_t(long long)>& ca, std::function<double(long long)>& va) {
+                    ca = [&](long long q) -> int64_t { return P.col[q]; };
+                    va = [&](long long q) -> double { return P.val[q]; };
+                }};
+    DevCSR64 AP;
+    spgemm_core(ctx, tm, A, acol, ub, pimg, AP);
+    d_pcol.reset();
+    d_pval.reset();
+    // R (A P): the image is A P on the device
+    const int64_t nr = R.nrows();
+    std::vector<int> rcol(R.nnz());
+    std::vector<int64_t> rub(nr, 0);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < nr; ++i) {
+        int64_t u = 0;
+        for (int64_t k = R.rp[i]; k < R.rp[i + 1]; ++k) {
+            rcol[k] = (int)R.col[k];
+            u += AP.rp[R.col[k] + 1] - AP.rp[R.col[k]];
+        }
+        rub[i] = u;
     }
-    HIP_CHECK(hipStreamSynchronize(s));
-    tm.lap("    spgemm: numeric + download");
-    for (size_t t = 0; t < host_rows.size(); ++t) {
-        int64_t p = C.rp[host_rows[t]];
-        for (auto& e : hostout[t]) C.col[p] = e.first, C.val[p++] = e.second;
-    }
-    return C;
+    tm.lap("    galerkin: R column map");
+    // host copies of A P only if some row of R (A P) overflows the LDS tables
+    std::vector<long long> apc;
+    std::vector<double> apv;
+    BImage apimg{AP.rp.data(), AP.d_rp.p, AP.d_col.p, AP.d_val.p, P.n_global_cols,
+                 [&](std::function<int64_t(long long)>& ca, std::function<double(long long)>& va) {
+                     const int64_t m = AP.nnz();
+                     apc.resize(m);
+                     apv.resize(m);
+                     if (m) {
+                         HIP_CHECK(hipMemcpy(apc.data(), AP.d_col.p, sizeof(long long) * m, hipMemcpyDeviceToHost));
+                         HIP_CHECK(hipMemcpy(apv.data(), AP.d_val.p, sizeof(double) * m, hipMemcpyDeviceToHost));
+                     }
+                     ca = [&](long long q) -> int64_t { return apc[q]; };
+                     va = [&](long long q) -> double { return apv[q]; };
+                 }};
+    DevCSR64 RAP;
+    spgemm_core(ctx, tm, R, rcol, rub, apimg, RAP);
+    return download(ctx, tm, R, P, RAP);
 }
 
 }  // namespace amg

@@ -75,7 +75,7 @@ std::vector<double> solve_7pt(amg::Context& ctx, bool graph, int* levels, bool* 
     amg::ParCSRMatrix A = amg::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 24, 24, 24);
     const int64_t n = A.local_rows(), f = A.first_row();
     amg::ParMultilevel ml(A, amg::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
-    if (graph) ml.set_graph(true);
+    ml.set_graph(graph);  // multi-rank default: on where the runtime is validated (ROCm 7.2)
     const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
     if (trace) std::fprintf(stderr, "[cxx] rows %lld setup done (%d levels)\n", (long long)n, ml.num_levels());
     double *xs = nullptr, *b = nullptr, *x = nullptr;
@@ -102,7 +102,7 @@ int run_solve(const char* golden) {
     amg::Context ctx(0);
     int levels = 0;
     bool used = false;
-    const std::vector<double> h = solve_7pt(ctx, false, &levels, &used);
+    const std::vector<double> h = solve_7pt(ctx, true, &levels, &used);
     for (size_t k = 0; k < h.size(); ++k) std::printf("%zu %.17g\n", k, h[k]);
     if (!used) {  // one rank: cycles replay a hipGraph by default
         std::fprintf(stderr, "expected hipGraph replay on one rank\n");
@@ -214,13 +214,15 @@ int mesh_alltoallv(void* user, const void* sendbuf, const int64_t* send_bytes, v
 // ncclSend/ncclRecv group on the comm stream + interior / boundary kernels) captured on the
 // context stream and replayed, compared with the eager result
 // AMG_CXX_GRAPH_MULT=3: V-cycles replayed from a captured graph, synchronised after each,
-// against the same cycles run eagerly by a second solver on the same matrix
-std::vector<double> graph_cycles(amg::Context& ctx) {
+// against the same cycles run eagerly by a second solver on the same matrix;
+// AMG_CXX_GRAPH_MULT=4: the same, the replays enqueued back to back (one synchronisation)
+std::vector<double> graph_cycles(amg::Context& ctx, bool sync_each) {
     amg::ParCSRMatrix A = amg::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 24, 24, 24);
     const int64_t n = A.local_rows(), f = A.first_row();
     amg::ParMultilevel mg(A, amg::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
     amg::ParMultilevel me(A, amg::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
     mg.set_graph(true);
+    me.set_graph(false);
     double *xs = nullptr, *b = nullptr, *xg = nullptr, *xe = nullptr;
     HIPOK(hipMalloc(&xs, n * sizeof(double)));
     HIPOK(hipMalloc(&b, n * sizeof(double)));
@@ -238,9 +240,11 @@ std::vector<double> graph_cycles(amg::Context& ctx) {
     for (int k = 0; k < 3; ++k) {
         mg.cycle(xg, b);
         std::fprintf(stderr, "[cxx] graph cycle %d enqueued (graph %d)\n", k, (int)mg.graph());
+        if (!sync_each) continue;
         ctx.synchronize();
         std::fprintf(stderr, "[cxx] graph cycle %d done\n", k);
     }
+    ctx.synchronize();
     std::vector<double> hg(n), he(n);
     HIPOK(hipMemcpy(hg.data(), xg, n * sizeof(double), hipMemcpyDeviceToHost));
     HIPOK(hipMemcpy(he.data(), xe, n * sizeof(double), hipMemcpyDeviceToHost));
@@ -305,7 +309,8 @@ int rank_main(Mesh& m, bool graph, const char* golden, int result_fd) {
     const char* gmode = std::getenv("AMG_CXX_GRAPH_MULT");
     const bool gm = gmode != nullptr;
     const std::vector<double> h = !gm ? solve_7pt(ctx, graph, &levels, &used)
-                                  : std::atoi(gmode) == 3 ? graph_cycles(ctx) : graph_mult(ctx);
+                                  : std::atoi(gmode) >= 3 ? graph_cycles(ctx, std::atoi(gmode) == 3)
+                                                          : graph_mult(ctx);
     if (gm) used = graph;
     const int64_t cnt = (int64_t)h.size();
     const char flag = used ? 1 : 0;

@@ -60,7 +60,19 @@ def test_cxx_errors_surface_as_exceptions():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nranks", [2, 3])
-def test_cxx_rccl_ranks_match_golden(nranks):
-    """N forked ranks, RCCL halo exchange (socket transport on one GPU), torch-free."""
-    _run(["ranks", str(nranks), GOLD], timeout=240)
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_cxx_rccl_ranks_match_golden(nranks, graph):
+    """N forked ranks, RCCL halo exchange (socket transport on one GPU), torch-free.  graph:
+    every rank captures whole V-cycles (halo send/recv groups, the coarse allgather and the
+    fused residual-norm allgather inside the graph) and replays them; the driver fails if a
+    rank fell back to eager cycles, and the history must still be the oracle's."""
+    _run(["ranks", str(nranks)] + (["graph"] if graph else []) + [GOLD], timeout=240)
+
+
+@pytest.mark.gpu
+def test_cxx_rccl_graph_cycles_equal_eager():
+    """Captured V-cycles replayed back to back (one synchronisation) equal the same cycles
+    run eagerly by a second solver, bit for bit, on both ranks."""
+    out = _run(["ranks", "2", "graph", GOLD], env_extra={"AMG_CXX_GRAPH_MULT": "4"})
+    assert "replay == eager on every rank" in out

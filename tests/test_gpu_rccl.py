@@ -108,3 +108,39 @@ def test_rccl_vcycle_bit_exact(oracle, tmp_path, nranks, spec, graph):
         assert np.all(np.abs(r["pcg"] - pcg_o) <= 1e-9 * pcg_o[0])
         assert np.array_equal(r["hist"], res[0]["hist"])  # every rank reports the same
         assert bool(r["graph_used"]) == graph  # captured and replayed, no eager fallback
+
+
+def _capture_validated(r):
+    """The runtime multi-rank whole-cycle capture was validated on."""
+    return int(r["hip_runtime"]) >= 70200000 and int(r["rccl"]) >= 22707
+
+
+@pytest.mark.parametrize("graph", [None, True], ids=["default", "graph"])
+def test_rccl_graph_policy_follows_runtime(oracle, tmp_path, graph):
+    """Under torch the library runs on torch's bundled HIP 7.0 + RCCL 2.26.6, where capturing
+    a cycle's RCCL groups segfaults in hipStreamEndCapture: the default stays eager and an
+    explicit set_graph(1) is refused with the versions named.  On ROCm 7.2's runtime (the
+    torch-free C++ caller, tests/test_cxx_caller.py) the same cycles are captured and replay
+    bit-exact."""
+    spec = dict(kind="7pt", dims=[16, 15, 18], coarsen="pmis", smoother="jacobi", rep=0, graph=graph)
+    res = run_rccl(2, spec, tmp_path)
+    for r in res:
+        ok = _capture_validated(r)
+        if graph is True and not ok:
+            msg = str(r["gate_error"])
+            assert "validated on HIP >= 7.2" in msg and str(int(r["rccl"])) in msg
+        else:
+            assert "gate_error" not in r
+            assert bool(r["graph_used"]) == ok
+            O = oracle
+            Ao = O.gen_7pt(*spec["dims"])
+            Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS["pmis"], smoother=O.SMOOTH_JACOBI))
+            for l in range(Ho.num_levels):
+                Ho.set_cuts(l, sorted({int(q["starts"][l]) for q in res}))
+            n = Ao.shape[0]
+            bo = Ao.spmv(O.vec_uniform(n, 42))
+            xo = np.zeros(n)
+            for k in range(3):
+                xo = Ho.cycle(xo, bo)
+                f, m = int(r["f"]), int(r["m"])
+                assert np.array_equal(r[f"x{k}"], xo[f:f + m]), ("cycle", k)

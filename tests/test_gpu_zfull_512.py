@@ -1,8 +1,11 @@
-"""configs[3] at its real size (BASELINE.json:10): 7-pt Poisson 512^3 = 134,217,728 rows and
+"""(Named to run after the other -m gpu files: a failure here cannot stop them under -x.)
+
+configs[3] at its real size (BASELINE.json:10): 7-pt Poisson 512^3 = 134,217,728 rows and
 937,951,232 nonzeros, near the int32 index ranges of the device formats, the device setup and
 the SpGEMM.  On one MI355X, with no scaling claim:
   * 1 rank, GPU setup (strength, PMIS, interpolation, transpose, Galerkin SpGEMM on the device);
-  * 8 loopback ranks (z-slabs of 64 planes, the configs[3] partition), host setup;
+  * 8 loopback ranks (z-slabs of 64 planes), GPU setup on every rank (halo states of each
+    round through the host exchange), the host's distributed transpose;
 and the two must agree: identical per-level global sizes and nonzero counts, and every rank's
 slice of the first V-cycle iterate bit-identical to the 1-rank iterate.  The plain-CSR A*1
 equals the integer row sums (the number of missing neighbours of each grid point), exactly.
@@ -101,7 +104,7 @@ def test_512cubed_one_rank_vs_eight_loopback_ranks(capfd, monkeypatch):
     ctx.synchronize()
     torch.cuda.empty_cache()
 
-    # ---- 8 loopback ranks, host setup ------------------------------------------------------
+    # ---- 8 loopback ranks ------------------------------------------------------------------
     world = "w512-" + uuid.uuid4().hex
     out = [None] * NRANKS
     errs = [None] * NRANKS
@@ -115,7 +118,7 @@ def test_512cubed_one_rank_vs_eight_loopback_ranks(capfd, monkeypatch):
             mr = ra.ParRugeStubenSolver(coarsen="pmis").setup(Ar)
             st = time.perf_counter() - tr
             if r == 0:
-                say(f"{NRANKS} ranks: host setup {st:.1f}s")
+                say(f"{NRANKS} ranks: setup {st:.1f}s")
             sizes = [(mr.level_info(l)["n_global"], mr.level_info(l)["nnz_global"]) for l in range(mr.num_levels)]
             with torch.cuda.stream(c.stream):
                 xr = ra.vector_uniform(c, m, f, 42)
