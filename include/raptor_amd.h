@@ -154,6 +154,11 @@ int amg_par_csr_info(amg_matrix A, amg_matrix_info* info);
 #define AMG_FORMAT_CSR 1
 #define AMG_FORMAT_BLOCKS 2
 int amg_par_csr_set_format(amg_matrix A, int32_t format);
+/* Diagnostic: a 64-bit FNV-1a digest over the device format arrays of A (block-aligned col /
+ * val streams, block list and headers, x-tile ids and indices, value tables and indices,
+ * diagonal slots, row ends), so two builds of one operator can be compared byte for byte
+ * (the GPU-built formats against the host builders, AMG_DEVICE_FORMATS=0). */
+int amg_par_csr_format_digest(amg_matrix A, uint64_t* digest);
 /* Host copy of the local rows (global column ids). */
 int amg_par_csr_export(amg_matrix A, int64_t* row_ptr, int64_t* col_global, double* val);
 

@@ -256,6 +256,13 @@ class ParCSRMatrix:
         self.info = self._info()
         return self
 
+    def format_digest(self) -> int:
+        """FNV-1a digest of this matrix's device format arrays (diagnostic: two builds of
+        one operator compare byte for byte)."""
+        d = C.c_uint64()
+        check(lib().amg_par_csr_format_digest(self.h, C.byref(d)))
+        return d.value
+
     def mult(self, x, y):
         check(lib().amg_par_csr_mult(self.h, _ptr(x), _ptr(y)))
         return y

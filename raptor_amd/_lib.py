@@ -116,6 +116,7 @@ SIGNATURES = {
     "amg_par_csr_info": (C.c_int, [_vp, C.POINTER(MatrixInfo)]),
     "amg_par_csr_export": (C.c_int, [_vp, _pi64, _pi64, _pf64]),
     "amg_par_csr_set_format": (C.c_int, [_vp, _i32]),
+    "amg_par_csr_format_digest": (C.c_int, [_vp, C.POINTER(C.c_uint64)]),
     "amg_par_graph_laplacian_create": (C.c_int, [_vp, _i64, _i64, C.c_uint64, C.POINTER(_vp)]),
     "amg_par_csr_read": (C.c_int, [_vp, C.c_char_p, C.POINTER(_vp)]),
     "amg_par_csr_write": (C.c_int, [_vp, C.c_char_p]),

@@ -100,6 +100,14 @@ static void amg_crash_handler(int sig) {
 
 // (re)installed at context creation and again right before a hipGraph capture: runtimes
 // loaded later (RCCL, a framework) may have replaced the handler in between
+// OpenMP threads of the host setup loops sleep as soon as a parallel region ends
+// (KMP_BLOCKTIME=0, unless the caller set it): the LLVM runtime's default keeps them spinning
+// for 200 ms, and on a CPU-quota'd host (a container's cgroup) two spinning teams -- the setup
+// thread's and the format worker's -- exhausted the quota and stalled the launching thread
+// for 5-10 ms in the middle of timed V-cycles (profiles/r3i_cycle_gaps.txt).  libomp reads the
+// variable when it initialises, at the library's first parallel region, after this runs.
+__attribute__((constructor)) static void amg_omp_defaults() { setenv("KMP_BLOCKTIME", "0", 0); }
+
 void amg::install_crash_handler() {
     const char* e = std::getenv("AMG_SEGV_BACKTRACE");
     if (!(e && std::atoi(e) != 0)) return;
@@ -358,6 +366,36 @@ int amg_par_csr_set_format(amg_matrix A, int32_t format) {
         set_device(*A->m->ctx);
         HIP_CHECK(hipStreamSynchronize(A->m->ctx->stream));
         A->m->set_format(format);
+    });
+}
+
+int amg_par_csr_format_digest(amg_matrix A, uint64_t* digest) {
+    return guard([&] {
+        AMG_CHECK(A && digest, "null argument");
+        DevMatrix& M = *A->m;
+        set_device(*M.ctx);
+        HIP_CHECK(hipStreamSynchronize(M.ctx->stream));
+        uint64_t h = 1469598103934665603ull;
+        auto mix = [&](const void* p, size_t bytes) {
+            std::vector<unsigned char> b(bytes);
+            if (bytes) HIP_CHECK(hipMemcpy(b.data(), p, bytes, hipMemcpyDeviceToHost));
+            for (size_t i = 0; i < 8; ++i) h = (h ^ ((bytes >> (8 * i)) & 0xff)) * 1099511628211ull;
+            for (unsigned char c : b) h = (h ^ c) * 1099511628211ull;
+        };
+        mix(M.rp.p, M.rp.n * sizeof(int));
+        mix(M.col.p, M.col.n * sizeof(int));
+        mix(M.val.p, M.val.n * sizeof(double));
+        mix(M.blocks.p, M.blocks.n * sizeof(int2));
+        mix(M.hdr.p, M.hdr.n * sizeof(int4));
+        mix(M.tile_fixed.p, M.tile_fixed.n * sizeof(int));
+        mix(M.lcol.p, M.lcol.n * sizeof(uint16_t));
+        mix(M.col16.p, M.col16.n * sizeof(uint16_t));
+        mix(M.gband.p, M.gband.n * sizeof(int4));
+        mix(M.vtab.p, M.vtab.n * sizeof(double));
+        mix(M.vidx.p, M.vidx.n);
+        mix(M.dvi.p, M.dvi.n);
+        mix(M.rend.p, M.rend.n * sizeof(uint16_t));
+        *digest = h;
     });
 }
 

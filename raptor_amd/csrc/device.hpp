@@ -61,6 +61,13 @@ constexpr int kTplChunks = 16;     // window chunks of kTPB slots (kTplWin / kTP
 constexpr int kTplWin = 16 * 256;  // x-window doubles per workgroup (32 KiB of LDS)
 constexpr int kTplRows = kTPB * kTplRPL;  // rows per template-kernel workgroup
 
+// Host <-> device copies of large pageable buffers (setup: operator uploads, Galerkin and
+// P / R downloads) through pinned staging: OpenMP threads fill one 32 MiB buffer while the
+// DMA engine drains the other.  Synchronous for the host.  Below 4 MiB, or with
+// AMG_STAGED_COPY=0, plain hipMemcpy.  copy_to_host waits for `after` (the producing stream).
+void copy_to_device(void* dst, const void* src, size_t bytes);
+void copy_to_host(void* dst, const void* src, size_t bytes, hipStream_t after);
+
 template <class T>
 struct DevBuf {
     T* p = nullptr;
@@ -90,7 +97,7 @@ struct DevBuf {
     }
     void upload(const T* h, size_t count) {
         alloc(count);
-        if (count) HIP_CHECK(hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice));
+        if (count) copy_to_device(p, h, count * sizeof(T));
     }
 };
 
@@ -126,6 +133,18 @@ struct Context {
 
 // Galerkin SpGEMM on the device (spgemm.hip); result downloaded as a host image
 HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, const HostCSR& B);
+// formats.hip: the per-nonzero device formats of DevMatrix::build_view built on the GPU
+// (AMG_DEVICE_FORMATS=0: the host builders); what the host block headers need back
+struct FormatHeaderInfo {
+    std::vector<int> vt_off, vt_len;  // per block: value-table offset (-1) and size
+    std::vector<char> dvi_ok;         // per block: every row's diagonal is a table slot
+    std::vector<int64_t> vofs;        // per block: offset in the value-index stream (empty: none)
+};
+bool device_formats();
+struct DevMatrix;
+void build_formats_device(DevMatrix& M, const std::vector<int>& hrp, const hvec<int>& hcol, const hvec<double>& hval,
+                          const std::vector<int2>& blocks, const std::vector<int>& tile_ptr,
+                          const std::vector<int>& tile_lines, const std::vector<int64_t>& koff, FormatHeaderInfo& out);
 // R (A P), A P kept on the device between the products where it can be (one rank)
 HostCSR galerkin_device(Context& ctx, const HostComm& comm, const HostCSR& R, const HostCSR& A,
                         const HostCSR& P);

@@ -13,6 +13,9 @@
 #include <cstdint>
 #include <deque>
 #include <functional>
+#include <memory>
+#include <type_traits>
+#include <utility>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -62,13 +65,37 @@ struct HostComm {
 // ---------------------------------------------------------------------------------
 // Rank-local rows of a row-partitioned CSR matrix (ParCSRMatrix host image, row a1).
 // ---------------------------------------------------------------------------------
+// std::allocator whose resize(n) leaves new scalars uninitialised (default-init): the
+// nonzero arrays of a HostCSR are written right after they are sized (device downloads,
+// parallel fills), so value-initialising them first would be a serial pass over GBs
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = DefaultInitAlloc<U>;
+    };
+    DefaultInitAlloc() = default;
+    template <class U>
+    DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... Args>
+    void construct(U* p, Args&&... args) {
+        ::new ((void*)p) U(std::forward<Args>(args)...);
+    }
+};
+template <class T>
+using hvec = std::vector<T, DefaultInitAlloc<T>>;
+
 struct HostCSR {
     int64_t n_global_rows = 0, n_global_cols = 0;
     std::vector<int64_t> row_starts;  // nranks+1: global row partition
     std::vector<int64_t> col_starts;  // nranks+1: partition of the column space (x owners)
     std::vector<int64_t> rp;          // n_local+1
-    std::vector<int64_t> col;         // global column ids, ascending per row
-    std::vector<double> val;
+    hvec<int64_t> col;                // global column ids, ascending per row
+    hvec<double> val;
 
     int64_t first_row(int rank) const { return row_starts[rank]; }
     int64_t n_local(int rank) const { return row_starts[rank + 1] - row_starts[rank]; }

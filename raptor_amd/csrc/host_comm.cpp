@@ -579,8 +579,8 @@ HostCSR gather_global(const HostComm& comm, const HostCSR& M) {
     std::vector<std::vector<double>> sv(comm.nranks);
     for (int r = 0; r < comm.nranks; ++r) {
         for (int64_t i = 0; i < n; ++i) sl[r].push_back(M.rp[i + 1] - M.rp[i]);
-        sc[r] = M.col;
-        sv[r] = M.val;
+        sc[r].assign(M.col.begin(), M.col.end());
+        sv[r].assign(M.val.begin(), M.val.end());
     }
     auto gl = comm.exchange(sl);
     auto gc = comm.exchange(sc);

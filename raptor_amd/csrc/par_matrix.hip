@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <unordered_map>
 
 #include "device.hpp"
@@ -37,6 +38,116 @@ struct ParZeros {
     T* begin() { return p.get(); }
 };
 
+// ---- staged host <-> device copies (device.hpp) ----------------------------------------
+namespace {
+
+constexpr size_t kStageChunk = size_t(32) << 20;
+
+bool staged_copies() {
+    static const bool on = [] {
+        const char* e = std::getenv("AMG_STAGED_COPY");
+        return !(e && *e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
+// two pinned chunks + a copy stream per (device, user); kept for the process lifetime
+struct Stage {
+    int device = -1;
+    bool busy = false;
+    hipStream_t s = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    char* buf[2] = {nullptr, nullptr};
+};
+
+std::mutex g_stage_mu;
+std::vector<Stage*> g_stages;
+
+Stage* stage_acquire() {
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> g(g_stage_mu);
+    for (Stage* st : g_stages)
+        if (!st->busy && st->device == dev) {
+            st->busy = true;
+            return st;
+        }
+    std::unique_ptr<Stage> st(new Stage());
+    st->device = dev;
+    HIP_CHECK(hipStreamCreateWithFlags(&st->s, hipStreamNonBlocking));
+    for (int b = 0; b < 2; ++b) {
+        HIP_CHECK(hipEventCreateWithFlags(&st->ev[b], hipEventDisableTiming));
+        HIP_CHECK(hipHostMalloc((void**)&st->buf[b], kStageChunk, hipHostMallocDefault));
+    }
+    st->busy = true;
+    g_stages.push_back(st.get());
+    return st.release();
+}
+
+void stage_release(Stage* st) {
+    std::lock_guard<std::mutex> g(g_stage_mu);
+    st->busy = false;
+}
+
+struct StageLease {
+    Stage* st;
+    StageLease() : st(stage_acquire()) {}
+    ~StageLease() { stage_release(st); }
+};
+
+void par_memcpy(void* dst, const void* src, size_t bytes) {
+    const int64_t parts = (int64_t)std::max<size_t>(1, bytes >> 21);  // 2 MiB pieces
+#pragma omp parallel for schedule(static)
+    for (int64_t q = 0; q < parts; ++q) {
+        const size_t a = bytes * (size_t)q / (size_t)parts, b = bytes * (size_t)(q + 1) / (size_t)parts;
+        std::memcpy((char*)dst + a, (const char*)src + a, b - a);
+    }
+}
+
+}  // namespace
+
+void copy_to_device(void* dst, const void* src, size_t bytes) {
+    if (bytes < (size_t(4) << 20) || !staged_copies()) {
+        if (bytes) HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+        return;
+    }
+    StageLease L;
+    Stage& S = *L.st;
+    size_t c = 0;
+    for (size_t off = 0; off < bytes; off += kStageChunk, ++c) {
+        const int b = (int)(c & 1);
+        const size_t len = std::min(kStageChunk, bytes - off);
+        if (c >= 2) HIP_CHECK(hipEventSynchronize(S.ev[b]));  // the DMA out of this buffer is done
+        par_memcpy(S.buf[b], (const char*)src + off, len);
+        HIP_CHECK(hipMemcpyAsync((char*)dst + off, S.buf[b], len, hipMemcpyHostToDevice, S.s));
+        HIP_CHECK(hipEventRecord(S.ev[b], S.s));
+    }
+    HIP_CHECK(hipStreamSynchronize(S.s));
+}
+
+void copy_to_host(void* dst, const void* src, size_t bytes, hipStream_t after) {
+    if (after) HIP_CHECK(hipStreamSynchronize(after));
+    if (bytes < (size_t(4) << 20) || !staged_copies()) {
+        if (bytes) HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+        return;
+    }
+    StageLease L;
+    Stage& S = *L.st;
+    const size_t nc = (bytes + kStageChunk - 1) / kStageChunk;
+    auto issue = [&](size_t c) {
+        const size_t off = c * kStageChunk, len = std::min(kStageChunk, bytes - off);
+        HIP_CHECK(hipMemcpyAsync(S.buf[c & 1], (const char*)src + off, len, hipMemcpyDeviceToHost, S.s));
+        HIP_CHECK(hipEventRecord(S.ev[c & 1], S.s));
+    };
+    issue(0);
+    for (size_t c = 0; c < nc; ++c) {
+        if (c + 1 < nc) issue(c + 1);  // into the other buffer, emptied in the previous round
+        HIP_CHECK(hipEventSynchronize(S.ev[c & 1]));
+        const size_t off = c * kStageChunk, len = std::min(kStageChunk, bytes - off);
+        par_memcpy((char*)dst + off, S.buf[c & 1], len);
+    }
+}
+
 Context::~Context() {
     loopback_leave(*this);
     if (nccl) (void)ncclCommDestroy(nccl);
@@ -55,16 +166,16 @@ struct BlockBuild {
     std::vector<int2> blocks;     // interior all-templated, other interior, then boundary blocks
     std::vector<int> tile_ptr;    // nb + 1
     std::vector<int> tile_lines;  // global line ids per block
-    std::vector<uint16_t> lcol;   // per nonzero (nnz + kPad)
+    hvec<uint16_t> lcol;          // per nonzero (nnz + kPad)
     int nb_int = 0, nb_bnd = 0, nb_skip = 0;  // nb_skip: leading interior all-templated blocks
 };
 
 // tplf (optional): per row 1 = handled by the template kernel; blocks then also break where it
 // changes, and all-templated interior blocks come first
-static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector<int>& col,
+static BlockBuild build_row_blocks(const std::vector<int>& rp, const hvec<int>& col,
                                    const std::vector<uint8_t>& cls, int64_t ncl, int64_t nhalo,
                                    const std::vector<uint8_t>* tplf = nullptr, int row_cap = kTPB,
-                                   bool line_cap = true) {
+                                   bool line_cap = true, bool want_lcol = true) {
     const int n = (int)rp.size() - 1;
     const int64_t hl0 = (ncl + 7) / 8;
     const size_t nlines = (size_t)(hl0 + (nhalo + 7) / 8) + 1;
@@ -75,7 +186,12 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
         bool bnd, tpl;
     };
     BlockBuild out;
-    out.lcol.assign(col.size() + kPad, 0);
+    // every entry below col.size() is written by the block that holds it; the pad is zero.
+    // want_lcol = false: the tile indices are built on the device (formats.hip)
+    if (want_lcol) {
+        out.lcol.resize(col.size() + kPad);
+        std::fill(out.lcol.begin() + (int64_t)(rp.back()), out.lcol.end(), (uint16_t)0);
+    }
     // The greedy cut runs independently on a fixed number of row chunks (each chunk starts a
     // block at its first row), in parallel: blocks never change the arithmetic (rows never
     // straddle a block), and a fixed chunk count keeps the cut independent of the thread count.
@@ -101,11 +217,12 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const std::vector
                 std::sort(lines.begin(), lines.end());
                 for (size_t q = 0; q < lines.size(); ++q) slot[lines[q]] = (int)q;
                 const bool tiled = (int)lines.size() <= kTileLines;
-                for (int k = rp[a]; k < rp[b]; ++k) {
-                    const int c = col[k];
-                    const int e = c < ncl ? (c & 7) : (int)((c - ncl) & 7);  // element within its line
-                    out.lcol[k] = tiled ? (uint16_t)(slot[line_of(c)] * 8 + e) : (uint16_t)0;
-                }
+                if (want_lcol)
+                    for (int k = rp[a]; k < rp[b]; ++k) {
+                        const int c = col[k];
+                        const int e = c < ncl ? (c & 7) : (int)((c - ncl) & 7);  // element within its line
+                        out.lcol[k] = tiled ? (uint16_t)(slot[line_of(c)] * 8 + e) : (uint16_t)0;
+                    }
                 rc.push_back({a, b, tiled ? lines : std::vector<int>(), cls[a] != 0,
                               tplf != nullptr && (*tplf)[a] != 0});
                 if (!tiled) rc.back().lines.assign(kTileLines + 1, 0);  // marker: untiled
@@ -282,8 +399,8 @@ struct TplBuild {
     int64_t rows = 0;
 };
 
-static TplBuild build_templates(const std::vector<int>& rp, const std::vector<int>& col,
-                                const std::vector<double>& val, const std::vector<double>& dinv,
+static TplBuild build_templates(const std::vector<int>& rp, const hvec<int>& col,
+                                const hvec<double>& val, const std::vector<double>& dinv,
                                 int64_t ncl) {
     const int n = (int)rp.size() - 1;
     TplBuild T;
@@ -459,7 +576,8 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
     AMG_CHECK(n_cols_local + plan.n_halo() < INT_MAX, "too many columns for int32");
     tm.lap("    build: halo plan");
 
-    std::vector<int> hrp(n_rows + 1), hcol(nnz);
+    std::vector<int> hrp(n_rows + 1);
+    hvec<int> hcol(nnz);  // every entry written below
     std::vector<uint8_t> cls(n_rows, 0);
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i <= n_rows; ++i) hrp[i] = (int)host.rp[i];
@@ -511,8 +629,9 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         // path): up to kGatherRPB rows per lane (profiles/r2n: P0 x += P e 162 -> 95 us; R
         // with 7+ entries per row was slower that way: R0 94 -> 106 us, sa27 R0 350 -> 415)
         gather_rpb = !square && nnz <= 4 * n_rows ? kGatherRPB : 1;
+        const bool dev_fmt = device_formats();
         BlockBuild bb = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(),
-                                         tplf.empty() ? nullptr : &tplf, kTPB * gather_rpb);
+                                         tplf.empty() ? nullptr : &tplf, kTPB * gather_rpb, true, !dev_fmt);
         nb_int = bb.nb_int;
         nb_bnd = bb.nb_bnd;
         tm.lap("    build: row blocks + x tiles");
@@ -547,7 +666,8 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         if (!tiled) {
             const char* e = std::getenv("AMG_GATHER_LINECAP");
             if (!(e && std::atoi(e) != 0)) {
-                bb = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(), nullptr, kTPB * gather_rpb, false);
+                bb = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(), nullptr, kTPB * gather_rpb, false,
+                                      !dev_fmt);
                 nb_int = bb.nb_int;
                 nb_bnd = bb.nb_bnd;
                 if (std::getenv("AMG_TRACE_BLOCKS"))
@@ -676,107 +796,118 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         for (size_t q = 0; q < nbk; ++q)
             koff[q + 1] = koff[q] + (int64_t)(hrp[bb.blocks[q].y] - hrp[bb.blocks[q].x] + 1) / 2 * 2;
         AMG_CHECK(koff[nbk] + kPad < INT_MAX, "local matrix exceeds int32 indexing");
-        {
-            ParZeros<int> cb((size_t)(koff[nbk] + kPad));
-            ParZeros<double> vb(cb.size());
-#pragma omp parallel for schedule(dynamic, 256)
-            for (size_t q = 0; q < nbk; ++q) {
-                const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
-                std::copy(hcol.begin() + kb, hcol.begin() + kb + nz, cb.begin() + koff[q]);
-                std::copy(host.val.begin() + kb, host.val.begin() + kb + nz, vb.begin() + koff[q]);
-            }
-            col.upload(cb.data(), cb.size());
-            val.upload(vb.data(), vb.size());
-            // gather operators: 16-bit column codes when every block's columns fit in <= 4
-            // bands of kGatherBand: a structured P / R block reads three
-            // planes' worth of columns, each a narrow band.  Lossless: the kernel decodes
-            // base[code >> 14] + (code & 0x3fff), the same column.
-            col16.reset();
-            gband.reset();
-            if (!tiled && nbk > 0) {
-                ParZeros<uint16_t> c16(cb.size());
-                std::vector<int4> gb(nbk, make_int4(0, 0, 0, 0));
-                int bad = 0;
-#pragma omp parallel for schedule(dynamic, 256) reduction(+ : bad)
-                for (size_t q = 0; q < nbk; ++q) {
-                    const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
-                    if (nz == 0 || nz > kCAP) continue;  // chunked path: int32 columns
-                    std::vector<int> u(cb.begin() + koff[q], cb.begin() + koff[q] + nz);
-                    std::sort(u.begin(), u.end());
-                    int base[4] = {0, 0, 0, 0}, nbnd = 0;
-                    for (int c : u) {
-                        if (nbnd == 0 || c - base[nbnd - 1] >= kGatherBand) {
-                            if (nbnd == 4) {
-                                nbnd = 5;
-                                break;
-                            }
-                            base[nbnd++] = c;
-                        }
-                    }
-                    if (nbnd > 4) {
-                        ++bad;
-                        continue;
-                    }
-                    for (int t = nbnd; t < 4; ++t) base[t] = base[nbnd - 1];
-                    gb[q] = make_int4(base[0], base[1], base[2], base[3]);
-                    for (int j = 0; j < nz; ++j) {
-                        const int c = cb[koff[q] + j];
-                        int t = nbnd - 1;
-                        while (c < base[t]) --t;
-                        c16[koff[q] + j] = (uint16_t)((t << 14) | (c - base[t]));
-                    }
-                }
-                if (bad == 0) {
-                    col16.upload(c16.data(), c16.size());
-                    gband.upload(gb.data(), gb.size());
-                }
-            }
-        }
-        if (tiled) {  // x tiles: the x-tile kernel only
-            // x-tile line ids at a fixed stride (kTileLines per block, padded with the block's
-            // last line), so the kernel loads them without waiting for the block header
-            ParZeros<int> fx(std::max<size_t>(nbk, 1) * kTileLines);
-#pragma omp parallel for schedule(static)
-            for (size_t q = 0; q < nbk; ++q) {
-                const int t0 = bb.tile_ptr[q], nt = bb.tile_ptr[q + 1] - t0;
-                if (nt <= 0 || nt > kTileLines) continue;
-                for (int j = 0; j < kTileLines; ++j)
-                    fx[q * kTileLines + j] = bb.tile_lines[t0 + std::min(j, nt - 1)];
-            }
-            tile_fixed.upload(fx.data(), fx.size());
-            // lane-major per block (lane_pos): lane t's 8 indices are 16 contiguous bytes,
-            // one 16-byte load per lane
-            ParZeros<uint16_t> perm(std::max<size_t>(nbk, 1) * kCAP);
-#pragma omp parallel for schedule(static)
-            for (size_t q = 0; q < nbk; ++q) {
-                const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
-                if (nz > kCAP) continue;
-                for (int j = 0; j < nz; ++j)
-                    perm[q * kCAP + lane_pos(j, kCAP / kTPB)] = bb.lcol[kb + j];
-            }
-            lcol.upload(perm.data(), perm.size());
-        } else {
-            tile_fixed.reset();
-            lcol.reset();
-        }
-        tm.lap("    build: col / val / tile layouts");
         std::vector<int> vt_off, vt_len;
-        std::vector<uint8_t> hdvi;
         std::vector<char> dvi_ok;
         std::vector<int64_t> vofs;
-        build_value_index(*this, host, hrp, bb, vt_off, vt_len, hdvi, dvi_ok, vofs);
-        if (n_vi_blocks > 0 && square) dvi.upload(hdvi.data(), hdvi.size());
-        else dvi.reset();
-        tm.lap("    build: value index");
-        {
-            // per row: end of its nonzeros relative to its block's first (<= kCAP: 16 bits)
-            std::vector<uint16_t> re((size_t)n_rows + 1, 0);
-            for (size_t q = 0; q < nbk; ++q) {
-                const int2 b = bb.blocks[q];
-                if (hrp[b.y] - hrp[b.x] > kCAP) continue;
-                for (int r = b.x; r < b.y; ++r) re[r] = (uint16_t)(hrp[r + 1] - hrp[b.x]);
+        if (dev_fmt) {
+            // per-nonzero streams built on the GPU from one upload of the CSR (formats.hip)
+            FormatHeaderInfo fi;
+            build_formats_device(*this, hrp, hcol, host.val, bb.blocks, bb.tile_ptr, bb.tile_lines, koff, fi);
+            vt_off = std::move(fi.vt_off);
+            vt_len = std::move(fi.vt_len);
+            dvi_ok = std::move(fi.dvi_ok);
+            vofs = std::move(fi.vofs);
+            tm.lap("    build: device col / val / tiles / value index / row ends");
+        } else {
+            {
+                ParZeros<int> cb((size_t)(koff[nbk] + kPad));
+                ParZeros<double> vb(cb.size());
+#pragma omp parallel for schedule(dynamic, 256)
+                for (size_t q = 0; q < nbk; ++q) {
+                    const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
+                    std::copy(hcol.begin() + kb, hcol.begin() + kb + nz, cb.begin() + koff[q]);
+                    std::copy(host.val.begin() + kb, host.val.begin() + kb + nz, vb.begin() + koff[q]);
+                }
+                col.upload(cb.data(), cb.size());
+                val.upload(vb.data(), vb.size());
             }
-            rend.upload(re.data(), re.size());
+            if (tiled) {  // x tiles: the x-tile kernel only
+                // x-tile line ids at a fixed stride (kTileLines per block, padded with the block's
+                // last line), so the kernel loads them without waiting for the block header
+                ParZeros<int> fx(std::max<size_t>(nbk, 1) * kTileLines);
+#pragma omp parallel for schedule(static)
+                for (size_t q = 0; q < nbk; ++q) {
+                    const int t0 = bb.tile_ptr[q], nt = bb.tile_ptr[q + 1] - t0;
+                    if (nt <= 0 || nt > kTileLines) continue;
+                    for (int j = 0; j < kTileLines; ++j)
+                        fx[q * kTileLines + j] = bb.tile_lines[t0 + std::min(j, nt - 1)];
+                }
+                tile_fixed.upload(fx.data(), fx.size());
+                // lane-major per block (lane_pos): lane t's 8 indices are 16 contiguous bytes,
+                // one 16-byte load per lane
+                ParZeros<uint16_t> perm(std::max<size_t>(nbk, 1) * kCAP);
+#pragma omp parallel for schedule(static)
+                for (size_t q = 0; q < nbk; ++q) {
+                    const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
+                    if (nz > kCAP) continue;
+                    for (int j = 0; j < nz; ++j)
+                        perm[q * kCAP + lane_pos(j, kCAP / kTPB)] = bb.lcol[kb + j];
+                }
+                lcol.upload(perm.data(), perm.size());
+            } else {
+                tile_fixed.reset();
+                lcol.reset();
+            }
+            tm.lap("    build: col / val / tile layouts");
+            std::vector<uint8_t> hdvi;
+            build_value_index(*this, host, hrp, bb, vt_off, vt_len, hdvi, dvi_ok, vofs);
+            if (n_vi_blocks > 0 && square) dvi.upload(hdvi.data(), hdvi.size());
+            else dvi.reset();
+            tm.lap("    build: value index");
+            {
+                // per row: end of its nonzeros relative to its block's first (<= kCAP: 16 bits)
+                std::vector<uint16_t> re((size_t)n_rows + 1, 0);
+                for (size_t q = 0; q < nbk; ++q) {
+                    const int2 b = bb.blocks[q];
+                    if (hrp[b.y] - hrp[b.x] > kCAP) continue;
+                    for (int r = b.x; r < b.y; ++r) re[r] = (uint16_t)(hrp[r + 1] - hrp[b.x]);
+                }
+                rend.upload(re.data(), re.size());
+            }
+        }
+        // gather operators: 16-bit column codes when every block's columns fit in <= 4
+        // bands of kGatherBand: a structured P / R block reads three
+        // planes' worth of columns, each a narrow band.  Lossless: the kernel decodes
+        // base[code >> 14] + (code & 0x3fff), the same column.
+        col16.reset();
+        gband.reset();
+        if (!tiled && nbk > 0) {
+            ParZeros<uint16_t> c16((size_t)(koff[nbk] + kPad));
+            std::vector<int4> gb(nbk, make_int4(0, 0, 0, 0));
+            int bad = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : bad)
+            for (size_t q = 0; q < nbk; ++q) {
+                const int kb = hrp[bb.blocks[q].x], nz = hrp[bb.blocks[q].y] - kb;
+                if (nz == 0 || nz > kCAP) continue;  // chunked path: int32 columns
+                std::vector<int> u(hcol.begin() + kb, hcol.begin() + kb + nz);
+                std::sort(u.begin(), u.end());
+                int base[4] = {0, 0, 0, 0}, nbnd = 0;
+                for (int c : u) {
+                    if (nbnd == 0 || c - base[nbnd - 1] >= kGatherBand) {
+                        if (nbnd == 4) {
+                            nbnd = 5;
+                            break;
+                        }
+                        base[nbnd++] = c;
+                    }
+                }
+                if (nbnd > 4) {
+                    ++bad;
+                    continue;
+                }
+                for (int t = nbnd; t < 4; ++t) base[t] = base[nbnd - 1];
+                gb[q] = make_int4(base[0], base[1], base[2], base[3]);
+                for (int j = 0; j < nz; ++j) {
+                    const int c = hcol[kb + j];
+                    int t = nbnd - 1;
+                    while (c < base[t]) --t;
+                    c16[koff[q] + j] = (uint16_t)((t << 14) | (c - base[t]));
+                }
+            }
+            if (bad == 0) {
+                col16.upload(c16.data(), c16.size());
+                gband.upload(gb.data(), gb.size());
+            }
         }
         // 32-byte block headers (two scalar loads per block):
         //   {r0, r1, koff, nnz}, {diag slot, tile lines | dvi flag << 16, value-table offset (-1),

@@ -553,8 +553,7 @@ void build_strength(hipStream_t s, int n, int lo, DevS& S, DevBuf<char>& tmp, Co
 
 std::vector<int32_t> download_ints(hipStream_t s, const int* p, int64_t n) {
     std::vector<int32_t> h((size_t)n);
-    if (n) HIP_CHECK(hipMemcpyAsync(h.data(), p, sizeof(int) * n, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    copy_to_host(h.data(), p, sizeof(int) * n, s);
     return h;
 }
 
@@ -796,8 +795,7 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
         P.rp.assign(hrp.begin(), hrp.end());
         P.col.assign(hcol.begin(), hcol.end());
         P.val.resize((size_t)pnnz);
-        if (pnnz) HIP_CHECK(hipMemcpyAsync(P.val.data(), pval.p, sizeof(double) * pnnz, hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipStreamSynchronize(s));
+        copy_to_host(P.val.data(), pval.p, sizeof(double) * pnnz, s);
         tm.lap("  device interpolation");
         return true;
     }
@@ -1047,11 +1045,9 @@ bool transpose_device(Context& ctx, const HostComm& comm, const HostCSR& P, Host
     R.rp.assign(hrp.begin(), hrp.end());
     R.col.resize(nnz);
     R.val.resize(nnz);
-    std::vector<long long> tc(nnz);
-    HIP_CHECK(hipMemcpyAsync(tc.data(), rcol.p, sizeof(long long) * nnz, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipMemcpyAsync(R.val.data(), rval.p, sizeof(double) * nnz, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    std::copy(tc.begin(), tc.end(), R.col.begin());
+    static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
+    copy_to_host(R.col.data(), rcol.p, sizeof(long long) * nnz, s);
+    copy_to_host(R.val.data(), rval.p, sizeof(double) * nnz, nullptr);
     return true;
 }
 

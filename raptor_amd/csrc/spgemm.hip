@@ -311,11 +311,8 @@ HostCSR download(Context& ctx, PhaseTimer& tm, const HostCSR& A, const HostCSR& 
     const int64_t cnnz = C.nnz();
     out.col.resize(cnnz);
     out.val.resize(cnnz);
-    if (cnnz) {
-        HIP_CHECK(hipMemcpyAsync(out.col.data(), C.d_col.p, sizeof(long long) * cnnz, hipMemcpyDeviceToHost, ctx.stream));
-        HIP_CHECK(hipMemcpyAsync(out.val.data(), C.d_val.p, sizeof(double) * cnnz, hipMemcpyDeviceToHost, ctx.stream));
-    }
-    HIP_CHECK(hipStreamSynchronize(ctx.stream));
+    copy_to_host(out.col.data(), C.d_col.p, sizeof(long long) * cnnz, ctx.stream);
+    copy_to_host(out.val.data(), C.d_val.p, sizeof(double) * cnnz, nullptr);
     tm.lap("    spgemm: download");
     return out;
 }
@@ -357,14 +354,10 @@ HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, cons
     d_brp.upload(brp.data(), brp.size());
     d_bcol.alloc((size_t)std::max<int64_t>(bnnz, 1));
     d_bval.alloc((size_t)std::max<int64_t>(bnnz, 1));
-    if (bl) {
-        HIP_CHECK(hipMemcpy(d_bcol.p, B.col.data(), sizeof(long long) * bl, hipMemcpyHostToDevice));
-        HIP_CHECK(hipMemcpy(d_bval.p, B.val.data(), sizeof(double) * bl, hipMemcpyHostToDevice));
-    }
-    if (bnnz > bl) {
-        HIP_CHECK(hipMemcpy(d_bcol.p + bl, G.col.data(), sizeof(long long) * (bnnz - bl), hipMemcpyHostToDevice));
-        HIP_CHECK(hipMemcpy(d_bval.p + bl, G.val.data(), sizeof(double) * (bnnz - bl), hipMemcpyHostToDevice));
-    }
+    copy_to_device(d_bcol.p, B.col.data(), sizeof(long long) * bl);
+    copy_to_device(d_bval.p, B.val.data(), sizeof(double) * bl);
+    copy_to_device(d_bcol.p + bl, G.col.data(), sizeof(long long) * (bnnz - bl));
+    copy_to_device(d_bval.p + bl, G.val.data(), sizeof(double) * (bnnz - bl));
     tm.lap("    spgemm: upload of B");
     BImage img{brp.data(), d_brp.p, d_bcol.p, d_bval.p, B.n_global_cols,
                [&](std::function<int64_t(long long)>& ca, std::function<double(long long)>& va) {
@@ -435,10 +428,8 @@ HostCSR galerkin_device(Context& ctx, const HostComm& comm, const HostCSR& R, co
                      const int64_t m = AP.nnz();
                      apc.resize(m);
                      apv.resize(m);
-                     if (m) {
-                         HIP_CHECK(hipMemcpy(apc.data(), AP.d_col.p, sizeof(long long) * m, hipMemcpyDeviceToHost));
-                         HIP_CHECK(hipMemcpy(apv.data(), AP.d_val.p, sizeof(double) * m, hipMemcpyDeviceToHost));
-                     }
+                     copy_to_host(apc.data(), AP.d_col.p, sizeof(long long) * m, ctx.stream);
+                     copy_to_host(apv.data(), AP.d_val.p, sizeof(double) * m, nullptr);
                      ca = [&](long long q) -> int64_t { return apc[q]; };
                      va = [&](long long q) -> double { return apv[q]; };
                  }};
