@@ -213,18 +213,14 @@ void build_formats_device(DevMatrix& M, const std::vector<int>& hrp, const hvec<
     const int nbk = (int)blocks.size();
     const int64_t nnz = (int64_t)hcol.size() - kPad;  // hcol carries kPad trailing zeros
     AMG_CHECK(nnz == hrp.back(), "format build: column array size");
-    // AMG_FMT_STREAM=ctx: the context stream (probe); default: a stream of the build's own
-    const char* fs = std::getenv("AMG_FMT_STREAM");
-    const bool own = !(fs && std::string(fs) == "ctx");
-    hipStream_t s = M.ctx->stream;
-    if (own) HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    // a stream of the build's own: the worker thread's builds run beside the setup thread's
+    // kernels on the context stream
+    hipStream_t s = nullptr;
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     struct StreamGuard {
         hipStream_t s;
-        bool own;
-        ~StreamGuard() {
-            if (own) (void)hipStreamDestroy(s);
-        }
-    } sg{s, own};
+        ~StreamGuard() { (void)hipStreamDestroy(s); }
+    } sg{s};
     // the CSR in local numbering (rp is M.rp, uploaded by the caller)
     DevBuf<int> dcol, dtp, dtl;
     DevBuf<double> dval;
