@@ -12,7 +12,7 @@ itself."""
 import numpy as np
 import pytest
 
-from tests.util import oracle_levels, to_dev, to_host
+from tests.util import oracle_levels, same_csr, to_dev, to_host
 
 pytestmark = pytest.mark.gpu
 
@@ -253,6 +253,38 @@ def test_sa27_npl16_vcycle_vs_oracle(ctx, oracle):
     _, h = ml.solve(ctx.zeros(n), db, max_iter=5)
     _, ho = Ho.solve(np.zeros(n), b, max_iter=5)
     assert np.all(np.abs(h - ho) <= 1e-10 * ho)
+
+
+@pytest.mark.slow
+def test_sa27_hierarchy_independent_oracle_64(ctx, oracle):
+    """configs[2]'s algorithm on a cube (27-pt anisotropic 64^3, 262k rows, 7M nnz) with an
+    INDEPENDENT oracle hierarchy (the independent sa27 comparison was only
+    256x24x16): strength with the per-level threshold, MIS(2) aggregates, smoothed P,
+    Galerkin -- every operator bit-identical -- then two hybrid-GS V-cycle iterates."""
+    import raptor_amd as ra
+
+    O = oracle
+    dims = (64, 64, 64)
+    Ao = O.gen_27pt(*dims)
+    A = ra.par_stencil_grid(ctx, "27pt", dims)
+    ml = ra.ParSmoothedAggregationSolver().setup(A)
+    Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS["sa"], smoother=O.SMOOTH_HYBRID_GS))
+    assert ml.num_levels == Ho.num_levels
+    for l in range(ml.num_levels):
+        if l > 0:
+            assert same_csr(ml.level_matrix(l, "A").to_scipy_local(), Ho.matrix(l, "A")), ("A", l)
+        if l + 1 < ml.num_levels:
+            assert same_csr(ml.level_matrix(l, "P").to_scipy_local(), Ho.matrix(l, "P")), ("P", l)
+            assert same_csr(ml.level_matrix(l, "R").to_scipy_local(), Ho.matrix(l, "R")), ("R", l)
+    n = Ao.shape[0]
+    b = Ao.spmv(O.vec_uniform(n, 42))
+    db = to_dev(ctx, b)
+    dx = ctx.zeros(n)
+    xo = np.zeros(n)
+    for _ in range(2):
+        ml.cycle(dx, db)
+        xo = Ho.cycle(xo, b)
+        assert np.array_equal(to_host(ctx, dx), xo)
 
 
 @pytest.mark.slow

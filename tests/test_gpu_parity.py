@@ -431,6 +431,42 @@ def test_full_size_spmv_and_cycle_256(ctx, oracle):
     assert np.array_equal(to_host(ctx, dx), xo)
 
 
+@pytest.mark.slow
+def test_full_size_hierarchy_independent_oracle_256(ctx, oracle):
+    """configs[1] at full size with an INDEPENDENT oracle hierarchy (the 256^3
+    cycle test built the oracle from the product's exported levels).  The oracle's serial
+    setup of 7-pt 256^3 (strength, PMIS, classical interpolation, transpose, Galerkin) against
+    the product's GPU setup: every P_l, R_l and A_{l+1} bit-identical, then two V-cycle iterates
+    and a 4-cycle solve history on the oracle's own hierarchy."""
+    import raptor_amd as ra
+
+    O = oracle
+    N = 256
+    A = ra.par_stencil_grid(ctx, "7pt", (N, N, N))
+    ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
+    Ao = O.gen_7pt(N, N, N)
+    Ho = O.Hierarchy(Ao, **O.DEFAULTS["pmis"])
+    assert ml.num_levels == Ho.num_levels
+    for l in range(ml.num_levels):
+        if l > 0:
+            assert same_csr(ml.level_matrix(l, "A").to_scipy_local(), Ho.matrix(l, "A")), ("A", l)
+        if l + 1 < ml.num_levels:
+            assert same_csr(ml.level_matrix(l, "P").to_scipy_local(), Ho.matrix(l, "P")), ("P", l)
+            assert same_csr(ml.level_matrix(l, "R").to_scipy_local(), Ho.matrix(l, "R")), ("R", l)
+    n = N ** 3
+    b = Ao.spmv(O.vec_uniform(n, 42))
+    db = to_dev(ctx, b)
+    dx = ctx.zeros(n)
+    xo = np.zeros(n)
+    for _ in range(2):
+        ml.cycle(dx, db)
+        xo = Ho.cycle(xo, b)
+        assert np.array_equal(to_host(ctx, dx), xo)
+    _, h = ml.solve(ctx.zeros(n), db, max_iter=4)
+    _, ho = Ho.solve(np.zeros(n), b, max_iter=4)
+    assert np.all(np.abs(h - ho) <= 1e-10 * ho)
+
+
 @pytest.mark.parametrize("coarsen,smoother", [("pmis", "jacobi"), ("sa", "hybrid_gs")])
 def test_pcg_matches_oracle(ctx, oracle, coarsen, smoother):
     """AMG-preconditioned CG: same hierarchy, same V-cycle bits; dot products differ only in
