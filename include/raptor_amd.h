@@ -142,6 +142,9 @@ typedef struct amg_matrix_info {
     int64_t residual_bytes;
     int64_t jacobi_bytes;
     int64_t gs_bytes;        /* sliced-ELL bytes of one hybrid GS sweep (0: not built)     */
+    int32_t tpl_master;      /* uniform-stencil rows: entries of the master template every *
+                              * template is a subsequence of (7, 27; 0: per-template      *
+                              * tables)                                    */
 } amg_matrix_info;
 int amg_par_csr_info(amg_matrix A, amg_matrix_info* info);
 

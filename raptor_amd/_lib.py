@@ -71,6 +71,7 @@ class MatrixInfo(C.Structure):
         ("residual_bytes", C.c_int64),
         ("jacobi_bytes", C.c_int64),
         ("gs_bytes", C.c_int64),
+        ("tpl_master", C.c_int32),
     ]
 
 

@@ -60,6 +60,9 @@ constexpr int kTplBands = 8;       // x-window bands
 constexpr int kTplChunks = 16;     // window chunks of kTPB slots (kTplWin / kTPB)
 constexpr int kTplWin = 16 * 256;  // x-window doubles per workgroup (32 KiB of LDS)
 constexpr int kTplRows = kTPB * kTplRPL;  // rows per template-kernel workgroup
+// uniform-stencil rows: every template a subsequence of one master
+// template; the kernels are instantiated for masters of these entry counts
+constexpr int kTplMasterMax = 27;
 
 // Host <-> device copies of large pageable buffers (setup: operator uploads, Galerkin and
 // P / R downloads) through pinned staging: OpenMP threads fill one 32 MiB buffer while the
@@ -265,6 +268,16 @@ struct DevMatrix {
     DevBuf<double> tpl_val, tpl_pd;
     int n_tpl = 0, n_tpl_ent = 0, nb_skip = 0;
     int64_t tpl_rows = 0;  // rows the template kernel handles
+    // uniform stencil: every template's (offset, value) entries are a
+    // subsequence of the master template's (tpl_mne entries, window slots tpl_mslot, values
+    // tpl_mval, diagonal entry tpl_mdiag), every template holds the diagonal and every 1/a_ii
+    // is tpl_mpd; tpl_mmask / gs_tmask: per (GS) template, bit e = has master entry e.
+    // tpl_mne = 0: not uniform.  tpl_mem / tpl_mep: master index of offset -1 / +1 (-1: none)
+    int tpl_mne = 0, tpl_mdiag = -1, tpl_mem = -1, tpl_mep = -1;
+    std::vector<int> tpl_mslot;
+    std::vector<double> tpl_mval;
+    double tpl_mpd = 0.0;
+    DevBuf<unsigned> tpl_mmask, gs_tmask;
     int64_t csr_fmt_bytes = 0;  // spmv_fmt_bytes with templates off (AMG_KERNEL_VARIANT)
     // storage format the level kernels use (AMG_FORMAT_*, amg_par_csr_set_format):
     // AUTO = templates + CSR blocks (default), BLOCKS = CSR blocks only, CSR = plain CSR

@@ -793,6 +793,13 @@ struct TplArgs {
     double* partial;
     const int* wsrc;  // march (variant bit 128): per window slot, the slot of the block one
                       // stride back that holds the same x (-1: load it)
+    // uniform stencil (MNE > 0 kernels, variant bit 512): hdr = per-template entry masks, nent
+    // = 0; the master's window slots and values (read from kernel arguments: scalar loads),
+    // its diagonal entry and 1/a_ii
+    int mdiag;
+    double mpd;
+    int mslot[kTplMasterMax];
+    double mval[kTplMasterMax];
 };
 
 // dynamic LDS: window | values | 1/a_ii (Jacobi only) | entry slots or offsets | headers.
@@ -851,7 +858,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tpl_xrs(const TplArgs& a) {
 }
 
 // template table into LDS (L2-resident; the caller's barrier publishes it)
-template <int MODE>
+template <int MODE, int MNE = 0>
 __device__ __forceinline__ void tpl_stage_table(const TplArgs& a, const TplLds& L) {
     const int tid = threadIdx.x;
     for (int k = tid; k < a.nent; k += kTPB) {
@@ -859,10 +866,11 @@ __device__ __forceinline__ void tpl_stage_table(const TplArgs& a, const TplLds& 
         L.val[k] = a.val[k];
     }
     if (tid < a.ntpl) {
-        L.hdr[tid] = a.hdr[tid];
-        if (MODE == KM_JACOBI) L.pd[tid] = a.pd[tid];
+        L.hdr[tid] = a.hdr[tid];  // MNE > 0: the template's entry mask
+        if (MODE == KM_JACOBI && MNE == 0) L.pd[tid] = a.pd[tid];
     }
-    if (tid == kTplNone) L.hdr[kTplNone] = (int)(255u << 24);  // length 0, no diagonal
+    // length 0, no diagonal / no master entry
+    if (tid == kTplNone) L.hdr[kTplNone] = MNE > 0 ? 0 : (int)(255u << 24);
 }
 
 // x offsets (relative to the block's first row) of the lane's window slots i_u = S (tid +
@@ -1081,6 +1089,88 @@ __device__ __forceinline__ double tpl_rows(const TplArgs& a, const TplLds& L, __
     return sq;
 }
 
+// Uniform-stencil rows (variant bit 512): every template is the master
+// template with entries removed (DevMatrix::tpl_mne), so a row is an entry mask.  The master's
+// values and window slots are kernel arguments (scalar registers, wave-uniform), and a lane
+// reads only x from the window: per entry one LDS read, one address add, one multiply and one
+// add, where tpl_rows reads slots and values from LDS tables and selects per entry (~10 VALU
+// per entry: the 27-pt kernels were VALU-issue bound, profiles/r2w_tpl_sq_instr.txt).  In a
+// wave whose rows are all the master the adds are unconditional; otherwise a lane adds only
+// the entries its row has.  Each row's products and their order are its own CSR row's:
+// results are bit-identical to tpl_rows (and the oracle).
+template <int MODE, bool NORM, int MNE>
+__device__ __forceinline__ double tpl_rows_master(const TplArgs& a, const TplLds& L, int r0, const int* id,
+                                                  const double* pb, const double* py) {
+    static_assert(MNE > 0 && MNE <= kTplMasterMax && MNE < 32, "master entry masks are 32-bit");
+    constexpr int R = kTplRPL;
+    constexpr unsigned kFull = (1u << MNE) - 1u;
+    const int tid = threadIdx.x;
+    unsigned m[R];
+    bool full = true;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        m[j] = (unsigned)L.hdr[id[j]];
+        full = full && m[j] == kFull;
+    }
+    const double* w = L.win + tid;
+    double s[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) s[j] = 0.0;
+    if (__all(full)) {
+#pragma unroll
+        for (int e = 0; e < MNE; ++e) {
+            const double v = a.mval[e];
+            const double* we = w + a.mslot[e];
+#pragma unroll
+            for (int j = 0; j < R; ++j) s[j] = s[j] + v * we[kTPB * j];
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < MNE; ++e) {
+            const double v = a.mval[e];
+            const double* we = w + a.mslot[e];
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                // the addend, not the add, is selected: s + (+0.0) == s bit for bit (s starts at
+                // +0.0 and a round-to-nearest sum is never -0.0 unless both terms are), and the
+                // load stays unconditional (a branch per entry serialised the LDS reads)
+                const double p = v * we[kTPB * j];
+                s[j] = s[j] + (((m[j] >> e) & 1u) ? p : 0.0);
+            }
+        }
+    }
+    double sq = 0.0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const bool own = id[j] != kTplNone;
+        double out;
+        if (MODE == KM_SPMV) {
+            out = s[j];
+        } else if (MODE == KM_SPMV_ADD) {
+            out = py[j] + s[j];
+        } else {
+            const double t = pb[j] - s[j];
+            if (NORM) sq += own ? t * t : 0.0;
+            // Jacobi: x_r from the window at the master's diagonal slot (every template has it)
+            out = MODE == KM_RESID ? t : w[a.mslot[a.mdiag] + kTPB * j] + a.omega * (a.mpd * t);
+        }
+        if (own) a.y[r0 + kTPB * j + tid] = out;
+    }
+    return sq;
+}
+
+template <int MODE, bool NORM, int NPL, int MNE>
+__device__ __forceinline__ double tpl_rows_any(const TplArgs& a, const TplLds& L, __amdgpu_buffer_rsrc_t xrs,
+                                               int r0, const int* id, const int* rr, const double* pb,
+                                               const double* py) {
+    if constexpr (MNE > 0) {
+        static_assert(NPL > 0, "uniform-stencil rows read the x window");
+        return tpl_rows_master<MODE, NORM, MNE>(a, L, r0, id, pb, py);
+    } else {
+        return tpl_rows<MODE, NORM, NPL>(a, L, xrs, r0, id, rr, pb, py);
+    }
+}
+
 template <bool NORM>
 __device__ __forceinline__ void tpl_partial(const TplArgs& a, int blk, double sq) {
     if (NORM) {
@@ -1102,7 +1192,7 @@ constexpr int tpl_waves(int npl) { return npl > 8 ? 4 : 6; }
 constexpr int tpl_march_waves(int npl, bool norm) { return npl == 8 ? (norm ? AMG_MARCH_NORM_WAVES : 7) : tpl_waves(npl); }
 
 // one workgroup per block of kTplRows rows
-template <int MODE, bool NORM, int NPL>
+template <int MODE, bool NORM, int NPL, int MNE = 0>
 __global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
     const TplLds L = tpl_lds_layout<MODE>(a);
     const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
@@ -1110,10 +1200,10 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
     const int r0 = blk * kTplRows;
     TplFetch<MODE, NPL> f;
     f.issue(a, xrs, r0);  // row operands and window first: independent of the table
-    tpl_stage_table<MODE>(a, L);
+    tpl_stage_table<MODE, MNE>(a, L);
     f.commit(a, L);
     __syncthreads();
-    tpl_partial<NORM>(a, blk, tpl_rows<MODE, NORM, NPL>(a, L, xrs, r0, f.id, f.rr, f.pb, f.py));
+    tpl_partial<NORM>(a, blk, tpl_rows_any<MODE, NORM, NPL, MNE>(a, L, xrs, r0, f.id, f.rr, f.pb, f.py));
 }
 
 // Persistent form of the window path: a grid of resident workgroups (a multiple of 8), XCD
@@ -1122,7 +1212,7 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
 // workgroups share.  The table is staged once; the next block's row operands and window are
 // fetched into registers while the current block is computed from LDS (double buffering
 // through registers), so the load latency overlaps the arithmetic.
-template <int MODE, bool NORM, int NPL>
+template <int MODE, bool NORM, int NPL, int MNE = 0>
 __global__ __launch_bounds__(kTPB, tpl_waves(NPL)) void tpl_persist_kernel(TplArgs a, int nblk) {
     static_assert(NPL > 0, "window path only");
     const TplLds L = tpl_lds_layout<MODE>(a);
@@ -1136,7 +1226,7 @@ __global__ __launch_bounds__(kTPB, tpl_waves(NPL)) void tpl_persist_kernel(TplAr
     TplFetch<MODE, NPL> f, c;
     f.issue_ids(a, blk * kTplRows);
     f.issue_window(a, xrs, blk * kTplRows);
-    tpl_stage_table<MODE>(a, L);
+    tpl_stage_table<MODE, MNE>(a, L);
     for (;;) {
         f.commit(a, L);
 #pragma unroll
@@ -1148,7 +1238,7 @@ __global__ __launch_bounds__(kTPB, tpl_waves(NPL)) void tpl_persist_kernel(TplAr
             f.issue_ids(a, nxt * kTplRows);
             f.issue_window(a, xrs, nxt * kTplRows);
         }
-        tpl_partial<NORM>(a, blk, tpl_rows<MODE, NORM, NPL>(a, L, xrs, blk * kTplRows, c.id, c.rr, c.pb, c.py));
+        tpl_partial<NORM>(a, blk, tpl_rows_any<MODE, NORM, NPL, MNE>(a, L, xrs, blk * kTplRows, c.id, c.rr, c.pb, c.py));
         if (nxt >= b1) break;
         __syncthreads();  // every wave is done reading the window before it is overwritten
         blk = nxt;
@@ -1161,7 +1251,7 @@ __global__ __launch_bounds__(kTPB, tpl_waves(NPL)) void tpl_persist_kernel(TplAr
 // the previous block's centre and +plane bands: those slots are copied inside LDS (wsrc) and
 // only the rest is loaded -- 1024 instead of 2048 doubles per 7-pt block.  The next block's
 // loaded slots and row ids are prefetched into registers during the current block.
-template <int MODE, bool NORM, int NPL>
+template <int MODE, bool NORM, int NPL, int MNE = 0>
 __global__ __launch_bounds__(kTPB, tpl_march_waves(NPL, NORM)) void tpl_march_kernel(TplArgs a, int nblk, int S, int nchunk) {
     static_assert(NPL > 0 && NPL % 2 == 0, "window path, slot pairs");
     constexpr int NP = NPL / 2;  // slot pairs per lane (16-byte loads and LDS copies)
@@ -1177,7 +1267,7 @@ __global__ __launch_bounds__(kTPB, tpl_march_waves(NPL, NORM)) void tpl_march_ke
         const int i = 2 * (tid + kTPB * u);
         src[u] = i < a.win ? a.wsrc[i] : -2;  // -2: pair past the window
     }
-    tpl_stage_table<MODE>(a, L);
+    tpl_stage_table<MODE, MNE>(a, L);
     const int K = (nblk + S - 1) / S;           // blocks per column
     const int per = (K + nchunk - 1) / nchunk;  // blocks per chain
     // chains ordered (chunk, column); XCD x = blockIdx % 8 takes a contiguous 1/8 of them, so
@@ -1220,7 +1310,7 @@ __global__ __launch_bounds__(kTPB, tpl_march_waves(NPL, NORM)) void tpl_march_ke
                                                xrs, (nb * kTplRows + gof[u]) * 8, 0, 0))
                                          : v2d_t{0.0, 0.0};
             }
-            tpl_partial<NORM>(a, blk, tpl_rows<MODE, NORM, NPL>(a, L, xrs, r0, c.id, c.rr, c.pb, c.py));
+            tpl_partial<NORM>(a, blk, tpl_rows_any<MODE, NORM, NPL, MNE>(a, L, xrs, r0, c.id, c.rr, c.pb, c.py));
         }
         __syncthreads();  // the next chain's first window overwrites this one
     }
@@ -1443,7 +1533,10 @@ struct TplGsArgs {
     int part_off;        // NORM: partial of block list entry q, wave w at part_off + 4 q + w
 };
 
-template <bool BACK, bool NORM, int NPL>
+// MNE > 0 (variant bit 512): uniform stencil, L.hdr holds each GS template's master-entry
+// mask (tpl_rows_master); the chain coupling is master entry EC (offset -1 forward, +1
+// backward: 2 / 4 of the 7-pt master, 12 / 14 of the 27-pt one -- launch_tpl_gs checks)
+template <bool BACK, bool NORM, int NPL, int MNE = 0>
 __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
     static_assert(NPL > 0, "window path only");
     constexpr int R = kTplRPL;
@@ -1456,22 +1549,79 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
     const int r0 = (g.blocks ? g.blocks[q] : q) * kTplRows;  // null list: every block (no dependent load)
     TplFetch<KM_RESID, NPL> f;  // ids, b, window
     f.issue(a, xrs, r0);
-    tpl_stage_table<KM_RESID>(a, L);
-    if (tid < a.ntpl) loffr[tid] = g.ke[tid];
+    tpl_stage_table<KM_RESID, MNE>(a, L);
+    if (MNE == 0 && tid < a.ntpl) loffr[tid] = g.ke[tid];
     f.commit(a, L);
     __syncthreads();
     double sq = 0.0;
+    // the chain neighbour is in the row's chunk (chunks = global multiples of B; the rank
+    // start is a multiple of 64 and B | 64, so pos = i mod B and only the rank end clips)
+    bool chain[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int i = r0 + kTPB * j + tid, pos = i & (g.B - 1);
+        chain[j] = BACK ? (pos != g.B - 1 && i + 1 < a.n) : pos != 0;
+    }
+    if constexpr (MNE > 0) {
+        static_assert(MNE == 7 || MNE == 27, "chain entry of the instantiated masters");
+        constexpr int EC = MNE == 27 ? (BACK ? 14 : 12) : (BACK ? 4 : 2);
+        constexpr unsigned kFull = (1u << MNE) - 1u;
+        unsigned m[R];
+        bool full = true;
+        double acc[R], sold[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            m[j] = (unsigned)L.hdr[f.id[j]];
+            full = full && m[j] == kFull;
+            acc[j] = f.pb[j];
+            sold[j] = 0.0;
+        }
+        const double* w = L.win + tid;
+        if (__all(full)) {
+#pragma unroll
+            for (int e = 0; e < MNE; ++e) {
+                const double v = a.mval[e];
+                const double* we = w + a.mslot[e];
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const double p = v * we[kTPB * j];
+                    if (NORM) sold[j] = sold[j] + p;
+                    if (e == EC) acc[j] = acc[j] - (chain[j] ? 0.0 : p);
+                    else acc[j] = acc[j] - p;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < MNE; ++e) {
+                const double v = a.mval[e];
+                const double* we = w + a.mslot[e];
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    // selected addends (tpl_rows_master): acc - (+0.0) == acc for every acc
+                    const double p = v * we[kTPB * j];
+                    const bool in = (m[j] >> e) & 1u;
+                    if (NORM) sold[j] = sold[j] + (in ? p : 0.0);
+                    acc[j] = acc[j] - (in && !(e == EC && chain[j]) ? p : 0.0);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            if (f.id[j] != kTplNone) {
+                a.y[r0 + kTPB * j + tid] = acc[j];
+                if (NORM) {
+                    const double rr = f.pb[j] - sold[j];
+                    sq += rr * rr;
+                }
+            }
+    } else {
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         const int lr = kTPB * j + tid, i = r0 + lr;
         const unsigned h = (unsigned)L.hdr[f.id[j]];
         const int st = (int)(h & 0xffffu), ln = (int)((h >> 16) & 0xffu);
-        // the chain neighbour is in the row's chunk (chunks = global multiples of B; the rank
-        // start is a multiple of 64 and B | 64, so pos = i mod B and only the rank end clips)
-        const int pos = i & (g.B - 1);
-        const bool chain = BACK ? (pos != g.B - 1 && i + 1 < a.n) : pos != 0;
         // template entry of the chain coupling (loffr holds the ntpl GS templates only)
-        const int ke = chain && f.id[j] != kTplNone ? loffr[f.id[j]] : -1;
+        const int ke = chain[j] && f.id[j] != kTplNone ? loffr[f.id[j]] : -1;
         double acc = f.pb[j], sold = 0.0;
         for (int k = 0; k < ln; k += 4) {  // 4 entries per step, as in tpl_rows
             const int e = st + k;
@@ -1493,6 +1643,7 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
                 sq += rr * rr;
             }
         }
+    }
     }
     if (NORM) {
         sq = wave_sum(sq);
@@ -1882,6 +2033,10 @@ int kernel_variant(const DevMatrix& A) {
         if (!(e && std::atoi(e) == 0)) var |= 256;
     }
     if (!A.col16.p) var &= ~256;
+    // 512: uniform-stencil template rows, default where the templates are
+    // one master's subsequences (DevMatrix::tpl_mne; AMG_TPL_MASTER=0 at build turns it off)
+    if (!ev && A.tpl_mne > 0) var |= 512;
+    if (A.tpl_mne == 0) var &= ~512;
     return var;
 }
 
@@ -1896,7 +2051,7 @@ int DevMatrix::norm_parts() const {
 // window path: the persistent kernel with a grid of exactly the resident workgroups (its
 // blocks are split statically, so a workgroup that waited for a slot would double the tail),
 // or one workgroup per block when that is no more (AMG_TPL_PERSIST=0: always one per block)
-template <int M, bool N, int P>
+template <int M, bool N, int P, int K>
 static void launch_tpl_window(hipStream_t s, const TplArgs& a, int g, size_t lds) {
     static const bool allow_persist = [] {
         const char* e = std::getenv("AMG_TPL_PERSIST");
@@ -1904,7 +2059,7 @@ static void launch_tpl_window(hipStream_t s, const TplArgs& a, int g, size_t lds
     }();
     if constexpr (P > 8) {  // larger windows: the one-block kernel (27-pt SpMV 146 us; the
                             // persistent form 164, marching 153: profiles/r2w_wide_forms.txt)
-        hipLaunchKernelGGL((tpl_kernel<M, N, P>), dim3(g), dim3(kTPB), lds, s, a);
+        hipLaunchKernelGGL((tpl_kernel<M, N, P, K>), dim3(g), dim3(kTPB), lds, s, a);
         return;
     }
     thread_local int cus = 0, occ = 0;
@@ -1915,14 +2070,14 @@ static void launch_tpl_window(hipStream_t s, const TplArgs& a, int g, size_t lds
         HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
     if (occ_lds != lds) {
-        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tpl_persist_kernel<M, N, P>, kTPB, lds));
+        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tpl_persist_kernel<M, N, P, K>, kTPB, lds));
         occ_lds = lds;
     }
     const int gp = std::min(g, cus * occ) / 8 * 8;
     if (allow_persist && gp >= 8 && g > gp)
-        hipLaunchKernelGGL((tpl_persist_kernel<M, N, P>), dim3(gp), dim3(kTPB), lds, s, a, g);
+        hipLaunchKernelGGL((tpl_persist_kernel<M, N, P, K>), dim3(gp), dim3(kTPB), lds, s, a, g);
     else
-        hipLaunchKernelGGL((tpl_kernel<M, N, P>), dim3(g), dim3(kTPB), lds, s, a);
+        hipLaunchKernelGGL((tpl_kernel<M, N, P, K>), dim3(g), dim3(kTPB), lds, s, a);
 }
 
 // AMG_TPL_MARCH_CHUNKS caps the chains per column (tests: longer chains, so the LDS reuse
@@ -1932,7 +2087,7 @@ int tpl_march_chunk_cap() {
     return e ? std::max(0, std::atoi(e)) : 0;
 }
 
-template <int M, bool N, int P>
+template <int M, bool N, int P, int K>
 static void launch_tpl_march(hipStream_t s, const TplArgs& a, int g, size_t lds, int S) {
     if constexpr (P > 0) {
         // CU count and occupancy per LDS size cached per instantiation (no runtime queries
@@ -1945,7 +2100,7 @@ static void launch_tpl_march(hipStream_t s, const TplArgs& a, int g, size_t lds,
             HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
         }
         if (occ_lds != lds) {
-            HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tpl_march_kernel<M, N, P>, kTPB, lds));
+            HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tpl_march_kernel<M, N, P, K>, kTPB, lds));
             occ_lds = lds;
         }
         const int res = std::max(8, std::max(1, occ) * ncu / 8 * 8);  // resident workgroups
@@ -1953,7 +2108,7 @@ static void launch_tpl_march(hipStream_t s, const TplArgs& a, int g, size_t lds,
         const int cap = tpl_march_chunk_cap();
         if (cap > 0) nchunk = std::min(nchunk, cap);
         const int gp = std::max(8, std::min(res, (S * nchunk + 7) / 8 * 8));
-        hipLaunchKernelGGL((tpl_march_kernel<M, N, P>), dim3(gp), dim3(kTPB), lds, s, a, g, S, nchunk);
+        hipLaunchKernelGGL((tpl_march_kernel<M, N, P, K>), dim3(gp), dim3(kTPB), lds, s, a, g, S, nchunk);
     }
 }
 
@@ -1989,15 +2144,31 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
     a.y = y;
     a.omega = omega;
     a.partial = partial;
+    // uniform stencil (variant bit 512): entry masks instead of the template tables
+    const int mne = win && (kernel_variant(A) & 512) ? A.tpl_mne : 0;
+    if (mne > 0) {
+        AMG_ASSERT(mne <= kTplMasterMax && (int)A.tpl_mslot.size() == mne && A.tpl_mmask.n >= (size_t)A.n_tpl);
+        a.hdr = (const int*)A.tpl_mmask.p;
+        a.nent = 0;
+        a.mdiag = A.tpl_mdiag;
+        a.mpd = A.tpl_mpd;
+        for (int e = 0; e < mne; ++e) a.mslot[e] = A.tpl_mslot[e], a.mval[e] = A.tpl_mval[e];
+    }
     const int npl = !win ? 0 : a.win <= 4 * kTPB ? 4 : a.win <= 8 * kTPB ? 8 : a.win <= 12 * kTPB ? 12 : 16;
     AMG_ASSERT(a.win <= npl * kTPB && a.win <= kTplWin);
     const size_t lds = tpl_lds_bytes(a.win, a.nent, mode == KM_JACOBI);
     const bool march = win && A.tpl_march_s > 0 && (kernel_variant(A) & 128);
     if (march) a.wsrc = A.tpl_wsrc.p;
-#define AMG_T2(M, N, P)                                                     \
-    do {                                                                    \
-        if (march) launch_tpl_march<M, N, P>(s, a, g, lds, A.tpl_march_s);  \
-        else launch_tpl_window<M, N, P>(s, a, g, lds);                      \
+#define AMG_T3(M, N, P, K)                                                     \
+    do {                                                                       \
+        if (march) launch_tpl_march<M, N, P, K>(s, a, g, lds, A.tpl_march_s);  \
+        else launch_tpl_window<M, N, P, K>(s, a, g, lds);                      \
+    } while (0)
+#define AMG_T2(M, N, P)                       \
+    do {                                      \
+        if (mne == 7) AMG_T3(M, N, P, 7);     \
+        else if (mne == 27) AMG_T3(M, N, P, 27); \
+        else AMG_T3(M, N, P, 0);              \
     } while (0)
 #define AMG_T(M, N)                              \
     do {                                         \
@@ -2024,6 +2195,7 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
     }
 #undef AMG_T
 #undef AMG_T2
+#undef AMG_T3
     HIP_CHECK(hipGetLastError());
 }
 
@@ -2227,12 +2399,32 @@ static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, co
     g.first_row = A.first_row;
     g.B = (int)A.gs_block;
     g.part_off = A.n_gs_slabs;
+    // uniform stencil (variant bit 512): GS-template entry masks; the kernel's chain entry is
+    // master entry 2 / 4 (7-pt) or 12 / 14 (27-pt): offsets -1 / +1
+    const int mne = (kernel_variant(A) & 512) && A.gs_tmask.p &&
+                            ((A.tpl_mne == 7 && A.tpl_mem == 2 && A.tpl_mep == 4) ||
+                             (A.tpl_mne == 27 && A.tpl_mem == 12 && A.tpl_mep == 14))
+                        ? A.tpl_mne
+                        : 0;
+    if (mne > 0) {
+        a.hdr = (const int*)A.gs_tmask.p;
+        a.nent = 0;
+        a.mdiag = A.tpl_mdiag;
+        a.mpd = A.tpl_mpd;
+        for (int e = 0; e < mne; ++e) a.mslot[e] = A.tpl_mslot[e], a.mval[e] = A.tpl_mval[e];
+    }
     const int npl = a.win <= 4 * kTPB ? 4 : a.win <= 8 * kTPB ? 8 : a.win <= 12 * kTPB ? 12 : 16;
     AMG_ASSERT(a.win <= npl * kTPB && a.win <= kTplWin);
     const size_t lds = tpl_gs_lds_bytes(a.win, a.nent, a.ntpl);
     const bool norm = partial != nullptr;
     const dim3 grid(g.nblk), blk(kTPB);
-#define AMG_G2(BK, NM, P) hipLaunchKernelGGL((tpl_gs_acc_kernel<BK, NM, P>), grid, blk, lds, s, g)
+#define AMG_G3(BK, NM, P, K) hipLaunchKernelGGL((tpl_gs_acc_kernel<BK, NM, P, K>), grid, blk, lds, s, g)
+#define AMG_G2(BK, NM, P)                          \
+    do {                                           \
+        if (mne == 7) AMG_G3(BK, NM, P, 7);        \
+        else if (mne == 27) AMG_G3(BK, NM, P, 27); \
+        else AMG_G3(BK, NM, P, 0);                 \
+    } while (0)
 #define AMG_G(BK, NM)                         \
     do {                                      \
         switch (npl) {                        \
@@ -2247,6 +2439,7 @@ static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, co
     else AMG_G(false, false);
 #undef AMG_G
 #undef AMG_G2
+#undef AMG_G3
     HIP_CHECK(hipGetLastError());
     TplGsChainArgs c{A.gs_racc.p, x, A.gs_tid.p, A.gs_tdl.p, backward ? A.gs_tcvp.p : A.gs_tcvm.p,
                      A.gs_tcf.p, A.n_gs_tpl, g.blocks, A.n_gs_tblk, (int)A.gs_block, (int)A.n_rows,

@@ -548,6 +548,62 @@ static TplBuild build_templates(const std::vector<int>& rp, const hvec<int>& col
     return T;
 }
 
+// Uniform stencil: a constant-coefficient stencil's boundary templates are
+// its interior template with entries removed.  When the longest template (the master) has a
+// kernel instantiation (7 or 27 entries) and every template's (offset, value bits) entries are
+// a subsequence of the master's -- in order, since offsets ascend -- and holds the master's
+// diagonal with the same 1/a_ii, a row is (master, entry mask): the kernels take values and
+// window slots from kernel arguments and skip the entries a row lacks.  The products and their
+// order are the row's own, so results are unchanged (bit-identical).
+static void find_master_template(DevMatrix& D, const TplBuild& tb, const std::vector<int>& ldo) {
+    D.tpl_mne = 0;
+    D.tpl_mdiag = D.tpl_mem = D.tpl_mep = -1;
+    D.tpl_mslot.clear();
+    D.tpl_mval.clear();
+    D.tpl_mmask.reset();
+    const char* env = std::getenv("AMG_TPL_MASTER");
+    if (env && std::atoi(env) == 0) return;
+    const int nt = (int)tb.hdr.size();
+    if (nt == 0) return;
+    auto start = [&](int t) { return tb.hdr[t] & 0xffff; };
+    auto len = [&](int t) { return (tb.hdr[t] >> 16) & 0xff; };
+    auto diag = [&](int t) { return (int)((unsigned)tb.hdr[t] >> 24); };
+    auto bits = [](double v) {
+        uint64_t u;
+        std::memcpy(&u, &v, sizeof(u));
+        return u;
+    };
+    int M = 0;
+    for (int t = 1; t < nt; ++t)
+        if (len(t) > len(M)) M = t;
+    const int ne = len(M);
+    if ((ne != 7 && ne != 27) || diag(M) == 255) return;
+    const int sm = start(M);
+    std::vector<unsigned> mask(nt, 0u);
+    for (int t = 0; t < nt; ++t) {
+        if (diag(t) == 255 || bits(tb.pd[t]) != bits(tb.pd[M])) return;
+        int e = 0;
+        for (int k = 0; k < len(t); ++k) {
+            const int o = tb.off[start(t) + k];
+            while (e < ne && tb.off[sm + e] != o) ++e;
+            if (e == ne || bits(tb.val[start(t) + k]) != bits(tb.val[sm + e])) return;
+            mask[t] |= 1u << e;
+            ++e;
+        }
+        if (!(mask[t] >> diag(M) & 1u)) return;
+    }
+    D.tpl_mne = ne;
+    D.tpl_mdiag = diag(M);
+    D.tpl_mpd = tb.pd[M];
+    for (int e = 0; e < ne; ++e) {
+        D.tpl_mslot.push_back(ldo[sm + e]);
+        D.tpl_mval.push_back(tb.val[sm + e]);
+        if (tb.off[sm + e] == -1) D.tpl_mem = e;
+        if (tb.off[sm + e] == 1) D.tpl_mep = e;
+    }
+    D.tpl_mmask.upload(mask.data(), mask.size());
+}
+
 void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
     build_view(c, h, replicated_view);
     host = std::move(h);
@@ -730,6 +786,7 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
                 }
                 tpl_win = base;
                 tpl_ldo.upload(ldo.data(), ldo.size());
+                find_master_template(*this, tb, ldo);
                 // z-marching: the shift D (a multiple of kTplRows, taken from the band
                 // starts) under which the most window slots of a block are slots of the block
                 // D rows back; used when at least a quarter of the window is reused
@@ -786,6 +843,10 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
             tpl_off.reset();
             tpl_val.reset();
             tpl_pd.reset();
+        }
+        if (tpl_win == 0) {
+            tpl_mne = 0;
+            tpl_mmask.reset();
         }
         tm.lap("    build: template window / march");
         blocks.upload(bb.blocks.data(), bb.blocks.size());
@@ -1025,6 +1086,7 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
     gs_tcf.reset();
     gs_tkem.reset();
     gs_tkep.reset();
+    gs_tmask.reset();
     gs_racc.reset();
     {
         const char* e = std::getenv("AMG_GS_TEMPLATES");
@@ -1110,6 +1172,12 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
                     gs_thdr.upload(gh.data(), gh.size());
                     gs_tdl.upload(gdl.data(), gdl.size());
                     gs_tblocks.upload(blist.data(), blist.size());
+                    if (tpl_mne > 0) {  // uniform stencil: a GS template's mask is its row template's
+                        std::vector<unsigned> tm_(n_tpl), gm(gbase.size());
+                        HIP_CHECK(hipMemcpy(tm_.data(), tpl_mmask.p, sizeof(unsigned) * n_tpl, hipMemcpyDeviceToHost));
+                        for (size_t k = 0; k < gbase.size(); ++k) gm[k] = tm_[gbase[k]];
+                        gs_tmask.upload(gm.data(), gm.size());
+                    }
                     n_gs_tpl = (int)gbase.size();
                     n_gs_tblk = (int)blist.size();
                 } else {

@@ -103,27 +103,33 @@ WIDE = [("27pt", (200, 8, 8), 12), ("27pt", (260, 8, 8), 16), ("27pt", (256, 16,
         ("27pt", (40, 40, 40), 8), ("7pt", (40, 40, 40), 8), ("5pt", (200, 60), 4)]
 
 
-@pytest.mark.parametrize("path", ["window", "march"])
+@pytest.mark.parametrize("path", ["window", "march", "generic", "generic_march"])
 @pytest.mark.parametrize("kind,dims,npl", WIDE, ids=[f"{k}-{'x'.join(map(str, d))}" for k, d, _ in WIDE])
 def test_template_window_lanes(ctx, oracle, monkeypatch, kind, dims, npl, path):
-    """tpl_kernel<*, *, NPL> (window) and tpl_march_kernel<*, *, NPL> (forced by variant bit
-    128, chains capped at one per column so every block after a chain's first copies its
-    reused slots inside LDS) at every lanes-per-row instantiation, all modes + norm."""
+    """tpl_kernel<*, *, NPL, MNE> (window) and tpl_march_kernel<*, *, NPL, MNE> (forced by
+    variant bit 128, chains capped at one per column so every block after a chain's first
+    copies its reused slots inside LDS) at every lanes-per-row instantiation, all modes + norm,
+    with uniform-stencil rows (MNE = 7 / 27: every template a subsequence of the master, bit
+    512, the default where it applies) and with the per-template tables (generic)."""
     import raptor_amd as ra
 
     O = oracle
-    if path == "march" and npl == 4:
+    if path.endswith("march") and npl == 4:
         pytest.skip("a window of <= 1024 doubles is one band: no reusing shift exists")
     gen = {"7pt": O.gen_7pt, "27pt": O.gen_27pt, "5pt": O.gen_5pt}[kind]
     Ao = gen(*dims)
-    if path == "march":
-        monkeypatch.setenv("AMG_KERNEL_VARIANT", "170")
+    if path.endswith("march"):
+        monkeypatch.setenv("AMG_KERNEL_VARIANT", "170" if path == "generic_march" else str(170 | 512))
         monkeypatch.setenv("AMG_TPL_MARCH_CHUNKS", "1")
+    if path.startswith("generic"):
+        monkeypatch.setenv("AMG_TPL_MASTER", "0")
     A = _dev(ra, ctx, Ao)
     inf = A.info
     assert inf["template_rows"] == Ao.shape[0]
     assert inf["tpl_lanes"] == npl, inf
-    if path == "march":
+    master = 0 if path.startswith("generic") else {"7pt": 7, "27pt": 27, "5pt": 0}[kind]
+    assert inf["tpl_master"] == master, inf
+    if path.endswith("march"):
         S = inf["tpl_march_shift"]
         assert S > 0, "no reusing shift found"
         blocks = -(-Ao.shape[0] // 512)
@@ -313,19 +319,24 @@ def test_full_size_27pt_256(ctx, oracle):
 GS_SHAPES = [("27pt", (260, 8, 8)), ("27pt", (40, 40, 40)), ("7pt", (37, 41, 29)), ("5pt", (200, 61))]
 
 
-@pytest.mark.parametrize("tpl_gs", [True, False], ids=["templates", "ell"])
+@pytest.mark.parametrize("tpl_gs", ["templates", "generic", "ell"])
 @pytest.mark.parametrize("kind,dims", GS_SHAPES, ids=[f"{k}-{'x'.join(map(str, d))}" for k, d in GS_SHAPES])
 def test_hybrid_gs_template_kernel(ctx, oracle, monkeypatch, kind, dims, tpl_gs):
     """l1 hybrid GS, forward / backward, block sizes 64, 32, 8, 1 (the template kernel needs B
     | 64) and 17, 48 (sliced ELL only): bit-identical to the oracle on templated stencils
-    (NPL 16, 8 and 4 windows; a last partial block), with the template kernel on and off."""
+    (NPL 16, 8 and 4 windows; a last partial block), with the template kernel on -- uniform-
+    stencil masks (7-pt, 27-pt) or per-template tables (generic) -- and off."""
     import raptor_amd as ra
 
     O = oracle
-    if not tpl_gs:
+    if tpl_gs == "ell":
         monkeypatch.setenv("AMG_GS_TEMPLATES", "0")
+    if tpl_gs == "generic":
+        monkeypatch.setenv("AMG_TPL_MASTER", "0")
     Ao = {"7pt": O.gen_7pt, "27pt": O.gen_27pt, "5pt": O.gen_5pt}[kind](*dims)
     A = _dev(ra, ctx, Ao)
+    expect = {"7pt": 7, "27pt": 27, "5pt": 0}[kind] if tpl_gs != "generic" else 0
+    assert A.info["tpl_master"] == expect
     n = Ao.shape[0]
     x, b = O.vec_uniform(n, 3), O.vec_uniform(n, 4)
     dx, db, out = to_dev(ctx, x), to_dev(ctx, b), ctx.empty(n)
@@ -339,18 +350,21 @@ def test_hybrid_gs_template_kernel(ctx, oracle, monkeypatch, kind, dims, tpl_gs)
     # row + table) when they are on, sliced ELL (>= 5 B per cell) when off
     A.hybrid_gs(dx, db, out, 8)
     per_row = A._info()["gs_bytes"] / n
-    assert (per_row < 60) if tpl_gs else (per_row > 60), per_row
+    assert (per_row < 60) if tpl_gs != "ell" else (per_row > 60), per_row
 
 
-@pytest.mark.parametrize("tpl_gs", [True, False], ids=["templates", "ell"])
+@pytest.mark.parametrize("tpl_gs", ["templates", "generic", "ell"])
 def test_sa_gs_vcycle_template_kernel(ctx, oracle, monkeypatch, tpl_gs):
     """SA + hybrid GS V-cycle and solve (fused forward-GS norm partials from both GS kernels)
-    against the oracle hierarchy, level-0 GS on the template kernel or on sliced ELL."""
+    against the oracle hierarchy, level-0 GS on the template kernel (uniform-stencil masks or
+    per-template tables) or on sliced ELL."""
     import raptor_amd as ra
 
     O = oracle
-    if not tpl_gs:
+    if tpl_gs == "ell":
         monkeypatch.setenv("AMG_GS_TEMPLATES", "0")
+    if tpl_gs == "generic":
+        monkeypatch.setenv("AMG_TPL_MASTER", "0")
     dims = (64, 40, 24)
     Ao = O.gen_27pt(*dims)
     A = ra.par_stencil_grid(ctx, "27pt", dims)
