@@ -52,6 +52,9 @@ constexpr int kTplMaxLen = 64;     // entries per template
 #ifndef AMG_TPL_BATCH  // build-time knob: window entries per batch in the template kernel (0: one)
 #define AMG_TPL_BATCH 0
 #endif
+#ifndef AMG_TPL_MASK_BRANCH  // build-time knob: masked uniform-stencil rows add under exec masks
+#define AMG_TPL_MASK_BRANCH 0
+#endif
 #ifndef AMG_TPL_RPL  // build-time knob for same-box A/B builds (scripts/gpu_libab.sh)
 #define AMG_TPL_RPL 2
 #endif

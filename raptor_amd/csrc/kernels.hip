@@ -887,7 +887,16 @@ __device__ __forceinline__ void tpl_slot_offsets(const TplArgs& a, int (&go)[NS]
 }
 
 // the row operands and x window of the rows block starting at r0, into registers
-template <int MODE, int NPL>
+// lane tid's row j of a block: local index tpl_lrow<ROT>(tid, j).  ROT (uniform-stencil kernels)
+// rotates the lanes by one row, so on a 256-wide grid the two x-boundary rows of a y line (local
+// 0 and 255) land in the same wave (lanes 255 and 254) and the other three waves hold interior
+// rows only -- waves with a boundary row take the masked path (tpl_rows_master)
+template <bool ROT>
+__device__ __forceinline__ int tpl_lrow(int tid, int j) {
+    return kTPB * j + (ROT ? ((tid + 1) & (kTPB - 1)) : tid);
+}
+
+template <int MODE, int NPL, bool ROT = false>
 struct TplFetch {
     static constexpr int R = kTplRPL, NP = NPL > 0 ? NPL : 1;
     int id[R], rr[R];
@@ -903,7 +912,7 @@ struct TplFetch {
     __device__ __forceinline__ void issue_ids(const TplArgs& a, int r0) {
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            const int r = r0 + kTPB * j + (int)threadIdx.x;
+            const int r = r0 + tpl_lrow<ROT>((int)threadIdx.x, j);
             rr[j] = min(r, a.n - 1);
             const int t = a.id[rr[j]];
             id[j] = r < a.n ? t : kTplNone;
@@ -1112,7 +1121,7 @@ __device__ __forceinline__ double tpl_rows_master(const TplArgs& a, const TplLds
         m[j] = (unsigned)L.hdr[id[j]];
         full = full && m[j] == kFull;
     }
-    const double* w = L.win + tid;
+    const double* w = L.win + tpl_lrow<true>(tid, 0);
     double s[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) s[j] = 0.0;
@@ -1129,6 +1138,23 @@ __device__ __forceinline__ double tpl_rows_master(const TplArgs& a, const TplLds
         for (int e = 0; e < MNE; ++e) {
             const double v = a.mval[e];
             const double* we = w + a.mslot[e];
+#if AMG_TPL_MASK_BRANCH
+            // exec-masked adds: the products are formed unconditionally (the asm pins them
+            // before the branch, so the LDS reads are not sunk into it), the add runs only in
+            // the lanes whose row has the entry
+            double p[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                p[j] = v * we[kTPB * j];
+                asm volatile("" : "+v"(p[j]));
+            }
+#pragma unroll
+            for (int j = 0; j < R; ++j)
+                if ((m[j] >> e) & 1u) {
+                    asm volatile("" : "+v"(s[j]));
+                    s[j] = s[j] + p[j];
+                }
+#else
 #pragma unroll
             for (int j = 0; j < R; ++j) {
                 // the addend, not the add, is selected: s + (+0.0) == s bit for bit (s starts at
@@ -1137,6 +1163,7 @@ __device__ __forceinline__ double tpl_rows_master(const TplArgs& a, const TplLds
                 const double p = v * we[kTPB * j];
                 s[j] = s[j] + (((m[j] >> e) & 1u) ? p : 0.0);
             }
+#endif
         }
     }
     double sq = 0.0;
@@ -1154,7 +1181,7 @@ __device__ __forceinline__ double tpl_rows_master(const TplArgs& a, const TplLds
             // Jacobi: x_r from the window at the master's diagonal slot (every template has it)
             out = MODE == KM_RESID ? t : w[a.mslot[a.mdiag] + kTPB * j] + a.omega * (a.mpd * t);
         }
-        if (own) a.y[r0 + kTPB * j + tid] = out;
+        if (own) a.y[r0 + tpl_lrow<true>(tid, j)] = out;
     }
     return sq;
 }
@@ -1198,7 +1225,7 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_kernel(TplArgs a) {
     const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int r0 = blk * kTplRows;
-    TplFetch<MODE, NPL> f;
+    TplFetch<MODE, NPL, (MNE > 0)> f;
     f.issue(a, xrs, r0);  // row operands and window first: independent of the table
     tpl_stage_table<MODE, MNE>(a, L);
     f.commit(a, L);
@@ -1223,7 +1250,7 @@ __global__ __launch_bounds__(kTPB, tpl_waves(NPL)) void tpl_persist_kernel(TplAr
     int blk = b0 + lw;
     if (blk >= b1) return;  // workgroup-uniform: no barrier is skipped by part of a group
     // f: the next block's ids and window (registers); c: the current block's row operands
-    TplFetch<MODE, NPL> f, c;
+    TplFetch<MODE, NPL, (MNE > 0)> f, c;
     f.issue_ids(a, blk * kTplRows);
     f.issue_window(a, xrs, blk * kTplRows);
     tpl_stage_table<MODE, MNE>(a, L);
@@ -1274,7 +1301,7 @@ __global__ __launch_bounds__(kTPB, tpl_march_waves(NPL, NORM)) void tpl_march_ke
     // the workgroups of one XCD walk neighbouring columns of the same planes side by side
     const int C = S * nchunk, x = blockIdx.x & 7, lw = blockIdx.x >> 3, nw = gridDim.x >> 3;
     const int c0 = x * (C >> 3) + min(x, C & 7), c1 = c0 + (C >> 3) + (x < (C & 7) ? 1 : 0);
-    TplFetch<MODE, NPL> f, c;
+    TplFetch<MODE, NPL, (MNE > 0)> f, c;
     v2d_t gv[NP];
     for (int ch = c0 + lw; ch < c1; ch += nw) {
         const int col = ch % S, t0 = (ch / S) * per, t1 = min(K, t0 + per);
@@ -1547,7 +1574,7 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
     const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
     const int q = xcd_remap(blockIdx.x, gridDim.x);
     const int r0 = (g.blocks ? g.blocks[q] : q) * kTplRows;  // null list: every block (no dependent load)
-    TplFetch<KM_RESID, NPL> f;  // ids, b, window
+    TplFetch<KM_RESID, NPL, (MNE > 0)> f;  // ids, b, window
     f.issue(a, xrs, r0);
     tpl_stage_table<KM_RESID, MNE>(a, L);
     if (MNE == 0 && tid < a.ntpl) loffr[tid] = g.ke[tid];
@@ -1559,7 +1586,7 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
     bool chain[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-        const int i = r0 + kTPB * j + tid, pos = i & (g.B - 1);
+        const int i = r0 + tpl_lrow<(MNE > 0)>(tid, j), pos = i & (g.B - 1);
         chain[j] = BACK ? (pos != g.B - 1 && i + 1 < a.n) : pos != 0;
     }
     if constexpr (MNE > 0) {
@@ -1576,7 +1603,7 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
             acc[j] = f.pb[j];
             sold[j] = 0.0;
         }
-        const double* w = L.win + tid;
+        const double* w = L.win + tpl_lrow<true>(tid, 0);
         if (__all(full)) {
 #pragma unroll
             for (int e = 0; e < MNE; ++e) {
@@ -1608,7 +1635,7 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
 #pragma unroll
         for (int j = 0; j < R; ++j)
             if (f.id[j] != kTplNone) {
-                a.y[r0 + kTPB * j + tid] = acc[j];
+                a.y[r0 + tpl_lrow<true>(tid, j)] = acc[j];
                 if (NORM) {
                     const double rr = f.pb[j] - sold[j];
                     sq += rr * rr;
@@ -1681,7 +1708,11 @@ __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
     double* sdl = chain_lds;
     double* scv = sdl + a.ntpl;
     int* scf = (int*)(scv + a.ntpl);
-    __shared__ __attribute__((aligned(16))) double sacc[64 * U], sx[64 * U];
+    // stage of one batch, row-major by batch row u with a padded stride (kSt = 65): lane c's
+    // walk reads u * kSt + c (consecutive lanes, no bank conflict); chunk-major [c][u] had a
+    // 64-byte lane stride and a 16-way conflict on every read of the walk
+    constexpr int kSt = 65;
+    __shared__ __attribute__((aligned(16))) double sacc[kSt * U], sx[kSt * U];
     __shared__ unsigned sid[64 * 2];
     const int lane = threadIdx.x;
     constexpr int kBit = BACK ? 2 : 1;
@@ -1726,9 +1757,11 @@ __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
         for (int bi = 0; bi < nb; ++bi) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int slot = (16 * u + (lane >> 2)) * U + 2 * (lane & 3);
-                *(v2d_t*)(sacc + slot) = ra[u];
-                *(v2d_t*)(sx + slot) = rx[u];
+                const int slot = 2 * (lane & 3) * kSt + 16 * u + (lane >> 2);
+                sacc[slot] = ra[u].x;
+                sacc[slot + kSt] = ra[u].y;
+                sx[slot] = rx[u].x;
+                sx[slot + kSt] = rx[u].y;
             }
             sid[2 * lane] = ri.x;
             sid[2 * lane + 1] = ri.y;
@@ -1740,21 +1773,23 @@ __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
             for (int t = 0; t < U; ++t) {
                 const int u = BACK ? U - 1 - t : t;
                 const int tp = (int)((iw[u >> 2] >> (8 * (u & 3))) & 0xffu);
-                double acc = sacc[lane * U + u];
+                double acc = sacc[u * kSt + lane];
                 // the chunk's first row in sweep order has no chain neighbour; a template
                 // without the neighbour entry (boundary row) has none either
                 if ((bi > 0 || t > 0) && scf[tp]) acc -= scv[tp] * prev;
-                prev = sx[lane * U + u] + acc * sdl[tp];
+                prev = sx[u * kSt + lane] + acc * sdl[tp];
                 out[u] = prev;
             }
             // x' back through the stage: whole 64-byte lines per 4 lanes, like the loads
 #pragma unroll
-            for (int u = 0; u < U; ++u) sacc[lane * U + u] = out[u];
+            for (int u = 0; u < U; ++u) sacc[u * kSt + lane] = out[u];
             __syncthreads();
             const int off = (BACK ? nb - 1 - bi : bi) * U;
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                *(v2d_t*)(a.y + ls[u] + off) = *(const v2d_t*)(sacc + (16 * u + (lane >> 2)) * U + 2 * (lane & 3));
+            for (int u = 0; u < 4; ++u) {
+                const int slot = 2 * (lane & 3) * kSt + 16 * u + (lane >> 2);
+                *(v2d_t*)(a.y + ls[u] + off) = v2d_t{sacc[slot], sacc[slot + kSt]};
+            }
             __syncthreads();  // the stage is rewritten by the next batch
         }
     } else if (live) {
@@ -2057,8 +2092,13 @@ static void launch_tpl_window(hipStream_t s, const TplArgs& a, int g, size_t lds
         const char* e = std::getenv("AMG_TPL_PERSIST");
         return !(e && std::atoi(e) == 0);
     }();
-    if constexpr (P > 8) {  // larger windows: the one-block kernel (27-pt SpMV 146 us; the
-                            // persistent form 164, marching 153: profiles/r2w_wide_forms.txt)
+    // larger windows: the one-block kernel (27-pt SpMV 146 us; the persistent form 164,
+    // marching 153: profiles/r2w_wide_forms.txt); AMG_TPL_WIDE_PERSIST=1: persistent (A/B)
+    static const bool wide_persist = [] {
+        const char* e = std::getenv("AMG_TPL_WIDE_PERSIST");
+        return e && std::atoi(e) != 0;
+    }();
+    if (P > 8 && !wide_persist) {
         hipLaunchKernelGGL((tpl_kernel<M, N, P, K>), dim3(g), dim3(kTPB), lds, s, a);
         return;
     }
