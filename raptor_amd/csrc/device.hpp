@@ -52,6 +52,9 @@ constexpr int kTplMaxLen = 64;     // entries per template
 #ifndef AMG_TPL_BATCH  // build-time knob: window entries per batch in the template kernel (0: one)
 #define AMG_TPL_BATCH 0
 #endif
+#ifndef AMG_TPL_SPLIT_READS  // build-time knob: uniform-stencil rows read each row's x separately
+#define AMG_TPL_SPLIT_READS 1
+#endif
 #ifndef AMG_TPL_MASK_BRANCH  // build-time knob: masked uniform-stencil rows add under exec masks
 #define AMG_TPL_MASK_BRANCH 0
 #endif

@@ -1107,6 +1107,21 @@ __device__ __forceinline__ double tpl_rows(const TplArgs& a, const TplLds& L, __
 // wave whose rows are all the master the adds are unconditional; otherwise a lane adds only
 // the entries its row has.  Each row's products and their order are its own CSR row's:
 // results are bit-identical to tpl_rows (and the oracle).
+// The lane's window base for each of its rows.  With AMG_TPL_SPLIT_READS the row stride (kTPB
+// doubles) is hidden from the compiler, so the rows' reads of one entry stay two ds_read_b64
+// (2 LDS cycles each) instead of being merged into one ds_read2st64_b64 (8 cycles for the same
+// 1 KiB: MI355X_MICROARCH.md, LDS table); costs one address add per entry
+template <int R>
+__device__ __forceinline__ void tpl_row_bases(const TplLds& L, const double* (&wr)[R]) {
+    int rs = kTPB;
+#if AMG_TPL_SPLIT_READS
+    asm volatile("" : "+v"(rs));
+#endif
+    const double* w0 = L.win + tpl_lrow<true>((int)threadIdx.x, 0);
+#pragma unroll
+    for (int j = 0; j < R; ++j) wr[j] = w0 + j * rs;
+}
+
 template <int MODE, bool NORM, int MNE>
 __device__ __forceinline__ double tpl_rows_master(const TplArgs& a, const TplLds& L, int r0, const int* id,
                                                   const double* pb, const double* py) {
@@ -1121,7 +1136,8 @@ __device__ __forceinline__ double tpl_rows_master(const TplArgs& a, const TplLds
         m[j] = (unsigned)L.hdr[id[j]];
         full = full && m[j] == kFull;
     }
-    const double* w = L.win + tpl_lrow<true>(tid, 0);
+    const double* wr[R];
+    tpl_row_bases<R>(L, wr);
     double s[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) s[j] = 0.0;
@@ -1129,15 +1145,15 @@ __device__ __forceinline__ double tpl_rows_master(const TplArgs& a, const TplLds
 #pragma unroll
         for (int e = 0; e < MNE; ++e) {
             const double v = a.mval[e];
-            const double* we = w + a.mslot[e];
+            const int c = a.mslot[e];
 #pragma unroll
-            for (int j = 0; j < R; ++j) s[j] = s[j] + v * we[kTPB * j];
+            for (int j = 0; j < R; ++j) s[j] = s[j] + v * wr[j][c];
         }
     } else {
 #pragma unroll
         for (int e = 0; e < MNE; ++e) {
             const double v = a.mval[e];
-            const double* we = w + a.mslot[e];
+            const int c = a.mslot[e];
 #if AMG_TPL_MASK_BRANCH
             // exec-masked adds: the products are formed unconditionally (the asm pins them
             // before the branch, so the LDS reads are not sunk into it), the add runs only in
@@ -1145,7 +1161,7 @@ __device__ __forceinline__ double tpl_rows_master(const TplArgs& a, const TplLds
             double p[R];
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                p[j] = v * we[kTPB * j];
+                p[j] = v * wr[j][c];
                 asm volatile("" : "+v"(p[j]));
             }
 #pragma unroll
@@ -1160,7 +1176,7 @@ __device__ __forceinline__ double tpl_rows_master(const TplArgs& a, const TplLds
                 // the addend, not the add, is selected: s + (+0.0) == s bit for bit (s starts at
                 // +0.0 and a round-to-nearest sum is never -0.0 unless both terms are), and the
                 // load stays unconditional (a branch per entry serialised the LDS reads)
-                const double p = v * we[kTPB * j];
+                const double p = v * wr[j][c];
                 s[j] = s[j] + (((m[j] >> e) & 1u) ? p : 0.0);
             }
 #endif
@@ -1179,7 +1195,7 @@ __device__ __forceinline__ double tpl_rows_master(const TplArgs& a, const TplLds
             const double t = pb[j] - s[j];
             if (NORM) sq += own ? t * t : 0.0;
             // Jacobi: x_r from the window at the master's diagonal slot (every template has it)
-            out = MODE == KM_RESID ? t : w[a.mslot[a.mdiag] + kTPB * j] + a.omega * (a.mpd * t);
+            out = MODE == KM_RESID ? t : wr[j][a.mslot[a.mdiag]] + a.omega * (a.mpd * t);
         }
         if (own) a.y[r0 + tpl_lrow<true>(tid, j)] = out;
     }
@@ -1603,15 +1619,16 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
             acc[j] = f.pb[j];
             sold[j] = 0.0;
         }
-        const double* w = L.win + tpl_lrow<true>(tid, 0);
+        const double* wr[R];
+        tpl_row_bases<R>(L, wr);
         if (__all(full)) {
 #pragma unroll
             for (int e = 0; e < MNE; ++e) {
                 const double v = a.mval[e];
-                const double* we = w + a.mslot[e];
+                const int c = a.mslot[e];
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
-                    const double p = v * we[kTPB * j];
+                    const double p = v * wr[j][c];
                     if (NORM) sold[j] = sold[j] + p;
                     if (e == EC) acc[j] = acc[j] - (chain[j] ? 0.0 : p);
                     else acc[j] = acc[j] - p;
@@ -1621,11 +1638,11 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
 #pragma unroll
             for (int e = 0; e < MNE; ++e) {
                 const double v = a.mval[e];
-                const double* we = w + a.mslot[e];
+                const int c = a.mslot[e];
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
                     // selected addends (tpl_rows_master): acc - (+0.0) == acc for every acc
-                    const double p = v * we[kTPB * j];
+                    const double p = v * wr[j][c];
                     const bool in = (m[j] >> e) & 1u;
                     if (NORM) sold[j] = sold[j] + (in ? p : 0.0);
                     acc[j] = acc[j] - (in && !(e == EC && chain[j]) ? p : 0.0);

@@ -4,7 +4,7 @@
 # GPU), and rocprofv3 --kernel-trace --stats of the bench command
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-R=r3z
+R=${R:-r3z}
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 880 --timeout-method thread > gpurun_out/${R}_tests.log 2>&1 || { tail -40 gpurun_out/${R}_tests.log; exit 1; }
 tail -2 gpurun_out/${R}_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${R}_smoke.log 2>&1 || { tail gpurun_out/${R}_smoke.log; exit 1; }
@@ -16,9 +16,11 @@ done
 AMG_BENCH_SHARED_GPU=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu-baseline --spmv-reps 5 > gpurun_out/${R}_n2_boxes.json 2> gpurun_out/${R}_n2_boxes.err || { tail -20 gpurun_out/${R}_n2_boxes.err; exit 1; }
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${R}_prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${R}_prof.log 2>&1 || { tail gpurun_out/${R}_prof.log; exit 1; }
 python scripts/trace_summary.py gpurun_out/${R}_prof/run_kernel_trace.csv > gpurun_out/${R}_trace_summary.txt
-python - <<'PY'
+export R; python - <<'PY'
 import json
-for f in ("r3z_bench", "r3z_sa27", "r3z_g3sub", "r3z_n2_boxes"):
+import os
+R = os.environ.get("R", "r3z")
+for f in (f"{R}_bench", f"{R}_sa27", f"{R}_g3sub", f"{R}_n2_boxes"):
     d = json.load(open(f"gpurun_out/{f}.json"))
     print(f, d["value"], d["ms_per_step"], "setup_s", d["config"].get("setup_s"), "roofline", d["roofline"]["frac"],
           "cpu", (d.get("cpu_baseline") or {}).get("value"))
