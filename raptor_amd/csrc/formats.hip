@@ -13,7 +13,7 @@ namespace amg {
 namespace {
 
 constexpr int kT = 256;
-static_assert(kT == kTPB && kT == kTileLines, "one thread per lane / tile line");
+static_assert(kT == kTPB && kTileLines % kT == 0, "one thread per lane, whole tile rows per thread");
 
 __device__ __forceinline__ size_t lane_pos_d(int j, int nu) {
     return (size_t)((j & (2 * kTPB - 1)) >> 1) * (size_t)nu + 2 * (size_t)(j / (2 * kTPB)) + (size_t)(j & 1);
@@ -41,12 +41,13 @@ __global__ __launch_bounds__(kT) void copy_blocks_kernel(const int2* __restrict_
 // x-tile line ids at a fixed stride, padded with the block's last line (0 for untiled blocks)
 __global__ __launch_bounds__(kT) void tile_fixed_kernel(const int* __restrict__ tile_ptr,
                                                         const int* __restrict__ tile_lines, int* __restrict__ fx) {
-    const int q = blockIdx.x, j = threadIdx.x;
+    const int q = blockIdx.x;
     const int t0 = tile_ptr[q], nt = tile_ptr[q + 1] - t0;
-    fx[(size_t)q * kTileLines + j] = (nt > 0 && nt <= kTileLines) ? tile_lines[t0 + min(j, nt - 1)] : 0;
+    for (int j = threadIdx.x; j < kTileLines; j += kT)
+        fx[(size_t)q * kTileLines + j] = (nt > 0 && nt <= kTileLines) ? tile_lines[t0 + min(j, nt - 1)] : 0;
 }
 
-// per entry: slot of its x line in the block's sorted tile * 8 + element in the line,
+// per entry: slot of its x line in the block's sorted tile * kLineW + element in the line,
 // lane-major (lane_pos); blocks over kCAP entries or without a tile keep zeros
 __global__ __launch_bounds__(kT) void tile_index_kernel(const int2* __restrict__ blocks, const int* __restrict__ rp,
                                                         const int* __restrict__ col, const int* __restrict__ tile_ptr,
@@ -57,18 +58,18 @@ __global__ __launch_bounds__(kT) void tile_index_kernel(const int2* __restrict__
     const int kb = rp[b.x], nz = rp[b.y] - kb;
     const int t0 = tile_ptr[q], nt = tile_ptr[q + 1] - t0;
     if (nz > kCAP || nt <= 0 || nt > kTileLines) return;
-    const int hl0 = (int)(((long long)ncl + 7) / 8);
+    const int hl0 = (int)(((long long)ncl + kLineW - 1) / kLineW);
     for (int j = threadIdx.x; j < nz; j += kT) {
         const int c = col[kb + j];
-        const int L = c < ncl ? c >> 3 : hl0 + ((c - ncl) >> 3);
-        const int e = c < ncl ? (c & 7) : ((c - ncl) & 7);
+        const int L = c < ncl ? c >> kLineShift : hl0 + ((c - ncl) >> kLineShift);
+        const int e = c < ncl ? (c & (kLineW - 1)) : ((c - ncl) & (kLineW - 1));
         int lo = 0, hi = nt;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             if (tile_lines[t0 + mid] < L) lo = mid + 1;
             else hi = mid;
         }
-        perm[(size_t)q * kCAP + lane_pos_d(j, kCAP / kTPB)] = (uint16_t)(lo * 8 + e);
+        perm[(size_t)q * kCAP + lane_pos_d(j, kCAP / kTPB)] = (uint16_t)(lo * kLineW + e);
     }
 }
 

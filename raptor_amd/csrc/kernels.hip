@@ -66,7 +66,7 @@ struct CsrArgs {
     const double* xh;  // halo part of x
     int ncl;           // number of local columns
     int nhalo;
-    int hl0;           // first halo line id = ceil(ncl / 8)
+    int hl0;           // first halo line id = ceil(ncl / kLineW)
     int wide_x;        // ncl >= 2 and nhalo != 1: 16-byte x-tile loads are in bounds
     int vi_packed;     // rectangular operator: VI indices packed NU per lane at header field 0
     const double* b;
@@ -182,9 +182,18 @@ __device__ __forceinline__ v2d_t load_pair(const double* base, int q, int n) {
 // in use (8 = full; the gather path of sparse rectangular blocks uses fewer).
 // Batch 1 of an x-tile block (depends on the block id only): what the persistent kernel
 // prefetches for its next block while the current one runs.
+// the x-tile line ids lane `lane` of wave `wv` loads (tile_line_ids) and where lane `lane`
+// finds the line of its 16-byte slot pair j (tile_line_src): 64-byte lines, 4 lanes per line,
+// line 16 wv + (lane >> 2) + 64 j; 32-byte lines, 2 lanes per line, line 32 wv + (lane >> 1) +
+// 128 j (each lane holds two ids: j = 0, 1 and j = 2, 3).  Either way slot pair j of lane t is
+// stage[2 t + 512 j].
+__device__ __forceinline__ int tile_id_index(int wv, int lane, int k) {
+    return kLineW == 8 ? 16 * wv + (lane & 15) + 64 * (lane >> 4) : 32 * wv + (lane & 31) + 128 * (lane >> 5) + 256 * k;
+}
+
 struct CsrPre {
     int4 h0, h1;
-    int tid_line;
+    int tid_line, tid_line2;
     v4u_t lq;
     v2u_t vq;
 };
@@ -194,7 +203,8 @@ __device__ __forceinline__ void csr_pre_tile(const CsrArgs& a, int bid, CsrPre& 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     p.h0 = a.hdr[2 * bid];
     p.h1 = a.hdr[2 * bid + 1];
-    p.tid_line = a.tile_ids[(size_t)bid * kTileLines + 16 * wv + (lane & 15) + 64 * (lane >> 4)];
+    p.tid_line = a.tile_ids[(size_t)bid * kTileLines + tile_id_index(wv, lane, 0)];
+    p.tid_line2 = kLineW == 4 ? a.tile_ids[(size_t)bid * kTileLines + tile_id_index(wv, lane, 1)] : 0;
     p.lq = __builtin_nontemporal_load((const v4u_t*)(a.lcol + (size_t)bid * kCAP + (size_t)tid * (kCAP / kTPB)));
     p.vq = v2u_t{0u, 0u};
     // square operators with value-indexed blocks hold kCAP index bytes for every block
@@ -215,12 +225,13 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     static_assert(!PRE || TILE, "prefetched batch 1: x-tile path only");
     static_assert(!C16 || !TILE, "column codes: gather path only");
-    int tid_line = 0;
+    int tid_line = 0, tid_line2 = 0;
     v4u_t lq = {0u, 0u, 0u, 0u};
     v2u_t vq = {0u, 0u};
     int4 h0, h1, gb = {0, 0, 0, 0};
     if constexpr (PRE > 0) {
         tid_line = pre->tid_line;
+        tid_line2 = pre->tid_line2;
         lq = pre->lq;
         vq = pre->vq;
         h0 = pre->h0;
@@ -228,9 +239,9 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
         if (nxt >= 0) csr_pre_tile<PRE == 2>(a, nxt, *pre);  // in flight during this block
     } else {
     if (TILE) {
-        // lane l of wave w fetches line 16w + (l & 15) + 64 (l >> 4): the 64 lines wave w's
-        // 16-byte tile slots need (slot j of lane l: line 16w + (l >> 2) + 64j)
-        tid_line = a.tile_ids[(size_t)bid * kTileLines + 16 * wv + (lane & 15) + 64 * (lane >> 4)];
+        // the lines wave w's 16-byte tile slots need (tile_id_index)
+        tid_line = a.tile_ids[(size_t)bid * kTileLines + tile_id_index(wv, lane, 0)];
+        if (kLineW == 4) tid_line2 = a.tile_ids[(size_t)bid * kTileLines + tile_id_index(wv, lane, 1)];
     }
     if (TILE) lq = __builtin_nontemporal_load((const v4u_t*)(a.lcol + (size_t)bid * kCAP + (size_t)tid * U));
     h0 = a.hdr[2 * bid];
@@ -319,26 +330,31 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     __builtin_amdgcn_sched_barrier(0);
     double xs[U];
     if (TILE) {
-        // slot pair j of lane l: line 16w + (l >> 2) + 64j, elements e, e + 1 with e = 2 (l & 3);
-        // element e of line L is column 8L + e (local) or halo entry 8(L - hl0) + e
-        const int e = 2 * (lane & 3);
+        // slot pair j of lane l: elements e, e + 1 of its line (tile_id_index), e = 2 (l & 3)
+        // (64-byte lines) or 2 (l & 1) (32-byte lines); element e of line L is column
+        // kLineW L + e (local) or halo entry kLineW (L - hl0) + e
+        const int e = kLineW == 8 ? 2 * (lane & 3) : 2 * (lane & 1);
+        auto line_of_pair = [&](int j) {
+            return kLineW == 8 ? __shfl(tid_line, (lane >> 2) + 16 * j, 64)
+                               : __shfl(j < 2 ? tid_line : tid_line2, (lane >> 1) + 32 * (j & 1), 64);
+        };
         if (a.wide_x) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int L = __shfl(tid_line, (lane >> 2) + 16 * j, 64);
-                const v2d_t p2 = L < a.hl0 ? load_pair(a.x, L * 8 + e, a.ncl)
-                                           : load_pair(a.xh, (L - a.hl0) * 8 + e, a.nhalo);
+                const int L = line_of_pair(j);
+                const v2d_t p2 = L < a.hl0 ? load_pair(a.x, L * kLineW + e, a.ncl)
+                                           : load_pair(a.xh, (L - a.hl0) * kLineW + e, a.nhalo);
                 xs[2 * j] = p2.x;
                 xs[2 * j + 1] = p2.y;
             }
         } else {  // a vector of one entry: 8-byte loads (degenerate coarse partitions)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int L = __shfl(tid_line, (lane >> 2) + 16 * j, 64);
+                const int L = line_of_pair(j);
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const double* p = L < a.hl0 ? a.x + min(L * 8 + e + h, a.ncl - 1)
-                                                : a.xh + min((L - a.hl0) * 8 + e + h, a.nhalo - 1);
+                    const double* p = L < a.hl0 ? a.x + min(L * kLineW + e + h, a.ncl - 1)
+                                                : a.xh + min((L - a.hl0) * kLineW + e + h, a.nhalo - 1);
                     xs[2 * j + h] = *p;
                 }
             }
@@ -352,7 +368,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     }
     if (VIB) tabl[tid] = tv;
     if (TILE || VIB) __syncthreads();
-    if (px_tile) px = stage[(h1.x + (rr >> 3) - (r0 >> 3)) * 8 + (rr & 7)];
+    if (px_tile) px = stage[(h1.x + (rr >> kLineShift) - (r0 >> kLineShift)) * kLineW + (rr & (kLineW - 1))];
     // 1 / a_ii from the table: the same correctly rounded division the host does for dinv
     if (pd_tab) pd = 1.0 / tabl[dv];
     if (VIB) {
@@ -467,7 +483,7 @@ __device__ __forceinline__ void block_partial(const CsrArgs& a, int bid, double 
 // C16: gather path with 16-bit column codes (DevMatrix::col16)
 template <int MODE, bool NORM, bool XCD, bool TILE, bool VI, int GRPB = 1, bool C16 = false>
 __global__ __launch_bounds__(kTPB, GRPB > 1 ? 7 : 8) void csr_block_kernel(CsrArgs a, int first_block) {
-    static_assert(kCAP / kTPB == 8 && kTileLines * 8 == kCAP && kTPB == 256,
+    static_assert(kCAP / kTPB == 8 && kTileLines * kLineW == kCAP && kTPB == 256,
                   "lane-major layouts assume 8 entries per lane, 4 waves");
     __shared__ __attribute__((aligned(16))) double stage[kCAP];  // x tile, then products
     __shared__ double tabl[VI ? 256 : 1];
@@ -2315,7 +2331,7 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
     AMG_ASSERT(!y2 || (mode == KM_SPMV && d2));
     CsrArgs a{A.hdr.p, A.tile_fixed.p, A.lcol.p, A.vidx.p, A.vtab.p, A.rend.p, A.dvi.p,
               A.rp.p, A.col.p, A.val.p,
-              x, A.halo.p, ncl, nh, (ncl + 7) / 8, (ncl >= 2 && nh != 1) ? 1 : 0, A.tiled ? 0 : 1,
+              x, A.halo.p, ncl, nh, (ncl + kLineW - 1) / kLineW, (ncl >= 2 && nh != 1) ? 1 : 0, A.tiled ? 0 : 1,
               b, y2 ? d2 : A.dinv.p, y, omega, partial, part_off, y2, nullptr, A.gband.p};
     const dim3 g(n_blocks);
     const int var = kernel_variant(A);

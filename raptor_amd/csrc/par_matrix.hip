@@ -158,9 +158,9 @@ Context::~Context() {
 }
 
 // Row blocks of the CSR-stream kernel: <= kCAP nonzeros, <= kTPB rows, one class (interior /
-// boundary), and <= kTileLines distinct 64-byte lines of x (8 doubles; local lines first,
+// boundary), and <= kTileLines distinct lines of x (kLineW doubles; local lines first,
 // then halo lines).  Each block gets its sorted line list ("x tile") and every nonzero a
-// 16-bit index into the tile: slot * 8 + (column & 7).  A single row touching more lines
+// 16-bit index into the tile: slot * kLineW + (column mod kLineW).  A single row touching more lines
 // than a tile holds becomes a block of its own and takes the untiled path.
 struct BlockBuild {
     std::vector<int2> blocks;     // interior all-templated, other interior, then boundary blocks
@@ -177,9 +177,9 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const hvec<int>& 
                                    const std::vector<uint8_t>* tplf = nullptr, int row_cap = kTPB,
                                    bool line_cap = true, bool want_lcol = true) {
     const int n = (int)rp.size() - 1;
-    const int64_t hl0 = (ncl + 7) / 8;
-    const size_t nlines = (size_t)(hl0 + (nhalo + 7) / 8) + 1;
-    auto line_of = [&](int c) -> int64_t { return c < ncl ? c >> 3 : hl0 + ((c - ncl) >> 3); };
+    const int64_t hl0 = (ncl + kLineW - 1) / kLineW;
+    const size_t nlines = (size_t)(hl0 + (nhalo + kLineW - 1) / kLineW) + 1;
+    auto line_of = [&](int c) -> int64_t { return c < ncl ? c >> kLineShift : hl0 + ((c - ncl) >> kLineShift); };
     struct Rec {
         int r0, r1;
         std::vector<int> lines;
@@ -220,8 +220,9 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const hvec<int>& 
                 if (want_lcol)
                     for (int k = rp[a]; k < rp[b]; ++k) {
                         const int c = col[k];
-                        const int e = c < ncl ? (c & 7) : (int)((c - ncl) & 7);  // element within its line
-                        out.lcol[k] = tiled ? (uint16_t)(slot[line_of(c)] * 8 + e) : (uint16_t)0;
+                        // element within its line
+                        const int e = c < ncl ? (c & (kLineW - 1)) : (int)((c - ncl) & (kLineW - 1));
+                        out.lcol[k] = tiled ? (uint16_t)(slot[line_of(c)] * kLineW + e) : (uint16_t)0;
                     }
                 rc.push_back({a, b, tiled ? lines : std::vector<int>(), cls[a] != 0,
                               tplf != nullptr && (*tplf)[a] != 0});
@@ -707,7 +708,8 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         {
             const char* e = std::getenv("AMG_RECT_TILE");
             const int mode = e ? std::atoi(e) : -1;
-            tiled = square || (mode != 0 && (mode == 1 || 2 * tile_lines_total <= (int64_t)nnz));
+            // (<= 32 tile bytes per nonzero: 0.5 lines of 64 B, 1 line of 32 B)
+            tiled = square || (mode != 0 && (mode == 1 || kLineW * tile_lines_total <= 4 * (int64_t)nnz));
         }
         if (std::getenv("AMG_TRACE_BLOCKS")) {
             const int64_t lines = tile_lines_total, full = tile_full;
@@ -973,7 +975,7 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         // 32-byte block headers (two scalar loads per block):
         //   {r0, r1, koff, nnz}, {diag slot, tile lines | dvi flag << 16, value-table offset (-1),
         //   table size}
-        // diag slot (square operators): tile position of line r0 / 8 when the lines of the
+        // diag slot (square operators): tile position of line r0 / kLineW when the lines of the
         // block's own rows are consecutive in its tile, so x[r] is read from the tile; else -1
         std::vector<int4> hh(std::max<size_t>(2 * nbk, 2), make_int4(0, 0, 0, 0));
         jac_extra_all = jac_extra_csr = 0;
@@ -982,7 +984,7 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
             const int t0 = bb.tile_ptr[q], nt = bb.tile_ptr[q + 1] - t0;
             int dslot = -1;
             if (square && nt > 0 && nt <= kTileLines) {
-                const int l0 = b.x >> 3, l1 = (b.y - 1) >> 3;
+                const int l0 = b.x >> kLineShift, l1 = (b.y - 1) >> kLineShift;
                 const int* tl = bb.tile_lines.data() + t0;
                 const int pos = (int)(std::lower_bound(tl, tl + nt, l0) - tl);
                 bool ok = pos + (l1 - l0) < nt;
