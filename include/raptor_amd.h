@@ -145,6 +145,8 @@ typedef struct amg_matrix_info {
     int32_t tpl_master;      /* uniform-stencil rows: entries of the master template every *
                               * template is a subsequence of (7, 27; 0: per-template      *
                               * tables)                                    */
+    int32_t tile_line_bytes; /* x-tile line width of the block kernels: 64 or 32 (0: no x  *
+                              * tile)                                      */
 } amg_matrix_info;
 int amg_par_csr_info(amg_matrix A, amg_matrix_info* info);
 

@@ -72,6 +72,7 @@ class MatrixInfo(C.Structure):
         ("jacobi_bytes", C.c_int64),
         ("gs_bytes", C.c_int64),
         ("tpl_master", C.c_int32),
+        ("tile_line_bytes", C.c_int32),
     ]
 
 

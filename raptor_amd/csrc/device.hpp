@@ -31,17 +31,12 @@ constexpr int kTPB = 256;   // threads per workgroup (4 waves of 64)
 constexpr int kCAP = 2048;
 constexpr int kGatherBand = 1 << 14;  // gather column-code band width (col16)  // nonzeros staged in LDS per workgroup (16 KiB of products)
 constexpr int kPad = kCAP;  // col/val padding (entries): unconditional loads past a block's end
-// x tile per workgroup: kTileLines lines of kLineW doubles = 16 KiB of LDS.  r3: 32-byte lines
-// (512 per tile; AMG_TILE_LINE=8 restores 256 lines of 64 B): a Galerkin row block reads a
-// few doubles of each line it touches, so half-lines fit more rows in the same 16 KiB -- the
-// 7-pt 256^3 level-2 operator needs 25,615 blocks instead of 40,250
-#ifndef AMG_TILE_LINE
-#define AMG_TILE_LINE 4
-#endif
-constexpr int kLineW = AMG_TILE_LINE;
-static_assert(kLineW == 4 || kLineW == 8, "x-tile lines of 32 or 64 bytes");
-constexpr int kLineShift = kLineW == 8 ? 3 : 2;
-constexpr int kTileLines = kCAP / kLineW;
+// x tile per workgroup: 16 KiB of LDS = kCAP doubles in lines of 8 doubles (256 lines of 64 B)
+// or, r3, 4 doubles (512 lines of 32 B): a Galerkin row block reads a few doubles of each line
+// it touches, so half-lines fit more rows in the same tile (the 7-pt 256^3 level-2 operator:
+// 40,250 -> 25,615 blocks).  Chosen per operator (DevMatrix::line_w)
+constexpr int kTileLines = kCAP / 8;     // 64-byte lines per tile
+constexpr int kTileLinesMax = kCAP / 4;  // 32-byte lines per tile
 constexpr int kNormParts = kTPB / 64;  // norm partials per CSR block (one per wave)
 constexpr int kGsWide = 128;     // sliced-ELL width from which hybrid GS uses the wide variant
 constexpr int kGatherRPB = 4;    // rows per lane of gather (rectangular-operator) row blocks
@@ -209,6 +204,7 @@ struct DevMatrix {
     DevBuf<uint16_t> rend;
     DevBuf<uint8_t> dvi;
     DevBuf<uint16_t> lcol;
+    int line_w = 8;  // doubles per x-tile line: 8 (64 B) or 4 (32 B)
     // gather operators (P, R): 16-bit column codes band << 14 | (col - band base) when every
     // block's columns fit in <= 4 bands of kGatherBand (gband: the block's 4 band bases);
     // null otherwise (int32 col).  Blocks of more than kCAP entries read col either way.

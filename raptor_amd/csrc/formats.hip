@@ -13,7 +13,7 @@ namespace amg {
 namespace {
 
 constexpr int kT = 256;
-static_assert(kT == kTPB && kTileLines % kT == 0, "one thread per lane, whole tile rows per thread");
+static_assert(kT == kTPB && kTileLines % kT == 0 && kTileLinesMax % kT == 0, "one thread per lane");
 
 __device__ __forceinline__ size_t lane_pos_d(int j, int nu) {
     return (size_t)((j & (2 * kTPB - 1)) >> 1) * (size_t)nu + 2 * (size_t)(j / (2 * kTPB)) + (size_t)(j & 1);
@@ -40,36 +40,38 @@ __global__ __launch_bounds__(kT) void copy_blocks_kernel(const int2* __restrict_
 
 // x-tile line ids at a fixed stride, padded with the block's last line (0 for untiled blocks)
 __global__ __launch_bounds__(kT) void tile_fixed_kernel(const int* __restrict__ tile_ptr,
-                                                        const int* __restrict__ tile_lines, int* __restrict__ fx) {
+                                                        const int* __restrict__ tile_lines, int tl,
+                                                        int* __restrict__ fx) {
     const int q = blockIdx.x;
     const int t0 = tile_ptr[q], nt = tile_ptr[q + 1] - t0;
-    for (int j = threadIdx.x; j < kTileLines; j += kT)
-        fx[(size_t)q * kTileLines + j] = (nt > 0 && nt <= kTileLines) ? tile_lines[t0 + min(j, nt - 1)] : 0;
+    for (int j = threadIdx.x; j < tl; j += kT)
+        fx[(size_t)q * tl + j] = (nt > 0 && nt <= tl) ? tile_lines[t0 + min(j, nt - 1)] : 0;
 }
 
-// per entry: slot of its x line in the block's sorted tile * kLineW + element in the line,
+// per entry: slot of its x line in the block's sorted tile * lw + element in the line,
 // lane-major (lane_pos); blocks over kCAP entries or without a tile keep zeros
 __global__ __launch_bounds__(kT) void tile_index_kernel(const int2* __restrict__ blocks, const int* __restrict__ rp,
                                                         const int* __restrict__ col, const int* __restrict__ tile_ptr,
-                                                        const int* __restrict__ tile_lines, int ncl,
+                                                        const int* __restrict__ tile_lines, int ncl, int lw,
                                                         uint16_t* __restrict__ perm) {
     const int q = blockIdx.x;
     const int2 b = blocks[q];
     const int kb = rp[b.x], nz = rp[b.y] - kb;
     const int t0 = tile_ptr[q], nt = tile_ptr[q + 1] - t0;
-    if (nz > kCAP || nt <= 0 || nt > kTileLines) return;
-    const int hl0 = (int)(((long long)ncl + kLineW - 1) / kLineW);
+    if (nz > kCAP || nt <= 0 || nt > kCAP / lw) return;
+    const int sh = lw == 8 ? 3 : 2;
+    const int hl0 = (int)(((long long)ncl + lw - 1) / lw);
     for (int j = threadIdx.x; j < nz; j += kT) {
         const int c = col[kb + j];
-        const int L = c < ncl ? c >> kLineShift : hl0 + ((c - ncl) >> kLineShift);
-        const int e = c < ncl ? (c & (kLineW - 1)) : ((c - ncl) & (kLineW - 1));
+        const int L = c < ncl ? c >> sh : hl0 + ((c - ncl) >> sh);
+        const int e = c < ncl ? (c & (lw - 1)) : ((c - ncl) & (lw - 1));
         int lo = 0, hi = nt;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             if (tile_lines[t0 + mid] < L) lo = mid + 1;
             else hi = mid;
         }
-        perm[(size_t)q * kCAP + lane_pos_d(j, kCAP / kTPB)] = (uint16_t)(lo * kLineW + e);
+        perm[(size_t)q * kCAP + lane_pos_d(j, kCAP / kTPB)] = (uint16_t)(lo * lw + e);
     }
 }
 
@@ -242,14 +244,15 @@ void build_formats_device(DevMatrix& M, const std::vector<int>& hrp, const hvec<
                            M.col.p, M.val.p);
     HIP_CHECK(hipGetLastError());
     if (M.tiled) {
-        M.tile_fixed.alloc((size_t)std::max(nbk, 1) * kTileLines);
+        M.tile_fixed.alloc((size_t)std::max(nbk, 1) * (kCAP / M.line_w));
         M.lcol.alloc((size_t)std::max(nbk, 1) * kCAP);
         HIP_CHECK(hipMemsetAsync(M.tile_fixed.p, 0, M.tile_fixed.n * sizeof(int), s));
         HIP_CHECK(hipMemsetAsync(M.lcol.p, 0, M.lcol.n * sizeof(uint16_t), s));
         if (nbk) {
-            hipLaunchKernelGGL(tile_fixed_kernel, dim3(nbk), dim3(kT), 0, s, dtp.p, dtl.p, M.tile_fixed.p);
+            hipLaunchKernelGGL(tile_fixed_kernel, dim3(nbk), dim3(kT), 0, s, dtp.p, dtl.p, kCAP / M.line_w,
+                               M.tile_fixed.p);
             hipLaunchKernelGGL(tile_index_kernel, dim3(nbk), dim3(kT), 0, s, M.blocks.p, M.rp.p, dcol.p, dtp.p, dtl.p,
-                               (int)M.n_cols_local, M.lcol.p);
+                               (int)M.n_cols_local, M.line_w, M.lcol.p);
         }
         HIP_CHECK(hipGetLastError());
     } else {

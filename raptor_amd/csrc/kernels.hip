@@ -53,7 +53,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 struct CsrArgs {
     const int4* hdr;         // 2 x int4 per block (par_matrix.hip): {r0, r1, k0, nnz},
                              // {diag slot, tile lines, value-table offset (-1), table size}
-    const int* tile_ids;     // kTileLines x-tile line ids per block (padded with the last)
+    const int* tile_ids;     // kCAP / LW x-tile line ids per block (padded with the last)
     const uint16_t* lcol;    // lane-major 16-bit tile indices (kCAP per block)
     const uint8_t* vidx;     // lane-major 1-byte value indices (kCAP per block)
     const double* vtab;      // value tables
@@ -66,7 +66,7 @@ struct CsrArgs {
     const double* xh;  // halo part of x
     int ncl;           // number of local columns
     int nhalo;
-    int hl0;           // first halo line id = ceil(ncl / kLineW)
+    int hl0;           // first halo line id = ceil(ncl / LW)
     int wide_x;        // ncl >= 2 and nhalo != 1: 16-byte x-tile loads are in bounds
     int vi_packed;     // rectangular operator: VI indices packed NU per lane at header field 0
     const double* b;
@@ -187,8 +187,9 @@ __device__ __forceinline__ v2d_t load_pair(const double* base, int q, int n) {
 // line 16 wv + (lane >> 2) + 64 j; 32-byte lines, 2 lanes per line, line 32 wv + (lane >> 1) +
 // 128 j (each lane holds two ids: j = 0, 1 and j = 2, 3).  Either way slot pair j of lane t is
 // stage[2 t + 512 j].
+template <int LW>
 __device__ __forceinline__ int tile_id_index(int wv, int lane, int k) {
-    return kLineW == 8 ? 16 * wv + (lane & 15) + 64 * (lane >> 4) : 32 * wv + (lane & 31) + 128 * (lane >> 5) + 256 * k;
+    return LW == 8 ? 16 * wv + (lane & 15) + 64 * (lane >> 4) : 32 * wv + (lane & 31) + 128 * (lane >> 5) + 256 * k;
 }
 
 struct CsrPre {
@@ -198,13 +199,14 @@ struct CsrPre {
     v2u_t vq;
 };
 
-template <bool VI>
+template <bool VI, int LW = 8>
 __device__ __forceinline__ void csr_pre_tile(const CsrArgs& a, int bid, CsrPre& p) {
+    constexpr int TL = kCAP / LW;  // line ids per block
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     p.h0 = a.hdr[2 * bid];
     p.h1 = a.hdr[2 * bid + 1];
-    p.tid_line = a.tile_ids[(size_t)bid * kTileLines + tile_id_index(wv, lane, 0)];
-    p.tid_line2 = kLineW == 4 ? a.tile_ids[(size_t)bid * kTileLines + tile_id_index(wv, lane, 1)] : 0;
+    p.tid_line = a.tile_ids[(size_t)bid * TL + tile_id_index<LW>(wv, lane, 0)];
+    p.tid_line2 = LW == 4 ? a.tile_ids[(size_t)bid * TL + tile_id_index<LW>(wv, lane, 1)] : 0;
     p.lq = __builtin_nontemporal_load((const v4u_t*)(a.lcol + (size_t)bid * kCAP + (size_t)tid * (kCAP / kTPB)));
     p.vq = v2u_t{0u, 0u};
     // square operators with value-indexed blocks hold kCAP index bytes for every block
@@ -215,7 +217,8 @@ __device__ __forceinline__ void csr_pre_tile(const CsrArgs& a, int bid, CsrPre& 
 // block nxt's batch 1 (2: with VI indices) unless nxt < 0
 // RPB: rows per lane (gather blocks of rectangular operators hold up to kTPB * kGatherRPB
 // rows; a short-row P block of 256 rows filled a quarter of its 2048-entry stage)
-template <int MODE, bool NORM, bool TILE, bool VIB, int NU, int PRE = 0, int RPB = 1, bool C16 = false>
+template <int MODE, bool NORM, bool TILE, bool VIB, int NU, int PRE = 0, int RPB = 1, bool C16 = false,
+          int LW = 8>
 __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* stage, double* tabl,
                                              int* rends, CsrPre* pre = nullptr, int nxt = -1) {
     constexpr int U = kCAP / kTPB;  // 8 lane slots
@@ -236,12 +239,12 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
         vq = pre->vq;
         h0 = pre->h0;
         h1 = pre->h1;
-        if (nxt >= 0) csr_pre_tile<PRE == 2>(a, nxt, *pre);  // in flight during this block
+        if (nxt >= 0) csr_pre_tile<PRE == 2, LW>(a, nxt, *pre);  // in flight during this block
     } else {
     if (TILE) {
         // the lines wave w's 16-byte tile slots need (tile_id_index)
-        tid_line = a.tile_ids[(size_t)bid * kTileLines + tile_id_index(wv, lane, 0)];
-        if (kLineW == 4) tid_line2 = a.tile_ids[(size_t)bid * kTileLines + tile_id_index(wv, lane, 1)];
+        tid_line = a.tile_ids[(size_t)bid * (kCAP / LW) + tile_id_index<LW>(wv, lane, 0)];
+        if (LW == 4) tid_line2 = a.tile_ids[(size_t)bid * (kCAP / LW) + tile_id_index<LW>(wv, lane, 1)];
     }
     if (TILE) lq = __builtin_nontemporal_load((const v4u_t*)(a.lcol + (size_t)bid * kCAP + (size_t)tid * U));
     h0 = a.hdr[2 * bid];
@@ -332,18 +335,18 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     if (TILE) {
         // slot pair j of lane l: elements e, e + 1 of its line (tile_id_index), e = 2 (l & 3)
         // (64-byte lines) or 2 (l & 1) (32-byte lines); element e of line L is column
-        // kLineW L + e (local) or halo entry kLineW (L - hl0) + e
-        const int e = kLineW == 8 ? 2 * (lane & 3) : 2 * (lane & 1);
+        // LW L + e (local) or halo entry LW (L - hl0) + e
+        const int e = LW == 8 ? 2 * (lane & 3) : 2 * (lane & 1);
         auto line_of_pair = [&](int j) {
-            return kLineW == 8 ? __shfl(tid_line, (lane >> 2) + 16 * j, 64)
-                               : __shfl(j < 2 ? tid_line : tid_line2, (lane >> 1) + 32 * (j & 1), 64);
+            return LW == 8 ? __shfl(tid_line, (lane >> 2) + 16 * j, 64)
+                           : __shfl(j < 2 ? tid_line : tid_line2, (lane >> 1) + 32 * (j & 1), 64);
         };
         if (a.wide_x) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int L = line_of_pair(j);
-                const v2d_t p2 = L < a.hl0 ? load_pair(a.x, L * kLineW + e, a.ncl)
-                                           : load_pair(a.xh, (L - a.hl0) * kLineW + e, a.nhalo);
+                const v2d_t p2 = L < a.hl0 ? load_pair(a.x, L * LW + e, a.ncl)
+                                           : load_pair(a.xh, (L - a.hl0) * LW + e, a.nhalo);
                 xs[2 * j] = p2.x;
                 xs[2 * j + 1] = p2.y;
             }
@@ -353,8 +356,8 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
                 const int L = line_of_pair(j);
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const double* p = L < a.hl0 ? a.x + min(L * kLineW + e + h, a.ncl - 1)
-                                                : a.xh + min((L - a.hl0) * kLineW + e + h, a.nhalo - 1);
+                    const double* p = L < a.hl0 ? a.x + min(L * LW + e + h, a.ncl - 1)
+                                                : a.xh + min((L - a.hl0) * LW + e + h, a.nhalo - 1);
                     xs[2 * j + h] = *p;
                 }
             }
@@ -368,7 +371,8 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     }
     if (VIB) tabl[tid] = tv;
     if (TILE || VIB) __syncthreads();
-    if (px_tile) px = stage[(h1.x + (rr >> kLineShift) - (r0 >> kLineShift)) * kLineW + (rr & (kLineW - 1))];
+    constexpr int LS = LW == 8 ? 3 : 2;
+    if (px_tile) px = stage[(h1.x + (rr >> LS) - (r0 >> LS)) * LW + (rr & (LW - 1))];
     // 1 / a_ii from the table: the same correctly rounded division the host does for dinv
     if (pd_tab) pd = 1.0 / tabl[dv];
     if (VIB) {
@@ -426,14 +430,14 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     return sq;
 }
 
-template <int MODE, bool NORM, bool TILE, bool VIB, int GRPB = 1, bool C16 = false>
+template <int MODE, bool NORM, bool TILE, bool VIB, int GRPB = 1, bool C16 = false, int LW = 8>
 __device__ __forceinline__ double block_dispatch(const CsrArgs& a, int bid, int nnz, double* stage,
                                                  double* tabl, int* rends) {
     constexpr int RP = (MODE == KM_SPMV || MODE == KM_SPMV_ADD) && !NORM ? GRPB : 1;
     if constexpr (TILE) {
         // a tiled short-row P holds up to kTPB * GRPB rows per block: every row is summed
         // (AMG_CSR_PRE_TILE=0 builds reach this branch)
-        return block_main<MODE, NORM, TILE, VIB, 8, 0, RP>(a, bid, stage, tabl, rends);
+        return block_main<MODE, NORM, TILE, VIB, 8, 0, RP, false, LW>(a, bid, stage, tabl, rends);
     } else {
         if (nnz > 4 * kTPB) return block_main<MODE, NORM, TILE, VIB, 8, 0, RP, C16>(a, bid, stage, tabl, rends);
         if (nnz > 2 * kTPB) return block_main<MODE, NORM, TILE, VIB, 4, 0, RP, C16>(a, bid, stage, tabl, rends);
@@ -481,9 +485,10 @@ __device__ __forceinline__ void block_partial(const CsrArgs& a, int bid, double 
 // GRPB: rows per lane of gather blocks (1, or kGatherRPB for short-row rectangular operators
 // whose blocks hold up to kTPB * kGatherRPB rows; DevMatrix::gather_rpb)
 // C16: gather path with 16-bit column codes (DevMatrix::col16)
-template <int MODE, bool NORM, bool XCD, bool TILE, bool VI, int GRPB = 1, bool C16 = false>
+// LW: doubles per x-tile line (8: 256 lines of 64 B, 4: 512 lines of 32 B; DevMatrix::line_w)
+template <int MODE, bool NORM, bool XCD, bool TILE, bool VI, int GRPB = 1, bool C16 = false, int LW = 8>
 __global__ __launch_bounds__(kTPB, GRPB > 1 ? 7 : 8) void csr_block_kernel(CsrArgs a, int first_block) {
-    static_assert(kCAP / kTPB == 8 && kTileLines * kLineW == kCAP && kTPB == 256,
+    static_assert(kCAP / kTPB == 8 && (LW == 8 || LW == 4) && kTPB == 256,
                   "lane-major layouts assume 8 entries per lane, 4 waves");
     __shared__ __attribute__((aligned(16))) double stage[kCAP];  // x tile, then products
     __shared__ double tabl[VI ? 256 : 1];
@@ -495,12 +500,12 @@ __global__ __launch_bounds__(kTPB, GRPB > 1 ? 7 : 8) void csr_block_kernel(CsrAr
         // round of loads less per block
         constexpr int PV = VI ? 2 : 1;
         CsrPre f;
-        csr_pre_tile<VI>(a, bid, f);
+        csr_pre_tile<VI, LW>(a, bid, f);
         const int4 h0 = f.h0, h1 = f.h1;
         double sq;
-        if (h0.w <= kCAP && (h1.y & 0xffff) <= kTileLines && h0.w > 0) {
-            if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV, GRPB>(a, bid, stage, tabl, rends, &f, -1);
-            else sq = block_main<MODE, NORM, true, false, 8, PV, GRPB>(a, bid, stage, tabl, rends, &f, -1);
+        if (h0.w <= kCAP && (h1.y & 0xffff) <= kCAP / LW && h0.w > 0) {
+            if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f, -1);
+            else sq = block_main<MODE, NORM, true, false, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f, -1);
         } else {
             sq = block_long<MODE, NORM>(a, h0, stage);
         }
@@ -510,9 +515,9 @@ __global__ __launch_bounds__(kTPB, GRPB > 1 ? 7 : 8) void csr_block_kernel(CsrAr
     const int4 h0 = a.hdr[2 * bid], h1 = a.hdr[2 * bid + 1];
     const int nnz = h0.w;
     double sq;
-    if (nnz <= kCAP && (!TILE || (h1.y & 0xffff) <= kTileLines) && nnz > 0) {
-        if (VI && h1.z >= 0) sq = block_dispatch<MODE, NORM, TILE, true, GRPB, C16>(a, bid, nnz, stage, tabl, rends);
-        else sq = block_dispatch<MODE, NORM, TILE, false, GRPB, C16>(a, bid, nnz, stage, tabl, rends);
+    if (nnz <= kCAP && (!TILE || (h1.y & 0xffff) <= kCAP / LW) && nnz > 0) {
+        if (VI && h1.z >= 0) sq = block_dispatch<MODE, NORM, TILE, true, GRPB, C16, LW>(a, bid, nnz, stage, tabl, rends);
+        else sq = block_dispatch<MODE, NORM, TILE, false, GRPB, C16, LW>(a, bid, nnz, stage, tabl, rends);
     } else {
         sq = block_long<MODE, NORM>(a, h0, stage);
     }
@@ -542,7 +547,7 @@ __global__ __launch_bounds__(kTPB, AMG_CSR_PERSIST_WAVES) void csr_persist_kerne
         const int nb = nxt < b1 ? first_block + nxt : -1;
         const int4 h0 = f.h0, h1 = f.h1;
         double sq;
-        if (h0.w <= kCAP && (h1.y & 0xffff) <= kTileLines && h0.w > 0) {
+        if (h0.w <= kCAP && (h1.y & 0xffff) <= kCAP / 8 && h0.w > 0) {  // 64-byte lines (launch_csr_stream)
             if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV>(a, bid, stage, tabl, rends, &f, nb);
             else sq = block_main<MODE, NORM, true, false, 8, PV>(a, bid, stage, tabl, rends, &f, nb);
         } else {
@@ -2308,7 +2313,19 @@ static void launch_csr_persist(hipStream_t s, int mode, bool norm, const CsrArgs
 }
 
 template <int M, bool N, bool X, bool T, bool V>
-static void launch_block(hipStream_t s, dim3 g, const CsrArgs& a, int first_block, bool rpb4) {
+static void launch_block(hipStream_t s, dim3 g, const CsrArgs& a, int first_block, bool rpb4, int lw) {
+    if constexpr (T) {
+        if (lw == 4) {  // 32-byte x-tile lines
+            if constexpr (!N && (M == KM_SPMV || M == KM_SPMV_ADD)) {
+                if (rpb4) {
+                    hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, kGatherRPB, false, 4>), g, dim3(kTPB), 0, s, a, first_block);
+                    return;
+                }
+            }
+            hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, 1, false, 4>), g, dim3(kTPB), 0, s, a, first_block);
+            return;
+        }
+    }
     if constexpr (!N && (M == KM_SPMV || M == KM_SPMV_ADD)) {
         if (!T && a.col16) {
             if (rpb4) hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, kGatherRPB, !T>), g, dim3(kTPB), 0, s, a, first_block);
@@ -2331,17 +2348,17 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
     AMG_ASSERT(!y2 || (mode == KM_SPMV && d2));
     CsrArgs a{A.hdr.p, A.tile_fixed.p, A.lcol.p, A.vidx.p, A.vtab.p, A.rend.p, A.dvi.p,
               A.rp.p, A.col.p, A.val.p,
-              x, A.halo.p, ncl, nh, (ncl + kLineW - 1) / kLineW, (ncl >= 2 && nh != 1) ? 1 : 0, A.tiled ? 0 : 1,
+              x, A.halo.p, ncl, nh, (ncl + A.line_w - 1) / A.line_w, (ncl >= 2 && nh != 1) ? 1 : 0, A.tiled ? 0 : 1,
               b, y2 ? d2 : A.dinv.p, y, omega, partial, part_off, y2, nullptr, A.gband.p};
     const dim3 g(n_blocks);
     const int var = kernel_variant(A);
     if (var & 256) a.col16 = A.col16.p;
-    if ((var & 64) && !(var & 4) && A.square) {  // persistent x-tile kernel: square operators
+    if ((var & 64) && !(var & 4) && A.square && A.line_w == 8) {  // persistent x-tile kernel: square operators, 64-byte lines
         launch_csr_persist(s, mode, norm, a, first_block, n_blocks, (var & 8) != 0);
         return;
     }
     const bool rpb4 = A.gather_rpb > 1;
-#define AMG_L1(M, N, X, T, V) launch_block<M, N, X, T, V>(s, g, a, first_block, rpb4)
+#define AMG_L1(M, N, X, T, V) launch_block<M, N, X, T, V>(s, g, a, first_block, rpb4, A.line_w)
 #define AMG_L2(M, N, V)                                               \
     do {                                                              \
         const bool xo = var & 2, tl = !(var & 4);                     \

@@ -158,9 +158,9 @@ Context::~Context() {
 }
 
 // Row blocks of the CSR-stream kernel: <= kCAP nonzeros, <= kTPB rows, one class (interior /
-// boundary), and <= kTileLines distinct lines of x (kLineW doubles; local lines first,
+// boundary), and <= kCAP / lw distinct lines of x (lw = 8 or 4 doubles; local lines first,
 // then halo lines).  Each block gets its sorted line list ("x tile") and every nonzero a
-// 16-bit index into the tile: slot * kLineW + (column mod kLineW).  A single row touching more lines
+// 16-bit index into the tile: slot * lw + (column mod lw).  A single row touching more lines
 // than a tile holds becomes a block of its own and takes the untiled path.
 struct BlockBuild {
     std::vector<int2> blocks;     // interior all-templated, other interior, then boundary blocks
@@ -175,11 +175,13 @@ struct BlockBuild {
 static BlockBuild build_row_blocks(const std::vector<int>& rp, const hvec<int>& col,
                                    const std::vector<uint8_t>& cls, int64_t ncl, int64_t nhalo,
                                    const std::vector<uint8_t>* tplf = nullptr, int row_cap = kTPB,
-                                   bool line_cap = true, bool want_lcol = true) {
+                                   bool line_cap = true, bool want_lcol = true, int lw = 8) {
     const int n = (int)rp.size() - 1;
-    const int64_t hl0 = (ncl + kLineW - 1) / kLineW;
-    const size_t nlines = (size_t)(hl0 + (nhalo + kLineW - 1) / kLineW) + 1;
-    auto line_of = [&](int c) -> int64_t { return c < ncl ? c >> kLineShift : hl0 + ((c - ncl) >> kLineShift); };
+    const int sh = lw == 8 ? 3 : 2, tl_cap = kCAP / lw;
+    AMG_ASSERT(lw == 8 || lw == 4);
+    const int64_t hl0 = (ncl + lw - 1) / lw;
+    const size_t nlines = (size_t)(hl0 + (nhalo + lw - 1) / lw) + 1;
+    auto line_of = [&](int c) -> int64_t { return c < ncl ? c >> sh : hl0 + ((c - ncl) >> sh); };
     struct Rec {
         int r0, r1;
         std::vector<int> lines;
@@ -216,17 +218,17 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const hvec<int>& 
                 if (b <= a) return;
                 std::sort(lines.begin(), lines.end());
                 for (size_t q = 0; q < lines.size(); ++q) slot[lines[q]] = (int)q;
-                const bool tiled = (int)lines.size() <= kTileLines;
+                const bool tiled = (int)lines.size() <= tl_cap;
                 if (want_lcol)
                     for (int k = rp[a]; k < rp[b]; ++k) {
                         const int c = col[k];
                         // element within its line
-                        const int e = c < ncl ? (c & (kLineW - 1)) : (int)((c - ncl) & (kLineW - 1));
-                        out.lcol[k] = tiled ? (uint16_t)(slot[line_of(c)] * kLineW + e) : (uint16_t)0;
+                        const int e = c < ncl ? (c & (lw - 1)) : (int)((c - ncl) & (lw - 1));
+                        out.lcol[k] = tiled ? (uint16_t)(slot[line_of(c)] * lw + e) : (uint16_t)0;
                     }
                 rc.push_back({a, b, tiled ? lines : std::vector<int>(), cls[a] != 0,
                               tplf != nullptr && (*tplf)[a] != 0});
-                if (!tiled) rc.back().lines.assign(kTileLines + 1, 0);  // marker: untiled
+                if (!tiled) rc.back().lines.assign(tl_cap + 1, 0);  // marker: untiled
                 lines.clear();
                 ++blk;
             };
@@ -246,7 +248,7 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const hvec<int>& 
                 const long long len = rp[r + 1] - rp[r];
                 collect(r, 2 * (int64_t)r);
                 if (r > r0 && (cls[r] != cls[r0] || acc + len > kCAP || r - r0 >= row_cap ||
-                               (line_cap && nl + (int)cand.size() > kTileLines) ||
+                               (line_cap && nl + (int)cand.size() > tl_cap) ||
                                (tplf && (*tplf)[r] != (*tplf)[r0]))) {
                     emit(r0, r);  // closes [r0, r); blk advances
                     r0 = r;
@@ -708,8 +710,7 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         {
             const char* e = std::getenv("AMG_RECT_TILE");
             const int mode = e ? std::atoi(e) : -1;
-            // (<= 32 tile bytes per nonzero: 0.5 lines of 64 B, 1 line of 32 B)
-            tiled = square || (mode != 0 && (mode == 1 || kLineW * tile_lines_total <= 4 * (int64_t)nnz));
+            tiled = square || (mode != 0 && (mode == 1 || 2 * tile_lines_total <= (int64_t)nnz));
         }
         if (std::getenv("AMG_TRACE_BLOCKS")) {
             const int64_t lines = tile_lines_total, full = tile_full;
@@ -721,6 +722,30 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         // and row caps, not the 256-line tile cap.  sa27's R1 (270 entries per row over ~200
         // lines each) was cut into blocks of ~1 row by that cap: one lane summing while 255
         // idled.  AMG_GATHER_LINECAP=1 keeps the cap (A/B)
+        // x-tile line width: operators whose blocks, cut at 256 lines of
+        // 64 B, run close to the cap (>= 3/4 full on average: Galerkin operators,
+        // restrictions) are cut again at 512 lines of 32 B (the 7-pt 256^3 A2: 40,250 ->
+        // 25,615 blocks; R0: same-box 76 -> 70 us); P-like operators (few lines per block)
+        // keep 64-byte lines and their 1 KiB of line ids per block (sa27 P0: 234 us at 64 B,
+        // 263 at 32 B).  AMG_TILE_LINE=8 / 4 forces the width.
+        line_w = 8;
+        if (tiled && !bb.blocks.empty()) {
+            const char* e = std::getenv("AMG_TILE_LINE");
+            const int force = e ? std::atoi(e) : 0;
+            const bool tryhalf = force == 4 || (force != 8 && 4 * tile_lines_total >= 3 * (int64_t)kTileLines *
+                                                                                         (int64_t)bb.blocks.size());
+            if (tryhalf) {
+                BlockBuild b4 = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(),
+                                                 tplf.empty() ? nullptr : &tplf, kTPB * gather_rpb, true, !dev_fmt, 4);
+                bb = std::move(b4);
+                line_w = 4;
+                nb_int = bb.nb_int;
+                nb_bnd = bb.nb_bnd;
+            }
+            if (std::getenv("AMG_TRACE_BLOCKS"))
+                std::fprintf(stderr, "[amg-blocks]   x-tile lines of %d B: %zu blocks\n", 8 * line_w, bb.blocks.size());
+            tm.lap("    build: row blocks, 32-byte lines");
+        }
         if (!tiled) {
             const char* e = std::getenv("AMG_GATHER_LINECAP");
             if (!(e && std::atoi(e) != 0)) {
@@ -885,15 +910,16 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
                 val.upload(vb.data(), vb.size());
             }
             if (tiled) {  // x tiles: the x-tile kernel only
-                // x-tile line ids at a fixed stride (kTileLines per block, padded with the block's
+                // x-tile line ids at a fixed stride (kCAP / line_w per block, padded with the block's
                 // last line), so the kernel loads them without waiting for the block header
-                ParZeros<int> fx(std::max<size_t>(nbk, 1) * kTileLines);
+                const int tlb = kCAP / line_w;
+                ParZeros<int> fx(std::max<size_t>(nbk, 1) * tlb);
 #pragma omp parallel for schedule(static)
                 for (size_t q = 0; q < nbk; ++q) {
                     const int t0 = bb.tile_ptr[q], nt = bb.tile_ptr[q + 1] - t0;
-                    if (nt <= 0 || nt > kTileLines) continue;
-                    for (int j = 0; j < kTileLines; ++j)
-                        fx[q * kTileLines + j] = bb.tile_lines[t0 + std::min(j, nt - 1)];
+                    if (nt <= 0 || nt > tlb) continue;
+                    for (int j = 0; j < tlb; ++j)
+                        fx[q * tlb + j] = bb.tile_lines[t0 + std::min(j, nt - 1)];
                 }
                 tile_fixed.upload(fx.data(), fx.size());
                 // lane-major per block (lane_pos): lane t's 8 indices are 16 contiguous bytes,
@@ -975,7 +1001,7 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         // 32-byte block headers (two scalar loads per block):
         //   {r0, r1, koff, nnz}, {diag slot, tile lines | dvi flag << 16, value-table offset (-1),
         //   table size}
-        // diag slot (square operators): tile position of line r0 / kLineW when the lines of the
+        // diag slot (square operators): tile position of line r0 / line_w when the lines of the
         // block's own rows are consecutive in its tile, so x[r] is read from the tile; else -1
         std::vector<int4> hh(std::max<size_t>(2 * nbk, 2), make_int4(0, 0, 0, 0));
         jac_extra_all = jac_extra_csr = 0;
@@ -983,8 +1009,9 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
             const int2 b = bb.blocks[q];
             const int t0 = bb.tile_ptr[q], nt = bb.tile_ptr[q + 1] - t0;
             int dslot = -1;
-            if (square && nt > 0 && nt <= kTileLines) {
-                const int l0 = b.x >> kLineShift, l1 = (b.y - 1) >> kLineShift;
+            if (square && nt > 0 && nt <= kCAP / line_w) {
+                const int ls = line_w == 8 ? 3 : 2;
+                const int l0 = b.x >> ls, l1 = (b.y - 1) >> ls;
                 const int* tl = bb.tile_lines.data() + t0;
                 const int pos = (int)(std::lower_bound(tl, tl + nt, l0) - tl);
                 bool ok = pos + (l1 - l0) < nt;
@@ -1021,11 +1048,11 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
             const int64_t fb0 = fb;
             fb += 32;
             if (nz == 0) continue;
-            if (nz > kCAP || (tiled && nt > kTileLines)) {  // long row: CSR stream
+            if (nz > kCAP || (tiled && nt > kCAP / line_w)) {  // long row: CSR stream
                 fb += 12 * (int64_t)nz;
                 continue;
             }
-            if (tiled) fb += 4 * kTileLines + 2 * kCAP;     // tile ids, tile indices
+            if (tiled) fb += 4 * (kCAP / line_w) + 2 * kCAP;  // tile ids, tile indices
             else if (col16.p) fb += 2 * (int64_t)nz + 16;  // column codes, band bases
             else fb += 4 * (int64_t)nz;                     // columns
             if (hh[2 * q + 1].z >= 0)

@@ -25,10 +25,14 @@ def _digests(ra, ctx, kind, dims, coarsen, smoother, monkeypatch, device, boxes=
     ("7pt", (40, 36, 44), "pmis", "jacobi"),
     ("27pt", (30, 28, 26), "sa", "hybrid_gs"),
     ("5pt", (300, 280), "pmis", "jacobi"),
+    ("7pt-lines32", (40, 36, 44), "pmis", "jacobi"),
 ])
 def test_device_formats_equal_host_builders(kind, dims, coarsen, smoother, monkeypatch):
     import raptor_amd as ra
 
+    if kind.endswith("-lines32"):  # 32-byte x-tile lines forced on every tiled operator
+        monkeypatch.setenv("AMG_TILE_LINE", "4")
+        kind = kind.split("-")[0]
     ctx = ra.Context(0)
     dev = _digests(ra, ctx, kind, dims, coarsen, smoother, monkeypatch, True)
     host = _digests(ra, ctx, kind, dims, coarsen, smoother, monkeypatch, False)

@@ -173,7 +173,9 @@ def test_march_reuse_shapes(ctx, oracle, monkeypatch, kind, dims):
 
 
 # ---- V-cycles on forced paths, against the oracle ----------------------------------------
-VPATHS = {"persist_csr": {"AMG_KERNEL_VARIANT": "106"},
+VPATHS = {"persist_csr": {"AMG_KERNEL_VARIANT": "106", "AMG_TILE_LINE": "8"},
+          "lines64": {"AMG_TILE_LINE": "8"},
+          "lines32": {"AMG_TILE_LINE": "4"},
           "march_chained": {"AMG_KERNEL_VARIANT": "170", "AMG_TPL_MARCH_CHUNKS": "1"},
           "blocks_only": {"AMG_KERNEL_VARIANT": "10"},
           "gather_int32": {"AMG_GATHER_C16": "0"},
@@ -193,6 +195,11 @@ def test_vcycle_paths_vs_oracle(ctx, oracle, monkeypatch, path):
         monkeypatch.setenv(k, v)
     A = ra.par_stencil_grid(ctx, "7pt", (64, 64, 40))
     ml = ra.ParRugeStubenSolver(coarsen="pmis", use_graph=path != "eager").setup(A)
+    if path.startswith("lines"):  # x-tile line width forced on every tiled operator
+        want = {"lines64": 64, "lines32": 32}[path]
+        widths = {ml.level_matrix(l, w).info["tile_line_bytes"] for l in range(ml.num_levels - 1)
+                  for w in ("A", "R")} - {0}
+        assert widths == {want}, widths
     H = O.Hierarchy(None, levels=oracle_levels(O, ml))
     n = A.local_rows
     b = O.vec_uniform(n, 9)
