@@ -727,7 +727,8 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         // restrictions) are cut again at 512 lines of 32 B (the 7-pt 256^3 A2: 40,250 ->
         // 25,615 blocks; R0: same-box 76 -> 70 us); P-like operators (few lines per block)
         // keep 64-byte lines and their 1 KiB of line ids per block (sa27 P0: 234 us at 64 B,
-        // 263 at 32 B).  AMG_TILE_LINE=8 / 4 forces the width.
+        // 263 at 32 B), and so do square operators the re-cut saves < 20 % of the blocks.
+        // AMG_TILE_LINE=8 / 4 forces the width.
         line_w = 8;
         if (tiled && !bb.blocks.empty()) {
             const char* e = std::getenv("AMG_TILE_LINE");
@@ -737,10 +738,15 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
             if (tryhalf) {
                 BlockBuild b4 = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(),
                                                  tplf.empty() ? nullptr : &tplf, kTPB * gather_rpb, true, !dev_fmt, 4);
-                bb = std::move(b4);
-                line_w = 4;
-                nb_int = bb.nb_int;
-                nb_bnd = bb.nb_bnd;
+                // square operators must lose >= 20 % of their blocks (the 7-pt A1: 50,573 ->
+                // 46,841 blocks ran 144 -> 149 us; A2: 40,281 -> 25,640 ran 125 -> 102 us);
+                // restrictions gain either way (R0 91 -> 88 us at -9 %, R1 61 -> 52 at -33 %)
+                if (force == 4 || !square || 5 * b4.blocks.size() <= 4 * bb.blocks.size()) {
+                    bb = std::move(b4);
+                    line_w = 4;
+                    nb_int = bb.nb_int;
+                    nb_bnd = bb.nb_bnd;
+                }
             }
             if (std::getenv("AMG_TRACE_BLOCKS"))
                 std::fprintf(stderr, "[amg-blocks]   x-tile lines of %d B: %zu blocks\n", 8 * line_w, bb.blocks.size());
