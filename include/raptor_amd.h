@@ -147,6 +147,9 @@ typedef struct amg_matrix_info {
                               * tables)                                    */
     int32_t tile_line_bytes; /* x-tile line width of the block kernels: 64 or 32 (0: no x  *
                               * tile)                                      */
+    int32_t gs_split;        /* 1: hybrid GS sweeps run split -- a CSR-block pass over the  *
+                              * old-value couplings + the in-chunk chain walk (4.2c)     */
+    int32_t pad0;
 } amg_matrix_info;
 int amg_par_csr_info(amg_matrix A, amg_matrix_info* info);
 

@@ -73,6 +73,8 @@ class MatrixInfo(C.Structure):
         ("gs_bytes", C.c_int64),
         ("tpl_master", C.c_int32),
         ("tile_line_bytes", C.c_int32),
+        ("gs_split", C.c_int32),
+        ("pad0", C.c_int32),
     ]
 
 

@@ -259,6 +259,18 @@ struct DevMatrix {
     DevBuf<uint8_t> gs_vid;
     DevBuf<double> gs_vtab;
     int gs_ndict = 0;
+    // split GS sweep (one rank or a replicated operator, no GS templates):
+    // gs_old[0 / 1] = this operator without the forward / backward sweep's in-chunk new-value
+    // couplings, in CSR-block format (its KM_GSACC pass leaves acc in gs_acc); gs_cslabs /
+    // gs_ccol / gs_cval[0 / 1] = the same slabs' sliced ELL holding only those couplings (the
+    // chain walk of hybrid_gs_kernel, acc read instead of b)
+    std::unique_ptr<DevMatrix> gs_old[2];
+    DevBuf<int4> gs_cslabs[2];
+    DevBuf<int> gs_ccol[2];
+    DevBuf<double> gs_cval[2];
+    DevBuf<double> gs_acc;
+    bool gs_split = false;
+    bool gs_cwide[2] = {false, false};
     // row templates (square operators): rows whose columns are all local, written as
     // (column - row) offsets, values and 1/a_ii; rows with identical triples share a template.
     // tpl_id per row (kTplNone: the CSR block kernel handles the row); per template
@@ -335,7 +347,10 @@ struct DevMatrix {
     int64_t n_halo() const { return plan.n_halo(); }
 };
 
-enum KernelMode { KM_SPMV = 0, KM_SPMV_ADD = 1, KM_RESID = 2, KM_JACOBI = 3 };
+// KM_GSACC (square, no norm): y_i = b_i - sum_j a_ij x_j, subtracted one product at a time in
+// CSR order (acc = b; acc -= a_ij x_j) -- the old-value half of an l1 hybrid GS sweep
+//  on an operator without the sweep's in-chunk couplings
+enum KernelMode { KM_SPMV = 0, KM_SPMV_ADD = 1, KM_RESID = 2, KM_JACOBI = 3, KM_GSACC = 4 };
 
 // launchers (kernels.hip); all enqueue on s
 // csr-stream variant bits in effect for A (DevMatrix::default_variant, VI and template bits,
@@ -353,6 +368,10 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
 // partials: slab q at q, template block list entry t, wave w at n_gs_slabs + 4 t + w
 void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const double* b,
                       double* y, bool backward, double* partial, int s0, int s1, bool tpl);
+// chain walk of a split GS sweep: every slab, acc (from the KM_GSACC pass of
+// A.gs_old) minus the in-chunk new-value couplings in sweep order, y = x + acc * dinv_l1
+void launch_gs_chain(hipStream_t s, const DevMatrix& A, const double* x, const double* acc,
+                     double* y, bool backward);
 // plain CSR (AMG_FORMAT_CSR): all rows, one launch; partials at [0, plain_blocks() * kNormParts)
 void launch_csr_plain(hipStream_t s, int mode, bool norm, const DevMatrix& A, const double* x,
                       const double* b, double* y, double omega, double* partial);

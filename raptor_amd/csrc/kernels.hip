@@ -98,6 +98,7 @@ __device__ __forceinline__ double xload(const CsrArgs& a, int c) {
 template <int MODE>
 __device__ __forceinline__ double epilogue(const CsrArgs& a, int r, double s, double* res) {
     if (MODE == KM_SPMV) return s;
+    if (MODE == KM_GSACC) return s;  // block_long: s already starts at b (an empty row: b)
     if (MODE == KM_SPMV_ADD) return a.y[r] + s;
     const double t = a.b[r] - s;
     *res = t;
@@ -322,7 +323,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     int dv = 0;
     if (MODE == KM_SPMV_ADD) px = a.y[rr];
     if (MODE == KM_SPMV && a.y2) pd = a.dinv[rr];  // store_y2
-    if (MODE == KM_RESID || MODE == KM_JACOBI) pb = a.b[rr];
+    if (MODE == KM_RESID || MODE == KM_JACOBI || MODE == KM_GSACC) pb = a.b[rr];
     if (MODE == KM_JACOBI) {
         if (pd_tab) dv = a.dvi[rr];
         else pd = a.dinv[rr];
@@ -391,6 +392,10 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
 #pragma unroll
         for (int u = 0; u < NU; ++u) pr[u] = v[u] * xs[u];
     }
+    if (MODE == KM_GSACC) {  // acc -= p is acc + (-p) bit for bit (negation is exact)
+#pragma unroll
+        for (int u = 0; u < U; ++u) pr[u] = -pr[u];
+    }
     if (TILE) {
 #pragma unroll
         for (int p = 0; p < U / 2; ++p) *(v2d_t*)(stage + 2 * tid + 2 * kTPB * p) = v2d_t{pr[2 * p], pr[2 * p + 1]};
@@ -411,10 +416,10 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
         }
     }
     const int e0 = tid ? rends[tid - 1] : 0;
-    double s = 0.0;
+    double s = MODE == KM_GSACC ? pb : 0.0;  // GSACC: acc = b, then acc -= a_ij x_j in order
     s = lds_row_sum(stage, e0, e1, s);
     double out, sq = 0.0;
-    if (MODE == KM_SPMV) {
+    if (MODE == KM_SPMV || MODE == KM_GSACC) {
         out = s;
     } else if (MODE == KM_SPMV_ADD) {
         out = px + s;
@@ -450,11 +455,13 @@ template <int MODE, bool NORM>
 __device__ __forceinline__ double block_long(const CsrArgs& a, int4 h0, double* stage) {
     const int tid = threadIdx.x;
     const int r0 = h0.x, r1 = h0.y, k0 = h0.z, nnz = h0.w;
-    double s = 0.0, sq = 0.0;
+    double s = MODE == KM_GSACC && nnz > 0 ? a.b[r0] : 0.0, sq = 0.0;
     for (int base = 0; base < nnz; base += kCAP) {
         const int cnt = min(kCAP, nnz - base);
-        for (int k = tid; k < cnt; k += kTPB)
-            stage[k] = a.val[k0 + base + k] * xload(a, a.col[k0 + base + k]);
+        for (int k = tid; k < cnt; k += kTPB) {
+            const double p = a.val[k0 + base + k] * xload(a, a.col[k0 + base + k]);
+            stage[k] = MODE == KM_GSACC ? -p : p;
+        }
         __syncthreads();
         if (tid == 0)
             s = lds_row_sum(stage, 0, cnt, s);
@@ -463,7 +470,7 @@ __device__ __forceinline__ double block_long(const CsrArgs& a, int4 h0, double* 
     for (int r = r0 + tid; r < r1; r += kTPB) {
         if (r == r0 || nnz == 0) {  // nnz == 0: every row of the block is empty
             double res = 0.0;
-            const double o = epilogue<MODE>(a, r, s, &res);
+            const double o = MODE == KM_GSACC && nnz == 0 ? a.b[r] : epilogue<MODE>(a, r, s, &res);
             a.y[r] = o;
             if (MODE == KM_SPMV && a.y2) store_y2<MODE>(a, r, o, a.dinv[r]);
             if (NORM) sq += res * res;
@@ -2353,7 +2360,7 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
     const dim3 g(n_blocks);
     const int var = kernel_variant(A);
     if (var & 256) a.col16 = A.col16.p;
-    if ((var & 64) && !(var & 4) && A.square && A.line_w == 8) {  // persistent x-tile kernel: square operators, 64-byte lines
+    if ((var & 64) && !(var & 4) && A.square && A.line_w == 8 && mode != KM_GSACC) {  // persistent x-tile kernel: square operators, 64-byte lines
         launch_csr_persist(s, mode, norm, a, first_block, n_blocks, (var & 8) != 0);
         return;
     }
@@ -2382,6 +2389,10 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
         case KM_JACOBI:
             if (norm) AMG_L(KM_JACOBI, true);
             else AMG_L(KM_JACOBI, false);
+            break;
+        case KM_GSACC:
+            AMG_CHECK(!norm && A.square, "GS acc pass: square operator, no norm");
+            AMG_L(KM_GSACC, false);
             break;
         default: throw Error(AMG_ERR_INTERNAL, "bad kernel mode");
     }
@@ -2572,6 +2583,29 @@ void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const 
         else AMG_GS(false, false, false);
     }
 #undef AMG_GS
+    HIP_CHECK(hipGetLastError());
+}
+
+// The chain walk of a split sweep is hybrid_gs_kernel itself on a sliced ELL that holds only
+// the in-chunk new-value couplings: acc starts from the KM_GSACC pass's b - (old couplings),
+// phase 1 finds nothing but chain entries (so it loads no x), phase 2 is unchanged.
+void launch_gs_chain(hipStream_t s, const DevMatrix& A, const double* x, const double* acc,
+                     double* y, bool backward) {
+    const int d = backward ? 1 : 0;
+    const int ns = A.n_gs_slabs;
+    if (ns <= 0) return;
+    GsArgs a{A.gs_cslabs[d].p, A.gs_ccol[d].p, A.gs_cval[d].p, x, A.halo.p, (int)A.n_cols_local, acc,
+             A.gs_dinv.p, y, (long long)A.first_row, (long long)A.gs_block, (int)A.n_rows,
+             ns, nullptr, nullptr, nullptr, 0, 0};
+    const bool wide = A.gs_cwide[d];
+    const dim3 grid(wide ? ns : (ns + 3) / 4), block(wide ? 64 : 256);
+    if (wide) {
+        if (backward) hipLaunchKernelGGL((hybrid_gs_kernel<true, true, false, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((hybrid_gs_kernel<false, true, false, false>), grid, block, 0, s, a);
+    } else {
+        if (backward) hipLaunchKernelGGL((hybrid_gs_kernel<true, false, false, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((hybrid_gs_kernel<false, false, false, false>), grid, block, 0, s, a);
+    }
     HIP_CHECK(hipGetLastError());
 }
 

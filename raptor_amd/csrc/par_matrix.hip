@@ -1345,6 +1345,116 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
     if (n_gs_tblk > 0)
         gs_bytes += 50 * (n_rows - ell_rows) + 16 * (int64_t)n_tpl_ent + 12 * (int64_t)n_gs_tpl;
     gs_wide = !slabs.empty() && cells >= (int64_t)kGsWide * (int64_t)slabs.size();
+
+    // Split sweeps: the old-value couplings as a CSR-block pass (KM_GSACC on A
+    // without the sweep's in-chunk new-value couplings -- the same entries in the same order,
+    // so acc is bit-identical) and the chain walk on a sliced ELL of the new-value couplings
+    // only.  One rank or a replicated operator (the pass is built as its own matrix), no GS
+    // template rows, and rows of >= AMG_GS_SPLIT_NPR entries on average (default 12: g3sub's
+    // 5.5-entry level 0 ran 60 -> 72 us per sweep split, its 45-entry level 1 121 -> 63 us;
+    // profiles/r3u_split_ab.txt; 0 forces it, tests).
+    gs_split = false;
+    for (int d = 0; d < 2; ++d) {
+        gs_old[d].reset();
+        gs_cslabs[d].reset();
+        gs_ccol[d].reset();
+        gs_cval[d].reset();
+    }
+    gs_acc.reset();
+    {
+        const char* e = std::getenv("AMG_GS_SPLIT_NPR");
+        const int64_t npr = e ? std::atoll(e) : (int64_t)12;
+        const char* off = std::getenv("AMG_GS_SPLIT");
+        const bool allow = !(off && std::atoi(off) == 0);
+        if (allow && n_gs_tblk == 0 && n_rows > 0 && nnz >= npr * n_rows &&
+            (ctx->host.nranks == 1 || replicated)) {
+            // in-chunk new-value coupling of row i (local ids): forward cs <= j < i, backward
+            // i < j < ce (hybrid_gs_kernel's [lo, hi))
+            auto chunk = [&](int64_t i, int64_t& cs, int64_t& ce) {
+                const int64_t g = first_row + i;
+                cs = std::max<int64_t>(0, (g / B) * B - first_row);
+                ce = std::min<int64_t>(n_rows, (g / B + 1) * B - first_row);
+            };
+            auto is_new = [&](int d, int64_t i, int64_t gc) {
+                if (gc < clo || gc >= chi) return false;
+                const int64_t j = gc - clo;
+                int64_t cs, ce;
+                chunk(i, cs, ce);
+                return d == 0 ? (j >= cs && j < i) : (j > i && j < ce);
+            };
+            int64_t ccells = 0;
+            for (int d = 0; d < 2; ++d) {
+                HostCSR h;
+                h.n_global_rows = host.n_global_rows;
+                h.n_global_cols = host.n_global_cols;
+                h.row_starts = host.row_starts;
+                h.col_starts = host.col_starts;
+                h.rp.assign((size_t)n_rows + 1, 0);
+                for (int64_t i = 0; i < n_rows; ++i) {
+                    int64_t c = 0;
+                    for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) c += !is_new(d, i, host.col[k]);
+                    h.rp[i + 1] = h.rp[i] + c;
+                }
+                h.col.resize((size_t)h.rp[n_rows]);
+                h.val.resize((size_t)h.rp[n_rows]);
+#pragma omp parallel for schedule(static)
+                for (int64_t i = 0; i < n_rows; ++i) {
+                    int64_t o = h.rp[i];
+                    for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k)
+                        if (!is_new(d, i, host.col[k])) {
+                            h.col[o] = host.col[k];
+                            h.val[o] = host.val[k];
+                            ++o;
+                        }
+                }
+                gs_old[d] = std::make_unique<DevMatrix>();
+                gs_old[d]->build(ctx, std::move(h), replicated);
+                gs_old[d]->set_format(AMG_FORMAT_BLOCKS);
+                // the chain ELL: same slabs, only the new-value couplings (CSR order)
+                std::vector<int4> cs = slabs;
+                int64_t cc = 0;
+                for (int4& sl : cs) {
+                    int w = 0;
+                    for (int l = 0; l < sl.y; ++l) {
+                        const int64_t i = sl.x + l;
+                        int c = 0;
+                        for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) c += is_new(d, i, host.col[k]);
+                        w = std::max(w, c);
+                    }
+                    sl.z = (int)cc;
+                    sl.w = w;
+                    cc += (w + 3) & ~3;
+                }
+                std::vector<int> ccol((size_t)(cc + 4) * 64, -1);
+                std::vector<double> cval(ccol.size(), 0.0);
+#pragma omp parallel for schedule(dynamic, 64)
+                for (size_t q = 0; q < cs.size(); ++q) {
+                    const int4 sl = cs[q];
+                    for (int l = 0; l < sl.y; ++l) {
+                        const int64_t i = sl.x + l;
+                        int c = 0;
+                        for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k)
+                            if (is_new(d, i, host.col[k])) {
+                                const size_t at = ((size_t)sl.z + (size_t)c++) * 64 + l;
+                                ccol[at] = (int)(host.col[k] - clo);
+                                cval[at] = host.val[k];
+                            }
+                    }
+                }
+                gs_cslabs[d].upload(cs.data(), cs.size());
+                gs_ccol[d].upload(ccol.data(), ccol.size());
+                gs_cval[d].upload(cval.data(), cval.size());
+                gs_cwide[d] = !cs.empty() && cc >= (int64_t)kGsWide * (int64_t)cs.size();
+                if (d == 0) ccells = cc;
+            }
+            gs_acc.alloc((size_t)n_rows);
+            gs_split = true;
+            // bytes per (forward) sweep: the pass (its stored format + b + acc out), then the
+            // chain ELL cells + slab headers + acc, x, dinv in and y out
+            gs_bytes = gs_old[0]->mode_bytes(KM_RESID) + 8 * n_rows + 12 * 64 * ccells +
+                       16 * (int64_t)slabs.size() + 32 * n_rows;
+        }
+    }
 }
 
 int64_t DevMatrix::format_generation = 0;
@@ -1459,6 +1569,11 @@ bool par_restrict_j0(DevMatrix& R, const double* r, double* bc, double* x0c, con
 void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block,
                    bool backward, double* partial) {
     A.ensure_gs_blocks(block);
+    if (A.gs_split && !partial) {  // split sweep: no halo (one rank / replicated)
+        par_apply(*A.gs_old[backward ? 1 : 0], KM_GSACC, x, b, A.gs_acc.p, 0.0, nullptr);
+        launch_gs_chain(A.ctx->stream, A, x, A.gs_acc.p, y, backward);
+        return;
+    }
     const bool comm = A.halo_begin(x);
     hipStream_t s = A.ctx->stream;
     // template blocks and interior slabs never read the halo: they run while it is in flight

@@ -326,18 +326,23 @@ def test_full_size_27pt_256(ctx, oracle):
 GS_SHAPES = [("27pt", (260, 8, 8)), ("27pt", (40, 40, 40)), ("7pt", (37, 41, 29)), ("5pt", (200, 61))]
 
 
-@pytest.mark.parametrize("tpl_gs", ["templates", "generic", "ell"])
+@pytest.mark.parametrize("tpl_gs", ["templates", "generic", "ell", "split"])
 @pytest.mark.parametrize("kind,dims", GS_SHAPES, ids=[f"{k}-{'x'.join(map(str, d))}" for k, d in GS_SHAPES])
 def test_hybrid_gs_template_kernel(ctx, oracle, monkeypatch, kind, dims, tpl_gs):
     """l1 hybrid GS, forward / backward, block sizes 64, 32, 8, 1 (the template kernel needs B
     | 64) and 17, 48 (sliced ELL only): bit-identical to the oracle on templated stencils
     (NPL 16, 8 and 4 windows; a last partial block), with the template kernel on -- uniform-
-    stencil masks (7-pt, 27-pt) or per-template tables (generic) -- and off."""
+    stencil masks (7-pt, 27-pt) or per-template tables (generic) -- and off: the one-kernel
+    sliced-ELL sweep (ell) or the split sweep (KM_GSACC block pass + chain walk, 4.2c)."""
     import raptor_amd as ra
 
     O = oracle
-    if tpl_gs == "ell":
+    if tpl_gs in ("ell", "split"):
         monkeypatch.setenv("AMG_GS_TEMPLATES", "0")
+    if tpl_gs == "split":
+        monkeypatch.setenv("AMG_GS_SPLIT_NPR", "0")
+    else:
+        monkeypatch.setenv("AMG_GS_SPLIT", "0")
     if tpl_gs == "generic":
         monkeypatch.setenv("AMG_TPL_MASTER", "0")
     Ao = {"7pt": O.gen_7pt, "27pt": O.gen_27pt, "5pt": O.gen_5pt}[kind](*dims)
@@ -352,7 +357,10 @@ def test_hybrid_gs_template_kernel(ctx, oracle, monkeypatch, kind, dims, tpl_gs)
         assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs(x, b, blk)), ("fwd", blk)
         A.hybrid_gs(dx, db, out, blk, backward=True)
         assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs_backward(x, b, blk)), ("bwd", blk)
+        assert A._info()["gs_split"] == (tpl_gs == "split"), blk
     assert A._info()["gs_bytes"] > 0
+    if tpl_gs == "split":
+        return
     # B = 8: every shape here has no in-chunk coupling but +-1 -> template kernels (50 B per
     # row + table) when they are on, sliced ELL (>= 5 B per cell) when off
     A.hybrid_gs(dx, db, out, 8)
@@ -360,22 +368,32 @@ def test_hybrid_gs_template_kernel(ctx, oracle, monkeypatch, kind, dims, tpl_gs)
     assert (per_row < 60) if tpl_gs != "ell" else (per_row > 60), per_row
 
 
-@pytest.mark.parametrize("tpl_gs", ["templates", "generic", "ell"])
+@pytest.mark.parametrize("tpl_gs", ["templates", "generic", "ell", "split", "nosplit"])
 def test_sa_gs_vcycle_template_kernel(ctx, oracle, monkeypatch, tpl_gs):
     """SA + hybrid GS V-cycle and solve (fused forward-GS norm partials from both GS kernels)
     against the oracle hierarchy, level-0 GS on the template kernel (uniform-stencil masks or
-    per-template tables) or on sliced ELL."""
+    per-template tables) or on sliced ELL; the other sweeps split by the default rule (KM_GSACC
+    pass + chain walk on rows of >= 12 entries), split on every level, or never (nosplit)."""
     import raptor_amd as ra
 
     O = oracle
-    if tpl_gs == "ell":
+    if tpl_gs in ("ell", "split"):
         monkeypatch.setenv("AMG_GS_TEMPLATES", "0")
+    if tpl_gs == "split":
+        monkeypatch.setenv("AMG_GS_SPLIT_NPR", "0")
+    if tpl_gs == "nosplit":
+        monkeypatch.setenv("AMG_GS_SPLIT", "0")
     if tpl_gs == "generic":
         monkeypatch.setenv("AMG_TPL_MASTER", "0")
     dims = (64, 40, 24)
     Ao = O.gen_27pt(*dims)
     A = ra.par_stencil_grid(ctx, "27pt", dims)
     ml = ra.ParSmoothedAggregationSolver().setup(A)
+    split = [ml.level_matrix(l, "A").info["gs_split"] for l in range(ml.num_levels - 1)]
+    if tpl_gs == "split":
+        assert all(split), split
+    if tpl_gs == "nosplit":
+        assert not any(split), split
     Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS["sa"], smoother=O.SMOOTH_HYBRID_GS))
     n = Ao.shape[0]
     b = Ao.spmv(O.vec_uniform(n, 42))
