@@ -262,15 +262,15 @@ struct DevMatrix {
     // split GS sweep (one rank or a replicated operator, no GS templates):
     // gs_old[0 / 1] = this operator without the forward / backward sweep's in-chunk new-value
     // couplings, in CSR-block format (its KM_GSACC pass leaves acc in gs_acc); gs_cslabs /
-    // gs_ccol / gs_cval[0 / 1] = the same slabs' sliced ELL holding only those couplings (the
-    // chain walk of hybrid_gs_kernel, acc read instead of b)
+    // gs_ccol / gs_cval[0 / 1] = the same slabs' sliced ELL holding only those couplings, in
+    // consumption order (backward: descending column) for gs_chain_kernel
     std::unique_ptr<DevMatrix> gs_old[2];
     DevBuf<int4> gs_cslabs[2];
     DevBuf<int> gs_ccol[2];
     DevBuf<double> gs_cval[2];
     DevBuf<double> gs_acc;
     bool gs_split = false;
-    bool gs_cwide[2] = {false, false};
+    int gs_cmaxw[2] = {0, 0};  // widest chain-ELL slab per direction (the kernel's LDS queue)
     // row templates (square operators): rows whose columns are all local, written as
     // (column - row) offsets, values and 1/a_ii; rows with identical triples share a template.
     // tpl_id per row (kTplNone: the CSR block kernel handles the row); per template

@@ -2586,9 +2586,64 @@ void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const 
     HIP_CHECK(hipGetLastError());
 }
 
-// The chain walk of a split sweep is hybrid_gs_kernel itself on a sliced ELL that holds only
-// the in-chunk new-value couplings: acc starts from the KM_GSACC pass's b - (old couplings),
-// phase 1 finds nothing but chain entries (so it loads no x), phase 2 is unchanged.
+// Chain walk of a split sweep: one wave per slab, lane = row.  The lane's
+// in-chunk new-value couplings come from a sliced ELL stored in consumption order (forward:
+// ascending j, backward: descending j; padding col -1) and are staged in the wave's LDS column
+// `lane` first, so phase 2 -- hybrid_gs_kernel's column sweep: at step t the row j that is final
+// now is broadcast with v_readlane, every lane whose next coupling is j subtracts a_ij x'_j --
+// reads its next entry from LDS instead of waiting on a global load inside the step loop.
+// acc comes from the KM_GSACC pass (b - old couplings), so the result is the oracle's.
+template <bool BACK, int W>
+__global__ __launch_bounds__(64) void gs_chain_kernel(GsArgs a) {
+    __shared__ double qv[W * 64];
+    __shared__ int qc[W * 64];
+    const int wave = __builtin_amdgcn_readfirstlane((int)blockIdx.x) + a.slab0;
+    if (wave >= a.nslab) return;
+    const int lane = threadIdx.x;
+    const int4 sl = a.slabs[wave];
+    const int r = sl.x + lane;
+    const bool live = lane < sl.y;
+    double acc = 0.0, xi = 0.0, dinv = 0.0;
+    if (live) {
+        acc = a.b[r];
+        xi = a.x[r];
+        dinv = a.dinv[r];
+    }
+    const size_t base = (size_t)sl.z * 64 + lane;
+    for (int k0 = 0; k0 < sl.w; k0 += 8) {  // sl.w <= W (launch_gs_chain); 8 loads in flight
+        int c[8];
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const bool in = k0 + u < sl.w;  // uniform
+            c[u] = in ? __builtin_nontemporal_load(a.col + base + (size_t)(k0 + u) * 64) : -1;
+            v[u] = in ? __builtin_nontemporal_load(a.val + base + (size_t)(k0 + u) * 64) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (k0 + u < sl.w) {
+                qc[(k0 + u) * 64 + lane] = c[u];
+                qv[(k0 + u) * 64 + lane] = v[u];
+            }
+        }
+    }
+    // each lane reads back only its own LDS column: no barrier
+    int p = 0;
+    int cn = sl.w > 0 ? qc[lane] : -1;
+    double vn = sl.w > 0 ? qv[lane] : 0.0;
+    for (int t = 0; t < sl.y; ++t) {
+        const int j = BACK ? sl.y - 1 - t : t;  // lane whose row is final now
+        const double xj = bcast_lane(xi + acc * dinv, j);
+        if (cn == sl.x + j) {
+            acc -= vn * xj;
+            ++p;
+            cn = p < sl.w ? qc[p * 64 + lane] : -1;
+            vn = p < sl.w ? qv[p * 64 + lane] : 0.0;
+        }
+    }
+    if (live) a.y[r] = xi + acc * dinv;
+}
+
 void launch_gs_chain(hipStream_t s, const DevMatrix& A, const double* x, const double* acc,
                      double* y, bool backward) {
     const int d = backward ? 1 : 0;
@@ -2597,15 +2652,18 @@ void launch_gs_chain(hipStream_t s, const DevMatrix& A, const double* x, const d
     GsArgs a{A.gs_cslabs[d].p, A.gs_ccol[d].p, A.gs_cval[d].p, x, A.halo.p, (int)A.n_cols_local, acc,
              A.gs_dinv.p, y, (long long)A.first_row, (long long)A.gs_block, (int)A.n_rows,
              ns, nullptr, nullptr, nullptr, 0, 0};
-    const bool wide = A.gs_cwide[d];
-    const dim3 grid(wide ? ns : (ns + 3) / 4), block(wide ? 64 : 256);
-    if (wide) {
-        if (backward) hipLaunchKernelGGL((hybrid_gs_kernel<true, true, false, false>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((hybrid_gs_kernel<false, true, false, false>), grid, block, 0, s, a);
-    } else {
-        if (backward) hipLaunchKernelGGL((hybrid_gs_kernel<true, false, false, false>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((hybrid_gs_kernel<false, false, false, false>), grid, block, 0, s, a);
-    }
+    const int w = A.gs_cmaxw[d];  // <= 63: in-chunk couplings of a <= 64-row chunk
+    AMG_ASSERT(w <= 64);
+#define AMG_GC(W)                                                                                  \
+    do {                                                                                           \
+        if (backward) hipLaunchKernelGGL((gs_chain_kernel<true, W>), dim3(ns), dim3(64), 0, s, a);  \
+        else hipLaunchKernelGGL((gs_chain_kernel<false, W>), dim3(ns), dim3(64), 0, s, a);          \
+    } while (0)
+    if (w <= 8) AMG_GC(8);
+    else if (w <= 16) AMG_GC(16);
+    else if (w <= 32) AMG_GC(32);
+    else AMG_GC(64);
+#undef AMG_GC
     HIP_CHECK(hipGetLastError());
 }
 

@@ -1433,18 +1433,22 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
                     for (int l = 0; l < sl.y; ++l) {
                         const int64_t i = sl.x + l;
                         int c = 0;
-                        for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k)
+                        // consumption order: forward ascending, backward descending column
+                        for (int64_t kk = host.rp[i]; kk < host.rp[i + 1]; ++kk) {
+                            const int64_t k = d == 0 ? kk : host.rp[i + 1] - 1 - (kk - host.rp[i]);
                             if (is_new(d, i, host.col[k])) {
                                 const size_t at = ((size_t)sl.z + (size_t)c++) * 64 + l;
                                 ccol[at] = (int)(host.col[k] - clo);
                                 cval[at] = host.val[k];
                             }
+                        }
                     }
                 }
                 gs_cslabs[d].upload(cs.data(), cs.size());
                 gs_ccol[d].upload(ccol.data(), ccol.size());
                 gs_cval[d].upload(cval.data(), cval.size());
-                gs_cwide[d] = !cs.empty() && cc >= (int64_t)kGsWide * (int64_t)cs.size();
+                gs_cmaxw[d] = 0;
+                for (const int4& sl : cs) gs_cmaxw[d] = std::max(gs_cmaxw[d], sl.w);
                 if (d == 0) ccells = cc;
             }
             gs_acc.alloc((size_t)n_rows);
