@@ -8,8 +8,16 @@ Workload (BASELINE.json configs[1], weak-scaled for --gpus N):
   PMIS coarsening + classical interpolation, 1 pre / 1 post Jacobi sweep (omega 2/3),
   dense solve at <= 256 rows; b = A x*, x* ~ U(-1,1) (splitmix64, seed 42), x0 = 0.
 One "step" = one ParMultilevel::solve iteration (V-cycle + residual norm) of the global
-problem.  Timed: K steps of amg_solver_solve (no host sync inside), barrier + device sync on
-both sides, max over ranks.  value = V-cycles/s x (global rows / 256^3): 256^3-equivalent
+problem.  Timed: K steps of amg_solver_solve (no host sync inside; cycles and the last norm
+replay captured hipGraphs on every rank count), barrier + device sync on both sides, max over
+ranks.
+
+No torch in this process: the library binds the ROCm HIP runtime and RCCL it was built
+against (a torch-first process binds torch's bundled HIP 7.0 / RCCL 2.26, where multi-rank
+graph capture is refused).  Device buffers and events go through the C-ABI
+(raptor_amd.Context.native); ranks find each other over a Unix-socket mesh keyed by the
+launcher's MASTER_PORT (raptor_amd.SocketComm: RCCL id, setup exchange, barriers, max over
+ranks).  value = V-cycles/s x (global rows / 256^3): 256^3-equivalent
 V-cycles per second, the whole-job aggregate (equals plain iterations/s at N=1).
 
 roofline: the level-0 ParCSRMatrix::mult on the plain CSR format (csr_plain_kernel: int32 row_ptr
@@ -19,8 +27,8 @@ default format (row templates / CSR-VI blocks) on the bytes that fo
 vcycle_kernels: every V-cycle operation of the large levels (eager, events), stored bytes and
 fraction of the 8 TB/s peak; the hipGraph'd durations are in profiles/ (rocprofv3).
 cpu_baseline (rank 0, N=1): the oracle's V-cycle (C, OpenMP) on the same hierarchy and
-inputs, timed for --cpu-seconds; "port" = this repo's CPU restatement (the reference
-has no AMG code).
+inputs, timed for --cpu-seconds at the host's CPU quota (cgroup cpu.max) and at 1 thread;
+"port" = this repo's CPU restatement (the reference has no AMG code).
 """
 from __future__ import annotations
 
@@ -80,19 +88,16 @@ def main():
     sys.stdout.flush()
     os.dup2(2, 1)
 
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-
     import raptor_amd as ra
 
+    assert "torch" not in sys.modules, "bench.py runs torch-free (DESIGN.md 5)"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    comm = None
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         device = local_rank
         if os.environ.get("AMG_BENCH_SHARED_GPU") == "1":
             # rehearsal of the N-GPU path on a 1-GPU box: every rank on device 0, each its own
@@ -101,12 +106,10 @@ def main():
             # a run are not a scaling measurement.
             device = 0
             os.environ["NCCL_HOSTID"] = f"amg-bench-rank{rank}"
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        torch.cuda.set_device(device)
-        ctx = ra.Context.distributed(device)
+        comm = ra.SocketComm(rank, world)
+        ctx = ra.Context.native(device, comm=comm)
     else:
-        torch.cuda.set_device(0)
-        ctx = ra.Context(0)
+        ctx = ra.Context.native(0)
 
     g3 = args.config == "g3sub"
     if g3:
@@ -122,7 +125,7 @@ def main():
 
     def barrier():
         if world > 1:
-            dist.barrier()
+            comm.barrier()
 
     t0 = time.perf_counter()
     sa27 = args.config == "sa27"
@@ -154,33 +157,32 @@ def main():
         " ".join(f"{i['n_global']}/{i['nnz_global']}" for i in infos))
 
     n = A.local_rows
-    with torch.cuda.stream(ctx.stream):
-        xs = ra.vector_uniform(ctx, n, A.first_row, 42)
-        b = ctx.empty(n)
-        A.mult(xs, b)
-        x = ctx.zeros(n)
-        y = ctx.empty(n)
+    xs = ra.vector_uniform(ctx, n, A.first_row, 42)
+    b = ctx.empty(n)
+    A.mult(xs, b)
+    x = ctx.zeros(n)
+    y = ctx.empty(n)
     ctx.synchronize()
 
-    # warmup (captures the hipGraph on 1 rank)
+    # warmup (captures the cycle and norm hipGraphs, on every rank)
     if args.warmup > 0:
         ml.solve(x, b, max_iter=args.warmup)
     x.zero_()
     ctx.synchronize()
-    torch.cuda.synchronize()
 
     barrier()
-    torch.cuda.synchronize()
+    ctx.synchronize()
     ts = time.perf_counter()
     _, hist = ml.solve(x, b, max_iter=args.steps)
     ctx.synchronize()
-    torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - ts
+    graph_used = ml.graph_enabled
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = comm.allreduce_max(dt)
+        graph_all = [bool(v) for v in comm.allgather_f64(1.0 if graph_used else 0.0)]
+    else:
+        graph_all = [graph_used]
     iters_per_s = args.steps / dt
     value = iters_per_s * scale
     conv = float((hist[-1] / hist[0]) ** (1.0 / max(1, len(hist) - 1))) if hist[0] > 0 else None
@@ -193,11 +195,7 @@ def main():
     # the kernels stream).  The per-iteration residual norm is fused into the next cycle's
     # first sweep, so a solve iteration moves one cycle's bytes.
     def allsum(v):
-        if world == 1:
-            return float(v)
-        t = torch.tensor([float(v)], dtype=torch.float64)
-        dist.all_reduce(t)
-        return float(t.item())
+        return float(v) if world == 1 else comm.allreduce_sum(float(v))
 
     cyc_bytes = allsum(ml.bytes_per_cycle())
     cyc_stored = allsum(sum(i["stored_bytes_per_cycle_local"] for i in infos))
@@ -205,38 +203,31 @@ def main():
     # ---- level kernels, timed live with HIP events on the context stream -----------------
     n = A.local_rows
 
-    def timed(fn, reps, flush=None):
-        """avg ms per launch of fn() over reps (HIP events on the context stream).  flush:
-        run before each launch and excluded (cache-cold timing: a 1 GiB copy evicts the
-        256 MiB Infinity Cache and the L2s)."""
-        with torch.cuda.stream(ctx.stream):
-            for _ in range(3):
-                fn()
-            if flush is None:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record(ctx.stream)
-                for _ in range(reps):
-                    fn()
-                e1.record(ctx.stream)
-                e1.synchronize()
-                return e0.elapsed_time(e1) / reps
-            tot = 0.0
-            for _ in range(reps):
-                flush()
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record(ctx.stream)
-                fn()
-                e1.record(ctx.stream)
-                e1.synchronize()
-                tot += e0.elapsed_time(e1)
-            return tot / reps
+    e0, e1 = ra.Event(ctx), ra.Event(ctx)
 
-    fl_src = ctx.empty(1 << 27)
+    def timed(fn, reps, flush=None):
+        """avg ms per launch of fn() over reps (HIP events recorded on the context stream, the
+        stream the kernels run on).  flush: run before each launch and excluded (cache-cold
+        timing: a 1 GiB copy evicts the 256 MiB Infinity Cache and the L2s)."""
+        for _ in range(3):
+            fn()
+        if flush is None:
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            return e0.elapsed_ms(e1) / reps
+        tot = 0.0
+        for _ in range(reps):
+            flush()
+            e0.record()
+            fn()
+            e1.record()
+            tot += e0.elapsed_ms(e1)
+        return tot / reps
+
+    fl_src = ra.vector_uniform(ctx, 1 << 27, 0, 9)
     fl_dst = ctx.empty(1 << 27)
-    with torch.cuda.stream(ctx.stream):
-        fl_src.fill_(1.0)
 
     def flush():
         ra.vector_copy(ctx, fl_src, fl_dst)
@@ -282,9 +273,8 @@ def main():
         nl = Al.local_rows
         P, R = ml.level_matrix(l, "P"), ml.level_matrix(l, "R")
         nc = P.local_cols
-        with torch.cuda.stream(ctx.stream):
-            xl, bl, tl = ra.vector_uniform(ctx, nl, 0, 5), ra.vector_uniform(ctx, nl, 0, 6), ctx.empty(nl)
-            xc, bc = ra.vector_uniform(ctx, nc, 0, 7), ctx.empty(R.local_rows)
+        xl, bl, tl = ra.vector_uniform(ctx, nl, 0, 5), ra.vector_uniform(ctx, nl, 0, 6), ctx.empty(nl)
+        xc, bc = ra.vector_uniform(ctx, nc, 0, 7), ctx.empty(R.local_rows)
         ai, pi, ri = Al.info, P.info, R.info
         if gs:
             Al.hybrid_gs(xl, bl, tl, 64)  # builds the sliced-ELL copy if the cycle has not
@@ -319,6 +309,11 @@ def main():
                     row["traffic"] = int(o["traffic_bytes"])
                     row["traffic_over_stored"] = o["traffic_over_stored"]
                     row["traffic_GBps"] = round(o["traffic_bytes"] / (row["us"] * 1e-6) / 1e9, 1)
+                else:
+                    # no counters for this library's format of the operation (the file was
+                    # taken on another build): said so, not silently dropped
+                    row["traffic"] = None
+                    row["traffic_stale"] = o is not None
         except (OSError, KeyError, ValueError):
             pass
     dominant = max(table, key=lambda t: t["us"]) if table else None
@@ -382,7 +377,8 @@ def main():
                               "even rows" if g3 else "z-slabs"),
                 "setup_s": round(setup_s, 2),
                 "reorder_s": None if reorder_s is None else round(reorder_s, 2),
-                "hipgraph": world == 1 and not args.no_graph,
+                "hipgraph": graph_used,
+                "hipgraph_all_ranks": graph_all,
             },
             "iters_per_s": round(iters_per_s, 3),
             "convergence_factor": conv,
@@ -440,8 +436,9 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), file=out_stream, flush=True)
+    del ml, A
     if world > 1:
-        dist.destroy_process_group()
+        comm.close()
 
 
 def _cpu_model():
@@ -454,13 +451,31 @@ def _cpu_model():
     return None
 
 
+def cpu_quota():
+    """CPUs this process may keep busy: the cgroup v2 quota (cpu.max "quota period"), capped by
+    the affinity mask; None when there is no quota ("max") or it cannot be read."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q == "max":
+            return None
+        cpus = max(1, int(float(q) / float(per) + 0.5))
+    except (OSError, ValueError):
+        return None
+    try:
+        cpus = min(cpus, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    return cpus
+
+
 def cpu_baseline(ml, b, seconds, scale, hybrid_gs=False):
     """Oracle V-cycle (C, OpenMP) on the product's own level operators, rank 0, N=1.
 
-    Timed twice, half of `seconds` each: with OpenMP's default team (OMP_NUM_THREADS, the
-    GPU box's CPU share of 16) and with one thread per CPU of the affinity mask (the whole
-    machine the job may be scheduled on; SURVEY.md 8(d) asks for all host cores).  `value` /
-    `cores` are the faster run; both are listed under `runs`."""
+    Timed at the host's CPU share -- the cgroup quota (cpu.max; 16 CPUs on the GPU box), else
+    OMP_NUM_THREADS / the affinity mask -- and at one thread, for half of `seconds` each.  More
+    threads than the quota only time the scheduler's throttling (a 256-thread team on a
+    16-CPU quota ran 31x slower than 16 threads, BENCH_r03.json), so no run exceeds it.
+    `value` / `cores` are the faster run; both are listed under `runs`."""
     import numpy as np
 
     from oracle import oracle as O
@@ -479,15 +494,17 @@ def cpu_baseline(ml, b, seconds, scale, hybrid_gs=False):
         levels.append(tuple(mats))
     H = O.Hierarchy(levels[0][0], levels=levels,
                     smoother=O.SMOOTH_HYBRID_GS if hybrid_gs else O.SMOOTH_JACOBI)
-    bh = b.cpu().numpy()
+    bh = b.numpy()
     try:
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         affinity = None
     L = O.lib()
     default_threads = int(L.orc_num_threads())
+    quota = cpu_quota()
+    share = quota or min(default_threads, affinity or default_threads)
     runs = []
-    for threads in dict.fromkeys([default_threads, affinity or default_threads]):
+    for threads in dict.fromkeys([share, 1]):
         L.orc_set_num_threads(threads)
         x = np.zeros(bh.size)
         x = H.cycle(x, bh)  # untimed first touch / thread start-up
@@ -500,7 +517,9 @@ def cpu_baseline(ml, b, seconds, scale, hybrid_gs=False):
             if el >= seconds / 2:
                 break
         runs.append({"threads": threads, "cycles": k, "seconds": round(el, 2),
-                     "value": round(k / el * scale, 4)})
+                     "value": round(k / el * scale, 4),
+                     "what": "host CPU share (cgroup quota)" if threads == quota and quota else
+                             "OMP_NUM_THREADS / affinity" if threads == share else "one thread"})
     L.orc_set_num_threads(default_threads)
     best = max(runs, key=lambda r: r["value"])
     return {
@@ -512,6 +531,7 @@ def cpu_baseline(ml, b, seconds, scale, hybrid_gs=False):
         "cpu_model": _cpu_model(),
         "nproc": os.cpu_count(),
         "affinity_cpus": affinity,
+        "cgroup_cpu_quota": quota,
         "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
         "sample": f"oracle V-cycles (C/OpenMP, same hierarchy and b): " +
                   ", ".join(f"{r['cycles']} in {r['seconds']}s at {r['threads']} threads" for r in runs) +

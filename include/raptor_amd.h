@@ -314,6 +314,24 @@ int amg_vector_copy(amg_context ctx, int64_t n, const double* src, double* dst);
  * it as the box's read-bandwidth ceiling: most level kernels read far more than they write. */
 int amg_vector_read(amg_context ctx, int64_t n, const double* src, double* partials, int64_t n_partials);
 
+/* ---- device memory and timing (torch-free callers) --------------------------------- */
+/* What a caller without a framework needs around the compute calls: device buffers, copies,
+ * and events on the context stream (bench.py and the RCCL workers use these so that the
+ * process binds the HIP runtime and RCCL the library was built against).  */
+int amg_device_malloc(amg_context ctx, int64_t bytes, void** out);
+/* waits for the context stream, then frees */
+int amg_device_free(amg_context ctx, void* p);
+/* bytes from src to dst, host or device on either side (unified addressing), ordered after
+ * the work already on the context stream; returns when the copy has landed.             */
+int amg_memcpy(amg_context ctx, void* dst, const void* src, int64_t bytes);
+/* device memset, enqueued on the context stream */
+int amg_memset_async(amg_context ctx, void* p, int value, int64_t bytes);
+typedef struct amg_event_s* amg_event;
+int amg_event_create(amg_context ctx, amg_event* out);
+int amg_event_record(amg_event e);                                   /* on the context stream */
+int amg_event_elapsed_ms(amg_event start, amg_event end, float* ms); /* waits for `end`       */
+int amg_event_destroy(amg_event e);
+
 #ifdef __cplusplus
 }
 #endif

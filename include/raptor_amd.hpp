@@ -3,13 +3,13 @@
 // BASELINE.json:5 asks for "the ParMultilevel/ParCSRMatrix API surface ... C++ host code calls
 // HIP through a thin extern-"C" layer" ("C++ facade: ParCSRMatrix ... and
 // ParMultilevel ... Below it, a thin extern "C" C-ABI").  These classes are that facade: RAII
-// owners of the opaque handles, C-ABI error codes turned into amg::Error on the C++ side only
+// owners of the opaque handles, C-ABI error codes turned into raptor_amd::Error on the C++ side only
 // (no exception ever crosses the C-ABI itself).  Vectors are device pointers (hipMalloc) of
 // the rank-local length, as in the C-ABI; all work runs on the context's HIP stream.
 //
-//   amg::Context ctx(0);
-//   amg::ParCSRMatrix A = amg::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 256, 256, 256);
-//   amg::ParMultilevel ml(A, amg::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
+//   raptor_amd::Context ctx(0);
+//   raptor_amd::ParCSRMatrix A = raptor_amd::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 256, 256, 256);
+//   raptor_amd::ParMultilevel ml(A, raptor_amd::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
 //   std::vector<double> hist = ml.solve(d_x, d_b, 20);
 #ifndef RAPTOR_AMD_HPP
 #define RAPTOR_AMD_HPP
@@ -22,7 +22,10 @@
 
 #include "raptor_amd.h"
 
-namespace amg {
+// The facade has its own namespace: the library's internals are namespace amg, and although
+// libraptor_amd.so exports only the amg_* C entry points (linker version script), distinct
+// names keep a caller's inline copies of these classes from ever meeting internal symbols.
+namespace raptor_amd {
 
 // a C-ABI error code and amg_last_error() of the failing call
 class Error : public std::runtime_error {
@@ -211,6 +214,6 @@ private:
     amg_solver h_ = nullptr;
 };
 
-}  // namespace amg
+}  // namespace raptor_amd
 
 #endif  // RAPTOR_AMD_HPP

@@ -13,7 +13,10 @@ shared library or a GPU is missing, it raises.
     ml.setup(A)
     x, hist = ml.solve(x, b, max_iter=20)
 
-Vectors are rank-local float64 torch tensors on the context's device.
+Vectors are rank-local float64 device vectors: torch tensors on the context's device, or --
+for a torch-free process (``Context.native``; the bench, so the library binds the ROCm HIP
+runtime and RCCL it was built against instead of torch's bundled copies) -- ``DeviceVector``s
+allocated through the C-ABI.
 """
 from __future__ import annotations
 
@@ -22,6 +25,7 @@ import os
 
 import numpy as np
 
+from ._sockcomm import SocketComm  # noqa: F401
 from ._lib import (  # noqa: F401  (re-exported constants)
     AMG_FORMAT_AUTO,
     AMG_FORMAT_BLOCKS,
@@ -46,6 +50,9 @@ from ._lib import (  # noqa: F401  (re-exported constants)
 
 __all__ = [
     "Context",
+    "DeviceVector",
+    "Event",
+    "SocketComm",
     "ParCSRMatrix",
     "ParMultilevel",
     "ParRugeStubenSolver",
@@ -64,11 +71,88 @@ def _torch():
     return torch
 
 
+class DeviceVector:
+    """float64 device vector of a native (torch-free) context, allocated through the C-ABI
+    (amg_device_malloc); freed when collected.  ``numpy()`` copies it to the host."""
+
+    def __init__(self, ctx: "Context", n: int):
+        self.ctx = ctx
+        self.n = int(n)
+        self.ptr = C.c_void_p()
+        check(lib().amg_device_malloc(ctx.h, 8 * self.n, C.byref(self.ptr)))
+
+    def numel(self) -> int:
+        return self.n
+
+    def __len__(self):
+        return self.n
+
+    def numpy(self) -> np.ndarray:
+        out = np.empty(self.n, np.float64)
+        if self.n:
+            check(lib().amg_memcpy(self.ctx.h, out.ctypes.data_as(C.c_void_p), self.ptr, 8 * self.n))
+        return out
+
+    def cpu(self):  # torch-tensor-like spelling for code that takes either kind
+        return self
+
+    def copy_from(self, arr):
+        a = np.ascontiguousarray(arr, np.float64)
+        if a.size != self.n:
+            raise ValueError("copy_from: sizes differ")
+        if self.n:
+            check(lib().amg_memcpy(self.ctx.h, self.ptr, a.ctypes.data_as(C.c_void_p), 8 * self.n))
+        return self
+
+    def zero_(self):
+        if self.n:
+            check(lib().amg_memset_async(self.ctx.h, self.ptr, 0, 8 * self.n))
+        return self
+
+    def __del__(self):
+        p = getattr(self, "ptr", None)
+        if p and p.value:
+            try:
+                lib().amg_device_free(self.ctx.h, p)
+            except Exception:
+                pass
+            self.ptr = None
+
+
+class Event:
+    """Timing event on a context's stream (amg_event_*): works for native and torch contexts."""
+
+    def __init__(self, ctx: "Context"):
+        self.ctx = ctx
+        self.h = C.c_void_p()
+        check(lib().amg_event_create(ctx.h, C.byref(self.h)))
+
+    def record(self):
+        check(lib().amg_event_record(self.h))
+        return self
+
+    def elapsed_ms(self, end: "Event") -> float:
+        ms = C.c_float()
+        check(lib().amg_event_elapsed_ms(self.h, end.h, C.byref(ms)))
+        return ms.value
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            try:
+                lib().amg_event_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+
 def _ptr(t):
-    """Device pointer of a float64 torch tensor (checked)."""
-    torch = _torch()
+    """Device pointer of a DeviceVector or a float64 torch tensor (checked)."""
     if t is None:
         return None
+    if isinstance(t, DeviceVector):
+        return t.ptr
+    torch = _torch()
     if not isinstance(t, torch.Tensor) or t.dtype != torch.float64 or not t.is_cuda:
         raise TypeError("vectors must be float64 CUDA(HIP) torch tensors")
     if not t.is_contiguous():
@@ -80,7 +164,11 @@ class Context:
     """One GPU / rank.  ``Context(device, stream)``; multi-rank via ``Context.distributed``.
 
     The context's HIP stream is a torch stream, so torch events and the C-ABI kernels share
-    one queue (``ctx.stream``)."""
+    one queue (``ctx.stream``).  ``Context.native(device)`` makes a torch-free context: its
+    own stream, ``DeviceVector``s for ``empty`` / ``zeros``, multi-rank over a ``SocketComm``
+    (``Context.native(device, comm=...)``)."""
+
+    native = False
 
     def __init__(self, device: int | None = None, stream=None):
         torch = _torch()
@@ -121,6 +209,32 @@ class Context:
         return ctx
 
     @classmethod
+    def native(cls, device: int = 0, comm=None):
+        """A torch-free context (no torch import): the library's own stream and device
+        buffers.  comm: a ``SocketComm`` for multi-rank runs (collective: every rank calls
+        this; rank 0's RCCL id travels over the mesh, the setup exchange too)."""
+        ctx = cls.__new__(cls)
+        ctx.native = True
+        ctx.device = int(device)
+        ctx.torch_device = None
+        ctx.stream = None
+        ctx.h = C.c_void_p()
+        check(lib().amg_context_create(ctx.device, None, C.byref(ctx.h)))
+        ctx.rank, ctx.nranks = 0, 1
+        ctx._keep = []
+        if comm is not None and comm.nranks > 1:
+            uid = (C.c_char * 128)()
+            if comm.rank == 0:
+                check(lib().amg_rccl_unique_id(uid))
+            raw = comm.bcast_bytes(bytes(uid) if comm.rank == 0 else None)
+            uid = (C.c_char * 128).from_buffer_copy(raw)
+            cb = comm.exchange_fn()
+            ctx._keep.append(cb)
+            check(lib().amg_context_set_comm(ctx.h, comm.rank, comm.nranks, uid, cb, None))
+            ctx.rank, ctx.nranks, ctx.comm = comm.rank, comm.nranks, comm
+        return ctx
+
+    @classmethod
     def loopback(cls, rank: int, nranks: int, world: str, device: int = 0, stream=None):
         """In-process virtual rank ``rank`` of ``nranks`` (one thread per rank, shared GPU):
         the multi-rank path with device-to-device copies in place of RCCL."""
@@ -134,11 +248,15 @@ class Context:
 
     def empty(self, n: int):
         """Allocate on the context's stream (torch's caching allocator is stream-aware)."""
+        if self.native:
+            return DeviceVector(self, n)
         torch = _torch()
         with torch.cuda.stream(self.stream):
             return torch.empty(int(n), dtype=torch.float64, device=self.torch_device)
 
     def zeros(self, n: int):
+        if self.native:
+            return DeviceVector(self, n).zero_()
         torch = _torch()
         with torch.cuda.stream(self.stream):
             return torch.zeros(int(n), dtype=torch.float64, device=self.torch_device)

@@ -149,6 +149,14 @@ SIGNATURES = {
     "amg_vector_uniform": (C.c_int, [_vp, _i64, _i64, C.c_uint64, _vp]),
     "amg_vector_copy": (C.c_int, [_vp, _i64, _vp, _vp]),
     "amg_vector_read": (C.c_int, [_vp, _i64, _vp, _vp, _i64]),
+    "amg_device_malloc": (C.c_int, [_vp, _i64, C.POINTER(_vp)]),
+    "amg_device_free": (C.c_int, [_vp, _vp]),
+    "amg_memcpy": (C.c_int, [_vp, _vp, _vp, _i64]),
+    "amg_memset_async": (C.c_int, [_vp, _vp, C.c_int, _i64]),
+    "amg_event_create": (C.c_int, [_vp, C.POINTER(_vp)]),
+    "amg_event_record": (C.c_int, [_vp]),
+    "amg_event_elapsed_ms": (C.c_int, [_vp, _vp, C.POINTER(C.c_float)]),
+    "amg_event_destroy": (C.c_int, [_vp]),
     "amg_host_hierarchy_build": (C.c_int, [C.c_int, C.c_int, ALLTOALLV_FN, _vp, _i64, _i64, _i64,
                                            _pi64, _pi64, _pf64, C.POINTER(Options),
                                            C.POINTER(_vp)]),

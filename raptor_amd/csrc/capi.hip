@@ -215,6 +215,7 @@ int amg_context_synchronize(amg_context ctx) {
         set_device(ctx->c);
         HIP_CHECK(hipStreamSynchronize(ctx->c.stream));
         HIP_CHECK(hipStreamSynchronize(ctx->c.comm_stream));
+        ctx->c.graph_inflight = false;
     });
 }
 
@@ -633,11 +634,7 @@ int amg_solver_set_graph(amg_solver S, int32_t enable) {
         std::string why;
         if (enable && S->s.ctx->host.nranks > 1) AMG_CHECK(Solver::rccl_graph_allowed(&why), why);
         S->s.use_graph = enable != 0;
-        for (auto& g : S->s.graphs)
-            if (g.exec) {
-                HIP_CHECK(hipGraphExecDestroy(g.exec));
-                g.exec = nullptr;
-            }
+        S->s.destroy_graphs();
     });
 }
 
@@ -848,6 +845,93 @@ int amg_vector_read(amg_context ctx, int64_t n, const double* src, double* parti
         AMG_CHECK(n_partials >= read_partials(n), "read: too few partial slots");
         set_device(ctx->c);
         launch_read(ctx->c.stream, n, src, partials);
+    });
+}
+
+int amg_device_malloc(amg_context ctx, int64_t bytes, void** out) {
+    return guard([&] {
+        AMG_CHECK(ctx && out && bytes >= 0, "bad argument");
+        set_device(ctx->c);
+        *out = nullptr;
+        if (bytes == 0) return;
+        const hipError_t e = hipMalloc(out, (size_t)bytes);
+        if (e == hipErrorOutOfMemory) {
+            (void)hipGetLastError();
+            throw Error(AMG_ERR_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes: out of device memory");
+        }
+        HIP_CHECK(e);
+    });
+}
+
+int amg_device_free(amg_context ctx, void* p) {
+    return guard([&] {
+        AMG_CHECK(ctx, "null context");
+        if (!p) return;
+        set_device(ctx->c);
+        HIP_CHECK(hipStreamSynchronize(ctx->c.stream));
+        HIP_CHECK(hipFree(p));
+    });
+}
+
+int amg_memcpy(amg_context ctx, void* dst, const void* src, int64_t bytes) {
+    return guard([&] {
+        AMG_CHECK(ctx && bytes >= 0, "bad argument");
+        if (bytes == 0) return;
+        AMG_CHECK(dst && src, "null pointer");
+        set_device(ctx->c);
+        HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, ctx->c.stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->c.stream));
+    });
+}
+
+int amg_memset_async(amg_context ctx, void* p, int value, int64_t bytes) {
+    return guard([&] {
+        AMG_CHECK(ctx && bytes >= 0, "bad argument");
+        if (bytes == 0) return;
+        AMG_CHECK(p, "null pointer");
+        set_device(ctx->c);
+        HIP_CHECK(hipMemsetAsync(p, value, (size_t)bytes, ctx->c.stream));
+    });
+}
+
+struct amg_event_s {
+    amg_context ctx = nullptr;
+    hipEvent_t e = nullptr;
+};
+
+int amg_event_create(amg_context ctx, amg_event* out) {
+    return guard([&] {
+        AMG_CHECK(ctx && out, "null argument");
+        set_device(ctx->c);
+        std::unique_ptr<amg_event_s> ev(new amg_event_s());
+        ev->ctx = ctx;
+        HIP_CHECK(hipEventCreate(&ev->e));
+        *out = ev.release();
+    });
+}
+
+int amg_event_record(amg_event e) {
+    return guard([&] {
+        AMG_CHECK(e, "null event");
+        set_device(e->ctx->c);
+        HIP_CHECK(hipEventRecord(e->e, e->ctx->c.stream));
+    });
+}
+
+int amg_event_elapsed_ms(amg_event start, amg_event end, float* ms) {
+    return guard([&] {
+        AMG_CHECK(start && end && ms, "null argument");
+        set_device(end->ctx->c);
+        HIP_CHECK(hipEventSynchronize(end->e));
+        HIP_CHECK(hipEventElapsedTime(ms, start->e, end->e));
+    });
+}
+
+int amg_event_destroy(amg_event e) {
+    return guard([&] {
+        if (!e) return;
+        (void)hipEventDestroy(e->e);
+        delete e;
     });
 }
 

@@ -140,6 +140,14 @@ struct Context {
     std::shared_ptr<LoopbackWorld> lb;
     void* lb_user = nullptr;  // host-exchange callback state for the loopback world
     int64_t mat_seq = 0;      // collective creation counter: matches matrices across ranks
+    // RCCL ordering between graph-launched and eager work on this communicator:
+    // `capturing` while a V-cycle is captured; `graph_inflight` from a multi-rank replay until
+    // the stream is known idle.  An eager RCCL enqueue while a replay's RCCL work is in flight
+    // deadlocks on RCCL's proxy (profiles/r4_rccl_graph_probe.txt), so eager_rccl_fence()
+    // waits for the replays first -- once per graph -> eager transition, not per cycle.
+    bool capturing = false;
+    bool graph_inflight = false;
+    void eager_rccl_fence();
     ~Context();
     // recv[q*count ..] = rank q's send[0..count) for every q (device pointers, on `stream`)
     void allgather(const double* send, double* recv, size_t count);
@@ -469,13 +477,26 @@ struct Solver {
         const double* x = nullptr;
         const double* b = nullptr;
         int64_t fmt_gen = -1;
-    } graphs[2];  // [0] plain cycle, [1] cycle that also appends ||b - A x_in||
+    } graphs[3];  // [0] plain cycle, [1] cycle that also appends ||b - A x_in||, [2] the
+                  // residual norm alone (solve's last norm)
+    enum { G_CYCLE = 0, G_CYCLE_NORM = 1, G_NORM = 2 };
+    // the graph in `slot` captured for (x, b) -- recaptured by `body` when stale.  Multi-rank
+    // with `agree`: the ranks decide together (host allgather of the stale flags, then of the
+    // capture / instantiate status), so no rank captures while a peer replays.  false: the
+    // solver fell back to eager cycles (every rank, together).
+    bool graph_ready(int slot, const double* x, const double* b, const std::function<void()>& body,
+                     bool agree);
+    void graph_launch(int slot);
+    void destroy_graphs();
 
     DevMatrix& Amat(size_t l) { return l == 0 ? *A0 : *levels[l].A; }
     void setup(DevMatrix& A, const amg_options& o);
     // one V-cycle; with_norm: the first level-0 Jacobi sweep also appends ||b - A x_in||
-    // to the device history (falls back to a separate residual when it cannot)
-    void cycle(double* x, const double* b, bool with_norm = false);
+    // to the device history (falls back to a separate residual when it cannot).  agree: the
+    // multi-rank graph decision is collective (false only where the caller made it already)
+    void cycle(double* x, const double* b, bool with_norm = false, bool agree = true);
+    // ||b - A x|| appended to the device history (the norm graph where graphs are on)
+    void residual_norm(double* x, const double* b, bool agree);
     // x0_in_t: level l's first pre-sweep from x = 0 already sits in levels[l].t (fused into
     // the restriction above, par_restrict_j0)
     void cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool with_norm, bool x0_in_t = false);

@@ -181,8 +181,26 @@ void loopback_before_pack(Context& c, const std::vector<int>& send_procs) {
     for (int q : send_procs) HIP_CHECK(hipStreamWaitEvent(c.stream, W.ev_done[q], 0));
 }
 
+// Graph-launched and eager RCCL work on one communicator: an eager group or
+// allgather enqueued while replayed groups are still in flight never completed on ROCm 7.2's
+// RCCL (profiles/r4_rccl_graph_probe.txt), so the first eager RCCL enqueue after replays waits
+// for them.  AMG_RCCL_EAGER_FENCE=0 drops the wait (the probe that reproduces the hang).
+void Context::eager_rccl_fence() {
+    if (!graph_inflight || capturing) return;
+    static const bool on = [] {
+        const char* e = std::getenv("AMG_RCCL_EAGER_FENCE");
+        return !(e && *e && std::atoi(e) == 0);
+    }();
+    graph_inflight = false;
+    if (!on) return;
+    static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
+    if (trace) std::fprintf(stderr, "[amg] rank %d eager fence (waiting for replays)\n", host.rank);
+    HIP_CHECK(hipStreamSynchronize(stream));
+}
+
 void Context::allgather(const double* send, double* recv, size_t count) {
     if (transport == TR_RCCL) {
+        eager_rccl_fence();
         static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
         if (trace) std::fprintf(stderr, "[amg] rank %d allgather %zu\n", host.rank, count);
         NCCL_CHECK(ncclAllGather(send, recv, count, ncclDouble, nccl, stream));

@@ -281,11 +281,8 @@ void Solver::ensure_hist(int32_t n) {
     if (hist.n >= (size_t)n) return;
     hist.alloc((size_t)n);
     sink.hist = hist.p;
-    for (auto& g : graphs)  // captured graphs baked the old pointer
-        if (g.exec) {
-            HIP_CHECK(hipGraphExecDestroy(g.exec));
-            g.exec = nullptr;
-        }
+    destroy_graphs();  // captured graphs baked the old pointer (collective: every rank's solve
+                       // sizes the history from the same max_iter)
 }
 
 // Hybrid GS sweeps forward before the coarse correction and backward after it (post):
@@ -395,75 +392,125 @@ bool Solver::can_fuse_norm() const {
            opt.pre_sweeps >= 1 && levels.size() >= 2;
 }
 
-void Solver::cycle(double* x, const double* b, bool with_norm) {
+void Solver::destroy_graphs() {
+    for (auto& g : graphs)
+        if (g.exec) {
+            HIP_CHECK(hipGraphExecDestroy(g.exec));
+            g.exec = nullptr;
+        }
+}
+
+// Capture `body` (enqueues on ctx->stream, RCCL groups included) into graphs[slot] unless the
+// graph for (x, b) and the current formats exists.  Multi-rank, the decision is collective:
+//  1. with `agree`, every rank's stale flag goes through the host exchange and all ranks
+//     recapture if any must (a caching allocator handing x a new address on one rank only
+//     would otherwise leave that rank capturing -- and waiting in the host exchange below --
+//     while its peers replay RCCL groups it never joins);
+//  2. the capture + instantiate status is exchanged: one rank's failure sends every rank to
+//     eager launches (an exception during capture raises on every rank).
+bool Solver::graph_ready(int slot, const double* x, const double* b, const std::function<void()>& body,
+                         bool agree) {
+    Graph& G = graphs[slot];
+    const HostComm& comm = ctx->host;
+    const bool multi = comm.nranks > 1;
+    bool stale = !G.exec || G.x != x || G.b != b || G.fmt_gen != DevMatrix::format_generation;
+    if (multi && agree) {
+        bool any = false;
+        for (int64_t v : comm.allgather((int64_t)(stale ? 1 : 0))) any = any || v != 0;
+        stale = any;
+    }
+    if (!stale) return true;
+    if (G.exec) HIP_CHECK(hipGraphExecDestroy(G.exec));
+    G.exec = nullptr;
+    hipStream_t s = ctx->stream;
+    static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
+    if (trace) std::fprintf(stderr, "[amg] rank %d capture begin (slot %d)\n", comm.rank, slot);
+    RoctxRange r("cycle: hipGraph capture");
+    install_crash_handler();
+    // a capture starts from an idle stream: RCCL work of earlier replays still in flight
+    // stays ordered before the captured groups by the stream, and nothing eager is pending
+    if (multi) ctx->eager_rccl_fence();
+    hipGraph_t g = nullptr;
+    std::string err;
+    HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    ctx->capturing = true;
+    try {
+        body();
+    } catch (const std::exception& e) {
+        err = e.what();
+    }
+    ctx->capturing = false;
+    const hipError_t ce = hipStreamEndCapture(s, &g);
+    if (ce != hipSuccess && err.empty()) err = std::string("hipStreamEndCapture: ") + hipGetErrorString(ce);
+    if (trace) std::fprintf(stderr, "[amg] rank %d capture end\n", comm.rank);
+    hipError_t ie = hipErrorUnknown;
+    if (err.empty() && g) ie = hipGraphInstantiate(&G.exec, g, nullptr, nullptr, 0);
+    if (g) (void)hipGraphDestroy(g);
+    if (ie != hipSuccess) {
+        (void)hipGetLastError();
+        G.exec = nullptr;
+    }
+    // 1 = ready, 0 = instantiate refused, -1 = the capture itself failed
+    const int64_t mine = !err.empty() ? -1 : ie == hipSuccess ? 1 : 0;
+    int64_t worst = mine;
+    if (multi)
+        for (int64_t v : comm.allgather(mine)) worst = std::min(worst, v);
+    if (worst == -1) {
+        destroy_graphs();
+        use_graph = false;
+        throw Error(AMG_ERR_INTERNAL, "V-cycle capture failed" + (err.empty() ? std::string(" on another rank")
+                                                                          : ": " + err));
+    }
+    if (worst == 0) {
+        // a graph some rank's runtime cannot instantiate: every rank runs eagerly from now on
+        // (identical results; only the launch overhead differs)
+        AMG_CHECK(multi, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+        destroy_graphs();
+        use_graph = false;
+        return false;
+    }
+    G.x = x;
+    G.b = b;
+    G.fmt_gen = DevMatrix::format_generation;
+    return true;
+}
+
+void Solver::graph_launch(int slot) {
+    RoctxRange r("cycle: hipGraph replay");
+    HIP_CHECK(hipGraphLaunch(graphs[slot].exec, ctx->stream));
+    static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
+    if (trace) std::fprintf(stderr, "[amg] rank %d graph launched (slot %d)\n", ctx->host.rank, slot);
+    // no host wait: the next replay orders behind this one on the stream, and the next eager
+    // RCCL enqueue waits once (Context::eager_rccl_fence)
+    if (ctx->host.nranks > 1) ctx->graph_inflight = true;
+}
+
+void Solver::cycle(double* x, const double* b, bool with_norm, bool agree) {
     AMG_ASSERT(!with_norm || can_fuse_norm());
-    if (!use_graph) {
-        RoctxRange r("cycle: eager");
-        cycle_rec(0, x, b, false, with_norm);
+    const int slot = with_norm ? G_CYCLE_NORM : G_CYCLE;
+    if (use_graph && graph_ready(slot, x, b, [&] { cycle_rec(0, x, b, false, with_norm); }, agree)) {
+        graph_launch(slot);
         return;
     }
-    hipStream_t s = ctx->stream;
-    Graph& G = graphs[with_norm ? 1 : 0];
-    if (!G.exec || G.x != x || G.b != b || G.fmt_gen != DevMatrix::format_generation) {
-        if (G.exec) HIP_CHECK(hipGraphExecDestroy(G.exec));
-        G.exec = nullptr;
-        hipGraph_t g = nullptr;
-        RoctxRange r("cycle: hipGraph capture");
-        static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
-        if (trace) std::fprintf(stderr, "[amg] rank %d capture begin\n", ctx->host.rank);
-        install_crash_handler();
-        // AMG_CAPTURE_MODE=global|relaxed: other capture modes (experiments; default thread-local)
-        static const hipStreamCaptureMode mode = [] {
-            const char* e = std::getenv("AMG_CAPTURE_MODE");
-            if (e && std::string(e) == "global") return hipStreamCaptureModeGlobal;
-            if (e && std::string(e) == "relaxed") return hipStreamCaptureModeRelaxed;
-            return hipStreamCaptureModeThreadLocal;
-        }();
-        HIP_CHECK(hipStreamBeginCapture(s, mode));
-        try {
-            cycle_rec(0, x, b, false, with_norm);
-        } catch (...) {
-            (void)hipStreamEndCapture(s, &g);
-            if (g) (void)hipGraphDestroy(g);
-            throw;
-        }
-        HIP_CHECK(hipStreamEndCapture(s, &g));
-        if (trace) std::fprintf(stderr, "[amg] rank %d capture end\n", ctx->host.rank);
-        const hipError_t ie = hipGraphInstantiate(&G.exec, g, nullptr, nullptr, 0);
-        HIP_CHECK(hipGraphDestroy(g));
-        if (ie != hipSuccess) (void)hipGetLastError();
-        AMG_CHECK(ie == hipSuccess || ctx->host.nranks > 1,
-                  std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
-        // multi-rank: the ranks decide together (host exchange), so no rank replays a graph
-        // whose RCCL groups a peer runs eagerly
-        bool all_ok = ie == hipSuccess;
-        if (ctx->host.nranks > 1)
-            for (int64_t v : ctx->host.allgather((int64_t)(ie == hipSuccess ? 1 : 0))) all_ok = all_ok && v == 1;
-        if (!all_ok) {
-            // a multi-rank graph some rank's runtime cannot instantiate: replay nothing, run
-            // eagerly from now on (identical results; only the launch overhead differs)
-            if (G.exec) (void)hipGraphExecDestroy(G.exec);
-            G.exec = nullptr;
-            use_graph = false;
-            cycle_rec(0, x, b, false, with_norm);
-            return;
-        }
-        G.x = x;
-        G.b = b;
-        G.fmt_gen = DevMatrix::format_generation;
-    }
-    RoctxRange r("cycle: hipGraph replay");
-    HIP_CHECK(hipGraphLaunch(G.exec, s));
-    static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
-    if (trace) std::fprintf(stderr, "[amg] rank %d graph launched\n", ctx->host.rank);
-    // a multi-rank replay completes before anything else is enqueued: replays queued back to
-    // back and followed by eager RCCL work never finished on the socket transport (the ROCm 7.2
-    // probes); one host wait per cycle.  AMG_RCCL_GRAPH_SYNC=0: no wait (probes)
-    static const bool sync_replay = [] {
-        const char* e = std::getenv("AMG_RCCL_GRAPH_SYNC");
+    RoctxRange r("cycle: eager");
+    cycle_rec(0, x, b, false, with_norm);
+}
+
+void Solver::residual_norm(double* x, const double* b, bool agree) {
+    DevMatrix& A = *A0;
+    double* r = levels[0].r.p;
+    // AMG_RCCL_NORM_GRAPH=0: the norm eager after graph-replayed cycles (probe of the eager
+    // fence)
+    static const bool norm_graph = [] {
+        const char* e = std::getenv("AMG_RCCL_NORM_GRAPH");
         return !(e && *e && std::atoi(e) == 0);
     }();
-    if (sync_replay && ctx->host.nranks > 1) HIP_CHECK(hipStreamSynchronize(s));
+    if (use_graph && (norm_graph || ctx->host.nranks == 1) &&
+        graph_ready(G_NORM, x, b, [&] { par_residual_norm(A, x, b, r, sink); }, agree)) {
+        graph_launch(G_NORM);
+        return;
+    }
+    par_residual_norm(A, x, b, r, sink);
 }
 
 int32_t Solver::solve(double* x, const double* b, int32_t max_iter, double tol, double* hist_host) {
@@ -471,30 +518,33 @@ int32_t Solver::solve(double* x, const double* b, int32_t max_iter, double tol, 
     RoctxRange range("ParMultilevel::solve");
     hipStream_t s = ctx->stream;
     ensure_hist(max_iter + 1);
+    if (ctx->host.nranks > 1) ctx->eager_rccl_fence();
     HIP_CHECK(hipMemsetAsync(hist_counter.p, 0, sizeof(int), s));
-    DevMatrix& A = *A0;
-    double* r = levels[0].r.p;
     int32_t it = 0;
+    // one collective graph decision per solve (x and b stay put for its cycles)
     if (tol <= 0.0 && can_fuse_norm()) {
         // ||b - A x_k|| comes out of cycle k+1's first Jacobi sweep (same b - Ax values);
-        // only the last norm needs its own residual pass.  No host sync in the loop.
-        for (; it < max_iter; ++it) cycle(x, b, true);
-        par_residual_norm(A, x, b, r, sink);
+        // only the last norm needs its own residual pass.  No host sync in the loop, and with
+        // graphs on, no eager work at all: cycles and the last norm replay captured graphs.
+        for (; it < max_iter; ++it) cycle(x, b, true, it == 0);
+        residual_norm(x, b, max_iter == 0);
     } else {
-        par_residual_norm(A, x, b, r, sink);
+        residual_norm(x, b, true);
         double r0 = 0.0;
         if (tol > 0.0) {
             HIP_CHECK(hipMemcpyAsync(&r0, hist.p, sizeof(double), hipMemcpyDeviceToHost, s));
             HIP_CHECK(hipStreamSynchronize(s));
+            ctx->graph_inflight = false;
         }
         while (it < max_iter) {
-            cycle(x, b, false);
-            par_residual_norm(A, x, b, r, sink);
+            cycle(x, b, false, it == 0);
+            residual_norm(x, b, false);
             ++it;
             if (tol > 0.0) {
                 double rn = 0.0;
                 HIP_CHECK(hipMemcpyAsync(&rn, hist.p + it, sizeof(double), hipMemcpyDeviceToHost, s));
                 HIP_CHECK(hipStreamSynchronize(s));
+                ctx->graph_inflight = false;
                 if (r0 > 0.0 && rn / r0 < tol) break;
             }
         }
@@ -502,6 +552,7 @@ int32_t Solver::solve(double* x, const double* b, int32_t max_iter, double tol, 
     HIP_CHECK(hipMemcpyAsync(hist_host, hist.p, sizeof(double) * (size_t)(it + 1),
                              hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    ctx->graph_inflight = false;
     return it;
 }
 
@@ -549,9 +600,11 @@ int32_t Solver::pcg(double* x, const double* b, int32_t max_iter, double tol, do
         dot(r, r, sc + SC_RN, true);
         launch_append(s, sc + SC_RN, hist.p, hist_counter.p);
     };
+    bool first = true;
     auto precondition = [&] {  // z = M^-1 r: one V-cycle from z = 0
         launch_zero(s, n, z);
-        cycle(z, r, false);
+        cycle(z, r, false, first);  // z, r stay put: one collective graph decision per pcg
+        first = false;
     };
     par_apply(A, KM_RESID, x, b, r, 0.0, nullptr);
     record_norm();
@@ -585,6 +638,7 @@ int32_t Solver::pcg(double* x, const double* b, int32_t max_iter, double tol, do
     HIP_CHECK(hipMemcpyAsync(hist_host, hist.p, sizeof(double) * (size_t)(it + 1),
                              hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    ctx->graph_inflight = false;
     return it;
 }
 

@@ -1516,6 +1516,7 @@ bool DevMatrix::halo_begin(const double* x) {
         return true;
     }
     if (plan.send_idx.empty() && plan.halo_gid.empty()) return false;
+    ctx->eager_rccl_fence();
     static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
     if (trace) std::fprintf(stderr, "[amg] rank %d halo_begin seq %lld send %zu recv %lld\n", comm.rank,
                             (long long)seq, plan.send_idx.size(), (long long)plan.n_halo());

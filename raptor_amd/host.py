@@ -2,7 +2,7 @@
 
 This is the exact setup code ``ParMultilevel.setup`` runs before uploading the hierarchy to
 the GPU, callable without a GPU so the CPU test suite can check
-it -- serial and multi-rank over gloo -- bit for bit against the oracle."""
+it -- serial and multi-rank over gloo or a ``SocketComm`` -- bit for bit against the oracle."""
 from __future__ import annotations
 
 import ctypes as C
@@ -16,6 +16,17 @@ _WHICH = {"A": 0, "P": 1, "R": 2}
 _NULL_FN = ALLTOALLV_FN()
 
 
+def _exchange(group, nranks):
+    """The setup exchange over `group`: a SocketComm (torch-free) or a torch.distributed group."""
+    from ._sockcomm import SocketComm
+
+    if isinstance(group, SocketComm):
+        return group.exchange_fn()
+    from ._comm import make_exchange
+
+    return make_exchange(group, nranks)
+
+
 class HostHierarchy:
     def __init__(self, n_global, first_row, row_ptr, col, val, options: Options, rank=0,
                  nranks=1, group=None):
@@ -24,9 +35,7 @@ class HostHierarchy:
         v = np.ascontiguousarray(val, np.float64)
         fn = _NULL_FN
         if nranks > 1:
-            from ._comm import make_exchange
-
-            fn = make_exchange(group, nranks)
+            fn = _exchange(group, nranks)
         self._fn = fn
         self.rank = rank
         self.h = C.c_void_p()
@@ -102,9 +111,7 @@ class HostCSR:
     def _fn(self):
         if self.nranks == 1:
             return _NULL_FN
-        from ._comm import make_exchange
-
-        self._keep = make_exchange(self.group, self.nranks)
+        self._keep = _exchange(self.group, self.nranks)
         return self._keep
 
     @classmethod

@@ -4,7 +4,7 @@
 //
 //   cxx_driver solve  <golden.txt>          7-pt 24^3, PMIS + Jacobi, 1 rank: ParMultilevel::
 //                                           solve history vs the committed oracle history
-//   cxx_driver errors                       C-ABI error codes surface as amg::Error
+//   cxx_driver errors                       C-ABI error codes surface as raptor_amd::Error
 //   cxx_driver ranks N [graph] <golden.txt> the same solve on N processes (fork), RCCL halo
 //                                           exchange; "graph": hipGraph-captured cycles
 //
@@ -18,6 +18,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -71,10 +72,10 @@ bool compare(const std::vector<double>& h, const std::vector<double>& g, const c
 }
 
 // one rank: 7-pt 24^3 slab, b = A x*, x0 = 0, 10 V-cycles; returns the history
-std::vector<double> solve_7pt(amg::Context& ctx, bool graph, int* levels, bool* graph_used) {
-    amg::ParCSRMatrix A = amg::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 24, 24, 24);
+std::vector<double> solve_7pt(raptor_amd::Context& ctx, bool graph, int* levels, bool* graph_used) {
+    raptor_amd::ParCSRMatrix A = raptor_amd::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 24, 24, 24);
     const int64_t n = A.local_rows(), f = A.first_row();
-    amg::ParMultilevel ml(A, amg::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
+    raptor_amd::ParMultilevel ml(A, raptor_amd::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
     ml.set_graph(graph);  // multi-rank default: on where the runtime is validated (ROCm 7.2)
     const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
     if (trace) std::fprintf(stderr, "[cxx] rows %lld setup done (%d levels)\n", (long long)n, ml.num_levels());
@@ -99,7 +100,7 @@ std::vector<double> solve_7pt(amg::Context& ctx, bool graph, int* levels, bool* 
 
 int run_solve(const char* golden) {
     const std::vector<double> g = read_golden(golden);
-    amg::Context ctx(0);
+    raptor_amd::Context ctx(0);
     int levels = 0;
     bool used = false;
     const std::vector<double> h = solve_7pt(ctx, true, &levels, &used);
@@ -112,16 +113,16 @@ int run_solve(const char* golden) {
 }
 
 int run_errors() {
-    amg::Context ctx(0);
+    raptor_amd::Context ctx(0);
     int fails = 0;
     // row_ptr[0] != 0 is rejected with AMG_ERR_INVALID, the message naming the problem
     const int64_t rp[3] = {1, 2, 3}, col[3] = {0, 1, 0};
     const double val[3] = {1.0, 1.0, 1.0};
     try {
-        amg::ParCSRMatrix bad(ctx, 2, 0, 2, rp, col, val);
+        raptor_amd::ParCSRMatrix bad(ctx, 2, 0, 2, rp, col, val);
         std::fprintf(stderr, "bad row_ptr accepted\n");
         ++fails;
-    } catch (const amg::Error& e) {
+    } catch (const raptor_amd::Error& e) {
         if (e.code() != AMG_ERR_INVALID || std::string(e.what()).find("row_ptr") == std::string::npos) {
             std::fprintf(stderr, "unexpected error %d: %s\n", e.code(), e.what());
             ++fails;
@@ -130,16 +131,16 @@ int run_errors() {
     // duplicate column in a row
     const int64_t rp2[3] = {0, 2, 3}, col2[3] = {1, 1, 1};
     try {
-        amg::ParCSRMatrix bad(ctx, 2, 0, 2, rp2, col2, val);
+        raptor_amd::ParCSRMatrix bad(ctx, 2, 0, 2, rp2, col2, val);
         std::fprintf(stderr, "duplicate column accepted\n");
         ++fails;
-    } catch (const amg::Error& e) {
+    } catch (const raptor_amd::Error& e) {
         if (e.code() != AMG_ERR_INVALID) ++fails;
     }
     // a valid 2x2 matrix: y = A x
     const int64_t rp3[3] = {0, 2, 4}, col3[4] = {0, 1, 0, 1};
     const double val3[4] = {2.0, -1.0, -1.0, 2.0};
-    amg::ParCSRMatrix A(ctx, 2, 0, 2, rp3, col3, val3);
+    raptor_amd::ParCSRMatrix A(ctx, 2, 0, 2, rp3, col3, val3);
     double hx[2] = {1.0, 3.0}, hy[2] = {0.0, 0.0};
     double *dx = nullptr, *dy = nullptr;
     HIPOK(hipMalloc(&dx, sizeof hx));
@@ -216,11 +217,11 @@ int mesh_alltoallv(void* user, const void* sendbuf, const int64_t* send_bytes, v
 // AMG_CXX_GRAPH_MULT=3: V-cycles replayed from a captured graph, synchronised after each,
 // against the same cycles run eagerly by a second solver on the same matrix;
 // AMG_CXX_GRAPH_MULT=4: the same, the replays enqueued back to back (one synchronisation)
-std::vector<double> graph_cycles(amg::Context& ctx, bool sync_each) {
-    amg::ParCSRMatrix A = amg::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 24, 24, 24);
+std::vector<double> graph_cycles(raptor_amd::Context& ctx, bool sync_each) {
+    raptor_amd::ParCSRMatrix A = raptor_amd::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 24, 24, 24);
     const int64_t n = A.local_rows(), f = A.first_row();
-    amg::ParMultilevel mg(A, amg::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
-    amg::ParMultilevel me(A, amg::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
+    raptor_amd::ParMultilevel mg(A, raptor_amd::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
+    raptor_amd::ParMultilevel me(A, raptor_amd::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
     mg.set_graph(true);
     me.set_graph(false);
     double *xs = nullptr, *b = nullptr, *xg = nullptr, *xe = nullptr;
@@ -252,8 +253,40 @@ std::vector<double> graph_cycles(amg::Context& ctx, bool sync_each) {
     return {hg == he && mg.graph() ? 1.0 : 0.0};
 }
 
-std::vector<double> graph_mult(amg::Context& ctx) {
-    amg::ParCSRMatrix A = amg::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 24, 24, 24);
+// AMG_CXX_GRAPH_MULT=5 (probe of the graph -> eager hand-off): 10 captured
+// V-cycles replayed back to back, no host wait, then (after AMG_CXX_PROBE_SLEEP_MS of host
+// sleep, default 0) an eager ParCSRMatrix residual norm -- a halo send/recv group on the comm
+// stream and an allgather on the compute stream.  With AMG_RCCL_EAGER_FENCE=0 the library does
+// not wait for the replays before that eager RCCL work.  Returns {1.0} when the norm equals an
+// eager solver's on the same iterate.
+std::vector<double> graph_then_eager(raptor_amd::Context& ctx) {
+    raptor_amd::ParCSRMatrix A = raptor_amd::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 24, 24, 24);
+    const int64_t n = A.local_rows(), f = A.first_row();
+    raptor_amd::ParMultilevel mg(A, raptor_amd::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
+    raptor_amd::ParMultilevel me(A, raptor_amd::ParMultilevel::options(AMG_PRESET_PMIS_JACOBI));
+    mg.set_graph(true);
+    me.set_graph(false);
+    double *xs = nullptr, *b = nullptr, *xg = nullptr, *xe = nullptr;
+    for (double** p : {&xs, &b, &xg, &xe}) HIPOK(hipMalloc(p, n * sizeof(double)));
+    ctx.uniform(n, f, 42, xs);
+    A.mult(xs, b);
+    HIPOK(hipMemsetAsync(xg, 0, n * sizeof(double), (hipStream_t)ctx.stream()));
+    HIPOK(hipMemsetAsync(xe, 0, n * sizeof(double), (hipStream_t)ctx.stream()));
+    for (int k = 0; k < 10; ++k) me.cycle(xe, b);
+    const double ne = A.residual_norm(xe, b);  // synchronises
+    std::fprintf(stderr, "[cxx] eager cycles done, norm %.17g\n", ne);
+    for (int k = 0; k < 10; ++k) mg.cycle(xg, b);
+    std::fprintf(stderr, "[cxx] 10 replays enqueued (graph %d)\n", (int)mg.graph());
+    const char* sl = std::getenv("AMG_CXX_PROBE_SLEEP_MS");
+    if (sl) std::this_thread::sleep_for(std::chrono::milliseconds(std::atoi(sl)));
+    const double ng = A.residual_norm(xg, b);
+    std::fprintf(stderr, "[cxx] eager norm after replays: %.17g\n", ng);
+    for (double* p : {xs, b, xg, xe}) HIPOK(hipFree(p));
+    return {ng == ne && mg.graph() ? 1.0 : 0.0};
+}
+
+std::vector<double> graph_mult(raptor_amd::Context& ctx) {
+    raptor_amd::ParCSRMatrix A = raptor_amd::ParCSRMatrix::stencil(ctx, AMG_STENCIL_7PT, 24, 24, 24);
     const int64_t n = A.local_rows(), f = A.first_row();
     hipStream_t s = (hipStream_t)ctx.stream();
     double *x = nullptr, *y0 = nullptr, *y1 = nullptr;
@@ -294,10 +327,10 @@ int rank_main(Mesh& m, bool graph, const char* golden, int result_fd) {
     // transport), as in tests/test_gpu_rccl.py
     const std::string hostid = "raptor-amd-cxx-" + std::to_string(m.rank);
     setenv("NCCL_HOSTID", hostid.c_str(), 1);
-    amg::Context ctx(0);
+    raptor_amd::Context ctx(0);
     std::vector<char> id(128);
     if (m.rank == 0) {
-        id = amg::Context::rccl_unique_id();
+        id = raptor_amd::Context::rccl_unique_id();
         for (int q = 1; q < m.nranks; ++q)
             if (!write_all(m.fd[q], id.data(), 128)) return 4;
     } else if (!read_all(m.fd[0], id.data(), 128)) {
@@ -308,9 +341,11 @@ int rank_main(Mesh& m, bool graph, const char* golden, int result_fd) {
     bool used = false;
     const char* gmode = std::getenv("AMG_CXX_GRAPH_MULT");
     const bool gm = gmode != nullptr;
+    const int gmv = gm ? std::atoi(gmode) : 0;
     const std::vector<double> h = !gm ? solve_7pt(ctx, graph, &levels, &used)
-                                  : std::atoi(gmode) >= 3 ? graph_cycles(ctx, std::atoi(gmode) == 3)
-                                                          : graph_mult(ctx);
+                                  : gmv == 5 ? graph_then_eager(ctx)
+                                  : gmv >= 3 ? graph_cycles(ctx, gmv == 3)
+                                             : graph_mult(ctx);
     if (gm) used = graph;
     const int64_t cnt = (int64_t)h.size();
     const char flag = used ? 1 : 0;
@@ -351,7 +386,7 @@ int run_ranks(int nranks, bool graph, const char* golden) {
             int rc = 6;
             try {
                 rc = rank_main(m, graph, golden, p[1]);
-            } catch (const amg::Error& e) {
+            } catch (const raptor_amd::Error& e) {
                 std::fprintf(stderr, "rank %d: %s\n", r, e.what());
             }
             close(p[1]);

@@ -1,7 +1,7 @@
 """The boundary as BASELINE.json:5 words it -- "C++ host code calls HIP through a thin
 extern-"C" layer": tests/cxx/cxx_driver.cpp is a compiled C++ program over the header-only
 facade include/raptor_amd.hpp (RAII Context / ParCSRMatrix / ParMultilevel, C-ABI error codes
-as amg::Error).  No Python or torch runs in its process, so the library binds the ROCm HIP
+as raptor_amd::Error).  No Python or torch runs in its process, so the library binds the ROCm HIP
 runtime and RCCL it was built against (tests/test_gpu_rccl.py runs under torch's bundled
 copies).  Its solve history must equal the oracle's (tests/golden/cxx_7pt24_hist.txt, made by
 tests/golden/gen_cxx_golden.py) within 1e-10 relative."""

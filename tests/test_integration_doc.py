@@ -28,7 +28,7 @@ def test_integration_c_example_compiles(tmp_path):
 
 def test_cxx_header_compiles_standalone(tmp_path):
     src = tmp_path / "facade.cpp"
-    src.write_text('#include "raptor_amd.hpp"\nint main() { return amg::ParMultilevel::options == nullptr; }\n')
+    src.write_text('#include "raptor_amd.hpp"\nint main() { return raptor_amd::ParMultilevel::options == nullptr; }\n')
     r = subprocess.run(["g++", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-fsyntax-only",
                         "-I", os.path.join(ROOT, "include"), str(src)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
