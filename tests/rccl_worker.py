@@ -1,7 +1,9 @@
 """One rank of tests/test_gpu_rccl.py: the product's RCCL transport, one process per rank.
 
 Launched by the test as a child process (never imported by it) with RANK / WORLD_SIZE /
-MASTER_* set.  Every rank joins a gloo group (setup-time exchange) and an RCCL communicator
+MASTER_* set.  spec["native"]: torch-free (raptor_amd.Context.native over a SocketComm, the
+bench's own form, on ROCm's HIP / RCCL); otherwise torch's gloo group and torch's bundled
+runtime.  Every rank joins the host exchange (setup) and an RCCL communicator
 (solve-time halo exchange, norm and coarse allgathers), runs the level kernels and a few
 V-cycles on its z-slab, and writes its slices to ``<out>.<rank>.npz``.  The parent compares
 them with the serial oracle: this is the path the bench takes for --gpus N > 1.
@@ -24,27 +26,56 @@ def main():
     out = sys.argv[2]
     sys.path.insert(0, ROOT)
     import numpy as np
-    import torch
-    import torch.distributed as dist
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
-    import raptor_amd as ra
+    native = bool(spec.get("native"))
+    if native:
+        # torch-free: the library binds ROCm's HIP runtime and RCCL; the ranks
+        # meet over raptor_amd.SocketComm, vectors are C-ABI device buffers
+        import raptor_amd as ra
 
-    ctx = ra.Context.distributed(0)
-    A = ra.par_stencil_grid(ctx, spec["kind"], spec["dims"])
+        comm = ra.SocketComm(rank, world)
+        ctx = ra.Context.native(0, comm=comm)
+
+        def host(t):
+            ctx.synchronize()
+            return t.numpy()
+
+        def barrier_and_close():
+            comm.barrier()
+            comm.close()
+
+        def zero(t):
+            t.zero_()
+    else:
+        import torch
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        import raptor_amd as ra
+
+        ctx = ra.Context.distributed(0)
+
+        def host(t):
+            ctx.synchronize()
+            return t.detach().cpu().numpy().copy()
+
+        def barrier_and_close():
+            dist.barrier()
+            dist.destroy_process_group()
+
+        def zero(t):
+            with torch.cuda.stream(ctx.stream):
+                t.zero_()
+
+    A = ra.par_stencil_grid(ctx, spec["kind"], spec["dims"], boxes=spec.get("boxes"))
     f, m = A.first_row, A.local_rows
     res = {"f": f, "m": m, "n_halo": A.info["n_halo"]}
 
-    def host(t):
-        ctx.synchronize()
-        return t.detach().cpu().numpy().copy()
-
-    with torch.cuda.stream(ctx.stream):
-        x = ra.vector_uniform(ctx, m, f, 3)
-        b = ra.vector_uniform(ctx, m, f, 4)
-        y = ctx.empty(m)
+    x = ra.vector_uniform(ctx, m, f, 3)
+    b = ra.vector_uniform(ctx, m, f, 4)
+    y = ctx.empty(m)
     A.mult(x, y)
     res["y"] = host(y)
     A.residual(x, b, y)
@@ -64,14 +95,12 @@ def main():
             raise
         res["gate_error"] = str(e)
         np.savez(f"{out}.{rank}.npz", **res)
-        dist.barrier()
-        dist.destroy_process_group()
+        barrier_and_close()
         return
     res["levels"] = ml.num_levels
     res["starts"] = np.array([ml.level_matrix(l, "A").first_row for l in range(ml.num_levels)])
-    with torch.cuda.stream(ctx.stream):
-        xs = ra.vector_uniform(ctx, m, f, 42)
-        bb = ctx.empty(m)
+    xs = ra.vector_uniform(ctx, m, f, 42)
+    bb = ctx.empty(m)
     A.mult(xs, bb)
     dx = ctx.zeros(m)
     for k in range(3):
@@ -81,14 +110,21 @@ def main():
     _, hist = ml.solve(dx, bb, max_iter=6)
     res["hist"] = hist
     res["xsolve"] = host(dx)
+    # a second solve: rank 0 alone moves its x to a new buffer (the others reuse theirs), so
+    # only rank 0's captured graphs are stale -- the ranks must decide to recapture together
+    if rank == 0:
+        dx = ctx.zeros(m)
+    else:
+        zero(dx)
+    _, hist2 = ml.solve(dx, bb, max_iter=6)
+    res["hist2"] = hist2
     dx = ctx.zeros(m)
     _, hp = ml.pcg(dx, bb, max_iter=5)
     res["pcg"] = hp
     res["graph_used"] = ml.graph_enabled
     np.savez(f"{out}.{rank}.npz", **res)
-    dist.barrier()
     del ml, A
-    dist.destroy_process_group()
+    barrier_and_close()
 
 
 if __name__ == "__main__":

@@ -68,14 +68,41 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("graph", [False], ids=["eager"])
+# configs[3]'s partition (2 x 2 x 2 boxes, the grid numbered box by box) at 8 ranks, larger
+# than the slab cases above
+BOX_CASES = [
+    (8, dict(kind="7pt", dims=[64, 64, 128], boxes=[2, 2, 2], coarsen="pmis", smoother="jacobi", rep=65536)),
+    (8, dict(kind="27pt", dims=[32, 32, 48], boxes=[2, 2, 2], coarsen="sa", smoother="hybrid_gs", rep=65536)),
+]
+
+# torch: torch's gloo group and bundled HIP 7.0 / RCCL 2.26 (eager multi-rank cycles);
+# native: the torch-free form the bench runs (SocketComm, ROCm 7.2 HIP / RCCL), where every
+# rank captures whole cycles and the last norm into hipGraphs and replays them
+MODES = {"torch-eager": dict(native=False, graph=False), "native-graph": dict(native=True, graph=True)}
+
+
+@pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("nranks,spec", CASES,
                          ids=[f"{n}r-{s['kind']}-{s['coarsen']}-rep{s['rep']}" for n, s in CASES])
-def test_rccl_vcycle_bit_exact(oracle, tmp_path, nranks, spec, graph):
+def test_rccl_vcycle_bit_exact(oracle, tmp_path, nranks, spec, mode):
+    _check_vs_oracle(oracle, tmp_path, nranks, dict(spec, **MODES[mode]))
+
+
+@pytest.mark.parametrize("nranks,spec", BOX_CASES,
+                         ids=[f"{n}r-{s['kind']}-{'x'.join(map(str, s['dims']))}-boxes" for n, s in BOX_CASES])
+def test_rccl_boxes_native_graph_bit_exact(oracle, tmp_path, nranks, spec):
+    _check_vs_oracle(oracle, tmp_path, nranks, dict(spec, **MODES["native-graph"]))
+
+
+def _check_vs_oracle(oracle, tmp_path, nranks, spec):
     O = oracle
-    spec = dict(spec, graph=graph)
+    graph = spec["graph"]
     res = run_rccl(nranks, spec, tmp_path)
     Ao = {"7pt": O.gen_7pt, "27pt": O.gen_27pt}[spec["kind"]](*spec["dims"])
+    if spec.get("boxes"):
+        from raptor_amd import box_order
+
+        Ao = O.permute(Ao, box_order(spec["dims"], spec["boxes"]))
     n = Ao.shape[0]
     assert sum(int(r["m"]) for r in res) == n
     x, b = O.vec_uniform(n, 3), O.vec_uniform(n, 4)
@@ -107,7 +134,11 @@ def test_rccl_vcycle_bit_exact(oracle, tmp_path, nranks, spec, graph):
         assert np.all(np.abs(r["hist"] - hist_o) <= 1e-10 * hist_o)
         assert np.all(np.abs(r["pcg"] - pcg_o) <= 1e-9 * pcg_o[0])
         assert np.array_equal(r["hist"], res[0]["hist"])  # every rank reports the same
+        # the second solve (rank 0 alone on a new x buffer: a collective recapture) repeats it
+        assert np.array_equal(r["hist2"], r["hist"])
         assert bool(r["graph_used"]) == graph  # captured and replayed, no eager fallback
+        if spec.get("native"):  # the torch-free process runs ROCm's runtime, not torch's
+            assert _capture_validated(r), (int(r["hip_runtime"]), int(r["rccl"]))
 
 
 def _capture_validated(r):

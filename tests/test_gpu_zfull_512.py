@@ -7,7 +7,9 @@ the SpGEMM.  On one MI355X, with no scaling claim:
   * 8 loopback ranks (z-slabs of 64 planes), GPU setup on every rank (halo states of each
     round through the host exchange), the host's distributed transpose;
 and the two must agree: identical per-level global sizes and nonzero counts, and every rank's
-slice of the first V-cycle iterate bit-identical to the 1-rank iterate.  The plain-CSR A*1
+slice of the first V-cycle iterate bit-identical to the 1-rank iterate.  Twice: z-slabs of the
+natural numbering, and the partition bench.py --gpus 8 runs -- 2 x 2 x 2 boxes of 256^3, the
+grid numbered box by box (the 1-rank reference is the same box-numbered operator on one rank).  The plain-CSR A*1
 equals the integer row sums (the number of missing neighbours of each grid point), exactly.
 At this size no oracle runs (it would take the CPU minutes per cycle); the properties above are
 size-independent, and the same code is bit-exact against the oracle at the smaller sizes of
@@ -40,17 +42,19 @@ def boundary_faces(torch, n, dims, device):
     return faces.to(torch.float64)
 
 
-def test_512cubed_one_rank_vs_eight_loopback_ranks(capfd, monkeypatch):
+@pytest.mark.parametrize("partition", ["slabs", "boxes"])
+def test_512cubed_one_rank_vs_eight_loopback_ranks(capfd, monkeypatch, partition):
     import torch
 
     import raptor_amd as ra
 
     t_start = time.perf_counter()
-    report = {}
+    report = {"partition": partition}
+    boxes = (2, 2, 2) if partition == "boxes" else None
 
     def say(msg):
         with capfd.disabled():
-            print(f"[512^3 {time.perf_counter() - t_start:7.1f}s] {msg}", flush=True)
+            print(f"[512^3 {partition} {time.perf_counter() - t_start:7.1f}s] {msg}", flush=True)
 
     monkeypatch.setenv("AMG_LOOPBACK_TIMEOUT", "900")
     n = DIMS[0] * DIMS[1] * DIMS[2]
@@ -58,25 +62,26 @@ def test_512cubed_one_rank_vs_eight_loopback_ranks(capfd, monkeypatch):
     # ---- 1 rank, device setup -------------------------------------------------------------
     ctx = ra.Context(0)
     t = time.perf_counter()
-    A = ra.par_stencil_grid(ctx, "7pt", DIMS)
+    A = ra.par_stencil_grid(ctx, "7pt", DIMS, boxes=boxes)
     report["matrix_s"] = time.perf_counter() - t
     assert A.local_rows == n == 134217728
     assert A.nnz == 937951232
     say(f"1 rank: A built ({A.nnz} nnz) in {report['matrix_s']:.1f}s")
-    with torch.cuda.stream(ctx.stream):
-        ones = ctx.empty(n).fill_(1.0)
-        y = ctx.empty(n)
-    A.set_format("csr")  # plain int32 row_ptr / col: 938M entries
-    A.mult(ones, y)
-    ctx.synchronize()
-    faces = boundary_faces(torch, n, DIMS, ctx.torch_device)
-    assert torch.equal(y, faces), "plain-CSR A*1 differs from the integer row sums"
-    A.set_format("auto")  # row templates
-    A.mult(ones, y)
-    ctx.synchronize()
-    assert torch.equal(y, faces), "template-format A*1 differs from the integer row sums"
-    del faces, ones
-    say("A*1 = integer row sums (plain CSR and row templates)")
+    if boxes is None:  # (the face count below is written in the natural numbering)
+        with torch.cuda.stream(ctx.stream):
+            ones = ctx.empty(n).fill_(1.0)
+            y = ctx.empty(n)
+        A.set_format("csr")  # plain int32 row_ptr / col: 938M entries
+        A.mult(ones, y)
+        ctx.synchronize()
+        faces = boundary_faces(torch, n, DIMS, ctx.torch_device)
+        assert torch.equal(y, faces), "plain-CSR A*1 differs from the integer row sums"
+        A.set_format("auto")  # row templates
+        A.mult(ones, y)
+        ctx.synchronize()
+        assert torch.equal(y, faces), "template-format A*1 differs from the integer row sums"
+        del faces, ones, y
+        say("A*1 = integer row sums (plain CSR and row templates)")
 
     t = time.perf_counter()
     ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
@@ -100,19 +105,19 @@ def test_512cubed_one_rank_vs_eight_loopback_ranks(capfd, monkeypatch):
     assert rn1 < 0.5 * rn0
     report["rn0"], report["rn1"] = rn0, rn1
     say(f"1 rank: first V-cycle done, ||r1||/||r0|| = {rn1 / rn0:.4f}")
-    del ml, A, xs, b, x, y
+    del ml, A, xs, b, x
     ctx.synchronize()
     torch.cuda.empty_cache()
 
     # ---- 8 loopback ranks ------------------------------------------------------------------
-    world = "w512-" + uuid.uuid4().hex
+    world = f"w512{partition}-" + uuid.uuid4().hex
     out = [None] * NRANKS
     errs = [None] * NRANKS
 
     def rank(r):
         try:
             c = ra.Context.loopback(r, NRANKS, world)
-            Ar = ra.par_stencil_grid(c, "7pt", DIMS)
+            Ar = ra.par_stencil_grid(c, "7pt", DIMS, boxes=boxes)
             f, m = Ar.first_row, Ar.local_rows
             tr = time.perf_counter()
             mr = ra.ParRugeStubenSolver(coarsen="pmis").setup(Ar)
@@ -145,12 +150,13 @@ def test_512cubed_one_rank_vs_eight_loopback_ranks(capfd, monkeypatch):
     report["setup_8rank_s"] = max(o[4] for o in out)
     say(f"{NRANKS} ranks: first V-cycle done")
     assert sum(o[1] for o in out) == n
-    assert [o[0] for o in out] == [r * n // NRANKS for r in range(NRANKS)]  # 64-plane z-slabs
+    # 64-plane z-slabs / one 256^3 box per rank: equal row counts either way
+    assert [o[0] for o in out] == [r * n // NRANKS for r in range(NRANKS)]
     for f, m, sizes, same, _ in out:
         assert sizes == sizes1, "level sizes / nnz differ between 1 and 8 ranks"
         assert same, f"rank slice [{f}, {f + m}) of the first V-cycle differs from the 1-rank iterate"
     rep_dir = os.environ.get("AMG_TEST_REPORT_DIR")
     if rep_dir:
-        with open(os.path.join(rep_dir, "test_512_report.json"), "w") as fh:
+        with open(os.path.join(rep_dir, f"test_512_{partition}_report.json"), "w") as fh:
             json.dump(report, fh)
     say(f"done: {report}")
