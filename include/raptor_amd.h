@@ -149,7 +149,8 @@ typedef struct amg_matrix_info {
                               * tile)                                      */
     int32_t gs_split;        /* 1: hybrid GS sweeps run split -- a CSR-block pass over the  *
                               * old-value couplings + the in-chunk chain walk (4.2c)     */
-    int32_t pad0;
+    int32_t gs_chain_maxw;   /* split sweeps: most in-chunk couplings of one row, forward |  *
+                              * backward << 16 (the chain walk's widest LDS-queue bucket) */
 } amg_matrix_info;
 int amg_par_csr_info(amg_matrix A, amg_matrix_info* info);
 

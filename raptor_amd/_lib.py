@@ -74,7 +74,7 @@ class MatrixInfo(C.Structure):
         ("tpl_master", C.c_int32),
         ("tile_line_bytes", C.c_int32),
         ("gs_split", C.c_int32),
-        ("pad0", C.c_int32),
+        ("gs_chain_maxw", C.c_int32),
     ]
 
 

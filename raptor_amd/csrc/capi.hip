@@ -361,7 +361,7 @@ int amg_par_csr_info(amg_matrix A, amg_matrix_info* info) {
         info->tpl_master = tpl && (info->kernel_variant & 512) ? m.tpl_mne : 0;
         info->tile_line_bytes = m.tiled && m.format != AMG_FORMAT_CSR ? 8 * m.line_w : 0;
         info->gs_split = m.gs_block > 0 && m.gs_split ? 1 : 0;
-        info->pad0 = 0;
+        info->gs_chain_maxw = info->gs_split ? m.gs_cmaxw[0] | m.gs_cmaxw[1] << 16 : 0;
     });
 }
 

@@ -39,6 +39,11 @@ constexpr int kTileLines = kCAP / 8;     // 64-byte lines per tile
 constexpr int kTileLinesMax = kCAP / 4;  // 32-byte lines per tile
 constexpr int kNormParts = kTPB / 64;  // norm partials per CSR block (one per wave)
 constexpr int kGsWide = 128;     // sliced-ELL width from which hybrid GS uses the wide variant
+// split-GS chain walk: LDS queue widths, W entries per lane (12 W * 64 bytes
+// per 64-lane workgroup), and the bucket of a slab whose widest lane has w couplings
+constexpr int kGsChainBuckets = 4;
+constexpr int kGsChainW[kGsChainBuckets] = {8, 16, 32, 64};
+inline int gs_chain_bucket(int w) { return w <= 8 ? 0 : w <= 16 ? 1 : w <= 32 ? 2 : 3; }
 constexpr int kGatherRPB = 4;    // rows per lane of gather (rectangular-operator) row blocks
 // CSR block header h1.y: tile lines (low 16 bits); bit kHdrDvi = a value-indexed square
 // block whose Jacobi takes 1/a_ii from its value table
@@ -278,7 +283,10 @@ struct DevMatrix {
     DevBuf<double> gs_cval[2];
     DevBuf<double> gs_acc;
     bool gs_split = false;
-    int gs_cmaxw[2] = {0, 0};  // widest chain-ELL slab per direction (the kernel's LDS queue)
+    int gs_cmaxw[2] = {0, 0};  // widest chain-ELL slab per direction
+    // chain slabs ordered by width bucket (gs_chain_bucket): bucket q is slabs
+    // [gs_cbucket[d][q], gs_cbucket[d][q + 1]), walked by gs_chain_kernel<., kGsChainW[q]>
+    int gs_cbucket[2][kGsChainBuckets + 1] = {};
     // row templates (square operators): rows whose columns are all local, written as
     // (column - row) offsets, values and 1/a_ii; rows with identical triples share a template.
     // tpl_id per row (kTplNone: the CSR block kernel handles the row); per template

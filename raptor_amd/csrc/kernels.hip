@@ -2652,18 +2652,27 @@ void launch_gs_chain(hipStream_t s, const DevMatrix& A, const double* x, const d
     GsArgs a{A.gs_cslabs[d].p, A.gs_ccol[d].p, A.gs_cval[d].p, x, A.halo.p, (int)A.n_cols_local, acc,
              A.gs_dinv.p, y, (long long)A.first_row, (long long)A.gs_block, (int)A.n_rows,
              ns, nullptr, nullptr, nullptr, 0, 0};
-    const int w = A.gs_cmaxw[d];  // <= 63: in-chunk couplings of a <= 64-row chunk
-    AMG_ASSERT(w <= 64);
-#define AMG_GC(W)                                                                                  \
-    do {                                                                                           \
-        if (backward) hipLaunchKernelGGL((gs_chain_kernel<true, W>), dim3(ns), dim3(64), 0, s, a);  \
-        else hipLaunchKernelGGL((gs_chain_kernel<false, W>), dim3(ns), dim3(64), 0, s, a);          \
+    AMG_ASSERT(A.gs_cmaxw[d] <= 64);  // <= 63: in-chunk couplings of a <= 64-row chunk
+    AMG_ASSERT(A.gs_cbucket[d][kGsChainBuckets] == ns);
+    // one launch per width bucket (slabs ordered by bucket at build): each sized for its
+    // own queue, so narrow slabs run at full occupancy beside a few wide ones
+    for (int q = 0; q < kGsChainBuckets; ++q) {
+        const int b0 = A.gs_cbucket[d][q], b1 = A.gs_cbucket[d][q + 1];
+        if (b1 <= b0) continue;
+        a.slab0 = b0;
+        a.nslab = b1;
+#define AMG_GC(W)                                                                                     \
+    do {                                                                                              \
+        if (backward) hipLaunchKernelGGL((gs_chain_kernel<true, W>), dim3(b1 - b0), dim3(64), 0, s, a); \
+        else hipLaunchKernelGGL((gs_chain_kernel<false, W>), dim3(b1 - b0), dim3(64), 0, s, a);         \
     } while (0)
-    if (w <= 8) AMG_GC(8);
-    else if (w <= 16) AMG_GC(16);
-    else if (w <= 32) AMG_GC(32);
-    else AMG_GC(64);
+        static_assert(kGsChainW[0] == 8 && kGsChainW[1] == 16 && kGsChainW[2] == 32 && kGsChainW[3] == 64, "");
+        if (q == 0) AMG_GC(8);
+        else if (q == 1) AMG_GC(16);
+        else if (q == 2) AMG_GC(32);
+        else AMG_GC(64);
 #undef AMG_GC
+    }
     HIP_CHECK(hipGetLastError());
 }
 

@@ -1444,6 +1444,16 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
                         }
                     }
                 }
+                // slabs grouped by the LDS queue their width needs (kGsChainW buckets), one
+                // chain launch per bucket: one wide slab no longer sizes every wave's queue
+                // (W = 64 is 48 KiB per 64-lane workgroup, 3 waves per CU).  The order of the
+                // slabs is free: each slab's rows are its own.
+                std::stable_sort(cs.begin(), cs.end(), [](const int4& a, const int4& b) {
+                    return gs_chain_bucket(a.w) < gs_chain_bucket(b.w);
+                });
+                for (int q = 0; q <= kGsChainBuckets; ++q) gs_cbucket[d][q] = 0;
+                for (const int4& sl : cs) ++gs_cbucket[d][gs_chain_bucket(sl.w) + 1];
+                for (int q = 0; q < kGsChainBuckets; ++q) gs_cbucket[d][q + 1] += gs_cbucket[d][q];
                 gs_cslabs[d].upload(cs.data(), cs.size());
                 gs_ccol[d].upload(ccol.data(), ccol.size());
                 gs_cval[d].upload(cval.data(), cval.size());

@@ -407,3 +407,47 @@ def test_sa_gs_vcycle_template_kernel(ctx, oracle, monkeypatch, tpl_gs):
     _, h = ml.solve(ctx.zeros(n), db, max_iter=5)
     _, ho = Ho.solve(np.zeros(n), b, max_iter=5)
     assert np.all(np.abs(h - ho) <= 1e-10 * ho)
+
+
+@pytest.mark.slow
+def test_full_size_sa27_split_sweeps_and_cycle_256(ctx, oracle, capfd):
+    """configs[2] at full size (27-pt anisotropic 256^3, SA + hybrid GS): the split sweeps of
+    the Galerkin levels (KM_GSACC block pass + the bucketed LDS-queue chain walk, DESIGN.md
+    4.2c) on the product's own level-1 and level-2 operators, forward and backward at B = 64,
+    bit-identical to the oracle's hybrid_gs on those operators -- with the chain walk's widest
+    in-chunk coupling count recorded -- then one full SA V-cycle iterate bit-identical to the
+    oracle's cycle on the product's exported hierarchy."""
+    import raptor_amd as ra
+
+    O = oracle
+    N = 256
+    A = ra.par_stencil_grid(ctx, "27pt", (N, N, N))
+    ml = ra.ParSmoothedAggregationSolver().setup(A)
+    assert ml.num_levels >= 4
+    n = N ** 3
+    b = O.vec_uniform(n, 42)
+    db = to_dev(ctx, b)
+    dx = ctx.zeros(n)
+    ml.cycle(dx, db)  # builds every level's GS formats (split where the rule takes it)
+    widths = {}
+    for l in (1, 2):
+        Al = ml.level_matrix(l, "A")
+        info = Al._info()
+        assert info["gs_split"] == 1, (l, info["gs_split"])
+        Ao = O.Csr.from_scipy(Al.to_scipy_local())
+        m = Ao.shape[0]
+        x, bl = O.vec_uniform(m, 5 + l), O.vec_uniform(m, 9 + l)
+        dxl, dbl, out = to_dev(ctx, x), to_dev(ctx, bl), ctx.empty(m)
+        Al.hybrid_gs(dxl, dbl, out, 64)
+        assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs(x, bl, 64)), ("forward", l)
+        Al.hybrid_gs(dxl, dbl, out, 64, backward=True)
+        assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs_backward(x, bl, 64)), ("backward", l)
+        w = Al._info()["gs_chain_maxw"]
+        widths[l] = (w & 0xFFFF, w >> 16)
+        assert 0 < widths[l][0] <= 63 and 0 < widths[l][1] <= 63, widths[l]
+        del Ao, dxl, dbl, out
+    with capfd.disabled():
+        print(f"\n[sa27 256^3] split-sweep chain widths (forward, backward) per level: {widths}", flush=True)
+    H = O.Hierarchy(None, levels=oracle_levels(O, ml), smoother=O.SMOOTH_HYBRID_GS)
+    xo = H.cycle(np.zeros(n), b)
+    assert np.array_equal(to_host(ctx, dx), xo)
