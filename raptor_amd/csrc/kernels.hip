@@ -1387,6 +1387,339 @@ __global__ __launch_bounds__(kTPB, tpl_march_waves(NPL, NORM)) void tpl_march_ke
     }
 }
 
+// ---- ring-marched uniform stencils (variant bit 1024) -------------------
+// A uniform-stencil operator (tpl_mne > 0) whose master offsets split into planes -- o_e =
+// dz_e D + q_e, dz_e in {-1, 0, 1}, D a multiple of kTplRows (one grid plane for the 7- and
+// 27-pt operators) -- is swept by chains of blocks one plane apart (c, c + S, c + 2S, ...,
+// S = D / kTplRows).  Block t of a chain reads three plane slabs: x[(c + S p) kTplRows + qlo +
+// i], i < wp, for p = t - 1, t, t + 1.  They live in a ring of four LDS slots (slab p in slot
+// p & 3), so a step loads ONE new slab (wp doubles for 512 rows: 1.5-2x the rows' own x,
+// where the one-shot kernel loads its whole 3-band window, 6x) and copies nothing inside LDS
+// (tpl_march_kernel copies the reused slots).  Slab t + 2 is loaded into registers while
+// block t is computed and written to its slot at the top of step t + 1 -- the slot of slab
+// t - 2, which no wave reads after the barrier of step t -- so a step has one barrier.  Each
+// row's sum is tpl_rows_master's: the master's products in CSR order, masked entries added as
+// +0.0 -- bit-identical to the oracle.
+struct TplRingArgs {
+    TplArgs t;           // x, b, y, omega, partial, n, ntpl, hdr = entry masks, id, master
+    int S;               // blocks per plane
+    int nblk;            // blocks of the operator
+    int nchunk;          // chains per column
+    int qlo;             // slab slot 0 = row qlo of the block's plane (even)
+    int wp;              // doubles per ring slot (even)
+    // per ring phase (block index t & 3) and master entry: LDS slot of the entry's column
+    // relative to the row, ((t + dz_e) & 3) wp + q_e - qlo (kernel arguments: read with
+    // scalar loads inside the row loop, like tpl_rows_master's mslot)
+    int rslot[4][kTplMasterMax];
+    // fused hybrid-GS sweep (tpl_gs_ring_kernel): per GS template 1 / (a_ii + l1), the chain
+    // coupling's value and presence bit; chunk size; partial offset (hybrid GS layout)
+    const double* dl;
+    const double* cv;
+    const int* cf;
+    int B;
+    int part_off;
+};
+
+template <int NPP>
+struct RingSlab {
+    v2d_t v[NPP];
+    // slab p of column col: pair u of this lane = slots 2 (tid + kTPB u), +1; loads past x
+    // (negative or >= n: the planes before the first and after the last) return 0
+    __device__ __forceinline__ void load(const TplRingArgs& g, __amdgpu_buffer_rsrc_t xrs, int col, int p) {
+        const int tid = threadIdx.x;
+        const int base = (col + g.S * p) * kTplRows + g.qlo;
+#pragma unroll
+        for (int u = 0; u < NPP; ++u) {
+            const int i = 2 * (tid + kTPB * u);
+            const int vo = i < g.wp && p >= 0 ? (base + i) * 8 : -16;
+            v[u] = __builtin_bit_cast(v2d_t, __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, 0, 0));
+        }
+    }
+    __device__ __forceinline__ void store(const TplRingArgs& g, double* win, int p) const {
+        const int tid = threadIdx.x;
+        double* slot = win + (p & 3) * g.wp;
+#pragma unroll
+        for (int u = 0; u < NPP; ++u) {
+            const int i = 2 * (tid + kTPB * u);
+            if (i < g.wp) *(v2d_t*)(slot + i) = v[u];
+        }
+    }
+};
+
+// the block's rows (lane tid's rows tpl_lrow<true>(tid, j)): tpl_rows_master with ring slots
+template <int MODE, bool NORM, int MNE>
+__device__ __forceinline__ double tpl_rows_ring(const TplArgs& a, const double* win, const int* hdr, int r0,
+                                                const int* id, const double* pb, const double* py,
+                                                const int* c, int cdiag) {
+    constexpr int R = kTplRPL;
+    constexpr unsigned kFull = (1u << MNE) - 1u;
+    const int tid = threadIdx.x;
+    unsigned m[R];
+    bool full = true;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        m[j] = (unsigned)hdr[id[j]];
+        full = full && m[j] == kFull;
+    }
+    int rs = kTPB;
+#if AMG_TPL_SPLIT_READS
+    asm volatile("" : "+v"(rs));  // two ds_read_b64 per entry, not one ds_read2st64_b64
+#endif
+    const double* w0 = win + tpl_lrow<true>(tid, 0);
+    const double* wr[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) wr[j] = w0 + j * rs;
+    double s[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) s[j] = 0.0;
+    if (__all(full)) {
+#pragma unroll
+        for (int e = 0; e < MNE; ++e) {
+            const double v = a.mval[e];
+#pragma unroll
+            for (int j = 0; j < R; ++j) s[j] = s[j] + v * wr[j][c[e]];
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < MNE; ++e) {
+            const double v = a.mval[e];
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const double p = v * wr[j][c[e]];
+                s[j] = s[j] + (((m[j] >> e) & 1u) ? p : 0.0);
+            }
+        }
+    }
+    double sq = 0.0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const bool own = id[j] != kTplNone;
+        double out;
+        if (MODE == KM_SPMV) {
+            out = s[j];
+        } else if (MODE == KM_SPMV_ADD) {
+            out = py[j] + s[j];
+        } else {
+            const double t = pb[j] - s[j];
+            if (NORM) sq += own ? t * t : 0.0;
+            out = MODE == KM_RESID ? t : wr[j][cdiag] + a.omega * (a.mpd * t);
+        }
+        if (own) a.y[r0 + tpl_lrow<true>(tid, j)] = out;
+    }
+    return sq;
+}
+
+// chains ordered (chunk, column); XCD x = blockIdx % 8 takes a contiguous 1/8 of them (the
+// workgroups of one XCD walk neighbouring columns of the same planes: shared L2 lines)
+struct RingChains {
+    int c0, c1, nw, lw, K, per;
+    __device__ __forceinline__ RingChains(const TplRingArgs& g) {
+        K = (g.nblk + g.S - 1) / g.S;
+        per = (K + g.nchunk - 1) / g.nchunk;
+        const int C = g.S * g.nchunk, x = blockIdx.x & 7;
+        lw = blockIdx.x >> 3;
+        nw = gridDim.x >> 3;
+        c0 = x * (C >> 3) + min(x, C & 7);
+        c1 = c0 + (C >> 3) + (x < (C & 7) ? 1 : 0);
+    }
+};
+
+template <int MODE, bool NORM, int MNE, int NPP>
+__global__ __launch_bounds__(kTPB, 4) void tpl_ring_kernel(TplRingArgs g) {
+    static_assert(MNE > 0 && MNE < 32, "uniform stencils only");
+    const TplArgs& a = g.t;
+    extern __shared__ __attribute__((aligned(16))) double ring_lds[];
+    double* win = ring_lds;
+    int* hdr = (int*)(win + 4 * g.wp);
+    const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
+    const int tid = threadIdx.x;
+    if (tid < a.ntpl) hdr[tid] = a.hdr[tid];
+    if (tid == kTplNone) hdr[kTplNone] = 0;
+    const RingChains rc(g);
+    TplFetch<MODE, 1, true> f, cur;
+    RingSlab<NPP> sl;
+    for (int ch = rc.c0 + rc.lw; ch < rc.c1; ch += rc.nw) {
+        const int col = ch % g.S, t0 = (ch / g.S) * rc.per, t1 = min(rc.K, t0 + rc.per);
+        if (t0 >= t1 || col + g.S * t0 >= g.nblk) continue;  // workgroup-uniform
+        // prologue: slabs t0 - 1 and t0 into their slots, slab t0 + 1 in registers
+        sl.load(g, xrs, col, t0 - 1);
+        sl.store(g, win, t0 - 1);
+        sl.load(g, xrs, col, t0);
+        sl.store(g, win, t0);
+        sl.load(g, xrs, col, t0 + 1);
+        f.issue_ids(a, (col + g.S * t0) * kTplRows);
+        for (int t = t0; t < t1; ++t) {
+            const int blk = col + g.S * t;
+            if (blk >= g.nblk) break;  // uniform
+            const int r0 = blk * kTplRows;
+            sl.store(g, win, t + 1);  // slot of slab t - 3: read last in step t - 2
+#pragma unroll
+            for (int j = 0; j < kTplRPL; ++j) cur.id[j] = f.id[j], cur.rr[j] = f.rr[j];
+            cur.issue_operands(a);
+            __syncthreads();  // slab t + 1 (and, first time, the masks) visible
+            if (t + 1 < t1) {  // in flight during the rows below
+                sl.load(g, xrs, col, t + 2);
+                if (blk + g.S < g.nblk) f.issue_ids(a, (blk + g.S) * kTplRows);
+            }
+            const int* c = g.rslot[t & 3];
+            const int cdiag = c[a.mdiag];
+            tpl_partial<NORM>(a, blk,
+                              tpl_rows_ring<MODE, NORM, MNE>(a, win, hdr, r0, cur.id, cur.pb, cur.py, c, cdiag));
+        }
+        __syncthreads();  // the next chain's prologue rewrites the ring
+    }
+}
+
+// Fused l1 hybrid-GS sweep on the ring (uniform stencil, every block on the GS template path,
+// n a multiple of kTplRows): per block, acc_i = b_i - the old-value couplings (tpl_gs_acc_kernel's
+// sum, lane = row) goes to LDS; then lane c of wave 0 walks chunk c of the block in sweep order
+// (tpl_gs_chain_kernel's recurrence: acc -= a_i,i-+1 x'_prev; x'_i = x_i + acc * dinv_l1, x_i from
+// the ring's centre slab) and the workgroup stores x' coalesced.  One kernel reads id, b and
+// x and writes x' (25 B per row) where the acc + chain pair moves 50 B per row.
+template <bool BACK, bool NORM, int MNE, int NPP>
+__global__ __launch_bounds__(kTPB, 4) void tpl_gs_ring_kernel(TplRingArgs g) {
+    static_assert(MNE == 7 || MNE == 27, "chain entry of the instantiated masters");
+    constexpr int R = kTplRPL;
+    constexpr int EC = MNE == 27 ? (BACK ? 14 : 12) : (BACK ? 4 : 2);
+    constexpr unsigned kFull = (1u << MNE) - 1u;
+    const TplArgs& a = g.t;
+    extern __shared__ __attribute__((aligned(16))) double ring_lds[];
+    double* win = ring_lds;
+    const int B = g.B, cpb = kTplRows / B, bs = B + 1;  // chunk stride in the stage (padded)
+    double* stage = win + 4 * g.wp;        // acc, then x' (cpb * (B + 1) doubles)
+    double* sdl = stage + cpb * bs;        // per GS template: 1 / (a_ii + l1)
+    double* scv = sdl + a.ntpl;            // chain coupling value
+    int* hdr = (int*)(scv + a.ntpl);       // entry masks (kTplMax + 1)
+    int* scf = hdr + kTplMax + 1;          // chain coupling present
+    uint8_t* sid = (uint8_t*)(scf + a.ntpl);  // per row of the block: GS template id
+    const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
+    const int tid = threadIdx.x, lane = tid & 63;
+    constexpr int kBit = BACK ? 2 : 1;
+    if (tid < a.ntpl) {
+        hdr[tid] = a.hdr[tid];
+        sdl[tid] = g.dl[tid];
+        scv[tid] = g.cv[tid];
+        scf[tid] = g.cf[tid] & kBit;
+    }
+    if (tid == kTplNone) hdr[kTplNone] = 0;
+    const RingChains rc(g);
+    TplFetch<KM_RESID, 1, true> f, cur;
+    RingSlab<NPP> sl;
+    for (int ch = rc.c0 + rc.lw; ch < rc.c1; ch += rc.nw) {
+        const int col = ch % g.S, t0 = (ch / g.S) * rc.per, t1 = min(rc.K, t0 + rc.per);
+        if (t0 >= t1 || col + g.S * t0 >= g.nblk) continue;  // workgroup-uniform
+        sl.load(g, xrs, col, t0 - 1);
+        sl.store(g, win, t0 - 1);
+        sl.load(g, xrs, col, t0);
+        sl.store(g, win, t0);
+        sl.load(g, xrs, col, t0 + 1);
+        f.issue_ids(a, (col + g.S * t0) * kTplRows);
+        for (int t = t0; t < t1; ++t) {
+            const int blk = col + g.S * t;
+            if (blk >= g.nblk) break;  // uniform
+            const int r0 = blk * kTplRows;
+            sl.store(g, win, t + 1);
+#pragma unroll
+            for (int j = 0; j < R; ++j) cur.id[j] = f.id[j], cur.rr[j] = f.rr[j];
+            cur.issue_operands(a);
+            __syncthreads();  // slab t + 1 visible; the previous block's stage stores done
+            if (t + 1 < t1) {
+                sl.load(g, xrs, col, t + 2);
+                if (blk + g.S < g.nblk) f.issue_ids(a, (blk + g.S) * kTplRows);
+            }
+            const int* c = g.rslot[t & 3];
+            // acc = b - old-value couplings in CSR order (tpl_gs_acc_kernel, MNE > 0 path)
+            bool chain[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const int i = r0 + tpl_lrow<true>(tid, j), pos = i & (B - 1);
+                chain[j] = BACK ? (pos != B - 1 && i + 1 < a.n) : pos != 0;
+            }
+            unsigned m[R];
+            bool full = true;
+            double acc[R], sold[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                m[j] = (unsigned)hdr[cur.id[j]];
+                full = full && m[j] == kFull;
+                acc[j] = cur.pb[j];
+                sold[j] = 0.0;
+            }
+            int rs = kTPB;
+#if AMG_TPL_SPLIT_READS
+            asm volatile("" : "+v"(rs));
+#endif
+            const double* w0 = win + tpl_lrow<true>(tid, 0);
+            const double* wr[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) wr[j] = w0 + j * rs;
+            if (__all(full)) {
+#pragma unroll
+                for (int e = 0; e < MNE; ++e) {
+                    const double v = a.mval[e];
+#pragma unroll
+                    for (int j = 0; j < R; ++j) {
+                        const double p = v * wr[j][c[e]];
+                        if (NORM) sold[j] = sold[j] + p;
+                        if (e == EC) acc[j] = acc[j] - (chain[j] ? 0.0 : p);
+                        else acc[j] = acc[j] - p;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < MNE; ++e) {
+                    const double v = a.mval[e];
+#pragma unroll
+                    for (int j = 0; j < R; ++j) {
+                        const double p = v * wr[j][c[e]];
+                        const bool in = (m[j] >> e) & 1u;
+                        if (NORM) sold[j] = sold[j] + (in ? p : 0.0);
+                        acc[j] = acc[j] - (in && !(e == EC && chain[j]) ? p : 0.0);
+                    }
+                }
+            }
+            double sq = 0.0;
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const int lr = tpl_lrow<true>(tid, j);
+                stage[(lr / B) * bs + (lr & (B - 1))] = acc[j];
+                sid[lr] = (uint8_t)cur.id[j];
+                if (NORM && cur.id[j] != kTplNone) {
+                    const double rr = cur.pb[j] - sold[j];
+                    sq += rr * rr;
+                }
+            }
+            if (NORM) {
+                sq = wave_sum(sq);
+                if (lane == 0) a.partial[g.part_off + 4 * blk + (tid >> 6)] = sq;
+            }
+            __syncthreads();  // acc and ids of the block in LDS
+            // the chain walk: lane c of wave 0 takes chunk c (rows c B .. c B + B - 1)
+            if (tid < cpb) {
+                const double* xc = win + (t & 3) * g.wp - g.qlo;  // x of local row lr at xc[lr]
+                double* st = stage + tid * bs;
+                double prev = 0.0;
+                for (int u = 0; u < B; ++u) {
+                    const int k = BACK ? B - 1 - u : u;
+                    const int lr = tid * B + k;
+                    const int tp = sid[lr];
+                    double ac = st[k];
+                    if (u > 0 && scf[tp]) ac -= scv[tp] * prev;
+                    prev = xc[lr] + ac * sdl[tp];
+                    st[k] = prev;
+                }
+            }
+            __syncthreads();  // x' of the block in LDS
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const int lr = tpl_lrow<true>(tid, j);
+                if (cur.id[j] != kTplNone) a.y[r0 + lr] = stage[(lr / B) * bs + (lr & (B - 1))];
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // l1 hybrid Gauss-Seidel (row a5; definition DESIGN.md 3).  One wavefront per slab of <= 64
 // rows (whole GS chunks), lane = row.
 //  phase 1: the lane walks its row in the slab's sliced-ELL layout (entry k of all lanes is
@@ -2117,6 +2450,10 @@ int kernel_variant(const DevMatrix& A) {
     // one master's subsequences (DevMatrix::tpl_mne; AMG_TPL_MASTER=0 at build turns it off)
     if (!ev && A.tpl_mne > 0) var |= 512;
     if (A.tpl_mne == 0) var &= ~512;
+    // 1024: plane-ring marching of uniform-stencil rows, default where the
+    // master splits into planes (DevMatrix::tpl_ring_s; AMG_TPL_RING=0 at build: off)
+    if (!ev && A.tpl_mne > 0 && A.tpl_ring_s > 0) var |= 1024;
+    if (A.tpl_mne == 0 || A.tpl_ring_s == 0 || !(var & 512)) var &= ~1024;
     return var;
 }
 
@@ -2197,6 +2534,50 @@ static void launch_tpl_march(hipStream_t s, const TplArgs& a, int g, size_t lds,
     }
 }
 
+// the ring geometry of A into g (uniform stencil with a plane split)
+static void ring_args(const DevMatrix& A, TplRingArgs& g) {
+    AMG_ASSERT(A.tpl_ring_s > 0 && (int)A.tpl_ring_dz.size() == A.tpl_mne && (int)A.tpl_ring_mq.size() == A.tpl_mne);
+    g.S = A.tpl_ring_s;
+    g.nblk = A.tpl_blocks();
+    g.qlo = A.tpl_ring_qlo;
+    g.wp = A.tpl_ring_wp;
+    for (int ph = 0; ph < 4; ++ph)
+        for (int e = 0; e < A.tpl_mne; ++e) g.rslot[ph][e] = ((ph + A.tpl_ring_dz[e]) & 3) * g.wp + A.tpl_ring_mq[e];
+    AMG_ASSERT(g.wp % 2 == 0 && g.wp <= 3 * 2 * kTPB && g.qlo % 2 == 0);
+}
+
+// a resident grid of chains (S columns x nchunk chunks of planes; XCD-contiguous, RingChains)
+template <class KernelT>
+static int ring_grid(KernelT kern, size_t lds, int S, int& nchunk) {
+    thread_local int ncu = 0;
+    if (ncu == 0) {
+        int dev = 0;
+        HIP_CHECK(hipGetDevice(&dev));
+        HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    int occ = 0;
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kTPB, lds));
+    const int res = std::max(8, std::max(1, occ) * ncu / 8 * 8);
+    nchunk = std::max(1, res / S);
+    const int cap = tpl_march_chunk_cap();
+    if (cap > 0) nchunk = std::min(nchunk, cap);
+    return std::max(8, std::min(res, (S * nchunk + 7) / 8 * 8));
+}
+
+template <int M, bool N, int K, int NPP>
+static void launch_ring_t(hipStream_t s, TplRingArgs& g, size_t lds) {
+    if constexpr (K > 0) {
+        thread_local int grid = 0, nchunk = 0, last_s = -1;
+        thread_local size_t last_lds = 0;
+        if (last_s != g.S || last_lds != lds) {
+            grid = ring_grid(tpl_ring_kernel<M, N, K, NPP>, lds, g.S, nchunk);
+            last_s = g.S, last_lds = lds;
+        }
+        g.nchunk = nchunk;
+        hipLaunchKernelGGL((tpl_ring_kernel<M, N, K, NPP>), dim3(grid), dim3(kTPB), lds, s, g);
+    }
+}
+
 void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const double* x,
                 const double* b, double* y, double omega, double* partial) {
     const int g = A.tpl_blocks();
@@ -2238,6 +2619,41 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
         a.mdiag = A.tpl_mdiag;
         a.mpd = A.tpl_mpd;
         for (int e = 0; e < mne; ++e) a.mslot[e] = A.tpl_mslot[e], a.mval[e] = A.tpl_mval[e];
+    }
+    if (mne > 0 && (kernel_variant(A) & 1024)) {
+        // plane ring: one slab per block from x, nothing copied in LDS
+        TplRingArgs g{};
+        g.t = a;
+        ring_args(A, g);
+        const int npp = (g.wp / 2 + kTPB - 1) / kTPB;
+        const size_t lds = 8 * (size_t)4 * g.wp + 4 * (size_t)(kTplMax + 1);
+#define AMG_R3(M, N, K)                                         \
+    do {                                                        \
+        if (npp <= 2) launch_ring_t<M, N, K, 2>(s, g, lds);     \
+        else launch_ring_t<M, N, K, 3>(s, g, lds);              \
+    } while (0)
+#define AMG_R(M, N)                                \
+    do {                                           \
+        if (mne == 7) AMG_R3(M, N, 7);             \
+        else AMG_R3(M, N, 27);                     \
+    } while (0)
+        switch (mode) {
+            case KM_SPMV: AMG_R(KM_SPMV, false); break;
+            case KM_SPMV_ADD: AMG_R(KM_SPMV_ADD, false); break;
+            case KM_RESID:
+                if (norm) AMG_R(KM_RESID, true);
+                else AMG_R(KM_RESID, false);
+                break;
+            case KM_JACOBI:
+                if (norm) AMG_R(KM_JACOBI, true);
+                else AMG_R(KM_JACOBI, false);
+                break;
+            default: throw Error(AMG_ERR_INTERNAL, "bad kernel mode");
+        }
+#undef AMG_R
+#undef AMG_R3
+        HIP_CHECK(hipGetLastError());
+        return;
     }
     const int npl = !win ? 0 : a.win <= 4 * kTPB ? 4 : a.win <= 8 * kTPB ? 8 : a.win <= 12 * kTPB ? 12 : 16;
     AMG_ASSERT(a.win <= npl * kTPB && a.win <= kTplWin);
@@ -2514,10 +2930,55 @@ static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, co
         a.mpd = A.tpl_mpd;
         for (int e = 0; e < mne; ++e) a.mslot[e] = A.tpl_mslot[e], a.mval[e] = A.tpl_mval[e];
     }
+    const bool norm = partial != nullptr;
+    if (mne > 0 && A.gs_ring && (kernel_variant(A) & 1024)) {
+        // fused sweep on the plane ring: acc and the chain walk in one kernel
+        TplRingArgs r{};
+        r.t = a;
+        r.t.y = y;
+        ring_args(A, r);
+        r.dl = A.gs_tdl.p;
+        r.cv = backward ? A.gs_tcvp.p : A.gs_tcvm.p;
+        r.cf = A.gs_tcf.p;
+        r.B = (int)A.gs_block;
+        r.part_off = A.n_gs_slabs;
+        const int npp = (r.wp / 2 + kTPB - 1) / kTPB;
+        const int cpb = kTplRows / r.B;
+        const size_t lds = 8 * ((size_t)4 * r.wp + (size_t)cpb * (r.B + 1) + 2 * (size_t)a.ntpl) +
+                           4 * ((size_t)kTplMax + 1 + a.ntpl) + kTplRows;
+#define AMG_GR3(BK, NM, K, P)                                                               \
+    do {                                                                                    \
+        thread_local int grid = 0, nchunk = 0, last_s = -1;                                 \
+        thread_local size_t last_lds = 0;                                                   \
+        if (last_s != r.S || last_lds != lds) {                                             \
+            grid = ring_grid(tpl_gs_ring_kernel<BK, NM, K, P>, lds, r.S, nchunk);           \
+            last_s = r.S, last_lds = lds;                                                   \
+        }                                                                                   \
+        r.nchunk = nchunk;                                                                  \
+        hipLaunchKernelGGL((tpl_gs_ring_kernel<BK, NM, K, P>), dim3(grid), dim3(kTPB), lds, s, r); \
+    } while (0)
+#define AMG_GR2(BK, NM, K)                 \
+    do {                                   \
+        if (npp <= 2) AMG_GR3(BK, NM, K, 2); \
+        else AMG_GR3(BK, NM, K, 3);        \
+    } while (0)
+#define AMG_GR(BK, NM)                      \
+    do {                                    \
+        if (mne == 7) AMG_GR2(BK, NM, 7);   \
+        else AMG_GR2(BK, NM, 27);           \
+    } while (0)
+        if (backward) AMG_GR(true, false);
+        else if (norm) AMG_GR(false, true);
+        else AMG_GR(false, false);
+#undef AMG_GR
+#undef AMG_GR2
+#undef AMG_GR3
+        HIP_CHECK(hipGetLastError());
+        return;
+    }
     const int npl = a.win <= 4 * kTPB ? 4 : a.win <= 8 * kTPB ? 8 : a.win <= 12 * kTPB ? 12 : 16;
     AMG_ASSERT(a.win <= npl * kTPB && a.win <= kTplWin);
     const size_t lds = tpl_gs_lds_bytes(a.win, a.nent, a.ntpl);
-    const bool norm = partial != nullptr;
     const dim3 grid(g.nblk), blk(kTPB);
 #define AMG_G3(BK, NM, P, K) hipLaunchKernelGGL((tpl_gs_acc_kernel<BK, NM, P, K>), grid, blk, lds, s, g)
 #define AMG_G2(BK, NM, P)                          \
