@@ -29,6 +29,7 @@ static thread_local std::string g_err;
 
 template <class F>
 static int guard(F&& f) {
+    omp_quiet_thread();
     try {
         f();
         return AMG_OK;
@@ -100,13 +101,6 @@ static void amg_crash_handler(int sig) {
 
 // (re)installed at context creation and again right before a hipGraph capture: runtimes
 // loaded later (RCCL, a framework) may have replaced the handler in between
-// OpenMP threads of the host setup loops sleep as soon as a parallel region ends
-// (KMP_BLOCKTIME=0, unless the caller set it): the LLVM runtime's default keeps them spinning
-// for 200 ms, and on a CPU-quota'd host (a container's cgroup) two spinning teams -- the setup
-// thread's and the format worker's -- exhausted the quota and stalled the launching thread
-// for 5-10 ms in the middle of timed V-cycles (profiles/r3i_cycle_gaps.txt).  libomp reads the
-// variable when it initialises, at the library's first parallel region, after this runs.
-__attribute__((constructor)) static void amg_omp_defaults() { setenv("KMP_BLOCKTIME", "0", 0); }
 
 void amg::install_crash_handler() {
     const char* e = std::getenv("AMG_SEGV_BACKTRACE");

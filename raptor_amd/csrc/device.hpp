@@ -330,6 +330,7 @@ struct DevMatrix {
     // (row_ptr / col / val exactly as SURVEY.md 8(d) prices them; pcol / pval are built when
     // the format is first selected: local | halo column numbering, 2 padding entries)
     int format = AMG_FORMAT_AUTO;
+    bool blocks_only = false;  // build only the CSR-block formats (the split-GS pass operators)
     DevBuf<int> pcol;
     DevBuf<double> pval;
     int plain_blocks() const { return (int)((n_rows + kTPB - 1) / kTPB); }

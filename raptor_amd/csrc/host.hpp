@@ -29,6 +29,15 @@ struct Error : std::runtime_error {
     int code;
     Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
+
+// OpenMP teams the library's host loops start from this thread sleep as soon as a parallel
+// region ends (kmp_set_blocktime(0) for this thread, once; KMP_BLOCKTIME in the environment
+// wins): libomp's default keeps them spinning for 200 ms, and on a CPU-quota'd host two
+// spinning teams -- the setup thread's and the format worker's -- exhausted the quota and
+// stalled the launching thread for 5-10 ms inside timed V-cycles (profiles/r3i_cycle_gaps.txt).
+// Per thread, so the host process's own OpenMP settings and environment are left alone.
+// Called at every C-ABI entry and by the format worker thread.
+void omp_quiet_thread();
 #define AMG_CHECK(cond, msg)                                                              \
     do {                                                                                  \
         if (!(cond)) throw ::amg::Error(AMG_ERR_INVALID, std::string(msg));               \

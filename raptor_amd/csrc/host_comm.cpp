@@ -13,7 +13,22 @@
 
 #include "host.hpp"
 
+
+// LLVM libomp extension (the library links libomp); weak, so a host-only build against
+// another OpenMP runtime (the sanitizer build with libgomp) just skips it
+extern "C" void kmp_set_blocktime(int) __attribute__((weak));
+
 namespace amg {
+
+void omp_quiet_thread() {
+    thread_local bool done = false;
+    if (done) return;
+    done = true;
+    const char* e = std::getenv("KMP_BLOCKTIME");
+    if ((e && *e) || !kmp_set_blocktime) return;
+    kmp_set_blocktime(0);
+}
+
 
 uint64_t mix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;

@@ -59,6 +59,7 @@ class FormatWorker {
     }
     void run(int device) {
         const hipError_t e = hipSetDevice(device);
+        omp_quiet_thread();
         for (;;) {
             std::function<void()> job;
             {

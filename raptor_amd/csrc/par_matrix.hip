@@ -724,7 +724,7 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
     TplBuild tb;
     n_tpl = n_tpl_ent = nb_skip = 0;
     tpl_rows = 0;
-    if (square && n_rows > 0) {
+    if (square && n_rows > 0 && !blocks_only) {
         const char* e = std::getenv("AMG_TPL_MIN_ROWS");
         const int64_t min_rows = e ? std::atoll(e) : (int64_t)16384;
         tb = build_templates(hrp, hcol, host.val, di, n_cols_local);
@@ -1472,9 +1472,13 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
                             ++o;
                         }
                 }
+                // CSR blocks only: no row templates (and so no windows, masks or march
+                // tables) are built for the pass's operator, and its format is set before
+                // the build -- no format_generation bump, no captured graph goes stale
                 gs_old[d] = std::make_unique<DevMatrix>();
+                gs_old[d]->blocks_only = true;
+                gs_old[d]->format = AMG_FORMAT_BLOCKS;
                 gs_old[d]->build(ctx, std::move(h), replicated);
-                gs_old[d]->set_format(AMG_FORMAT_BLOCKS);
                 // the chain ELL: same slabs, only the new-value couplings (CSR order)
                 std::vector<int4> cs = slabs;
                 int64_t cc = 0;
