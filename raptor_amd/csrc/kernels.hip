@@ -79,6 +79,7 @@ struct CsrArgs {
                        // level's first Jacobi sweep from x = 0, fused into the restriction)
     const uint16_t* col16;  // gather operators: 16-bit column codes (C16 kernels), with
     const int4* gband;      // the block's 4 band bases: col = base[code >> 14] + (code & 0x3fff)
+    int nblk;               // blocks of this launch (paired x-tile kernel: 2 per workgroup)
 };
 
 // the fused second output of a restriction (CsrArgs::y2): jacobi_zero_kernel's expression;
@@ -493,13 +494,44 @@ __device__ __forceinline__ void block_partial(const CsrArgs& a, int bid, double 
 // whose blocks hold up to kTPB * kGatherRPB rows; DevMatrix::gather_rpb)
 // C16: gather path with 16-bit column codes (DevMatrix::col16)
 // LW: doubles per x-tile line (8: 256 lines of 64 B, 4: 512 lines of 32 B; DevMatrix::line_w)
-template <int MODE, bool NORM, bool XCD, bool TILE, bool VI, int GRPB = 1, bool C16 = false, int LW = 8>
-__global__ __launch_bounds__(kTPB, GRPB > 1 ? 7 : 8) void csr_block_kernel(CsrArgs a, int first_block) {
+// PAIR (x-tile path, variant bit 2048): each workgroup runs two consecutive blocks, issuing
+// the second block's batch 1 (header, line ids, tile / VI indices) with the first's, so the
+// second block waits on one dependent round of loads instead of two
+template <int MODE, bool NORM, bool XCD, bool TILE, bool VI, int GRPB = 1, bool C16 = false, int LW = 8,
+          bool PAIR = false>
+__global__ __launch_bounds__(kTPB, GRPB > 1 || PAIR ? 7 : 8) void csr_block_kernel(CsrArgs a, int first_block) {
     static_assert(kCAP / kTPB == 8 && (LW == 8 || LW == 4) && kTPB == 256,
                   "lane-major layouts assume 8 entries per lane, 4 waves");
+    static_assert(!PAIR || (TILE && AMG_CSR_PRE_TILE), "paired blocks: x-tile path");
     __shared__ __attribute__((aligned(16))) double stage[kCAP];  // x tile, then products
     __shared__ double tabl[VI ? 256 : 1];
     __shared__ int rends[kTPB * GRPB];
+    if constexpr (PAIR) {
+        constexpr int PV = VI ? 2 : 1;
+        const int w = XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+        const int b0 = first_block + 2 * w, b1 = b0 + 1;
+        const bool has1 = 2 * w + 1 < a.nblk;  // workgroup-uniform
+        CsrPre f0, f1;
+        csr_pre_tile<VI, LW>(a, b0, f0);
+        if (has1) csr_pre_tile<VI, LW>(a, b1, f1);  // in flight during block b0
+        auto run = [&](int bid, CsrPre& f) {
+            const int4 h0 = f.h0, h1 = f.h1;
+            double sq;
+            if (h0.w <= kCAP && (h1.y & 0xffff) <= kCAP / LW && h0.w > 0) {
+                if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f, -1);
+                else sq = block_main<MODE, NORM, true, false, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f, -1);
+            } else {
+                sq = block_long<MODE, NORM>(a, h0, stage);
+            }
+            block_partial<NORM>(a, bid, sq);
+        };
+        run(b0, f0);
+        if (has1) {
+            __syncthreads();  // the stage and row ends are rewritten by block b1
+            run(b1, f1);
+        }
+        return;
+    }
     const int bid = first_block + (XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x);
     if constexpr (TILE && AMG_CSR_PRE_TILE) {
         // square operators: batch 1 (tile line ids, tile / VI indices: fixed offsets from the
@@ -2735,8 +2767,25 @@ static void launch_csr_persist(hipStream_t s, int mode, bool norm, const CsrArgs
     HIP_CHECK(hipGetLastError());
 }
 
+// AMG_CSR_PAIR=1: square x-tile operators run two blocks per workgroup (A/B)
+static bool csr_pair() {
+    static const bool on = [] {
+        const char* e = std::getenv("AMG_CSR_PAIR");
+        return e && *e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+
 template <int M, bool N, bool X, bool T, bool V>
 static void launch_block(hipStream_t s, dim3 g, const CsrArgs& a, int first_block, bool rpb4, int lw) {
+    if constexpr (T && AMG_CSR_PRE_TILE) {
+        if (a.nblk >= 2 && !rpb4 && csr_pair()) {
+            const dim3 gp((unsigned)((a.nblk + 1) / 2));
+            if (lw == 4) hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, 1, false, 4, true>), gp, dim3(kTPB), 0, s, a, first_block);
+            else hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, 1, false, 8, true>), gp, dim3(kTPB), 0, s, a, first_block);
+            return;
+        }
+    }
     if constexpr (T) {
         if (lw == 4) {  // 32-byte x-tile lines
             if constexpr (!N && (M == KM_SPMV || M == KM_SPMV_ADD)) {
@@ -2772,7 +2821,7 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
     CsrArgs a{A.hdr.p, A.tile_fixed.p, A.lcol.p, A.vidx.p, A.vtab.p, A.rend.p, A.dvi.p,
               A.rp.p, A.col.p, A.val.p,
               x, A.halo.p, ncl, nh, (ncl + A.line_w - 1) / A.line_w, (ncl >= 2 && nh != 1) ? 1 : 0, A.tiled ? 0 : 1,
-              b, y2 ? d2 : A.dinv.p, y, omega, partial, part_off, y2, nullptr, A.gband.p};
+              b, y2 ? d2 : A.dinv.p, y, omega, partial, part_off, y2, nullptr, A.gband.p, n_blocks};
     const dim3 g(n_blocks);
     const int var = kernel_variant(A);
     if (var & 256) a.col16 = A.col16.p;

@@ -15,5 +15,8 @@ run ringtests 600 python -u -m pytest tests/test_gpu_kernel_paths.py -x -q --tim
 run bench7 400 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 8
 cp gpurun_out/${R}_bench7.log gpurun_out/${R}_bench7.txt
 run sa27 400 python bench.py --config sa27 --steps 20 --warmup 5 --cpu-seconds 6
+run sa27_noring 400 env AMG_TPL_RING=0 AMG_GS_RING=0 python bench.py --config sa27 --steps 20 --warmup 5 --no-cpu-baseline
+run bench7_noring 400 env AMG_TPL_RING=0 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
+run bench7_pair 400 env AMG_CSR_PAIR=1 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
 run n2 400 env AMG_BENCH_SHARED_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu-baseline --spmv-reps 5
 R=$R bash scripts/gpu_graph_probe.sh
