@@ -252,42 +252,85 @@ GhostRows fetch_rows(const HostComm& comm, const HaloPlan& plan, const HostCSR& 
 }
 
 // ----------------------------------------------------------------------------------
-// Distributed transpose: R = P^T.  Entries (J, i, v) go to owner(J); each received
-// buffer is in ascending i, buffers are processed in rank order => rows of R sorted.
+// Distributed transpose: R = P^T.  Entries (J, i, v) go to owner(J) as 24-byte records in ONE
+// exchange; each rank's records leave in ascending i, the received buffers are placed in rank
+// order => every row of R is in ascending global column.  Bucketing and placement run as
+// OpenMP loops (per-thread counts, then exclusive offsets: the record order equals the serial
+// loop's), so the host part stays a small fraction of the exchange on N ranks.
 // ----------------------------------------------------------------------------------
 HostCSR transpose(const HostComm& comm, const HostCSR& P) {
+    struct Rec {
+        int64_t j, i;
+        double v;
+    };
     HostCSR R;
     R.n_global_rows = P.n_global_cols;
     R.n_global_cols = P.n_global_rows;
     R.row_starts = P.col_starts;
     R.col_starts = P.row_starts;
-    int64_t i0 = P.row_starts[comm.rank];
-    std::vector<std::vector<int64_t>> sj(comm.nranks), si(comm.nranks);
-    std::vector<std::vector<double>> sv(comm.nranks);
-    for (int64_t i = 0; i < P.nrows(); ++i)
-        for (int64_t k = P.rp[i]; k < P.rp[i + 1]; ++k) {
-            int o = owner_of(P.col_starts, P.col[k]);
-            sj[o].push_back(P.col[k]);
-            si[o].push_back(i0 + i);
-            sv[o].push_back(P.val[k]);
+    const int nr = comm.nranks;
+    const int64_t i0 = P.row_starts[comm.rank], n = P.nrows();
+    const int nt = std::max(1, std::min(omp_get_max_threads(), (int)(n / 4096 + 1)));
+    // owner of every entry, and per (thread, owner) counts over contiguous row ranges
+    std::vector<int> own((size_t)P.nnz());
+    std::vector<int64_t> tc((size_t)nt * nr, 0);
+#pragma omp parallel num_threads(nt)
+    {
+        const int t = omp_get_thread_num();
+        const int64_t r0 = n * t / nt, r1 = n * (t + 1) / nt;
+        int64_t* c = tc.data() + (size_t)t * nr;
+        for (int64_t k = P.rp[r0]; k < P.rp[r1]; ++k) {
+            const int o = owner_of(P.col_starts, P.col[k]);
+            own[k] = o;
+            ++c[o];
         }
-    auto rj = comm.exchange(sj);
-    auto ri = comm.exchange(si);
-    auto rv = comm.exchange(sv);
-    int64_t lo = R.row_starts[comm.rank], n = R.row_starts[comm.rank + 1] - lo;
-    R.rp.assign(n + 1, 0);
-    for (int r = 0; r < comm.nranks; ++r)
-        for (int64_t J : rj[r]) R.rp[J - lo + 1]++;
-    for (int64_t t = 0; t < n; ++t) R.rp[t + 1] += R.rp[t];
-    R.col.resize(R.rp[n]);
-    R.val.resize(R.rp[n]);
-    std::vector<int64_t> pos(R.rp.begin(), R.rp.end() - 1);
-    for (int r = 0; r < comm.nranks; ++r)
-        for (size_t t = 0; t < rj[r].size(); ++t) {
-            int64_t p = pos[rj[r][t] - lo]++;
-            R.col[p] = ri[r][t];
-            R.val[p] = rv[r][t];
+    }
+    // record offsets: owner-major, thread order inside an owner (= ascending i)
+    std::vector<int64_t> off((size_t)nt * nr), sb(nr, 0);
+    int64_t pos = 0;
+    for (int o = 0; o < nr; ++o) {
+        for (int t = 0; t < nt; ++t) {
+            off[(size_t)t * nr + o] = pos;
+            pos += tc[(size_t)t * nr + o];
         }
+        sb[o] = 0;
+    }
+    std::vector<Rec> sbuf((size_t)pos);
+#pragma omp parallel num_threads(nt)
+    {
+        const int t = omp_get_thread_num();
+        const int64_t r0 = n * t / nt, r1 = n * (t + 1) / nt;
+        int64_t* w = off.data() + (size_t)t * nr;
+        for (int64_t i = r0; i < r1; ++i)
+            for (int64_t k = P.rp[i]; k < P.rp[i + 1]; ++k) sbuf[(size_t)w[own[k]]++] = {P.col[k], i0 + i, P.val[k]};
+    }
+    std::vector<int64_t> cnt(nr, 0);
+    for (int o = 0; o < nr; ++o)
+        for (int t = 0; t < nt; ++t) cnt[o] += tc[(size_t)t * nr + o];
+    const std::vector<int64_t> rcnt = comm.alltoall_counts(cnt);
+    std::vector<int64_t> rb(nr);
+    int64_t rtot = 0;
+    for (int o = 0; o < nr; ++o) {
+        sb[o] = cnt[o] * (int64_t)sizeof(Rec);
+        rb[o] = rcnt[o] * (int64_t)sizeof(Rec);
+        rtot += rcnt[o];
+    }
+    std::vector<Rec> rbuf((size_t)rtot);
+    comm.alltoallv(sbuf.data(), sb, rbuf.data(), rb);
+    std::vector<Rec>().swap(sbuf);
+    const int64_t lo = R.row_starts[comm.rank], m = R.row_starts[comm.rank + 1] - lo;
+    R.rp.assign(m + 1, 0);
+    for (const Rec& e : rbuf) R.rp[e.j - lo + 1]++;
+    for (int64_t t = 0; t < m; ++t) R.rp[t + 1] += R.rp[t];
+    R.col.resize(R.rp[m]);
+    R.val.resize(R.rp[m]);
+    // placement in received order (rank order, ascending i inside a rank)
+    std::vector<int64_t> at(R.rp.begin(), R.rp.end() - 1);
+    for (const Rec& e : rbuf) {
+        const int64_t p = at[e.j - lo]++;
+        R.col[p] = e.i;
+        R.val[p] = e.v;
+    }
     return R;
 }
 

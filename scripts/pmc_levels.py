@@ -10,7 +10,7 @@ sys.path.insert(0, ROOT)
 import raptor_amd as ra  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-ctx = ra.Context(0)
+ctx = ra.Context.native(0)  # torch-free, like bench.py
 A = ra.par_stencil_grid(ctx, "7pt", (N, N, N))
 ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
 mats = [("A0", A)] + [(f"A{l}", ml.level_matrix(l, "A")) for l in (1, 2)] + \

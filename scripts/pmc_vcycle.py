@@ -11,12 +11,11 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-import torch  # noqa: E402
-
 import raptor_amd as ra  # noqa: E402
 
+# torch-free, like bench.py: the library on the ROCm runtime it was built for
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-ctx = ra.Context(0)
+ctx = ra.Context.native(0)
 A = ra.par_stencil_grid(ctx, "7pt", (N, N, N))
 ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
 ops = []
@@ -32,9 +31,8 @@ for l in range(ml.num_levels - 1):
     Al = A if l == 0 else ml.level_matrix(l, "A")
     P, R = ml.level_matrix(l, "P"), ml.level_matrix(l, "R")
     nl, nc = Al.local_rows, P.local_cols
-    with torch.cuda.stream(ctx.stream):
-        xl, bl, tl = ra.vector_uniform(ctx, nl, 0, 5), ra.vector_uniform(ctx, nl, 0, 6), ctx.empty(nl)
-        xc, bc = ra.vector_uniform(ctx, nc, 0, 7), ctx.empty(R.local_rows)
+    xl, bl, tl = ra.vector_uniform(ctx, nl, 0, 5), ra.vector_uniform(ctx, nl, 0, 6), ctx.empty(nl)
+    xc, bc = ra.vector_uniform(ctx, nc, 0, 7), ctx.empty(R.local_rows)
     table = [("Jacobi", lambda: Al.jacobi(xl, bl, tl), Al.info["jacobi_bytes"]),
              ("residual", lambda: Al.residual(xl, bl, tl), Al.info["residual_bytes"]),
              ("restrict R r", lambda: R.mult(tl, bc), R.info["spmv_bytes"]),
