@@ -2599,11 +2599,12 @@ static int ring_grid(KernelT kern, size_t lds, int S, int& nchunk) {
 template <int M, bool N, int K, int NPP>
 static void launch_ring_t(hipStream_t s, TplRingArgs& g, size_t lds) {
     if constexpr (K > 0) {
-        thread_local int grid = 0, nchunk = 0, last_s = -1;
+        thread_local int grid = 0, nchunk = 0, last_s = -1, last_cap = -1;
         thread_local size_t last_lds = 0;
-        if (last_s != g.S || last_lds != lds) {
+        const int cap = tpl_march_chunk_cap();
+        if (last_s != g.S || last_lds != lds || last_cap != cap) {
             grid = ring_grid(tpl_ring_kernel<M, N, K, NPP>, lds, g.S, nchunk);
-            last_s = g.S, last_lds = lds;
+            last_s = g.S, last_lds = lds, last_cap = cap;
         }
         g.nchunk = nchunk;
         hipLaunchKernelGGL((tpl_ring_kernel<M, N, K, NPP>), dim3(grid), dim3(kTPB), lds, s, g);
@@ -2997,11 +2998,12 @@ static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, co
                            4 * ((size_t)kTplMax + 1 + a.ntpl) + kTplRows;
 #define AMG_GR3(BK, NM, K, P)                                                               \
     do {                                                                                    \
-        thread_local int grid = 0, nchunk = 0, last_s = -1;                                 \
+        thread_local int grid = 0, nchunk = 0, last_s = -1, last_cap = -1;                  \
         thread_local size_t last_lds = 0;                                                   \
-        if (last_s != r.S || last_lds != lds) {                                             \
+        const int cap = tpl_march_chunk_cap();                                              \
+        if (last_s != r.S || last_lds != lds || last_cap != cap) {                          \
             grid = ring_grid(tpl_gs_ring_kernel<BK, NM, K, P>, lds, r.S, nchunk);           \
-            last_s = r.S, last_lds = lds;                                                   \
+            last_s = r.S, last_lds = lds, last_cap = cap;                                   \
         }                                                                                   \
         r.nchunk = nchunk;                                                                  \
         hipLaunchKernelGGL((tpl_gs_ring_kernel<BK, NM, K, P>), dim3(grid), dim3(kTPB), lds, s, r); \
