@@ -168,7 +168,7 @@ class Context:
     own stream, ``DeviceVector``s for ``empty`` / ``zeros``, multi-rank over a ``SocketComm``
     (``Context.native(device, comm=...)``)."""
 
-    native = False
+    is_native = False  # torch-free context (Context.native)
 
     def __init__(self, device: int | None = None, stream=None):
         torch = _torch()
@@ -214,7 +214,7 @@ class Context:
         buffers.  comm: a ``SocketComm`` for multi-rank runs (collective: every rank calls
         this; rank 0's RCCL id travels over the mesh, the setup exchange too)."""
         ctx = cls.__new__(cls)
-        ctx.native = True
+        ctx.is_native = True
         ctx.device = int(device)
         ctx.torch_device = None
         ctx.stream = None
@@ -248,14 +248,14 @@ class Context:
 
     def empty(self, n: int):
         """Allocate on the context's stream (torch's caching allocator is stream-aware)."""
-        if self.native:
+        if self.is_native:
             return DeviceVector(self, n)
         torch = _torch()
         with torch.cuda.stream(self.stream):
             return torch.empty(int(n), dtype=torch.float64, device=self.torch_device)
 
     def zeros(self, n: int):
-        if self.native:
+        if self.is_native:
             return DeviceVector(self, n).zero_()
         torch = _torch()
         with torch.cuda.stream(self.stream):
