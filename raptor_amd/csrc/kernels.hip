@@ -1455,15 +1455,17 @@ struct TplRingArgs {
 template <int NPP>
 struct RingSlab {
     v2d_t v[NPP];
-    // slab p of column col: pair u of this lane = slots 2 (tid + kTPB u), +1; loads past x
-    // (negative or >= n: the planes before the first and after the last) return 0
+    // slab p of column col: pair u of this lane = slots 2 (tid + kTPB u), +1.  Rows before 0 or
+    // past n - 1 load 0 through the buffer bounds (a negative offset is out of range too); a
+    // slab of plane -1 may still hold real rows (the split D need not be a grid plane: a block
+    // of plane 0 can hold rows whose -D neighbours are rows of block 0)
     __device__ __forceinline__ void load(const TplRingArgs& g, __amdgpu_buffer_rsrc_t xrs, int col, int p) {
         const int tid = threadIdx.x;
         const int base = (col + g.S * p) * kTplRows + g.qlo;
 #pragma unroll
         for (int u = 0; u < NPP; ++u) {
             const int i = 2 * (tid + kTPB * u);
-            const int vo = i < g.wp && p >= 0 ? (base + i) * 8 : -16;
+            const int vo = i < g.wp ? (base + i) * 8 : -16;
             v[u] = __builtin_bit_cast(v2d_t, __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, 0, 0));
         }
     }
@@ -1556,6 +1558,52 @@ struct RingChains {
     }
 };
 
+// Per-chain pipeline of the ring kernels: slabs two steps ahead in registers (sA / sB: the
+// slab of step t + 1 is stored at the top of step t, the load of slab t + 3 goes into the same
+// registers after the barrier), row ids two blocks ahead and b / y one block ahead (fA / fB), so
+// a step waits on no load it issued itself.  run_chain calls body(t, blk, r0, f) for each block
+// of the chain with f = that block's ids and operands, one barrier per step.
+template <int MODE, int NPP>
+struct RingPipe {
+    RingSlab<NPP> sA, sB;
+    TplFetch<MODE, 1, true> fA, fB;
+
+    template <class Body>
+    __device__ __forceinline__ void run_chain(const TplRingArgs& g, __amdgpu_buffer_rsrc_t xrs, double* win,
+                                              int col, int t0, int t1, Body&& body) {
+        const TplArgs& a = g.t;
+        auto blk_of = [&](int t) { return col + g.S * t; };
+        auto valid = [&](int t) { return t < t1 && blk_of(t) < g.nblk; };
+        // prologue: slabs t0 - 1, t0 into the ring; t0 + 1, t0 + 2 into registers; ids and
+        // operands of block t0, ids of block t0 + 1
+        sA.load(g, xrs, col, t0 - 1);
+        sA.store(g, win, t0 - 1);
+        sA.load(g, xrs, col, t0);
+        sA.store(g, win, t0);
+        sA.load(g, xrs, col, t0 + 1);
+        if (valid(t0 + 1)) sB.load(g, xrs, col, t0 + 2);
+        fA.issue_ids(a, blk_of(t0) * kTplRows);
+        fA.issue_operands(a);
+        if (valid(t0 + 1)) fB.issue_ids(a, blk_of(t0 + 1) * kTplRows);
+        auto step = [&](int t, RingSlab<NPP>& sn, TplFetch<MODE, 1, true>& fc, TplFetch<MODE, 1, true>& fo) {
+            const int blk = blk_of(t);
+            sn.store(g, win, t + 1);  // slot of slab t - 3: read last in step t - 2
+            __syncthreads();          // slab t + 1 visible; every wave is done with step t - 1
+            if (valid(t + 2)) sn.load(g, xrs, col, t + 3);
+            if (valid(t + 1)) fo.issue_operands(a);
+            body(t, blk, blk * kTplRows, fc);
+            if (valid(t + 2)) fc.issue_ids(a, blk_of(t + 2) * kTplRows);
+        };
+        for (int t = t0;; t += 2) {
+            if (!valid(t)) break;
+            step(t, sA, fA, fB);
+            if (!valid(t + 1)) break;
+            step(t + 1, sB, fB, fA);
+        }
+        __syncthreads();  // the next chain's prologue rewrites the ring
+    }
+};
+
 template <int MODE, bool NORM, int MNE, int NPP>
 __global__ __launch_bounds__(kTPB, 4) void tpl_ring_kernel(TplRingArgs g) {
     static_assert(MNE > 0 && MNE < 32, "uniform stencils only");
@@ -1568,46 +1616,25 @@ __global__ __launch_bounds__(kTPB, 4) void tpl_ring_kernel(TplRingArgs g) {
     if (tid < a.ntpl) hdr[tid] = a.hdr[tid];
     if (tid == kTplNone) hdr[kTplNone] = 0;
     const RingChains rc(g);
-    TplFetch<MODE, 1, true> f, cur;
-    RingSlab<NPP> sl;
+    RingPipe<MODE, NPP> pipe;
     for (int ch = rc.c0 + rc.lw; ch < rc.c1; ch += rc.nw) {
         const int col = ch % g.S, t0 = (ch / g.S) * rc.per, t1 = min(rc.K, t0 + rc.per);
         if (t0 >= t1 || col + g.S * t0 >= g.nblk) continue;  // workgroup-uniform
-        // prologue: slabs t0 - 1 and t0 into their slots, slab t0 + 1 in registers
-        sl.load(g, xrs, col, t0 - 1);
-        sl.store(g, win, t0 - 1);
-        sl.load(g, xrs, col, t0);
-        sl.store(g, win, t0);
-        sl.load(g, xrs, col, t0 + 1);
-        f.issue_ids(a, (col + g.S * t0) * kTplRows);
-        for (int t = t0; t < t1; ++t) {
-            const int blk = col + g.S * t;
-            if (blk >= g.nblk) break;  // uniform
-            const int r0 = blk * kTplRows;
-            sl.store(g, win, t + 1);  // slot of slab t - 3: read last in step t - 2
-#pragma unroll
-            for (int j = 0; j < kTplRPL; ++j) cur.id[j] = f.id[j], cur.rr[j] = f.rr[j];
-            cur.issue_operands(a);
-            __syncthreads();  // slab t + 1 (and, first time, the masks) visible
-            if (t + 1 < t1) {  // in flight during the rows below
-                sl.load(g, xrs, col, t + 2);
-                if (blk + g.S < g.nblk) f.issue_ids(a, (blk + g.S) * kTplRows);
-            }
+        pipe.run_chain(g, xrs, win, col, t0, t1, [&](int t, int blk, int r0, const TplFetch<MODE, 1, true>& f) {
             const int* c = g.rslot[t & 3];
             const int cdiag = c[a.mdiag];
-            tpl_partial<NORM>(a, blk,
-                              tpl_rows_ring<MODE, NORM, MNE>(a, win, hdr, r0, cur.id, cur.pb, cur.py, c, cdiag));
-        }
-        __syncthreads();  // the next chain's prologue rewrites the ring
+            tpl_partial<NORM>(a, blk, tpl_rows_ring<MODE, NORM, MNE>(a, win, hdr, r0, f.id, f.pb, f.py, c, cdiag));
+        });
     }
 }
 
 // Fused l1 hybrid-GS sweep on the ring (uniform stencil, every block on the GS template path,
-// n a multiple of kTplRows): per block, acc_i = b_i - the old-value couplings (tpl_gs_acc_kernel's
-// sum, lane = row) goes to LDS; then lane c of wave 0 walks chunk c of the block in sweep order
-// (tpl_gs_chain_kernel's recurrence: acc -= a_i,i-+1 x'_prev; x'_i = x_i + acc * dinv_l1, x_i from
-// the ring's centre slab) and the workgroup stores x' coalesced.  One kernel reads id, b and
-// x and writes x' (25 B per row) where the acc + chain pair moves 50 B per row.
+// n a multiple of kTplRows): per block, acc_i = b_i - the old-value couplings
+// (tpl_gs_acc_kernel's sum, lane = row) goes to LDS; then lane c of wave 0 walks chunk c of the
+// block in sweep order (tpl_gs_chain_kernel's recurrence: acc -= a_i,i-+1 x'_prev; x'_i = x_i +
+// acc * dinv_l1, x_i from the ring's centre slab), eight rows per batch with every LDS read of
+// the batch issued before its dependent chain, and the workgroup stores x' coalesced.  One
+// kernel reads id, b and x and writes x' (25 B per row) where the acc + chain pair moves 50 B.
 template <bool BACK, bool NORM, int MNE, int NPP>
 __global__ __launch_bounds__(kTPB, 4) void tpl_gs_ring_kernel(TplRingArgs g) {
     static_assert(MNE == 7 || MNE == 27, "chain entry of the instantiated masters");
@@ -1635,30 +1662,11 @@ __global__ __launch_bounds__(kTPB, 4) void tpl_gs_ring_kernel(TplRingArgs g) {
     }
     if (tid == kTplNone) hdr[kTplNone] = 0;
     const RingChains rc(g);
-    TplFetch<KM_RESID, 1, true> f, cur;
-    RingSlab<NPP> sl;
+    RingPipe<KM_RESID, NPP> pipe;
     for (int ch = rc.c0 + rc.lw; ch < rc.c1; ch += rc.nw) {
         const int col = ch % g.S, t0 = (ch / g.S) * rc.per, t1 = min(rc.K, t0 + rc.per);
         if (t0 >= t1 || col + g.S * t0 >= g.nblk) continue;  // workgroup-uniform
-        sl.load(g, xrs, col, t0 - 1);
-        sl.store(g, win, t0 - 1);
-        sl.load(g, xrs, col, t0);
-        sl.store(g, win, t0);
-        sl.load(g, xrs, col, t0 + 1);
-        f.issue_ids(a, (col + g.S * t0) * kTplRows);
-        for (int t = t0; t < t1; ++t) {
-            const int blk = col + g.S * t;
-            if (blk >= g.nblk) break;  // uniform
-            const int r0 = blk * kTplRows;
-            sl.store(g, win, t + 1);
-#pragma unroll
-            for (int j = 0; j < R; ++j) cur.id[j] = f.id[j], cur.rr[j] = f.rr[j];
-            cur.issue_operands(a);
-            __syncthreads();  // slab t + 1 visible; the previous block's stage stores done
-            if (t + 1 < t1) {
-                sl.load(g, xrs, col, t + 2);
-                if (blk + g.S < g.nblk) f.issue_ids(a, (blk + g.S) * kTplRows);
-            }
+        pipe.run_chain(g, xrs, win, col, t0, t1, [&](int t, int blk, int r0, const TplFetch<KM_RESID, 1, true>& f) {
             const int* c = g.rslot[t & 3];
             // acc = b - old-value couplings in CSR order (tpl_gs_acc_kernel, MNE > 0 path)
             bool chain[R];
@@ -1672,9 +1680,9 @@ __global__ __launch_bounds__(kTPB, 4) void tpl_gs_ring_kernel(TplRingArgs g) {
             double acc[R], sold[R];
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                m[j] = (unsigned)hdr[cur.id[j]];
+                m[j] = (unsigned)hdr[f.id[j]];
                 full = full && m[j] == kFull;
-                acc[j] = cur.pb[j];
+                acc[j] = f.pb[j];
                 sold[j] = 0.0;
             }
             int rs = kTPB;
@@ -1715,9 +1723,9 @@ __global__ __launch_bounds__(kTPB, 4) void tpl_gs_ring_kernel(TplRingArgs g) {
             for (int j = 0; j < R; ++j) {
                 const int lr = tpl_lrow<true>(tid, j);
                 stage[(lr / B) * bs + (lr & (B - 1))] = acc[j];
-                sid[lr] = (uint8_t)cur.id[j];
-                if (NORM && cur.id[j] != kTplNone) {
-                    const double rr = cur.pb[j] - sold[j];
+                sid[lr] = (uint8_t)f.id[j];
+                if (NORM && f.id[j] != kTplNone) {
+                    const double rr = f.pb[j] - sold[j];
                     sq += rr * rr;
                 }
             }
@@ -1726,29 +1734,45 @@ __global__ __launch_bounds__(kTPB, 4) void tpl_gs_ring_kernel(TplRingArgs g) {
                 if (lane == 0) a.partial[g.part_off + 4 * blk + (tid >> 6)] = sq;
             }
             __syncthreads();  // acc and ids of the block in LDS
-            // the chain walk: lane c of wave 0 takes chunk c (rows c B .. c B + B - 1)
+            // the chain walk: lane c of wave 0 takes chunk c (rows c B .. c B + B - 1), eight rows
+            // per batch (B is a power of two >= 8): the batch's LDS reads first, then its chain
             if (tid < cpb) {
                 const double* xc = win + (t & 3) * g.wp - g.qlo;  // x of local row lr at xc[lr]
                 double* st = stage + tid * bs;
                 double prev = 0.0;
-                for (int u = 0; u < B; ++u) {
-                    const int k = BACK ? B - 1 - u : u;
-                    const int lr = tid * B + k;
-                    const int tp = sid[lr];
-                    double ac = st[k];
-                    if (u > 0 && scf[tp]) ac -= scv[tp] * prev;
-                    prev = xc[lr] + ac * sdl[tp];
-                    st[k] = prev;
+                for (int u0 = 0; u0 < B; u0 += 8) {
+                    int kk[8], tp[8];
+                    double ac[8], xv[8], dl[8], cv[8];
+                    bool has[8];
+#pragma unroll
+                    for (int v = 0; v < 8; ++v) {
+                        kk[v] = BACK ? B - 1 - (u0 + v) : u0 + v;
+                        tp[v] = sid[tid * B + kk[v]];
+                        ac[v] = st[kk[v]];
+                        xv[v] = xc[tid * B + kk[v]];
+                    }
+#pragma unroll
+                    for (int v = 0; v < 8; ++v) {
+                        dl[v] = sdl[tp[v]];
+                        cv[v] = scv[tp[v]];
+                        has[v] = (u0 + v > 0) && scf[tp[v]] != 0;
+                    }
+#pragma unroll
+                    for (int v = 0; v < 8; ++v) {
+                        double acv = ac[v];
+                        if (has[v]) acv -= cv[v] * prev;
+                        prev = xv[v] + acv * dl[v];
+                        st[kk[v]] = prev;
+                    }
                 }
             }
             __syncthreads();  // x' of the block in LDS
 #pragma unroll
             for (int j = 0; j < R; ++j) {
                 const int lr = tpl_lrow<true>(tid, j);
-                if (cur.id[j] != kTplNone) a.y[r0 + lr] = stage[(lr / B) * bs + (lr & (B - 1))];
+                if (f.id[j] != kTplNone) a.y[r0 + lr] = stage[(lr / B) * bs + (lr & (B - 1))];
             }
-        }
-        __syncthreads();
+        });
     }
 }
 

@@ -10,10 +10,12 @@ grep -v "amdgpu.ids" /tmp/t.log | tail -c 60000 > gpurun_out/${R}_tests.log
 tail -30 gpurun_out/${R}_tests.log
 echo "tests rc=$rc"
 [ $rc -ge 124 ] && exit 1
-for cfg in 7pt sa27; do
-  timeout -k 10 400 python bench.py --config $cfg --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${R}_$cfg.json 2> /tmp/b.err || { tail -c 2000 /tmp/b.err; exit 1; }
+for leg in 7pt:ring 7pt:noring sa27:ring sa27:noring sa27:nogsring; do
+  cfg=${leg%%:*}; v=${leg##*:}
+  case $v in noring) ev="AMG_TPL_RING=0";; nogsring) ev="AMG_GS_RING=0";; *) ev="AMG_NOTHING=0";; esac
+  env $ev timeout -k 10 400 python bench.py --config $cfg --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${R}_${cfg}_$v.json 2> /tmp/b.err || { tail -c 2000 /tmp/b.err; exit 1; }
   python -c "
-import json; d=json.load(open('gpurun_out/${R}_$cfg.json'))
-print('$cfg', d['value'], d['ms_per_step'], d['runtime'], d['config']['hipgraph'], d['roofline']['frac'])
+import json; d=json.load(open('gpurun_out/${R}_${cfg}_$v.json'))
+print('$leg', d['value'], d['ms_per_step'], d['runtime'], d['config']['hipgraph'], d['roofline']['frac'])
 for r in d['vcycle_kernels']: print('   ', r['level'], r['op'], r['us'], r['frac'])"
 done
