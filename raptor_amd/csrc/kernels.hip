@@ -1182,6 +1182,109 @@ __device__ __forceinline__ void tpl_row_bases(const TplLds& L, const double* (&w
     for (int j = 0; j < R; ++j) wr[j] = w0 + j * rs;
 }
 
+// The master's products of a lane's R rows, s[j] += v_e x_e in CSR order (masked entries add
+// +0.0: s + (+0.0) == s bit for bit, s starts at +0.0 and a round-to-nearest sum is never -0.0
+// unless both terms are).  With AMG_TPL_MASTER_EB > 0 the window reads of EB entries are all
+// issued before their products (the scheduler otherwise waited on LDS every two or three
+// entries: ~11 exposed LDS round trips per 27-pt block, profiles/r4_tpl_isa.txt).
+template <int MNE, int R, class Slot, class Val>
+__device__ __forceinline__ void tpl_master_sums(const double* const (&wr)[R], const unsigned (&m)[R], bool full,
+                                                Slot slot, Val val, double (&s)[R]) {
+    constexpr int EB = AMG_TPL_MASTER_EB > 0 ? (AMG_TPL_MASTER_EB < MNE ? AMG_TPL_MASTER_EB : MNE) : 1;
+    if (full) {
+#pragma unroll
+        for (int e0 = 0; e0 < MNE; e0 += EB) {
+            double xv[EB][R];
+#pragma unroll
+            for (int u = 0; u < EB; ++u)
+#pragma unroll
+                for (int j = 0; j < R; ++j) xv[u][j] = e0 + u < MNE ? wr[j][slot(e0 + u)] : 0.0;
+            if (AMG_TPL_MASTER_EB > 0) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < EB; ++u)
+#pragma unroll
+                for (int j = 0; j < R; ++j)
+                    if (e0 + u < MNE) s[j] = s[j] + val(e0 + u) * xv[u][j];
+        }
+    } else {
+#pragma unroll
+        for (int e0 = 0; e0 < MNE; e0 += EB) {
+            double xv[EB][R];
+#pragma unroll
+            for (int u = 0; u < EB; ++u)
+#pragma unroll
+                for (int j = 0; j < R; ++j) xv[u][j] = e0 + u < MNE ? wr[j][slot(e0 + u)] : 0.0;
+            if (AMG_TPL_MASTER_EB > 0) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < EB; ++u) {
+                const int e = e0 + u;
+                if (e >= MNE) continue;
+                const double v = val(e);
+#if AMG_TPL_MASK_BRANCH
+                double p[R];
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    p[j] = v * xv[u][j];
+                    asm volatile("" : "+v"(p[j]));
+                }
+#pragma unroll
+                for (int j = 0; j < R; ++j)
+                    if ((m[j] >> e) & 1u) {
+                        asm volatile("" : "+v"(s[j]));
+                        s[j] = s[j] + p[j];
+                    }
+#else
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    // the addend, not the add, is selected (a branch per entry serialised the reads)
+                    const double p = v * xv[u][j];
+                    s[j] = s[j] + (((m[j] >> e) & 1u) ? p : 0.0);
+                }
+#endif
+            }
+        }
+    }
+}
+
+// tpl_master_sums for the hybrid-GS old-value pass: acc[j] -= v_e x_e over the master's
+// entries except the chain coupling EC of a row whose chain neighbour is in its chunk, sold[j]
+// (NORM) += every product of the row (its A x for the residual norm); the same batched reads
+template <int MNE, int EC, bool NORM, int R, class Slot, class Val>
+__device__ __forceinline__ void tpl_master_gs_sums(const double* const (&wr)[R], const unsigned (&m)[R], bool full,
+                                                   const bool (&chain)[R], Slot slot, Val val, double (&acc)[R],
+                                                   double (&sold)[R]) {
+    constexpr int EB = AMG_TPL_GS_EB > 0 ? (AMG_TPL_GS_EB < MNE ? AMG_TPL_GS_EB : MNE) : 1;
+#pragma unroll
+    for (int e0 = 0; e0 < MNE; e0 += EB) {
+        double xv[EB][R];
+#pragma unroll
+        for (int u = 0; u < EB; ++u)
+#pragma unroll
+            for (int j = 0; j < R; ++j) xv[u][j] = e0 + u < MNE ? wr[j][slot(e0 + u)] : 0.0;
+        if (AMG_TPL_GS_EB > 0) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+            const int e = e0 + u;
+            if (e >= MNE) continue;
+            const double v = val(e);
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const double p = v * xv[u][j];
+                if (full) {
+                    if (NORM) sold[j] = sold[j] + p;
+                    if (e == EC) acc[j] = acc[j] - (chain[j] ? 0.0 : p);
+                    else acc[j] = acc[j] - p;
+                } else {
+                    // selected addends (tpl_rows_master): acc - (+0.0) == acc for every acc
+                    const bool in = (m[j] >> e) & 1u;
+                    if (NORM) sold[j] = sold[j] + (in ? p : 0.0);
+                    acc[j] = acc[j] - (in && !(e == EC && chain[j]) ? p : 0.0);
+                }
+            }
+        }
+    }
+}
+
 template <int MODE, bool NORM, int MNE>
 __device__ __forceinline__ double tpl_rows_master(const TplArgs& a, const TplLds& L, int r0, const int* id,
                                                   const double* pb, const double* py) {
@@ -1201,47 +1304,7 @@ __device__ __forceinline__ double tpl_rows_master(const TplArgs& a, const TplLds
     double s[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) s[j] = 0.0;
-    if (__all(full)) {
-#pragma unroll
-        for (int e = 0; e < MNE; ++e) {
-            const double v = a.mval[e];
-            const int c = a.mslot[e];
-#pragma unroll
-            for (int j = 0; j < R; ++j) s[j] = s[j] + v * wr[j][c];
-        }
-    } else {
-#pragma unroll
-        for (int e = 0; e < MNE; ++e) {
-            const double v = a.mval[e];
-            const int c = a.mslot[e];
-#if AMG_TPL_MASK_BRANCH
-            // exec-masked adds: the products are formed unconditionally (the asm pins them
-            // before the branch, so the LDS reads are not sunk into it), the add runs only in
-            // the lanes whose row has the entry
-            double p[R];
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                p[j] = v * wr[j][c];
-                asm volatile("" : "+v"(p[j]));
-            }
-#pragma unroll
-            for (int j = 0; j < R; ++j)
-                if ((m[j] >> e) & 1u) {
-                    asm volatile("" : "+v"(s[j]));
-                    s[j] = s[j] + p[j];
-                }
-#else
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                // the addend, not the add, is selected: s + (+0.0) == s bit for bit (s starts at
-                // +0.0 and a round-to-nearest sum is never -0.0 unless both terms are), and the
-                // load stays unconditional (a branch per entry serialised the LDS reads)
-                const double p = v * wr[j][c];
-                s[j] = s[j] + (((m[j] >> e) & 1u) ? p : 0.0);
-            }
-#endif
-        }
-    }
+    tpl_master_sums<MNE, R>(wr, m, __all(full), [&](int e) { return a.mslot[e]; }, [&](int e) { return a.mval[e]; }, s);
     double sq = 0.0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -1506,24 +1569,7 @@ __device__ __forceinline__ double tpl_rows_ring(const TplArgs& a, const double* 
     double s[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) s[j] = 0.0;
-    if (__all(full)) {
-#pragma unroll
-        for (int e = 0; e < MNE; ++e) {
-            const double v = a.mval[e];
-#pragma unroll
-            for (int j = 0; j < R; ++j) s[j] = s[j] + v * wr[j][c[e]];
-        }
-    } else {
-#pragma unroll
-        for (int e = 0; e < MNE; ++e) {
-            const double v = a.mval[e];
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                const double p = v * wr[j][c[e]];
-                s[j] = s[j] + (((m[j] >> e) & 1u) ? p : 0.0);
-            }
-        }
-    }
+    tpl_master_sums<MNE, R>(wr, m, __all(full), [&](int e) { return c[e]; }, [&](int e) { return a.mval[e]; }, s);
     double sq = 0.0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -1693,31 +1739,12 @@ __global__ __launch_bounds__(kTPB, 4) void tpl_gs_ring_kernel(TplRingArgs g) {
             const double* wr[R];
 #pragma unroll
             for (int j = 0; j < R; ++j) wr[j] = w0 + j * rs;
-            if (__all(full)) {
-#pragma unroll
-                for (int e = 0; e < MNE; ++e) {
-                    const double v = a.mval[e];
-#pragma unroll
-                    for (int j = 0; j < R; ++j) {
-                        const double p = v * wr[j][c[e]];
-                        if (NORM) sold[j] = sold[j] + p;
-                        if (e == EC) acc[j] = acc[j] - (chain[j] ? 0.0 : p);
-                        else acc[j] = acc[j] - p;
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int e = 0; e < MNE; ++e) {
-                    const double v = a.mval[e];
-#pragma unroll
-                    for (int j = 0; j < R; ++j) {
-                        const double p = v * wr[j][c[e]];
-                        const bool in = (m[j] >> e) & 1u;
-                        if (NORM) sold[j] = sold[j] + (in ? p : 0.0);
-                        acc[j] = acc[j] - (in && !(e == EC && chain[j]) ? p : 0.0);
-                    }
-                }
-            }
+            if (__all(full))
+                tpl_master_gs_sums<MNE, EC, NORM, R>(wr, m, true, chain, [&](int e) { return c[e]; },
+                                                     [&](int e) { return a.mval[e]; }, acc, sold);
+            else
+                tpl_master_gs_sums<MNE, EC, NORM, R>(wr, m, false, chain, [&](int e) { return c[e]; },
+                                                     [&](int e) { return a.mval[e]; }, acc, sold);
             double sq = 0.0;
 #pragma unroll
             for (int j = 0; j < R; ++j) {
@@ -2038,34 +2065,12 @@ __global__ __launch_bounds__(kTPB, 6) void tpl_gs_acc_kernel(TplGsArgs g) {
         }
         const double* wr[R];
         tpl_row_bases<R>(L, wr);
-        if (__all(full)) {
-#pragma unroll
-            for (int e = 0; e < MNE; ++e) {
-                const double v = a.mval[e];
-                const int c = a.mslot[e];
-#pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    const double p = v * wr[j][c];
-                    if (NORM) sold[j] = sold[j] + p;
-                    if (e == EC) acc[j] = acc[j] - (chain[j] ? 0.0 : p);
-                    else acc[j] = acc[j] - p;
-                }
-            }
-        } else {
-#pragma unroll
-            for (int e = 0; e < MNE; ++e) {
-                const double v = a.mval[e];
-                const int c = a.mslot[e];
-#pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    // selected addends (tpl_rows_master): acc - (+0.0) == acc for every acc
-                    const double p = v * wr[j][c];
-                    const bool in = (m[j] >> e) & 1u;
-                    if (NORM) sold[j] = sold[j] + (in ? p : 0.0);
-                    acc[j] = acc[j] - (in && !(e == EC && chain[j]) ? p : 0.0);
-                }
-            }
-        }
+        if (__all(full))
+            tpl_master_gs_sums<MNE, EC, NORM, R>(wr, m, true, chain, [&](int e) { return a.mslot[e]; },
+                                                 [&](int e) { return a.mval[e]; }, acc, sold);
+        else
+            tpl_master_gs_sums<MNE, EC, NORM, R>(wr, m, false, chain, [&](int e) { return a.mslot[e]; },
+                                                 [&](int e) { return a.mval[e]; }, acc, sold);
 #pragma unroll
         for (int j = 0; j < R; ++j)
             if (f.id[j] != kTplNone) {
