@@ -66,10 +66,10 @@ constexpr int kTplMaxLen = 64;     // entries per template
 #define AMG_TPL_SPLIT_READS 1
 #endif
 #ifndef AMG_TPL_MASTER_EB  // build-time knob: uniform-stencil window reads issued per batch (0: scheduler's choice)
-#define AMG_TPL_MASTER_EB 9
+#define AMG_TPL_MASTER_EB 0
 #endif
 #ifndef AMG_TPL_GS_EB  // build-time knob: the same for the hybrid-GS old-value pass (more live values per entry)
-#define AMG_TPL_GS_EB 5
+#define AMG_TPL_GS_EB 0
 #endif
 #ifndef AMG_TPL_MASK_BRANCH  // build-time knob: masked uniform-stencil rows add under exec masks
 #define AMG_TPL_MASK_BRANCH 0

@@ -2511,8 +2511,10 @@ int kernel_variant(const DevMatrix& A) {
     // one master's subsequences (DevMatrix::tpl_mne; AMG_TPL_MASTER=0 at build turns it off)
     if (!ev && A.tpl_mne > 0) var |= 512;
     if (A.tpl_mne == 0) var &= ~512;
-    // 1024: plane-ring marching of uniform-stencil rows, default where the
-    // master splits into planes (DevMatrix::tpl_ring_s; AMG_TPL_RING=0 at build: off)
+    // 1024: plane-ring marching of uniform-stencil rows where the master
+    // splits into planes (DevMatrix::tpl_ring_s, found only with AMG_TPL_RING=1 at matrix
+    // creation: measured slower than the z-march (7-pt) and the one-shot window kernel (27-pt),
+    // profiles/r4_ring_ab.txt)
     if (!ev && A.tpl_mne > 0 && A.tpl_ring_s > 0) var |= 1024;
     if (A.tpl_mne == 0 || A.tpl_ring_s == 0 || !(var & 512)) var &= ~1024;
     return var;

@@ -560,8 +560,8 @@ static void find_plane_ring(DevMatrix& D, const std::vector<int>& moff) {
     D.tpl_ring_s = D.tpl_ring_qlo = D.tpl_ring_wp = 0;
     D.tpl_ring_dz.clear();
     D.tpl_ring_mq.clear();
-    const char* env = std::getenv("AMG_TPL_RING");
-    if (env && std::atoi(env) == 0) return;
+    const char* env = std::getenv("AMG_TPL_RING");  // opt-in (kernel_variant: r4_ring_ab.txt)
+    if (!(env && std::atoi(env) == 1)) return;
     if (D.n_rows % 2 != 0) return;  // 16-byte pair loads never straddle the end of x
     int64_t best_wp = INT64_MAX, best_d = 0;
     std::vector<int64_t> cand;
@@ -1397,12 +1397,12 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
     int64_t ell_rows = 0;
     for (const int4& sl : slabs) ell_rows += sl.y;
     gs_bytes = (gs_ndict > 0 ? 5 : 12) * 64 * cells + 16 * (int64_t)slabs.size() + 32 * ell_rows;
-    // the fused plane-ring sweep: a uniform 3D stencil whose every block is on
-    // the GS template path, whole 512-row blocks, chunks of 8..512 rows; AMG_GS_RING=0: the
-    // acc + chain kernel pair
+    // the fused plane-ring sweep (AMG_GS_RING=1): a uniform 3D stencil whose
+    // every block is on the GS template path, whole 512-row blocks, chunks of 8..512 rows;
+    // otherwise the acc + chain kernel pair
     {
-        const char* e = std::getenv("AMG_GS_RING");
-        gs_ring = !(e && *e && std::atoi(e) == 0) && n_gs_tblk > 0 && n_gs_tblk == tpl_blocks() && tpl_mne > 0 &&
+        const char* e = std::getenv("AMG_GS_RING");  // opt-in: slower than the pair (r4_ring_ab.txt)
+        gs_ring = (e && *e && std::atoi(e) == 1) && n_gs_tblk > 0 && n_gs_tblk == tpl_blocks() && tpl_mne > 0 &&
                   tpl_ring_s > 0 && gs_tmask.p && n_rows % kTplRows == 0 && B >= 8 && kTplRows % B == 0;
     }
     // template rows: acc kernel 1 B id + b + x (window) + acc out; chain kernel acc + x + id + y;

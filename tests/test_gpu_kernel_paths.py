@@ -111,7 +111,7 @@ def test_template_window_lanes(ctx, oracle, monkeypatch, kind, dims, npl, path):
     copies its reused slots inside LDS) at every lanes-per-row instantiation, all modes + norm,
     with uniform-stencil rows (MNE = 7 / 27: every template a subsequence of the master, bit
     512) and with the per-template tables (generic); and the plane ring (tpl_ring_kernel,
-    bit 1024, the default for uniform 3D stencils: DESIGN.md 4.0 r4)."""
+    bit 1024, opt-in with AMG_TPL_RING=1 for uniform 3D stencils: DESIGN.md 4.0 r4)."""
     import raptor_amd as ra
 
     O = oracle
@@ -124,6 +124,7 @@ def test_template_window_lanes(ctx, oracle, monkeypatch, kind, dims, npl, path):
     if path == "window":
         monkeypatch.setenv("AMG_TPL_RING", "0")
     if path == "ring":
+        monkeypatch.setenv("AMG_TPL_RING", "1")
         monkeypatch.setenv("AMG_TPL_MARCH_CHUNKS", "2")  # long chains: every ring phase
     if path.endswith("march"):
         monkeypatch.setenv("AMG_KERNEL_VARIANT", "170" if path == "generic_march" else str(170 | 512))
@@ -160,6 +161,7 @@ def test_template_plane_ring(ctx, oracle, monkeypatch, kind, dims, chunks):
     import raptor_amd as ra
 
     O = oracle
+    monkeypatch.setenv("AMG_TPL_RING", "1")
     if chunks != "0":
         monkeypatch.setenv("AMG_TPL_MARCH_CHUNKS", chunks)
     Ao = (O.gen_7pt if kind == "7pt" else O.gen_27pt)(*dims)
@@ -358,7 +360,7 @@ GS_SHAPES = [("27pt", (260, 8, 8)), ("27pt", (40, 40, 40)), ("7pt", (37, 41, 29)
              ("27pt", (64, 32, 16)), ("7pt", (32, 32, 24))]
 
 
-@pytest.mark.parametrize("tpl_gs", ["templates", "pair", "generic", "ell", "split"])
+@pytest.mark.parametrize("tpl_gs", ["templates", "ring", "generic", "ell", "split"])
 @pytest.mark.parametrize("kind,dims", GS_SHAPES, ids=[f"{k}-{'x'.join(map(str, d))}" for k, d in GS_SHAPES])
 def test_hybrid_gs_template_kernel(ctx, oracle, monkeypatch, kind, dims, tpl_gs):
     """l1 hybrid GS, forward / backward, block sizes 64, 32, 8, 1 (the template kernel needs B
@@ -366,14 +368,15 @@ def test_hybrid_gs_template_kernel(ctx, oracle, monkeypatch, kind, dims, tpl_gs)
     (NPL 16, 8 and 4 windows; a last partial block), with the template kernel on -- uniform-
     stencil masks (7-pt, 27-pt) or per-template tables (generic) -- and off: the one-kernel
     sliced-ELL sweep (ell) or the split sweep (KM_GSACC block pass + chain walk, 4.2c).
-    templates: the fused plane-ring sweep (tpl_gs_ring_kernel) where it applies (uniform 3D
-    stencil, n a multiple of 512 rows, 8 <= B | 512), else the acc + chain pair; pair: the pair
-    always (AMG_GS_RING=0)."""
+    templates: the acc + chain pair (the default); ring: the fused plane-ring sweep
+    (tpl_gs_ring_kernel, AMG_TPL_RING=1 AMG_GS_RING=1) where it applies (uniform 3D stencil, n
+    a multiple of 512 rows, 8 <= B | 512), else the pair."""
     import raptor_amd as ra
 
     O = oracle
-    if tpl_gs == "pair":
-        monkeypatch.setenv("AMG_GS_RING", "0")
+    if tpl_gs == "ring":
+        monkeypatch.setenv("AMG_TPL_RING", "1")
+        monkeypatch.setenv("AMG_GS_RING", "1")
     if tpl_gs in ("ell", "split"):
         monkeypatch.setenv("AMG_GS_TEMPLATES", "0")
     if tpl_gs == "split":
