@@ -23,6 +23,9 @@ step sa27 400 python bench.py --config sa27 --steps 20 --warmup 5 --cpu-seconds 
 step g3sub 400 python bench.py --config g3sub --steps 20 --warmup 5 --cpu-seconds 8
 step n2 400 env AMG_BENCH_SHARED_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu-baseline --spmv-reps 5
 step n8 900 env AMG_BENCH_SHARED_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 8 --steps 5 --warmup 2 --no-cpu-baseline --spmv-reps 3
+if [ -n "$WITH_SETUP" ]; then
+  step setup8 600 env AMG_TIMING=1 python -u scripts/setup_ranks.py 256 8 boxes
+fi
 python - <<'PY'
 import json, os
 R = os.environ.get("R", "r4c")
