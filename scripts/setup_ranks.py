@@ -5,12 +5,14 @@ N loopback ranks (threads sharing this GPU), for SURVEY.md 8f row f1 (VERDICT r3
 
 Prints one JSON line: setup seconds per rank count.  The phase timers go to stderr (rank 0)."""
 import json
+import os
 import sys
 import threading
 import time
 import uuid
 
-import raptor_amd as ra
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import raptor_amd as ra  # noqa: E402
 
 
 def main():
