@@ -285,11 +285,9 @@ struct ARows {
 // sign opposite to a_kk.  Same loops and order as host_setup.cpp interp_classical().
 // cf / cmap of halo points through R.D (hcf, hcmap); P columns are global coarse ids.
 template <bool FILL>
-__global__ void interp_kernel(ARows R, DCsr S, const int* cf, const int* hcf, const int* cmap,
-                              const int* hcmap, int* cnt, const int* prp, int* pcol, double* pval) {
+__device__ void interp_row_serial(const ARows& R, const DCsr& S, const int* cf, const int* hcf, const int* cmap,
+                                  const int* hcmap, int* cnt, const int* prp, int* pcol, double* pval, int i) {
     const DCsr& A = R.A;
-    const int i = blockIdx.x * kT + threadIdx.x;
-    if (i >= A.n) return;
     if (cf[i] == ST_C) {
         if (FILL) {
             pcol[prp[i]] = cmap[i];
@@ -380,6 +378,146 @@ __global__ void interp_kernel(ARows R, DCsr S, const int* cf, const int* hcf, co
         }
     }
     for (q = q0; q < q0 + nci; ++q) pval[q] = -pval[q] / d;
+}
+
+template <bool FILL>
+__global__ void interp_kernel(ARows R, DCsr S, const int* cf, const int* hcf, const int* cmap,
+                              const int* hcmap, int* cnt, const int* prp, int* pcol, double* pval) {
+    const int i = blockIdx.x * kT + threadIdx.x;
+    if (i < R.A.n) interp_row_serial<FILL>(R, S, cf, hcf, cmap, hcmap, cnt, prp, pcol, pval, i);
+}
+
+// Wave-per-row form of interp_kernel for operators with long rows (the Galerkin levels: a
+// thread per row walked 50-100-entry rows and their neighbours' rows serially, 13-52 ms per
+// launch on grids of 3-4,249 workgroups).  The same sums in the same order:
+//  * lanes classify the row's entries (strong / C / diagonal) into LDS and form s_k of the
+//    strong F neighbours, one neighbour per lane (s_k's own loop is serial, as in s_of);
+//  * lane 0 forms d in the host's two passes (weak couplings in row order, then the strong F
+//    neighbours with s_k == 0 in row order);
+//  * lane q forms num_j of the q-th strong C neighbour: a_ij, then + (a_ik a_kj) / s_k over the
+//    strong F neighbours k in row order -- one accumulator per lane, the host's k order.
+// Rows longer than kIwMax entries run interp_kernel's loops on lane 0.
+constexpr int kIwWaves = 4, kIwMax = 512;
+enum { IW_STRONG = 1, IW_C = 2, IW_DIAG = 4, IW_POS = 8 };
+
+template <bool FILL>
+__device__ void interp_row_serial(const ARows& R, const DCsr& S, const int* cf, const int* hcf, const int* cmap,
+                                  const int* hcmap, int* cnt, const int* prp, int* pcol, double* pval, int i);
+
+template <bool FILL>
+__global__ __launch_bounds__(64 * kIwWaves) void interp_wave_kernel(ARows R, DCsr S, const int* cf, const int* hcf,
+                                                                    const int* cmap, const int* hcmap, int* cnt,
+                                                                    const int* prp, int* pcol, double* pval) {
+    __shared__ unsigned char fl_s[kIwWaves][kIwMax];
+    __shared__ double sv_s[kIwWaves][kIwMax];
+    const DCsr& A = R.A;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i = blockIdx.x * kIwWaves + w;
+    if (i >= A.n) return;  // wave-uniform
+    unsigned char* fl = fl_s[w];
+    double* sv = sv_s[w];
+    const int b0 = A.rp[i], e0 = A.rp[i + 1], len = e0 - b0;
+    if (cf[i] == ST_C || len > kIwMax) {
+        if (lane == 0) interp_row_serial<FILL>(R, S, cf, hcf, cmap, hcmap, cnt, prp, pcol, pval, i);
+        return;
+    }
+    const int gi = A.lo + i;
+    auto is_c = [&](int g) { return R.D.get(cf, hcf, g) == ST_C; };
+    auto in_ci = [&](int m) { return m != gi && strong(S, i, m) && is_c(m); };
+    // entry classes; nci = strong C neighbours
+    int nci = 0;
+    for (int k0 = 0; k0 < len; k0 += 64) {
+        const int k = k0 + lane;
+        unsigned char f = 0;
+        if (k < len) {
+            const int j = A.col[b0 + k];
+            if (j == gi) {
+                f = IW_DIAG;
+            } else if (strong(S, i, j)) {
+                f = IW_STRONG | (is_c(j) ? IW_C : 0);
+            }
+            fl[k] = f;
+        }
+        nci += __popcll(__ballot(f == (IW_STRONG | IW_C)));
+    }
+    if (!FILL) {
+        if (lane == 0) cnt[i] = nci;
+        return;
+    }
+    if (nci == 0) return;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // s_k of the strong F neighbours (interp_kernel's s_of), one per lane
+    for (int k0 = 0; k0 < len; k0 += 64) {
+        const int k = k0 + lane;
+        if (k < len && fl[k] == IW_STRONG) {
+            const int kk = A.col[b0 + k];
+            int b, e;
+            const int* rc;
+            const double* rv;
+            R.row(kk, b, e, rc, rv);
+            double akk = 0.0;
+            for (int u = b; u < e; ++u)
+                if (rc[u] == kk) {
+                    akk = rv[u];
+                    break;
+                }
+            const bool pos = akk > 0.0;
+            double sk = 0.0;
+            for (int u = b; u < e; ++u) {
+                const double v = rv[u];
+                if ((pos ? v < 0.0 : v > 0.0) && in_ci(rc[u])) sk += v;
+            }
+            sv[k] = sk;
+            if (pos) fl[k] = IW_STRONG | IW_POS;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // d: a_ii (first diagonal entry), + weak couplings in row order, + strong F with s_k == 0
+    double d = 0.0;
+    if (lane == 0) {
+        for (int k = 0; k < len; ++k)
+            if (fl[k] & IW_DIAG) {
+                d = A.val[b0 + k];
+                break;
+            }
+        for (int k = 0; k < len; ++k)
+            if (fl[k] == 0) d += A.val[b0 + k];
+        for (int k = 0; k < len; ++k)
+            if ((fl[k] & (IW_STRONG | IW_C)) == IW_STRONG && sv[k] == 0.0) d += A.val[b0 + k];
+    }
+    d = __shfl(d, 0, 64);
+    // num_j, lane = strong C neighbour (q order = row order)
+    const int q0 = prp[i];
+    int qbase = 0;
+    for (int k0 = 0; k0 < len; k0 += 64) {
+        const int kj = k0 + lane;
+        const bool isc = kj < len && fl[kj] == (IW_STRONG | IW_C);
+        const unsigned long long m = __ballot(isc);
+        if (isc) {
+            const int q = qbase + __popcll(m & ((1ull << lane) - 1ull));
+            const int j = A.col[b0 + kj];
+            double num = A.val[b0 + kj];
+            for (int k = 0; k < len; ++k) {
+                const unsigned char f = fl[k];
+                if ((f & (IW_STRONG | IW_C)) != IW_STRONG) continue;
+                const double sk = sv[k];
+                if (sk == 0.0) continue;
+                const int kk = A.col[b0 + k];
+                int b, e;
+                const int* rc;
+                const double* rv;
+                R.row(kk, b, e, rc, rv);
+                const int uj = dfind(rc, b, e, j);
+                const bool pos = (f & IW_POS) != 0;
+                if (uj >= 0 && (pos ? rv[uj] < 0.0 : rv[uj] > 0.0)) num += (A.val[b0 + k] * rv[uj]) / sk;
+            }
+            pcol[q0 + q] = R.D.get(cmap, hcmap, j);
+            pval[q0 + q] = -num / d;
+        }
+        qbase += __popcll(m);
+    }
 }
 
 // ---- MIS(2) aggregation -----------------------------------------------------------------
@@ -775,14 +913,26 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
         DevBuf<double> pval;
         pcnt.alloc((size_t)n + 1);
         HIP_CHECK(hipMemsetAsync(pcnt.p, 0, sizeof(int) * pcnt.n, s));
-        if (n)
+        // long rows (the Galerkin levels): a wave per row (interp_wave_kernel); AMG_INTERP_WAVE_NPR
+        // sets the average row length from which it is taken (default 12; 0: always)
+        const char* wenv = std::getenv("AMG_INTERP_WAVE_NPR");
+        const int wave_npr = wenv && *wenv ? std::atoi(wenv) : 12;
+        const bool wave = n > 0 && A.nnz() >= (int64_t)wave_npr * n;
+        const dim3 wgrid((unsigned)((n + kIwWaves - 1) / kIwWaves)), wblk(64 * kIwWaves);
+        if (n && wave)
+            hipLaunchKernelGGL(interp_wave_kernel<false>, wgrid, wblk, 0, s, Ar, Sv, cf.p, acf.p, cmap.p, acmap.p,
+                               pcnt.p, nullptr, nullptr, nullptr);
+        else if (n)
             hipLaunchKernelGGL(interp_kernel<false>, dim3(grid1(n)), dim3(kT), 0, s, Ar, Sv, cf.p, acf.p, cmap.p,
                                acmap.p, pcnt.p, nullptr, nullptr, nullptr);
         prp.alloc((size_t)n + 1);
         const int64_t pnnz = exclusive_scan(s, pcnt.p, prp.p, n, tmp);
         pcol.alloc((size_t)std::max<int64_t>(pnnz, 1));
         pval.alloc((size_t)std::max<int64_t>(pnnz, 1));
-        if (n)
+        if (n && wave)
+            hipLaunchKernelGGL(interp_wave_kernel<true>, wgrid, wblk, 0, s, Ar, Sv, cf.p, acf.p, cmap.p, acmap.p,
+                               nullptr, prp.p, pcol.p, pval.p);
+        else if (n)
             hipLaunchKernelGGL(interp_kernel<true>, dim3(grid1(n)), dim3(kT), 0, s, Ar, Sv, cf.p, acf.p, cmap.p,
                                acmap.p, nullptr, prp.p, pcol.p, pval.p);
         HIP_CHECK(hipGetLastError());

@@ -259,13 +259,21 @@ def test_spgemm_large_rows(ctx, oracle):
     assert same_csr(C.to_scipy_local(), (Ao @ Ao).to_scipy())
 
 
+@pytest.mark.parametrize("interp", ["default", "wave", "thread"])
 @pytest.mark.parametrize("kind,dims,coarsen", [("7pt", (22, 21, 20), "pmis"), ("27pt", (30, 28, 26), "sa"),
                                                ("5pt", (70, 61), "pmis"), ("7pt", (19, 18, 17), "sa")])
-def test_device_setup_equals_host(ctx, oracle, kind, dims, coarsen):
+def test_device_setup_equals_host(ctx, oracle, monkeypatch, kind, dims, coarsen, interp):
     """setup_device = 1 (strength, PMIS / MIS(2), P and R = P^T on the GPU, SURVEY 8f row
     f1), 2 (Galerkin SpGEMM only) and 0 (host): identical hierarchies -- every level's A,
-    P, R and integer split bit for bit -- and R A P via matmat reproduces A_1."""
+    P, R and integer split bit for bit -- and R A P via matmat reproduces A_1.  Classical
+    interpolation with a wave per row on every level (wave), a thread per row everywhere
+    (thread), or the default rule (a wave per row from 12 entries per row on average)."""
     import raptor_amd as ra
+
+    if interp != "default" and coarsen != "pmis":
+        pytest.skip("classical interpolation only")
+    if interp != "default":
+        monkeypatch.setenv("AMG_INTERP_WAVE_NPR", "0" if interp == "wave" else "1000000")
 
     A = ra.par_stencil_grid(ctx, kind, dims)
     ms = [ra.ParMultilevel(coarsen=coarsen, setup_device=m).setup(A) for m in (1, 2, 0)]
