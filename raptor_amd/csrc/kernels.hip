@@ -3197,20 +3197,10 @@ void launch_gs_chain(hipStream_t s, const DevMatrix& A, const double* x, const d
              ns, nullptr, nullptr, nullptr, 0, 0};
     AMG_ASSERT(A.gs_cmaxw[d] <= 64);  // <= 63: in-chunk couplings of a <= 64-row chunk
     AMG_ASSERT(A.gs_cbucket[d][kGsChainBuckets] == ns);
-    // one launch per width bucket (slabs ordered by bucket at build): each sized for its
-    // own queue, so narrow slabs run at full occupancy beside a few wide ones.
-    // AMG_GS_CHAIN_BUCKETS=0 (A/B): one launch over every slab, the widest slab's queue
-    static const bool buckets = [] {
-        const char* e = std::getenv("AMG_GS_CHAIN_BUCKETS");
-        return !(e && *e && std::atoi(e) == 0);
-    }();
-    const int qmax = gs_chain_bucket(A.gs_cmaxw[d]);
+    // one launch per non-empty width bucket (DevMatrix::gs_cbucket: by default every slab is
+    // in the widest slab's bucket, one launch; AMG_GS_CHAIN_BUCKETS=1 sorts them by width)
     for (int q = 0; q < kGsChainBuckets; ++q) {
-        int b0 = A.gs_cbucket[d][q], b1 = A.gs_cbucket[d][q + 1];
-        if (!buckets) {
-            if (q != qmax) continue;
-            b0 = 0, b1 = ns;
-        }
+        const int b0 = A.gs_cbucket[d][q], b1 = A.gs_cbucket[d][q + 1];
         if (b1 <= b0) continue;
         a.slab0 = b0;
         a.nslab = b1;

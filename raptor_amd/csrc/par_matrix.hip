@@ -1513,15 +1513,22 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
                         }
                     }
                 }
-                // slabs grouped by the LDS queue their width needs (kGsChainW buckets), one
-                // chain launch per bucket: one wide slab no longer sizes every wave's queue
-                // (W = 64 is 48 KiB per 64-lane workgroup, 3 waves per CU).  The order of the
-                // slabs is free: each slab's rows are its own.
-                std::stable_sort(cs.begin(), cs.end(), [](const int4& a, const int4& b) {
-                    return gs_chain_bucket(a.w) < gs_chain_bucket(b.w);
-                });
+                // AMG_GS_CHAIN_BUCKETS=1: slabs grouped by the LDS queue their width needs
+                // (kGsChainW buckets), one chain launch per bucket, so one wide slab does not
+                // size every wave's queue.  Measured slower (g3sub 1560 -> 1360 V-cycles/s:
+                // the sweeps were not faster and the coarse levels paid the extra launches,
+                // profiles/r4f_g3sub_buckets.txt), so by default every slab sits in the
+                // widest slab's bucket: one launch.  The order of the slabs is free.
+                const char* be = std::getenv("AMG_GS_CHAIN_BUCKETS");
+                const bool by_width = be && *be && std::atoi(be) == 1;
+                if (by_width)
+                    std::stable_sort(cs.begin(), cs.end(), [](const int4& a, const int4& b) {
+                        return gs_chain_bucket(a.w) < gs_chain_bucket(b.w);
+                    });
+                int wmax = 0;
+                for (const int4& sl : cs) wmax = std::max(wmax, sl.w);
                 for (int q = 0; q <= kGsChainBuckets; ++q) gs_cbucket[d][q] = 0;
-                for (const int4& sl : cs) ++gs_cbucket[d][gs_chain_bucket(sl.w) + 1];
+                for (const int4& sl : cs) ++gs_cbucket[d][gs_chain_bucket(by_width ? sl.w : wmax) + 1];
                 for (int q = 0; q < kGsChainBuckets; ++q) gs_cbucket[d][q + 1] += gs_cbucket[d][q];
                 gs_cslabs[d].upload(cs.data(), cs.size());
                 gs_ccol[d].upload(ccol.data(), ccol.size());

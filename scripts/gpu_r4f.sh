@@ -13,4 +13,9 @@ for cfg in 7pt g3sub; do
   python scripts/trace_summary.py gpurun_out/${R}_prof_$cfg/run_kernel_trace.csv > gpurun_out/${R}_${cfg}_trace_summary.txt
   head -25 gpurun_out/${R}_${cfg}_trace_summary.txt
 done
+for v in 1 0 1 0; do
+  AMG_GS_CHAIN_BUCKETS=$v timeout -k 10 300 python bench.py --config g3sub --steps 40 --warmup 5 --no-cpu-baseline > gpurun_out/${R}_g3sub_b$v.json 2> /tmp/g.err || { tail -5 /tmp/g.err; exit 1; }
+  python -c "
+import json; d=json.load(open('gpurun_out/${R}_g3sub_b$v.json')); print('g3sub buckets=$v', d['value'], d['ms_per_step'], [(r['level'], r['op'][:6], r['us']) for r in d['vcycle_kernels'] if 'GS' in r['op']])"
+done
 echo r4f-done

@@ -360,7 +360,7 @@ GS_SHAPES = [("27pt", (260, 8, 8)), ("27pt", (40, 40, 40)), ("7pt", (37, 41, 29)
              ("27pt", (64, 32, 16)), ("7pt", (32, 32, 24))]
 
 
-@pytest.mark.parametrize("tpl_gs", ["templates", "ring", "generic", "ell", "split"])
+@pytest.mark.parametrize("tpl_gs", ["templates", "ring", "generic", "ell", "split", "split_buckets"])
 @pytest.mark.parametrize("kind,dims", GS_SHAPES, ids=[f"{k}-{'x'.join(map(str, d))}" for k, d in GS_SHAPES])
 def test_hybrid_gs_template_kernel(ctx, oracle, monkeypatch, kind, dims, tpl_gs):
     """l1 hybrid GS, forward / backward, block sizes 64, 32, 8, 1 (the template kernel needs B
@@ -377,10 +377,12 @@ def test_hybrid_gs_template_kernel(ctx, oracle, monkeypatch, kind, dims, tpl_gs)
     if tpl_gs == "ring":
         monkeypatch.setenv("AMG_TPL_RING", "1")
         monkeypatch.setenv("AMG_GS_RING", "1")
-    if tpl_gs in ("ell", "split"):
+    if tpl_gs in ("ell", "split", "split_buckets"):
         monkeypatch.setenv("AMG_GS_TEMPLATES", "0")
-    if tpl_gs == "split":
+    if tpl_gs.startswith("split"):
         monkeypatch.setenv("AMG_GS_SPLIT_NPR", "0")
+        if tpl_gs == "split_buckets":  # chain walk launched per width bucket
+            monkeypatch.setenv("AMG_GS_CHAIN_BUCKETS", "1")
     else:
         monkeypatch.setenv("AMG_GS_SPLIT", "0")
     if tpl_gs == "generic":
@@ -397,9 +399,9 @@ def test_hybrid_gs_template_kernel(ctx, oracle, monkeypatch, kind, dims, tpl_gs)
         assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs(x, b, blk)), ("fwd", blk)
         A.hybrid_gs(dx, db, out, blk, backward=True)
         assert np.array_equal(to_host(ctx, out), Ao.hybrid_gs_backward(x, b, blk)), ("bwd", blk)
-        assert A._info()["gs_split"] == (tpl_gs == "split"), blk
+        assert A._info()["gs_split"] == tpl_gs.startswith("split"), blk
     assert A._info()["gs_bytes"] > 0
-    if tpl_gs == "split":
+    if tpl_gs.startswith("split"):
         return
     # B = 8: every shape here has no in-chunk coupling but +-1 -> template kernels (50 B per
     # row + table) when they are on, sliced ELL (>= 5 B per cell) when off
@@ -452,7 +454,7 @@ def test_sa_gs_vcycle_template_kernel(ctx, oracle, monkeypatch, tpl_gs):
 @pytest.mark.slow
 def test_full_size_sa27_split_sweeps_and_cycle_256(ctx, oracle, capfd):
     """configs[2] at full size (27-pt anisotropic 256^3, SA + hybrid GS): the split sweeps of
-    the Galerkin levels (KM_GSACC block pass + the bucketed LDS-queue chain walk, DESIGN.md
+    the Galerkin levels (KM_GSACC block pass + the LDS-queue chain walk, DESIGN.md
     4.2c) on the product's own level-1 and level-2 operators, forward and backward at B = 64,
     bit-identical to the oracle's hybrid_gs on those operators -- with the chain walk's widest
     in-chunk coupling count recorded -- then one full SA V-cycle iterate bit-identical to the
