@@ -154,6 +154,34 @@ void launch_bin(hipStream_t s, const std::vector<int>& rows, DevBuf<int>& drows,
 
 namespace {
 
+// rows of a device CSR gathered into 16-byte (column, value) records: wave w copies row
+// rows[w] to out[off[w]...] (ghost rows of A P for the ranks that asked for them)
+struct PackRec {
+    long long c;
+    double v;
+};
+
+__global__ __launch_bounds__(kWave) void pack_rows_kernel(int nrows, const long long* __restrict__ rows,
+                                                          const long long* __restrict__ off,
+                                                          const long long* __restrict__ rp,
+                                                          const long long* __restrict__ col,
+                                                          const double* __restrict__ val, PackRec* __restrict__ out) {
+    const int w = blockIdx.x;
+    if (w >= nrows) return;
+    const long long r = rows[w], b = rp[r], e = rp[r + 1], o = off[w];
+    for (long long k = b + threadIdx.x; k < e; k += kWave) out[o + (k - b)] = PackRec{col[k], val[k]};
+}
+
+// received records into the B image's column / value arrays
+__global__ void unpack_recs_kernel(long long n, const PackRec* __restrict__ in, long long* __restrict__ col,
+                                   double* __restrict__ val) {
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (t < n) {
+        col[t] = in[t].c;
+        val[t] = in[t].v;
+    }
+}
+
 // C = A * B with B's row image on the device: brp (host and device copies), bcol, bval.
 // acol: A's columns as rows of that image; ub: per row the bound sum_k |B_k|.  C stays on
 // the device (crp also on the host); rows that overflow the largest LDS table are computed on
@@ -369,12 +397,163 @@ HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, cons
     return download(ctx, tm, A, B, C);
 }
 
+namespace {
+
+// Several ranks: A P stays on the device between the two products.  The
+// rows of A P that other ranks' R columns reference are gathered on the device
+// (pack_rows_kernel), and only those travel: download, one host all-to-all-v, upload behind
+// this rank's own rows, which are copied device to device into the B image of R (A P).  Same
+// products and order as the two spgemm_device calls it replaces: bit-identical.
+HostCSR galerkin_device_dist(Context& ctx, const HostComm& comm, const HostCSR& R, const HostCSR& A,
+                             const HostCSR& P) {
+    AMG_CHECK(A.col_starts == P.row_starts && R.col_starts == A.row_starts, "galerkin: partitions differ");
+    PhaseTimer tm(comm);
+    hipStream_t s = ctx.stream;
+    static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
+    // ---- A P: B image = [P's rows | ghost rows of P] (spgemm_device's first product)
+    DevCSR64 AP;
+    {
+        HaloPlan plan = halo_plan_for_cols(comm, A);
+        GhostRows G = fetch_rows(comm, plan, P);
+        const int64_t n = A.nrows(), nbl = P.nrows(), lo = P.row_starts[comm.rank], hi = P.row_starts[comm.rank + 1];
+        std::vector<long long> brp(nbl + plan.n_halo() + 1);
+        for (int64_t r = 0; r <= nbl; ++r) brp[r] = P.rp[r];
+        for (int64_t t = 0; t < plan.n_halo(); ++t) brp[nbl + t + 1] = P.rp[nbl] + G.rp[t + 1];
+        std::vector<int> acol(A.nnz());
+        std::vector<int64_t> ub(n, 0);
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < n; ++i) {
+            int64_t u = 0;
+            for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+                const int64_t c = A.col[k];
+                const int64_t r = (c >= lo && c < hi) ? c - lo : nbl + plan.find(c);
+                acol[k] = (int)r;
+                u += brp[r + 1] - brp[r];
+            }
+            ub[i] = u;
+        }
+        const int64_t bl = P.nnz(), bnnz = brp.back();
+        DevBuf<long long> d_brp, d_bcol;
+        DevBuf<double> d_bval;
+        d_brp.upload(brp.data(), brp.size());
+        d_bcol.alloc((size_t)std::max<int64_t>(bnnz, 1));
+        d_bval.alloc((size_t)std::max<int64_t>(bnnz, 1));
+        copy_to_device(d_bcol.p, P.col.data(), sizeof(long long) * bl);
+        copy_to_device(d_bval.p, P.val.data(), sizeof(double) * bl);
+        copy_to_device(d_bcol.p + bl, G.col.data(), sizeof(long long) * (bnnz - bl));
+        copy_to_device(d_bval.p + bl, G.val.data(), sizeof(double) * (bnnz - bl));
+        tm.lap("    galerkin: A P column map, P image");
+        BImage img{brp.data(), d_brp.p, d_bcol.p, d_bval.p, P.n_global_cols,
+                   [&](std::function<int64_t(long long)>& ca, std::function<double(long long)>& va) {
+                       ca = [&](long long q) -> int64_t { return q < bl ? P.col[q] : G.col[q - bl]; };
+                       va = [&](long long q) -> double { return q < bl ? P.val[q] : G.val[q - bl]; };
+                   }};
+        spgemm_core(ctx, tm, A, acol, ub, img, AP);
+    }
+    // ---- ghost rows of A P for R's off-rank columns, gathered on the device
+    const int64_t nl = A.nrows(), lo = A.row_starts[comm.rank], hi = A.row_starts[comm.rank + 1];
+    HaloPlan rplan = halo_plan_for_cols(comm, R);
+    std::vector<int64_t> len(nl), hlen(rplan.n_halo());
+    for (int64_t i = 0; i < nl; ++i) len[i] = AP.rp[i + 1] - AP.rp[i];
+    rplan.forward(comm, len.data(), hlen.data());
+    std::vector<long long> grp(rplan.n_halo() + 1, 0);
+    for (int64_t t = 0; t < rplan.n_halo(); ++t) grp[t + 1] = grp[t] + hlen[t];
+    const int64_t nsend = (int64_t)rplan.send_idx.size();
+    std::vector<long long> soff(nsend + 1, 0);
+    for (int64_t t = 0; t < nsend; ++t) soff[t + 1] = soff[t] + len[rplan.send_idx[t]];
+    std::vector<PackRec> sbuf((size_t)soff[nsend]), rbuf((size_t)grp.back());
+    if (nsend > 0 && soff[nsend] > 0) {
+        DevBuf<long long> d_rows, d_off;
+        DevBuf<PackRec> d_out;
+        std::vector<long long> rows(rplan.send_idx.begin(), rplan.send_idx.end());
+        d_rows.upload(rows.data(), rows.size());
+        d_off.upload(soff.data(), soff.size());
+        d_out.alloc((size_t)soff[nsend]);
+        for (int64_t w0 = 0; w0 < nsend; w0 += (int64_t)1 << 24) {
+            const int cnt = (int)std::min<int64_t>((int64_t)1 << 24, nsend - w0);
+            hipLaunchKernelGGL(pack_rows_kernel, dim3(cnt), dim3(kWave), 0, s, cnt, d_rows.p + w0, d_off.p + w0,
+                               AP.d_rp.p, AP.d_col.p, AP.d_val.p, d_out.p);
+        }
+        HIP_CHECK(hipGetLastError());
+        copy_to_host(sbuf.data(), d_out.p, sizeof(PackRec) * sbuf.size(), s);
+    }
+    std::vector<int64_t> sb(comm.nranks, 0), rb(comm.nranks, 0);
+    for (size_t p = 0; p < rplan.send_procs.size(); ++p)
+        sb[rplan.send_procs[p]] = (soff[rplan.send_ptr[p + 1]] - soff[rplan.send_ptr[p]]) * (int64_t)sizeof(PackRec);
+    for (size_t p = 0; p < rplan.recv_procs.size(); ++p)
+        rb[rplan.recv_procs[p]] = (grp[rplan.recv_ptr[p + 1]] - grp[rplan.recv_ptr[p]]) * (int64_t)sizeof(PackRec);
+    comm.alltoallv(sbuf.data(), sb, rbuf.data(), rb);
+    std::vector<PackRec>().swap(sbuf);
+    tm.lap("    galerkin: ghost rows of A P (device gather, exchange)");
+    // ---- R (A P): B image = [A P's rows (device to device) | ghost rows]
+    const int64_t apl = AP.nnz(), gnnz = grp.back(), bnnz = apl + gnnz;
+    std::vector<long long> brp(nl + rplan.n_halo() + 1);
+    for (int64_t r = 0; r <= nl; ++r) brp[r] = AP.rp[r];
+    for (int64_t t = 0; t < rplan.n_halo(); ++t) brp[nl + t + 1] = apl + grp[t + 1];
+    DevBuf<long long> d_brp, d_bcol;
+    DevBuf<double> d_bval;
+    d_brp.upload(brp.data(), brp.size());
+    d_bcol.alloc((size_t)std::max<int64_t>(bnnz, 1));
+    d_bval.alloc((size_t)std::max<int64_t>(bnnz, 1));
+    if (apl) {
+        HIP_CHECK(hipMemcpyAsync(d_bcol.p, AP.d_col.p, sizeof(long long) * apl, hipMemcpyDeviceToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(d_bval.p, AP.d_val.p, sizeof(double) * apl, hipMemcpyDeviceToDevice, s));
+    }
+    if (gnnz) {
+        DevBuf<PackRec> d_in;
+        d_in.upload(rbuf.data(), rbuf.size());
+        hipLaunchKernelGGL(unpack_recs_kernel, dim3((unsigned)((gnnz + 255) / 256)), dim3(256), 0, s, (long long)gnnz,
+                           d_in.p, d_bcol.p + apl, d_bval.p + apl);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(s));  // d_in is freed at the end of this scope
+    }
+    const int64_t nr = R.nrows();
+    std::vector<int> rcol(R.nnz());
+    std::vector<int64_t> rub(nr, 0);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < nr; ++i) {
+        int64_t u = 0;
+        for (int64_t k = R.rp[i]; k < R.rp[i + 1]; ++k) {
+            const int64_t c = R.col[k];
+            const int64_t r = (c >= lo && c < hi) ? c - lo : nl + rplan.find(c);
+            rcol[k] = (int)r;
+            u += brp[r + 1] - brp[r];
+        }
+        rub[i] = u;
+    }
+    AP.d_col.reset();
+    AP.d_val.reset();
+    tm.lap("    galerkin: R column map, A P image");
+    // host copies of the image only if some row of R (A P) overflows the LDS tables
+    std::vector<long long> hc;
+    std::vector<double> hv;
+    BImage img{brp.data(), d_brp.p, d_bcol.p, d_bval.p, P.n_global_cols,
+               [&](std::function<int64_t(long long)>& ca, std::function<double(long long)>& va) {
+                   hc.resize(bnnz);
+                   hv.resize(bnnz);
+                   copy_to_host(hc.data(), d_bcol.p, sizeof(long long) * bnnz, s);
+                   copy_to_host(hv.data(), d_bval.p, sizeof(double) * bnnz, nullptr);
+                   ca = [&](long long q) -> int64_t { return hc[q]; };
+                   va = [&](long long q) -> double { return hv[q]; };
+               }};
+    DevCSR64 RAP;
+    spgemm_core(ctx, tm, R, rcol, rub, img, RAP);
+    return download(ctx, tm, R, P, RAP);
+}
+
+}  // namespace
+
 // R (A P) with A P kept on the device between the two products (one rank: no ghost rows, so
-// A P's rows are the B image of the second product as they stand).  Several ranks: the two
-// spgemm_device calls (the ghost rows of A P come from other ranks).
+// A P's rows are the B image of the second product as they stand; several ranks:
+// galerkin_device_dist, the ghost rows of A P gathered on the device).  AMG_GALERKIN_DIST=0:
+// several ranks run the two spgemm_device calls (A P through the host), the round-3 form.
 HostCSR galerkin_device(Context& ctx, const HostComm& comm, const HostCSR& R, const HostCSR& A,
                         const HostCSR& P) {
-    if (comm.nranks > 1) return spgemm_device(ctx, comm, R, spgemm_device(ctx, comm, A, P));
+    if (comm.nranks > 1) {
+        const char* e = std::getenv("AMG_GALERKIN_DIST");
+        if (e && *e && std::atoi(e) == 0) return spgemm_device(ctx, comm, R, spgemm_device(ctx, comm, A, P));
+        return galerkin_device_dist(ctx, comm, R, A, P);
+    }
     AMG_CHECK(A.col_starts == P.row_starts && R.col_starts == A.row_starts, "galerkin: partitions differ");
     PhaseTimer tm(comm);
     const int64_t n = A.nrows();
