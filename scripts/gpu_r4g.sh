@@ -1,11 +1,12 @@
 #!/bin/bash
 # round-4 GPU suite, part 1: every -m gpu test except the slow full-size ones, one process,
-# per-test time limit; the log is kept short (tail) in gpurun_out.
+# per-test time limit; progress streams into gpurun_out (one line per test).
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 R=${R:-r4g}
-timeout -k 10 1080 python -u -m pytest tests -m "gpu and not slow" -x -q --timeout 300 --timeout-method thread \
-  -p no:cacheprovider --durations=15 > /tmp/t.log 2>&1
+SEL=${SEL:-gpu and not slow}
+timeout -k 10 1080 python -u -m pytest tests -m "$SEL" -x -v --timeout 600 --timeout-method thread \
+  -p no:cacheprovider --durations=15 ${EXTRA_ARGS} > gpurun_out/${R}_tests.log 2>&1
 rc=$?
-grep -v "amdgpu.ids" /tmp/t.log | tail -c 40000 > gpurun_out/${R}_tests.log
-tail -40 gpurun_out/${R}_tests.log
+grep -oE "(PASSED|FAILED|ERROR|SKIPPED)" gpurun_out/${R}_tests.log | sort | uniq -c
+tail -25 gpurun_out/${R}_tests.log
 echo "tests rc=$rc"
