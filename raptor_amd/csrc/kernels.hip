@@ -2926,11 +2926,8 @@ static void launch_csr_persist(hipStream_t s, int mode, bool norm, const CsrArgs
 
 // AMG_CSR_PAIR=1: square x-tile operators run two blocks per workgroup (A/B)
 static bool csr_pair() {
-    static const bool on = [] {
-        const char* e = std::getenv("AMG_CSR_PAIR");
-        return e && *e && std::atoi(e) != 0;
-    }();
-    return on;
+    const char* e = std::getenv("AMG_CSR_PAIR");  // read per launch (tests flip it in-process)
+    return e && *e && std::atoi(e) != 0;
 }
 
 template <int M, bool N, bool X, bool T, bool V>
@@ -3036,10 +3033,8 @@ void launch_csr_plain(hipStream_t s, int mode, bool norm, const DevMatrix& A, co
 #endif
     // the pipelined persistent kernel where every block fits one LDS chunk (AMG_PLAIN_PIPE=0:
     // one workgroup per block)
-    static const bool pipe_env = [] {
-        const char* e = std::getenv("AMG_PLAIN_PIPE");
-        return !(e && *e && std::atoi(e) == 0);
-    }();
+    const char* pe = std::getenv("AMG_PLAIN_PIPE");  // read per launch (tests flip it in-process)
+    const bool pipe_env = !(pe && *pe && std::atoi(pe) == 0);
     const bool pipe = pipe_env && A.plain_maxblk <= kCAP && g >= 8;
     thread_local int pipe_grid = 0;
     if (pipe && pipe_grid == 0) {
