@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <initializer_list>
 #include <memory>
 #include <string>
 #include <vector>
@@ -508,6 +509,7 @@ struct Solver {
     // solver fell back to eager cycles (every rank, together).
     bool graph_ready(int slot, const double* x, const double* b, const std::function<void()>& body,
                      bool agree);
+    void agree_stale(std::initializer_list<int> slots, const double* x, const double* b);
     void graph_launch(int slot);
     void destroy_graphs();
 

@@ -476,6 +476,30 @@ bool Solver::graph_ready(int slot, const double* x, const double* b, const std::
     return true;
 }
 
+// One collective staleness decision for every graph slot a call will replay (multi-rank): a
+// slot stale on any rank is dropped on every rank, so the later graph_ready(.., agree = false)
+// calls capture -- and meet in the capture's status exchange -- on all ranks or on none.
+// (Deciding per slot inside the loop hung: solve's last-norm graph was stale on the rank whose
+// x had moved and fresh on the others, so one rank waited in the status exchange.)
+void Solver::agree_stale(std::initializer_list<int> slots, const double* x, const double* b) {
+    const HostComm& comm = ctx->host;
+    if (!use_graph || comm.nranks <= 1) return;
+    bool stale = false;
+    for (int slot : slots) {
+        const Graph& G = graphs[slot];
+        stale = stale || !G.exec || G.x != x || G.b != b || G.fmt_gen != DevMatrix::format_generation;
+    }
+    bool any = false;
+    for (int64_t v : comm.allgather((int64_t)(stale ? 1 : 0))) any = any || v != 0;
+    if (!any) return;
+    if (ctx->graph_inflight) ctx->eager_rccl_fence();  // replays of the graphs dropped below
+    for (int slot : slots) {
+        Graph& G = graphs[slot];
+        if (G.exec) HIP_CHECK(hipGraphExecDestroy(G.exec));
+        G.exec = nullptr;
+    }
+}
+
 void Solver::graph_launch(int slot) {
     RoctxRange r("cycle: hipGraph replay");
     HIP_CHECK(hipGraphLaunch(graphs[slot].exec, ctx->stream));
@@ -522,15 +546,18 @@ int32_t Solver::solve(double* x, const double* b, int32_t max_iter, double tol, 
     if (ctx->host.nranks > 1) ctx->eager_rccl_fence();
     HIP_CHECK(hipMemsetAsync(hist_counter.p, 0, sizeof(int), s));
     int32_t it = 0;
-    // one collective graph decision per solve (x and b stay put for its cycles)
+    // one collective graph decision per solve, over every slot it replays (x and b stay put
+    // for its cycles)
     if (tol <= 0.0 && can_fuse_norm()) {
         // ||b - A x_k|| comes out of cycle k+1's first Jacobi sweep (same b - Ax values);
         // only the last norm needs its own residual pass.  No host sync in the loop, and with
         // graphs on, no eager work at all: cycles and the last norm replay captured graphs.
-        for (; it < max_iter; ++it) cycle(x, b, true, it == 0);
-        residual_norm(x, b, max_iter == 0);
+        agree_stale({G_CYCLE_NORM, G_NORM}, x, b);
+        for (; it < max_iter; ++it) cycle(x, b, true, false);
+        residual_norm(x, b, false);
     } else {
-        residual_norm(x, b, true);
+        agree_stale({G_CYCLE, G_NORM}, x, b);
+        residual_norm(x, b, false);
         double r0 = 0.0;
         if (tol > 0.0) {
             HIP_CHECK(hipMemcpyAsync(&r0, hist.p, sizeof(double), hipMemcpyDeviceToHost, s));
@@ -538,7 +565,7 @@ int32_t Solver::solve(double* x, const double* b, int32_t max_iter, double tol, 
             ctx->graph_inflight = false;
         }
         while (it < max_iter) {
-            cycle(x, b, false, it == 0);
+            cycle(x, b, false, false);
             residual_norm(x, b, false);
             ++it;
             if (tol > 0.0) {

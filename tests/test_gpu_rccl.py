@@ -30,7 +30,8 @@ def _free_port():
     return p
 
 
-def run_rccl(nranks, spec, tmp_path, timeout=240):
+def run_rccl(nranks, spec, tmp_path, timeout=160):
+    # (below the GPU runner's 180 s silence limit: a hung rank fails the test with its log)
     port = _free_port()
     out = str(tmp_path / "rank")
     procs = []
