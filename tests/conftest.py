@@ -30,3 +30,18 @@ def ctx():
     import raptor_amd as ra
 
     return ra.Context(0)
+
+
+@pytest.fixture
+def say(capfd, request):
+    """Progress line on the terminal (capture bypassed) for the long full-size tests, so a
+    phase that takes minutes is never mistaken for a hang."""
+    import time
+
+    t0 = time.perf_counter()
+
+    def _say(msg):
+        with capfd.disabled():
+            print(f"[{request.node.name} {time.perf_counter() - t0:7.1f}s] {msg}", flush=True)
+
+    return _say

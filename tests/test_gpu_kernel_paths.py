@@ -308,7 +308,7 @@ def test_sa27_npl16_vcycle_vs_oracle(ctx, oracle):
 
 
 @pytest.mark.slow
-def test_sa27_hierarchy_independent_oracle_64(ctx, oracle):
+def test_sa27_hierarchy_independent_oracle_64(ctx, oracle, say):
     """configs[2]'s algorithm on a cube (27-pt anisotropic 64^3, 262k rows, 7M nnz) with an
     INDEPENDENT oracle hierarchy (the independent sa27 comparison was only
     256x24x16): strength with the per-level threshold, MIS(2) aggregates, smoothed P,
@@ -340,7 +340,7 @@ def test_sa27_hierarchy_independent_oracle_64(ctx, oracle):
 
 
 @pytest.mark.slow
-def test_full_size_27pt_256(ctx, oracle):
+def test_full_size_27pt_256(ctx, oracle, say):
     """BASELINE.json configs[2] size: 27-pt 256^3 (449M nnz).  The level-0 kernels the sa27
     bench runs -- the NPL-16 template kernel in every mode with the norm, and the l1 hybrid
     GS on the 1-byte value dictionary, forward and backward -- bit-identical to the oracle."""
@@ -351,7 +351,9 @@ def test_full_size_27pt_256(ctx, oracle):
     A = ra.par_stencil_grid(ctx, "27pt", (N, N, N))
     assert A.info["tpl_lanes"] == 16 and A.info["template_rows"] == N ** 3
     Ao = O.gen_27pt(N, N, N)
+    say("operators built; all modes")
     all_modes_equal(ctx, O, A, Ao, seed=17)
+    say("hybrid GS")
     n = N ** 3
     x, b = O.vec_uniform(n, 5), O.vec_uniform(n, 6)
     dx, db, out = to_dev(ctx, x), to_dev(ctx, b), ctx.empty(n)
@@ -458,7 +460,7 @@ def test_sa_gs_vcycle_template_kernel(ctx, oracle, monkeypatch, tpl_gs):
 
 
 @pytest.mark.slow
-def test_full_size_sa27_split_sweeps_and_cycle_256(ctx, oracle, capfd):
+def test_full_size_sa27_split_sweeps_and_cycle_256(ctx, oracle, capfd, say):
     """configs[2] at full size (27-pt anisotropic 256^3, SA + hybrid GS): the split sweeps of
     the Galerkin levels (KM_GSACC block pass + the LDS-queue chain walk, DESIGN.md
     4.2c) on the product's own level-1 and level-2 operators, forward and backward at B = 64,
@@ -472,6 +474,7 @@ def test_full_size_sa27_split_sweeps_and_cycle_256(ctx, oracle, capfd):
     A = ra.par_stencil_grid(ctx, "27pt", (N, N, N))
     ml = ra.ParSmoothedAggregationSolver().setup(A)
     assert ml.num_levels >= 4
+    say("setup done")
     n = N ** 3
     b = O.vec_uniform(n, 42)
     db = to_dev(ctx, b)
@@ -479,6 +482,7 @@ def test_full_size_sa27_split_sweeps_and_cycle_256(ctx, oracle, capfd):
     ml.cycle(dx, db)  # builds every level's GS formats (split where the rule takes it)
     widths = {}
     for l in (1, 2):
+        say(f"level {l} split sweeps")
         Al = ml.level_matrix(l, "A")
         info = Al._info()
         assert info["gs_split"] == 1, (l, info["gs_split"])
@@ -496,6 +500,8 @@ def test_full_size_sa27_split_sweeps_and_cycle_256(ctx, oracle, capfd):
         del Ao, dxl, dbl, out
     with capfd.disabled():
         print(f"\n[sa27 256^3] split-sweep chain widths (forward, backward) per level: {widths}", flush=True)
+    say("exporting the hierarchy to the oracle")
     H = O.Hierarchy(None, levels=oracle_levels(O, ml), smoother=O.SMOOTH_HYBRID_GS)
+    say("oracle cycle")
     xo = H.cycle(np.zeros(n), b)
     assert np.array_equal(to_host(ctx, dx), xo)

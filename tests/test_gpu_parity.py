@@ -406,7 +406,7 @@ def test_solve_tolerance_stops(ctx):
 
 
 @pytest.mark.slow
-def test_full_size_spmv_and_cycle_256(ctx, oracle):
+def test_full_size_spmv_and_cycle_256(ctx, oracle, say):
     """BASELINE.json configs[1] size: 7-pt 256^3 (117M nnz).  GPU SpMV bit-exact vs the
     oracle at full size; A*1 equals the exact integer row sums; one full V-cycle iterate
     bit-exact vs the oracle on the same hierarchy."""
@@ -430,8 +430,11 @@ def test_full_size_spmv_and_cycle_256(ctx, oracle):
     Ao = O.gen_7pt(N, N, N)
     assert np.array_equal(to_host(ctx, y), Ao.spmv(x))
     del Ao
+    say("SpMV bit-exact; setup")
     ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
+    say("setup done; exporting the hierarchy to the oracle")
     H = O.Hierarchy(None, levels=oracle_levels(O, ml))
+    say("oracle cycle")
     b = to_host(ctx, y)
     dx = ctx.zeros(n)
     ml.cycle(dx, y)
@@ -440,7 +443,7 @@ def test_full_size_spmv_and_cycle_256(ctx, oracle):
 
 
 @pytest.mark.slow
-def test_full_size_hierarchy_independent_oracle_256(ctx, oracle):
+def test_full_size_hierarchy_independent_oracle_256(ctx, oracle, say):
     """configs[1] at full size with an INDEPENDENT oracle hierarchy (the 256^3
     cycle test built the oracle from the product's exported levels).  The oracle's serial
     setup of 7-pt 256^3 (strength, PMIS, classical interpolation, transpose, Galerkin) against
@@ -452,10 +455,13 @@ def test_full_size_hierarchy_independent_oracle_256(ctx, oracle):
     N = 256
     A = ra.par_stencil_grid(ctx, "7pt", (N, N, N))
     ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
+    say("GPU setup done; oracle setup (serial)")
     Ao = O.gen_7pt(N, N, N)
     Ho = O.Hierarchy(Ao, **O.DEFAULTS["pmis"])
     assert ml.num_levels == Ho.num_levels
+    say("oracle setup done; comparing levels")
     for l in range(ml.num_levels):
+        say(f"level {l}")
         if l > 0:
             assert same_csr(ml.level_matrix(l, "A").to_scipy_local(), Ho.matrix(l, "A")), ("A", l)
         if l + 1 < ml.num_levels:
