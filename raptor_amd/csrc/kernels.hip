@@ -2306,31 +2306,35 @@ __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) ls[u] = cstart(q0 + 16 * u + (lane >> 2)) + 2 * (lane & 3);
         const int nb = a.B / U;
-        v2d_t ra[4], rx[4];
-        v2u_t ri;
-        auto load = [&](int bi) {
+        // two batches of loads in flight (register sets A / B alternate): batch bi + 2 is
+        // issued as soon as batch bi's set is in LDS, so a batch's loads have two walks and
+        // write-backs to arrive (one batch ahead left the kernel at ~4.2 TB/s)
+        struct Batch {
+            v2d_t ra[4], rx[4];
+            v2u_t ri;
+        };
+        auto load = [&](int bi, Batch& L) {
             const int off = (BACK ? nb - 1 - bi : bi) * U;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                ra[u] = __builtin_nontemporal_load((const v2d_t*)(a.racc + ls[u] + off));
-                rx[u] = *(const v2d_t*)(a.x + ls[u] + off);
+                L.ra[u] = __builtin_nontemporal_load((const v2d_t*)(a.racc + ls[u] + off));
+                L.rx[u] = *(const v2d_t*)(a.x + ls[u] + off);
             }
-            ri = *(const v2u_t*)(a.id + c0 + off);
+            L.ri = *(const v2u_t*)(a.id + c0 + off);
         };
-        load(0);
-        for (int bi = 0; bi < nb; ++bi) {
+        auto step = [&](int bi, Batch& L) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int slot = 2 * (lane & 3) * kSt + 16 * u + (lane >> 2);
-                sacc[slot] = ra[u].x;
-                sacc[slot + kSt] = ra[u].y;
-                sx[slot] = rx[u].x;
-                sx[slot + kSt] = rx[u].y;
+                sacc[slot] = L.ra[u].x;
+                sacc[slot + kSt] = L.ra[u].y;
+                sx[slot] = L.rx[u].x;
+                sx[slot + kSt] = L.rx[u].y;
             }
-            sid[2 * lane] = ri.x;
-            sid[2 * lane + 1] = ri.y;
+            sid[2 * lane] = L.ri.x;
+            sid[2 * lane + 1] = L.ri.y;
             __syncthreads();
-            if (bi + 1 < nb) load(bi + 1);  // in flight during the walk below
+            if (bi + 2 < nb) load(bi + 2, L);  // in flight during two walks
             double out[U];
             const unsigned iw[2] = {sid[2 * lane], sid[2 * lane + 1]};
 #pragma unroll
@@ -2355,6 +2359,25 @@ __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
                 *(v2d_t*)(a.y + ls[u] + off) = v2d_t{sacc[slot], sacc[slot + kSt]};
             }
             __syncthreads();  // the stage is rewritten by the next batch
+        };
+        Batch L2[2];
+        if (nb == 8) {
+            // B = 64 (the bench's chunk): straight-line code, so the wait before each batch's
+            // LDS stores counts exactly the later batch's loads and the write-backs (in the
+            // loop form the compiler's count also waited for the batch two ahead)
+            load(0, L2[0]);
+            load(1, L2[1]);
+#pragma unroll
+            for (int bi = 0; bi < 8; ++bi) {
+                step(bi, L2[bi & 1]);
+            }
+        } else {
+            load(0, L2[0]);
+            if (nb > 1) load(1, L2[1]);
+            for (int bi = 0; bi < nb; bi += 2) {
+                step(bi, L2[0]);
+                if (bi + 1 < nb) step(bi + 1, L2[1]);
+            }
         }
     } else if (live) {
         // clipped chunk (the rank's last rows), a partial wave, or B not a multiple of 8
