@@ -2263,8 +2263,8 @@ struct TplGsChainArgs {
 // once) into LDS while the previous batch is walked, then lane c walks chunk c's 8 rows from
 // LDS.  (Lane c loading its own chunk's lines took 161 us per 27-pt 256^3 sweep: 64 distinct
 // lines per wave instruction, each fetched again by the next quarter-line load.)
-template <bool BACK>
-__global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
+template <bool BACK, bool DEEP2>
+__global__ __launch_bounds__(64, DEEP2 ? 4 : 1) void tpl_gs_chain_kernel(TplGsChainArgs a) {
     constexpr int U = 8;
     // per-GS-template tables sized by the launch (ntpl entries; 27-pt: 27): a wave-sized
     // workgroup with 5 KiB of fixed 256-entry tables fit 11 per CU, 3.7 TB/s on the 27-pt sweep
@@ -2334,7 +2334,8 @@ __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
             sid[2 * lane] = L.ri.x;
             sid[2 * lane + 1] = L.ri.y;
             __syncthreads();
-            if (bi + 2 < nb) load(bi + 2, L);  // in flight during two walks
+            constexpr int D = DEEP2 ? 2 : 1;
+            if (bi + D < nb) load(bi + D, L);  // in flight during the next D walks
             double out[U];
             const unsigned iw[2] = {sid[2 * lane], sid[2 * lane + 1]};
 #pragma unroll
@@ -2360,24 +2361,17 @@ __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
             }
             __syncthreads();  // the stage is rewritten by the next batch
         };
-        Batch L2[2];
-        if (nb == 8) {
-            // B = 64 (the bench's chunk): straight-line code, so the wait before each batch's
-            // LDS stores counts exactly the later batch's loads and the write-backs (in the
-            // loop form the compiler's count also waited for the batch two ahead)
+        Batch L2[DEEP2 ? 2 : 1];
+        if constexpr (DEEP2) {
             load(0, L2[0]);
-            load(1, L2[1]);
-#pragma unroll
-            for (int bi = 0; bi < 8; ++bi) {
-                step(bi, L2[bi & 1]);
+            if (nb > 1) load(1, L2[DEEP2 ? 1 : 0]);
+            for (int bi = 0; bi < nb; bi += 2) {
+                step(bi, L2[0]);
+                if (bi + 1 < nb) step(bi + 1, L2[DEEP2 ? 1 : 0]);
             }
         } else {
             load(0, L2[0]);
-            if (nb > 1) load(1, L2[1]);
-            for (int bi = 0; bi < nb; bi += 2) {
-                step(bi, L2[0]);
-                if (bi + 1 < nb) step(bi + 1, L2[1]);
-            }
+            for (int bi = 0; bi < nb; ++bi) step(bi, L2[0]);
         }
     } else if (live) {
         // clipped chunk (the rank's last rows), a partial wave, or B not a multiple of 8
@@ -3258,8 +3252,13 @@ static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, co
     const long long nch = (long long)A.n_gs_tblk * (kTplRows / A.gs_block);
     const dim3 cg((unsigned)((nch + 63) / 64)), cb(64);
     const size_t clds = (size_t)c.ntpl * (8 + 8 + 4);
-    if (backward) hipLaunchKernelGGL((tpl_gs_chain_kernel<true>), cg, cb, clds, s, c);
-    else hipLaunchKernelGGL((tpl_gs_chain_kernel<false>), cg, cb, clds, s, c);
+    // two batches of loads in flight (AMG_GS_CHAIN_DEEP=0: one, the round-3 form)
+    const char* de = std::getenv("AMG_GS_CHAIN_DEEP");
+    const bool deep = !(de && *de && std::atoi(de) == 0);
+    if (backward && deep) hipLaunchKernelGGL((tpl_gs_chain_kernel<true, true>), cg, cb, clds, s, c);
+    else if (backward) hipLaunchKernelGGL((tpl_gs_chain_kernel<true, false>), cg, cb, clds, s, c);
+    else if (deep) hipLaunchKernelGGL((tpl_gs_chain_kernel<false, true>), cg, cb, clds, s, c);
+    else hipLaunchKernelGGL((tpl_gs_chain_kernel<false, false>), cg, cb, clds, s, c);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -3320,17 +3319,21 @@ __global__ __launch_bounds__(64) void gs_chain_kernel(GsArgs a) {
         dinv = a.dinv[r];
     }
     const size_t base = (size_t)sl.z * 64 + lane;
-    for (int k0 = 0; k0 < sl.w; k0 += 8) {  // sl.w <= W (launch_gs_chain); 8 loads in flight
-        int c[8];
-        double v[8];
+    // the slab's couplings into the LDS queue: up to 32 entries per lane in flight at once (one
+    // memory round for W <= 32, two for W = 64).  Loading 8 at a time put W / 8 dependent
+    // rounds in every wave's life (~11 us per launch whatever the grid, profiles/r4f_*)
+    constexpr int KR = W < 32 ? W : 32;  // entries per round
+    for (int k0 = 0; k0 < sl.w; k0 += KR) {  // sl.w <= W (launch_gs_chain)
+        int c[KR];
+        double v[KR];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < KR; ++u) {
             const bool in = k0 + u < sl.w;  // uniform
             c[u] = in ? __builtin_nontemporal_load(a.col + base + (size_t)(k0 + u) * 64) : -1;
             v[u] = in ? __builtin_nontemporal_load(a.val + base + (size_t)(k0 + u) * 64) : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < KR; ++u) {
             if (k0 + u < sl.w) {
                 qc[(k0 + u) * 64 + lane] = c[u];
                 qv[(k0 + u) * 64 + lane] = v[u];
