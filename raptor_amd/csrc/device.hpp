@@ -340,7 +340,6 @@ struct DevMatrix {
     bool blocks_only = false;  // build only the CSR-block formats (the split-GS pass operators)
     DevBuf<int> pcol;
     DevBuf<double> pval;
-    int64_t plain_maxblk = 0;  // most nonzeros of a 256-row block from its first pair (csr_plain_pipe_kernel)
     int plain_blocks() const { return (int)((n_rows + kTPB - 1) / kTPB); }
     // SURVEY.md 8(d) plain-CSR SpMV bytes: 12 nnz + 4 (n + 1) + 8 (local + halo columns) + 8 n
     int64_t csr_plain_bytes() const {

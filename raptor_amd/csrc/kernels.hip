@@ -682,131 +682,6 @@ __global__ __launch_bounds__(kTPB, 8) void csr_plain_kernel(PlainArgs a) {
     }
 }
 
-// Persistent, software-pipelined plain CSR.  csr_plain_kernel's block waits
-// on three dependent rounds of loads (row_ptr -> val / col -> x), and 71 % of its wave cycles
-// are such waits (profiles/r3r_plain_compact_ab.txt).  Here a resident grid (XCD x = blockIdx %
-// 8 owning a contiguous 1/8 of the blocks) walks its blocks with the rounds of three blocks in
-// flight: while block i is summed, block i + 1's x gathers and row operands and block i + 2's
-// val / col pairs are loading, and block i + 3's nonzero range comes through scalar loads.
-// Same chunk, same products, same LDS row sums and partial slots as csr_plain_kernel:
-// bit-identical.  Taken when every block's nonzeros fit one LDS chunk (DevMatrix::plain_maxblk).
-#ifndef AMG_PLAIN_PIPE_WAVES  // build-time knob: waves per SIMD the pipelined kernel is built for
-#define AMG_PLAIN_PIPE_WAVES 6
-#endif
-struct PlainV {  // block i + 2: val / col pairs and the lane's row extent
-    v2d_t vv[4];
-    v2i_t cc[4];
-    int rs, re, base;
-};
-struct PlainX {  // block i + 1: products' operands and the row's epilogue operands
-    double xv[8];
-    v2d_t vv[4];
-    int rs, re, base;
-    double pb, pd, px;
-};
-
-template <int MODE, bool NORM>
-__global__ __launch_bounds__(kTPB, AMG_PLAIN_PIPE_WAVES) void csr_plain_pipe_kernel(PlainArgs a, int nblk) {
-    __shared__ __attribute__((aligned(16))) double stage[kCAP];
-    const int tid = threadIdx.x;
-    const int xcd = blockIdx.x & 7, lw = blockIdx.x >> 3, per = gridDim.x >> 3;
-    const int q = nblk >> 3, rem = nblk & 7;
-    const int b0 = xcd * q + min(xcd, rem), b1 = b0 + q + (xcd < rem ? 1 : 0);
-    if (b0 + lw >= b1) return;  // workgroup-uniform
-    const int nb = (b1 - (b0 + lw) + per - 1) / per;
-    auto blk_of = [&](int i) { return b0 + lw + i * per; };
-    // block i's nonzero range [k0, k1): scalar loads (uniform), issued three blocks ahead
-    auto krange = [&](int i, int& k0, int& k1) {
-        const int r0 = blk_of(i) * kTPB, r1 = min(a.n, r0 + kTPB);
-        k0 = a.rp[r0];
-        k1 = a.rp[r1];
-    };
-    auto load_v = [&](int i, int k0, int k1, PlainV& v) {
-        const int r0 = blk_of(i) * kTPB, r1 = min(a.n, r0 + kTPB);
-        const int rr = min(r0 + tid, r1 - 1);
-        v.rs = a.rp[rr];
-        v.re = a.rp[rr + 1];
-        v.base = k0 & ~1;
-        const int plast = max(k1 - 1, 0) & ~1;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int qq = min(v.base + 2 * tid + 2 * kTPB * p, plast);
-            v.vv[p] = __builtin_nontemporal_load((const v2d_t*)(a.val + qq));
-            v.cc[p] = __builtin_nontemporal_load((const v2i_t*)(a.col + qq));
-        }
-    };
-    auto load_x = [&](int i, const PlainV& v, PlainX& x) {
-        const int r0 = blk_of(i) * kTPB, r1 = min(a.n, r0 + kTPB);
-        const int rr = min(r0 + tid, r1 - 1);
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            x.xv[2 * p] = plain_x(a, v.cc[p].x);
-            x.xv[2 * p + 1] = plain_x(a, v.cc[p].y);
-            x.vv[p] = v.vv[p];
-        }
-        x.rs = v.rs, x.re = v.re, x.base = v.base;
-        x.pb = x.pd = x.px = 0.0;
-        if (MODE == KM_SPMV_ADD) x.px = a.y[rr];
-        if (MODE == KM_RESID || MODE == KM_JACOBI) x.pb = a.b[rr];
-        if (MODE == KM_JACOBI) {
-            x.pd = a.dinv[rr];
-            x.px = a.x[rr];
-        }
-    };
-    PlainV v1, v2;  // blocks i + 1 (until its gathers issue) and i + 2
-    PlainX xc;      // block i
-    int k0n = 0, k1n = 0;  // block i + 3's range
-    // prologue: block 0 through the gathers, block 1's pairs, block 2's range
-    {
-        int k0, k1;
-        krange(0, k0, k1);
-        load_v(0, k0, k1, v1);
-        if (nb > 1) {
-            krange(1, k0, k1);
-            load_v(1, k0, k1, v2);
-        }
-        if (nb > 2) krange(2, k0n, k1n);
-        load_x(0, v1, xc);
-        v1 = v2;
-    }
-    for (int i = 0; i < nb; ++i) {
-        // issue: block i + 1's gathers (its pairs arrived during block i - 1), block i + 2's
-        // pairs, block i + 3's range
-        PlainX xn;
-        if (i + 1 < nb) load_x(i + 1, v1, xn);
-        if (i + 2 < nb) {
-            load_v(i + 2, k0n, k1n, v2);
-            v1 = v2;
-        }
-        if (i + 3 < nb) krange(i + 3, k0n, k1n);
-        // block i: products into the stage, row sums in CSR order, epilogue
-        const int r0 = blk_of(i) * kTPB, r1 = min(a.n, r0 + kTPB), r = r0 + tid;
-        const bool own = r < r1;
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-            *(v2d_t*)(stage + 2 * tid + 2 * kTPB * p) = v2d_t{xc.vv[p].x * xc.xv[2 * p], xc.vv[p].y * xc.xv[2 * p + 1]};
-        __syncthreads();
-        const double sum = lds_row_sum(stage, xc.rs - xc.base, xc.re - xc.base, 0.0);
-        double out, sq = 0.0;
-        if (MODE == KM_SPMV) {
-            out = sum;
-        } else if (MODE == KM_SPMV_ADD) {
-            out = xc.px + sum;
-        } else {
-            const double t = xc.pb - sum;
-            if (NORM) sq = own ? t * t : 0.0;
-            out = MODE == KM_RESID ? t : xc.px + a.omega * (xc.pd * t);
-        }
-        if (own) a.y[r] = out;
-        if (NORM) {
-            sq = wave_sum(sq);
-            if ((tid & 63) == 0) a.partial[blk_of(i) * kNormParts + (tid >> 6)] = sq;
-        }
-        __syncthreads();  // the stage is rewritten by block i + 1
-        xc = xn;
-    }
-}
-
 // Two 256-row blocks per workgroup (AMG_PLAIN_RB=2, A/B knob): both blocks' val / col pairs
 // are loaded before the first block's x gathers, so a workgroup keeps twice the bytes in
 // flight across its dependent rounds (rp -> val / col -> x).  Same rows, same per-block sums
@@ -2263,8 +2138,8 @@ struct TplGsChainArgs {
 // once) into LDS while the previous batch is walked, then lane c walks chunk c's 8 rows from
 // LDS.  (Lane c loading its own chunk's lines took 161 us per 27-pt 256^3 sweep: 64 distinct
 // lines per wave instruction, each fetched again by the next quarter-line load.)
-template <bool BACK, bool DEEP2>
-__global__ __launch_bounds__(64, DEEP2 ? 4 : 1) void tpl_gs_chain_kernel(TplGsChainArgs a) {
+template <bool BACK>
+__global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
     constexpr int U = 8;
     // per-GS-template tables sized by the launch (ntpl entries; 27-pt: 27): a wave-sized
     // workgroup with 5 KiB of fixed 256-entry tables fit 11 per CU, 3.7 TB/s on the 27-pt sweep
@@ -2306,36 +2181,31 @@ __global__ __launch_bounds__(64, DEEP2 ? 4 : 1) void tpl_gs_chain_kernel(TplGsCh
 #pragma unroll
         for (int u = 0; u < 4; ++u) ls[u] = cstart(q0 + 16 * u + (lane >> 2)) + 2 * (lane & 3);
         const int nb = a.B / U;
-        // two batches of loads in flight (register sets A / B alternate): batch bi + 2 is
-        // issued as soon as batch bi's set is in LDS, so a batch's loads have two walks and
-        // write-backs to arrive (one batch ahead left the kernel at ~4.2 TB/s)
-        struct Batch {
-            v2d_t ra[4], rx[4];
-            v2u_t ri;
-        };
-        auto load = [&](int bi, Batch& L) {
+        v2d_t ra[4], rx[4];
+        v2u_t ri;
+        auto load = [&](int bi) {
             const int off = (BACK ? nb - 1 - bi : bi) * U;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                L.ra[u] = __builtin_nontemporal_load((const v2d_t*)(a.racc + ls[u] + off));
-                L.rx[u] = *(const v2d_t*)(a.x + ls[u] + off);
+                ra[u] = __builtin_nontemporal_load((const v2d_t*)(a.racc + ls[u] + off));
+                rx[u] = *(const v2d_t*)(a.x + ls[u] + off);
             }
-            L.ri = *(const v2u_t*)(a.id + c0 + off);
+            ri = *(const v2u_t*)(a.id + c0 + off);
         };
-        auto step = [&](int bi, Batch& L) {
+        load(0);
+        for (int bi = 0; bi < nb; ++bi) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int slot = 2 * (lane & 3) * kSt + 16 * u + (lane >> 2);
-                sacc[slot] = L.ra[u].x;
-                sacc[slot + kSt] = L.ra[u].y;
-                sx[slot] = L.rx[u].x;
-                sx[slot + kSt] = L.rx[u].y;
+                sacc[slot] = ra[u].x;
+                sacc[slot + kSt] = ra[u].y;
+                sx[slot] = rx[u].x;
+                sx[slot + kSt] = rx[u].y;
             }
-            sid[2 * lane] = L.ri.x;
-            sid[2 * lane + 1] = L.ri.y;
+            sid[2 * lane] = ri.x;
+            sid[2 * lane + 1] = ri.y;
             __syncthreads();
-            constexpr int D = DEEP2 ? 2 : 1;
-            if (bi + D < nb) load(bi + D, L);  // in flight during the next D walks
+            if (bi + 1 < nb) load(bi + 1);  // in flight during the walk below
             double out[U];
             const unsigned iw[2] = {sid[2 * lane], sid[2 * lane + 1]};
 #pragma unroll
@@ -2360,18 +2230,6 @@ __global__ __launch_bounds__(64, DEEP2 ? 4 : 1) void tpl_gs_chain_kernel(TplGsCh
                 *(v2d_t*)(a.y + ls[u] + off) = v2d_t{sacc[slot], sacc[slot + kSt]};
             }
             __syncthreads();  // the stage is rewritten by the next batch
-        };
-        Batch L2[DEEP2 ? 2 : 1];
-        if constexpr (DEEP2) {
-            load(0, L2[0]);
-            if (nb > 1) load(1, L2[DEEP2 ? 1 : 0]);
-            for (int bi = 0; bi < nb; bi += 2) {
-                step(bi, L2[0]);
-                if (bi + 1 < nb) step(bi + 1, L2[DEEP2 ? 1 : 0]);
-            }
-        } else {
-            load(0, L2[0]);
-            for (int bi = 0; bi < nb; ++bi) step(bi, L2[0]);
         }
     } else if (live) {
         // clipped chunk (the rank's last rows), a partial wave, or B not a multiple of 8
@@ -3048,32 +2906,10 @@ void launch_csr_plain(hipStream_t s, int mode, bool norm, const DevMatrix& A, co
 #ifndef AMG_PLAIN_RB  // build-time A/B knob: 256-row blocks per plain-CSR workgroup (1 or 2)
 #define AMG_PLAIN_RB 1
 #endif
-    // the pipelined persistent kernel where every block fits one LDS chunk (AMG_PLAIN_PIPE=0:
-    // one workgroup per block)
-    const char* pe = std::getenv("AMG_PLAIN_PIPE");  // read per launch (tests flip it in-process)
-    const bool pipe_env = !(pe && *pe && std::atoi(pe) == 0);
-    const bool pipe = pipe_env && A.plain_maxblk <= kCAP && g >= 8;
-    thread_local int pipe_grid = 0;
-    if (pipe && pipe_grid == 0) {
-        int dev = 0, cus = 0, per_cu = 0;
-        HIP_CHECK(hipGetDevice(&dev));
-        HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, csr_plain_pipe_kernel<KM_SPMV, false>, kTPB, 0));
-        pipe_grid = std::max(8, (cus * std::max(per_cu, 1)) & ~7);
-    }
-    const int pg = pipe ? std::min(pipe_grid, (g + 7) & ~7) : 0;
 #if AMG_PLAIN_RB == 2
-#define AMG_PL(M, N)                                                                                        \
-    do {                                                                                                    \
-        if (pipe) hipLaunchKernelGGL((csr_plain_pipe_kernel<M, N>), dim3(pg), dim3(kTPB), 0, s, a, g);       \
-        else hipLaunchKernelGGL((csr_plain2_kernel<M, N>), dim3((g + 1) / 2), dim3(kTPB), 0, s, a, g);       \
-    } while (0)
+#define AMG_PL(M, N) hipLaunchKernelGGL((csr_plain2_kernel<M, N>), dim3((g + 1) / 2), dim3(kTPB), 0, s, a, g)
 #else
-#define AMG_PL(M, N)                                                                                        \
-    do {                                                                                                    \
-        if (pipe) hipLaunchKernelGGL((csr_plain_pipe_kernel<M, N>), dim3(pg), dim3(kTPB), 0, s, a, g);       \
-        else hipLaunchKernelGGL((csr_plain_kernel<M, N>), dim3(g), dim3(kTPB), 0, s, a);                    \
-    } while (0)
+#define AMG_PL(M, N) hipLaunchKernelGGL((csr_plain_kernel<M, N>), dim3(g), dim3(kTPB), 0, s, a)
 #endif
     switch (mode) {
         case KM_SPMV: AMG_PL(KM_SPMV, false); break;
@@ -3252,13 +3088,8 @@ static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, co
     const long long nch = (long long)A.n_gs_tblk * (kTplRows / A.gs_block);
     const dim3 cg((unsigned)((nch + 63) / 64)), cb(64);
     const size_t clds = (size_t)c.ntpl * (8 + 8 + 4);
-    // two batches of loads in flight (AMG_GS_CHAIN_DEEP=0: one, the round-3 form)
-    const char* de = std::getenv("AMG_GS_CHAIN_DEEP");
-    const bool deep = !(de && *de && std::atoi(de) == 0);
-    if (backward && deep) hipLaunchKernelGGL((tpl_gs_chain_kernel<true, true>), cg, cb, clds, s, c);
-    else if (backward) hipLaunchKernelGGL((tpl_gs_chain_kernel<true, false>), cg, cb, clds, s, c);
-    else if (deep) hipLaunchKernelGGL((tpl_gs_chain_kernel<false, true>), cg, cb, clds, s, c);
-    else hipLaunchKernelGGL((tpl_gs_chain_kernel<false, false>), cg, cb, clds, s, c);
+    if (backward) hipLaunchKernelGGL((tpl_gs_chain_kernel<true>), cg, cb, clds, s, c);
+    else hipLaunchKernelGGL((tpl_gs_chain_kernel<false>), cg, cb, clds, s, c);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -1579,10 +1579,6 @@ void DevMatrix::set_format(int f) {
         }
         pcol.upload(pc.data(), pc.size());
         pval.upload(pv.data(), pv.size());
-        // widest 256-row block, counted from its first even entry (the kernels' first pair)
-        plain_maxblk = 0;
-        for (int64_t r0 = 0; r0 < n_rows; r0 += kTPB)
-            plain_maxblk = std::max<int64_t>(plain_maxblk, host.rp[std::min<int64_t>(n_rows, r0 + kTPB)] - (host.rp[r0] & ~(int64_t)1));
     }
     if (f != AMG_FORMAT_CSR) {
         // the plain arrays (12 B per nonzero) are rebuilt when CSR is selected again; hipFree

@@ -2,7 +2,7 @@
 
 traffic = 2 x FETCH_SIZE + WRITE_SIZE (bytes; FETCH_SIZE reads half the bytes of wide
 streaming loads on gfx950, MI355X_MICROARCH.md "HBM"), averaged over the SpMV launches of
-the 7-pt 256^3 level-0 operator (by default the plain-CSR kernel: csr_plain_pipe_kernel<0>, or csr_plain_kernel<0> with AMG_PLAIN_PIPE=0).  Writes a JSON
+the 7-pt 256^3 level-0 operator (by default the plain-CSR kernel csr_plain_kernel<0>).  Writes a JSON
 that bench.py reports as roofline.traffic."""
 import csv
 import json
@@ -20,7 +20,7 @@ def per_dispatch(path):
     return vals, meta
 
 
-def main(prefix, out, kernels=("csr_plain_pipe_kernel<0", "csr_plain_kernel<0")):
+def main(prefix, out, kernels=("csr_plain_kernel<0",)):
     f, meta = per_dispatch(f"{prefix}_FETCH_SIZE/run_counter_collection.csv")
     w, _ = per_dispatch(f"{prefix}_WRITE_SIZE/run_counter_collection.csv")
     # level-0 operator = first matrix in pmc_levels.py: its first 3 SpMV launches (the

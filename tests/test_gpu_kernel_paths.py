@@ -56,20 +56,15 @@ def _ragged(O):
 
 
 # ---- storage formats ------------------------------------------------------------------
-@pytest.mark.parametrize("fmt", ["csr", "csr_one_block", "blocks"])
+@pytest.mark.parametrize("fmt", ["csr", "blocks"])
 @pytest.mark.parametrize("name", ["7pt_20", "5pt_37x29", "27pt_13", "ragged", "7pt_odd"])
 def test_formats_bit_exact(ctx, oracle, monkeypatch, name, fmt):
-    """AMG_FORMAT_CSR (plain row_ptr / col / val, DESIGN.md 4.5: the pipelined persistent
-    kernel where every block fits one LDS chunk, csr_one_block: one workgroup per block) and
-    AMG_FORMAT_BLOCKS (CSR blocks on every row, templates off): all modes bit-identical to the
-    oracle, including empty rows, a 3000-entry row (two LDS chunks) and an odd nonzero count
-    (padding pair)."""
+    """AMG_FORMAT_CSR (plain row_ptr / col / val) and AMG_FORMAT_BLOCKS (CSR
+    blocks on every row, templates off): all modes bit-identical to the oracle, including
+    empty rows, a 3000-entry row (two LDS chunks) and an odd nonzero count (padding pair)."""
     import raptor_amd as ra
 
     O = oracle
-    if fmt == "csr_one_block":
-        monkeypatch.setenv("AMG_PLAIN_PIPE", "0")
-        fmt = "csr"
     Ao = {"7pt_20": lambda: O.gen_7pt(20, 20, 20), "5pt_37x29": lambda: O.gen_5pt(37, 29),
           "27pt_13": lambda: O.gen_27pt(13, 13, 13), "ragged": lambda: _ragged(O),
           "7pt_odd": lambda: O.gen_7pt(7, 5, 3)}[name]()
