@@ -8,4 +8,5 @@ R=${R:-r4m}
 R=${R}p bash scripts/gpu_r4_pmc.sh || exit 1
 R=${R}l bash scripts/gpu_r4l.sh || exit 1
 NO_TESTS=1 R=${R}z bash scripts/gpu_r4c.sh || exit 1
+R=${R}n bash scripts/gpu_r4n.sh || exit 1
 echo r4m-done
