@@ -2140,7 +2140,10 @@ struct TplGsChainArgs {
 // lines per wave instruction, each fetched again by the next quarter-line load.)
 template <bool BACK>
 __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
-    constexpr int U = 8;
+    // 16 rows per batch: a chunk's batch is one whole 128-byte line of acc, x and y (8 rows =
+    // half lines left the other half to be fetched again a batch later: FETCH_SIZE 1.84x the
+    // algorithmic reads, WRITE_SIZE 1.25x, profiles/r4mn_gs_pmc.txt)
+    constexpr int U = 16;
     // per-GS-template tables sized by the launch (ntpl entries; 27-pt: 27): a wave-sized
     // workgroup with 5 KiB of fixed 256-entry tables fit 11 per CU, 3.7 TB/s on the 27-pt sweep
     extern __shared__ __attribute__((aligned(16))) double chain_lds[];
@@ -2152,7 +2155,7 @@ __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
     // 64-byte lane stride and a 16-way conflict on every read of the walk
     constexpr int kSt = 65;
     __shared__ __attribute__((aligned(16))) double sacc[kSt * U], sx[kSt * U];
-    __shared__ unsigned sid[64 * 2];
+    __shared__ unsigned sid[64 * (U / 4)];
     const int lane = threadIdx.x;
     constexpr int kBit = BACK ? 2 : 1;
     for (int k = lane; k < a.ntpl; k += 64) {
@@ -2171,43 +2174,46 @@ __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
     const bool live = qc < nq;
     const int c0 = live ? cstart(qc) : 0;
     const int c1 = live ? min(c0 + a.B, a.n) : 0;
-    // fast path: B % 8 == 0 and every chunk of the wave whole (wave-uniform)
+    // fast path: B % U == 0 and every chunk of the wave whole (wave-uniform)
     const bool whole = a.B % U == 0 && q0 + 64 <= nq && __all(c1 - c0 == a.B);
     __syncthreads();
     double prev = 0.0;
     if (whole) {
-        // load assignment u (4 per array): line of chunk 16 u + lane / 4, 16-byte piece lane % 4
-        int ls[4];
+        // load assignment u (8 per array): line of chunk 8 u + lane / 8, 16-byte piece lane % 8
+        constexpr int NL = U / 2;  // 16-byte pieces per lane per array
+        int ls[NL];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) ls[u] = cstart(q0 + 16 * u + (lane >> 2)) + 2 * (lane & 3);
+        for (int u = 0; u < NL; ++u) ls[u] = cstart(q0 + (64 / NL) * u + lane / NL) + 2 * (lane % NL);
         const int nb = a.B / U;
-        v2d_t ra[4], rx[4];
-        v2u_t ri;
+        v2d_t ra[NL], rx[NL];
+        v4u_t ri;  // the lane's chunk's U one-byte template ids of the batch
         auto load = [&](int bi) {
             const int off = (BACK ? nb - 1 - bi : bi) * U;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < NL; ++u) {
                 ra[u] = __builtin_nontemporal_load((const v2d_t*)(a.racc + ls[u] + off));
                 rx[u] = *(const v2d_t*)(a.x + ls[u] + off);
             }
-            ri = *(const v2u_t*)(a.id + c0 + off);
+            ri = *(const v4u_t*)(a.id + c0 + off);
         };
+        // stage slot of load piece u: rows 2 (lane % NL), + 1 of chunk (64 / NL) u + lane / NL
+        auto slot_of = [&](int u) { return 2 * (lane % NL) * kSt + (64 / NL) * u + lane / NL; };
         load(0);
         for (int bi = 0; bi < nb; ++bi) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int slot = 2 * (lane & 3) * kSt + 16 * u + (lane >> 2);
+            for (int u = 0; u < NL; ++u) {
+                const int slot = slot_of(u);
                 sacc[slot] = ra[u].x;
                 sacc[slot + kSt] = ra[u].y;
                 sx[slot] = rx[u].x;
                 sx[slot + kSt] = rx[u].y;
             }
-            sid[2 * lane] = ri.x;
-            sid[2 * lane + 1] = ri.y;
+            *(v4u_t*)(sid + 4 * lane) = ri;
             __syncthreads();
             if (bi + 1 < nb) load(bi + 1);  // in flight during the walk below
             double out[U];
-            const unsigned iw[2] = {sid[2 * lane], sid[2 * lane + 1]};
+            const v4u_t iv = *(const v4u_t*)(sid + 4 * lane);
+            const unsigned iw[4] = {iv.x, iv.y, iv.z, iv.w};
 #pragma unroll
             for (int t = 0; t < U; ++t) {
                 const int u = BACK ? U - 1 - t : t;
@@ -2219,20 +2225,20 @@ __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
                 prev = sx[u * kSt + lane] + acc * sdl[tp];
                 out[u] = prev;
             }
-            // x' back through the stage: whole 64-byte lines per 4 lanes, like the loads
+            // x' back through the stage: whole 128-byte lines per 8 lanes, like the loads
 #pragma unroll
             for (int u = 0; u < U; ++u) sacc[u * kSt + lane] = out[u];
             __syncthreads();
             const int off = (BACK ? nb - 1 - bi : bi) * U;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int slot = 2 * (lane & 3) * kSt + 16 * u + (lane >> 2);
+            for (int u = 0; u < NL; ++u) {
+                const int slot = slot_of(u);
                 *(v2d_t*)(a.y + ls[u] + off) = v2d_t{sacc[slot], sacc[slot + kSt]};
             }
             __syncthreads();  // the stage is rewritten by the next batch
         }
     } else if (live) {
-        // clipped chunk (the rank's last rows), a partial wave, or B not a multiple of 8
+        // clipped chunk (the rank's last rows), a partial wave, or B not a multiple of U
         for (int t = 0; t < c1 - c0; ++t) {
             const int i = BACK ? c1 - 1 - t : c0 + t;
             const int tp = a.id[i];
