@@ -3,9 +3,10 @@
 # A/B against the 8-row build (raptor_amd/lib_ab_u8.so) on sa27, then its counters.
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 R=${R:-r4o}
-SEL=gpu KSEL="hybrid_gs or sa_gs or sa27 or full_size_27pt or vcycle_bit_exact" R=${R}t bash scripts/gpu_r4g.sh
-grep -q "tests rc=0" <(tail -3 gpurun_out/${R}t_tests.log; echo) || true
-grep -qE "[0-9]+ passed" gpurun_out/${R}t_tests.log && ! grep -qE "failed|error" gpurun_out/${R}t_tests.log || { echo "tests not green"; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+  -k "hybrid_gs or sa_gs or sa27 or full_size_27pt or vcycle_bit_exact" > gpurun_out/${R}_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/${R}_tests.log; echo "tests rc=$rc"
+[ $rc -ne 0 ] && exit 1
 for i in 1 2; do
   for lib in libraptor_amd lib_ab_u8; do
     RAPTOR_AMD_LIB=raptor_amd/$lib.so timeout -k 10 300 python bench.py --config sa27 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${R}_${lib}_$i.json 2> /tmp/b.err || { tail -5 /tmp/b.err; exit 1; }
