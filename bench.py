@@ -299,8 +299,9 @@ def main():
     # PMC-measured traffic of the same operations (scripts/gpu_pmc_vcycle.sh, 7-pt 256^3):
     # 2 x FETCH_SIZE + WRITE_SIZE per launch beside the stored-format byte model; a ratio
     # above 1.1 is wasted traffic (re-reads), below 1 means cache hits served part of the model
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_vcycle_kernels.json")
-    if args.config == "7pt" and grid == (256, 256, 256) and world == 1 and os.path.exists(pmc_path):
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_vcycle_kernels.json" if args.config == "7pt"
+                            else f"pmc_vcycle_kernels_{args.config}.json")
+    if args.config in ("7pt", "sa27") and grid == (256, 256, 256) and world == 1 and os.path.exists(pmc_path):
         try:
             pm = {(o["level"], o["op"]): o for o in json.load(open(pmc_path))["ops"]}
             for row in table:

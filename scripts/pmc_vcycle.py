@@ -15,9 +15,14 @@ import raptor_amd as ra  # noqa: E402
 
 # torch-free, like bench.py: the library on the ROCm runtime it was built for
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+CFG = sys.argv[2] if len(sys.argv) > 2 else "7pt"  # "sa27": configs[2]'s operations (bench.py --config sa27)
 ctx = ra.Context.native(0)
-A = ra.par_stencil_grid(ctx, "7pt", (N, N, N))
-ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
+if CFG == "sa27":
+    A = ra.par_stencil_grid(ctx, "27pt", (N, N, N))
+    ml = ra.ParSmoothedAggregationSolver().setup(A)
+else:
+    A = ra.par_stencil_grid(ctx, "7pt", (N, N, N))
+    ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
 ops = []
 
 
@@ -33,10 +38,18 @@ for l in range(ml.num_levels - 1):
     nl, nc = Al.local_rows, P.local_cols
     xl, bl, tl = ra.vector_uniform(ctx, nl, 0, 5), ra.vector_uniform(ctx, nl, 0, 6), ctx.empty(nl)
     xc, bc = ra.vector_uniform(ctx, nc, 0, 7), ctx.empty(R.local_rows)
-    table = [("Jacobi", lambda: Al.jacobi(xl, bl, tl), Al.info["jacobi_bytes"]),
-             ("residual", lambda: Al.residual(xl, bl, tl), Al.info["residual_bytes"]),
-             ("restrict R r", lambda: R.mult(tl, bc), R.info["spmv_bytes"]),
-             ("interp x += P e", lambda: P.mult_add(xc, xl), P.info["mult_add_bytes"])]
+    if CFG == "sa27":  # hybrid GS(64) sweeps; gs_bytes after the first sweep builds the formats
+        Al.hybrid_gs(xl, bl, tl, 64)
+        table = [("pre GS (forward)", lambda: Al.hybrid_gs(xl, bl, tl, 64), Al._info()["gs_bytes"]),
+                 ("residual", lambda: Al.residual(xl, bl, tl), Al.info["residual_bytes"]),
+                 ("restrict R r", lambda: R.mult(tl, bc), R.info["spmv_bytes"]),
+                 ("interp x += P e", lambda: P.mult_add(xc, xl), P.info["mult_add_bytes"]),
+                 ("post GS (backward)", lambda: Al.hybrid_gs(xl, bl, tl, 64, backward=True), Al._info()["gs_bytes"])]
+    else:
+        table = [("Jacobi", lambda: Al.jacobi(xl, bl, tl), Al.info["jacobi_bytes"]),
+                 ("residual", lambda: Al.residual(xl, bl, tl), Al.info["residual_bytes"]),
+                 ("restrict R r", lambda: R.mult(tl, bc), R.info["spmv_bytes"]),
+                 ("interp x += P e", lambda: P.mult_add(xc, xl), P.info["mult_add_bytes"])]
     for name, fn, nbytes in table:
         fn()  # warm (first-use builds, caches): outside the segment
         ctx.synchronize()
