@@ -66,12 +66,6 @@ constexpr int kTplMaxLen = 64;     // entries per template
 #ifndef AMG_TPL_SPLIT_READS  // build-time knob: uniform-stencil rows read each row's x separately
 #define AMG_TPL_SPLIT_READS 1
 #endif
-#ifndef AMG_TPL_MASTER_EB  // build-time knob: uniform-stencil window reads issued per batch (0: scheduler's choice)
-#define AMG_TPL_MASTER_EB 0
-#endif
-#ifndef AMG_TPL_GS_EB  // build-time knob: the same for the hybrid-GS old-value pass (more live values per entry)
-#define AMG_TPL_GS_EB 0
-#endif
 #ifndef AMG_TPL_MASK_BRANCH  // build-time knob: masked uniform-stencil rows add under exec masks
 #define AMG_TPL_MASK_BRANCH 0
 #endif

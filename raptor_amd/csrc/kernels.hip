@@ -682,100 +682,6 @@ __global__ __launch_bounds__(kTPB, 8) void csr_plain_kernel(PlainArgs a) {
     }
 }
 
-// Two 256-row blocks per workgroup (AMG_PLAIN_RB=2, A/B knob): both blocks' val / col pairs
-// are loaded before the first block's x gathers, so a workgroup keeps twice the bytes in
-// flight across its dependent rounds (rp -> val / col -> x).  Same rows, same per-block sums
-// and partial slots as csr_plain_kernel: bit-identical.  Blocks whose nonzeros exceed one
-// LDS chunk take the chunked loop of the one-block kernel.
-template <int MODE, bool NORM>
-__device__ __forceinline__ void plain_block_epilogue(const PlainArgs& a, int blk, int r, bool own, int rr,
-                                                     double s) {
-    double out, sq = 0.0;
-    if (MODE == KM_SPMV) {
-        out = s;
-    } else if (MODE == KM_SPMV_ADD) {
-        out = a.y[rr] + s;
-    } else {
-        const double t = a.b[rr] - s;
-        if (NORM) sq = own ? t * t : 0.0;
-        out = MODE == KM_RESID ? t : a.x[rr] + a.omega * (a.dinv[rr] * t);
-    }
-    if (own) a.y[r] = out;
-    if (NORM) {
-        sq = wave_sum(sq);
-        if ((threadIdx.x & 63) == 0) a.partial[blk * kNormParts + (threadIdx.x >> 6)] = sq;
-    }
-}
-
-template <int MODE, bool NORM>
-__global__ __launch_bounds__(kTPB, 8) void csr_plain2_kernel(PlainArgs a, int nblk) {
-    __shared__ __attribute__((aligned(16))) double stage[kCAP];
-    const int tid = threadIdx.x;
-    const int pb = xcd_remap(blockIdx.x, gridDim.x);
-    int bl[2], r0[2], r1[2], k0[2], k1[2], rs[2], re[2], rr[2];
-    bool own[2], fast = true;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        bl[h] = min(2 * pb + h, nblk - 1);  // an odd last block: the second half repeats it, masked
-        r0[h] = bl[h] * kTPB;
-        r1[h] = min(a.n, r0[h] + kTPB);
-        k0[h] = a.rp[r0[h]];
-        k1[h] = a.rp[r1[h]];
-        const int r = r0[h] + tid;
-        own[h] = r < r1[h] && 2 * pb + h < nblk;
-        rr[h] = r < r1[h] ? r : r1[h] - 1;
-        rs[h] = a.rp[rr[h]];
-        re[h] = a.rp[rr[h] + 1];
-        fast = fast && k1[h] - (k0[h] & ~1) <= kCAP;
-    }
-    if (!fast) {  // long rows: block by block, chunked (csr_plain_kernel's loop)
-        for (int h = 0; h < 2; ++h) {
-            if (2 * pb + h >= nblk) break;
-            const int plast = max(k1[h] - 1, 0) & ~1;
-            double s = 0.0;
-            for (int base = k0[h] & ~1; base < k1[h]; base += kCAP) {
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const int q = min(base + 2 * tid + 2 * kTPB * p, plast);
-                    const v2d_t vv = __builtin_nontemporal_load((const v2d_t*)(a.val + q));
-                    const v2i_t cc = __builtin_nontemporal_load((const v2i_t*)(a.col + q));
-                    *(v2d_t*)(stage + 2 * tid + 2 * kTPB * p) = v2d_t{vv.x * plain_x(a, cc.x), vv.y * plain_x(a, cc.y)};
-                }
-                __syncthreads();
-                const int lo = max(rs[h], base) - base, hi = min(re[h], base + kCAP) - base;
-                s = lds_row_sum(stage, lo, hi, s);
-                __syncthreads();
-            }
-            plain_block_epilogue<MODE, NORM>(a, bl[h], r0[h] + tid, own[h], rr[h], s);
-        }
-        return;
-    }
-    v2d_t vv[2][4];
-    v2i_t cc[2][4];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int plast = max(k1[h] - 1, 0) & ~1;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int q = min((k0[h] & ~1) + 2 * tid + 2 * kTPB * p, plast);
-            vv[h][p] = __builtin_nontemporal_load((const v2d_t*)(a.val + q));
-            cc[h][p] = __builtin_nontemporal_load((const v2i_t*)(a.col + q));
-        }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        if (h == 1 && 2 * pb + 1 >= nblk) break;  // workgroup-uniform
-        const int base = k0[h] & ~1;
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-            *(v2d_t*)(stage + 2 * tid + 2 * kTPB * p) =
-                v2d_t{vv[h][p].x * plain_x(a, cc[h][p].x), vv[h][p].y * plain_x(a, cc[h][p].y)};
-        __syncthreads();
-        const double s = lds_row_sum(stage, rs[h] - base, re[h] - base, 0.0);
-        __syncthreads();  // the second block overwrites the stage
-        plain_block_epilogue<MODE, NORM>(a, bl[h], r0[h] + tid, own[h], rr[h], s);
-    }
-}
 
 // STREAM-copy ceiling (bench.py): one pass, 4 x 16-byte pairs per lane (1 KiB-strided, so a
 // wave instruction moves 1 KiB), plain loads and stores.  Same-box probe (profiles/
@@ -1184,13 +1090,12 @@ __device__ __forceinline__ void tpl_row_bases(const TplLds& L, const double* (&w
 
 // The master's products of a lane's R rows, s[j] += v_e x_e in CSR order (masked entries add
 // +0.0: s + (+0.0) == s bit for bit, s starts at +0.0 and a round-to-nearest sum is never -0.0
-// unless both terms are).  With AMG_TPL_MASTER_EB > 0 the window reads of EB entries are all
-// issued before their products (the scheduler otherwise waited on LDS every two or three
-// entries: ~11 exposed LDS round trips per 27-pt block, profiles/r4_tpl_isa.txt).
+// unless both terms are).  (Issuing the window reads of 9 entries before their products, a
+// round-4 build knob, ran slower: profiles/r4_ring_ab.txt.)
 template <int MNE, int R, class Slot, class Val>
 __device__ __forceinline__ void tpl_master_sums(const double* const (&wr)[R], const unsigned (&m)[R], bool full,
                                                 Slot slot, Val val, double (&s)[R]) {
-    constexpr int EB = AMG_TPL_MASTER_EB > 0 ? (AMG_TPL_MASTER_EB < MNE ? AMG_TPL_MASTER_EB : MNE) : 1;
+    constexpr int EB = 1;
     if (full) {
 #pragma unroll
         for (int e0 = 0; e0 < MNE; e0 += EB) {
@@ -1199,7 +1104,6 @@ __device__ __forceinline__ void tpl_master_sums(const double* const (&wr)[R], co
             for (int u = 0; u < EB; ++u)
 #pragma unroll
                 for (int j = 0; j < R; ++j) xv[u][j] = e0 + u < MNE ? wr[j][slot(e0 + u)] : 0.0;
-            if (AMG_TPL_MASTER_EB > 0) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < EB; ++u)
 #pragma unroll
@@ -1214,7 +1118,6 @@ __device__ __forceinline__ void tpl_master_sums(const double* const (&wr)[R], co
             for (int u = 0; u < EB; ++u)
 #pragma unroll
                 for (int j = 0; j < R; ++j) xv[u][j] = e0 + u < MNE ? wr[j][slot(e0 + u)] : 0.0;
-            if (AMG_TPL_MASTER_EB > 0) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < EB; ++u) {
                 const int e = e0 + u;
@@ -1253,7 +1156,7 @@ template <int MNE, int EC, bool NORM, int R, class Slot, class Val>
 __device__ __forceinline__ void tpl_master_gs_sums(const double* const (&wr)[R], const unsigned (&m)[R], bool full,
                                                    const bool (&chain)[R], Slot slot, Val val, double (&acc)[R],
                                                    double (&sold)[R]) {
-    constexpr int EB = AMG_TPL_GS_EB > 0 ? (AMG_TPL_GS_EB < MNE ? AMG_TPL_GS_EB : MNE) : 1;
+    constexpr int EB = 1;
 #pragma unroll
     for (int e0 = 0; e0 < MNE; e0 += EB) {
         double xv[EB][R];
@@ -1261,7 +1164,6 @@ __device__ __forceinline__ void tpl_master_gs_sums(const double* const (&wr)[R],
         for (int u = 0; u < EB; ++u)
 #pragma unroll
             for (int j = 0; j < R; ++j) xv[u][j] = e0 + u < MNE ? wr[j][slot(e0 + u)] : 0.0;
-        if (AMG_TPL_GS_EB > 0) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
             const int e = e0 + u;
@@ -2909,14 +2811,7 @@ void launch_csr_plain(hipStream_t s, int mode, bool norm, const DevMatrix& A, co
     AMG_ASSERT(A.pcol.p != nullptr && A.pval.p != nullptr);
     PlainArgs a{A.rp.p, A.pcol.p, A.pval.p, x, A.halo.p, (int)A.n_cols_local, (int)A.n_rows,
                 b, A.dinv.p, y, omega, partial};
-#ifndef AMG_PLAIN_RB  // build-time A/B knob: 256-row blocks per plain-CSR workgroup (1 or 2)
-#define AMG_PLAIN_RB 1
-#endif
-#if AMG_PLAIN_RB == 2
-#define AMG_PL(M, N) hipLaunchKernelGGL((csr_plain2_kernel<M, N>), dim3((g + 1) / 2), dim3(kTPB), 0, s, a, g)
-#else
 #define AMG_PL(M, N) hipLaunchKernelGGL((csr_plain_kernel<M, N>), dim3(g), dim3(kTPB), 0, s, a)
-#endif
     switch (mode) {
         case KM_SPMV: AMG_PL(KM_SPMV, false); break;
         case KM_SPMV_ADD: AMG_PL(KM_SPMV_ADD, false); break;
