@@ -4,7 +4,7 @@
 # a timeout or crash ends the script.
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 R=${R:-r4f}
-R=${R}n bash scripts/gpu_r4_n2prof.sh > gpurun_out/${R}_n2prof.txt 2>&1; rc=$?
+R=${R}n bash scripts/r4/gpu_r4_n2prof.sh > gpurun_out/${R}_n2prof.txt 2>&1; rc=$?
 tail -40 gpurun_out/${R}_n2prof.txt; [ $rc -ne 0 ] && exit 1
 AMG_TIMING=1 timeout -k 10 600 python -u scripts/setup_ranks.py 256 8 boxes > gpurun_out/${R}_setup8.json 2> gpurun_out/${R}_setup8.err
 rc=$?; echo "setup8 rc=$rc $(cat gpurun_out/${R}_setup8.json)"; [ $rc -ge 124 ] && exit 1

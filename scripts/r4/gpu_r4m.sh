@@ -5,8 +5,8 @@
 # time-limited; a timeout or crash ends the script.
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 R=${R:-r4m}
-R=${R}p bash scripts/gpu_r4_pmc.sh || exit 1
-R=${R}l bash scripts/gpu_r4l.sh || exit 1
-NO_TESTS=1 R=${R}z bash scripts/gpu_r4c.sh || exit 1
-R=${R}n bash scripts/gpu_r4n.sh || exit 1
+R=${R}p bash scripts/r4/gpu_r4_pmc.sh || exit 1
+R=${R}l bash scripts/r4/gpu_r4l.sh || exit 1
+NO_TESTS=1 R=${R}z bash scripts/r4/gpu_r4c.sh || exit 1
+R=${R}n bash scripts/r4/gpu_r4n.sh || exit 1
 echo r4m-done

@@ -15,4 +15,4 @@ import json; d=json.load(open('gpurun_out/${R}_${lib}_$i.json'))
 print('$lib', d['value'], d['ms_per_step'], [(k['level'], k['op'].split()[0], k['us']) for k in d['vcycle_kernels'] if 'GS' in k['op']])"
   done
 done
-R=${R}n bash scripts/gpu_r4n.sh
+R=${R}n bash scripts/r4/gpu_r4n.sh

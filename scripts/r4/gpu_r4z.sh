@@ -9,4 +9,4 @@ rc=$?
 grep -oE "(PASSED|FAILED|ERROR|SKIPPED)" gpurun_out/${R}_tests.log | sort | uniq -c
 tail -3 gpurun_out/${R}_tests.log; echo "tests rc=$rc"
 [ $rc -ne 0 ] && exit 1
-NO_TESTS=1 R=${R}b bash scripts/gpu_r4c.sh
+NO_TESTS=1 R=${R}b bash scripts/r4/gpu_r4c.sh
