@@ -1,9 +1,10 @@
 """Block-cut simulation for SA restrictions: x-tile lines per block for the
 product's row order vs rows sorted by their first / median column, on the oracle's sa27
-hierarchy.  Usage: python scripts/dev/r_block_lines.py 64"""
+hierarchy.  Usage: python tests/analysis_r_block_lines.py 64 (analysis, not a test:
+it lives under tests/ because it runs the oracle)"""
 import os, sys, time
 import numpy as np
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from oracle import oracle as O
 N = int(sys.argv[1])
 t = time.time()
