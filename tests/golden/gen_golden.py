@@ -6,7 +6,13 @@ oracle is pinned here by implementations that share no code with it:
     residual, Jacobi, transposes and Galerkin products R (A P);
   * numpy uint64 arithmetic -- the splitmix64 vector generator and hashes;
   * small pure-Python loop restatements -- RS first pass, PMIS, MIS(2) aggregation, hybrid GS
-    (small sizes only), written from DESIGN.md section 3, not from the C code.
+    (small sizes only), written from DESIGN.md section 3, not from the C code;
+  * (r5) the floating-point setup and the cycle, restated the same way:
+    classical (modified) interpolation weights, SA's tentative prolongator T, rho and smoothed
+    P = T - (4/3 rho) (D^-1 A T), the Gauss-Jordan coarse inverse (numpy row operations), the
+    64-way interleaved butterfly coarse solve, and whole hierarchies + V-cycles built from
+    these restatements, scipy's Galerkin products and the loop smoothers only
+    (setup_<case>.npz).
 Run: python tests/golden/gen_golden.py   (writes the .npz files next to this script)
 """
 from __future__ import annotations
@@ -252,6 +258,227 @@ def hybrid_gs_backward(A, x, b, block):
     return out
 
 
+# --------------------------------------------------------------------------------------
+# floating-point setup and the V-cycle, restated from DESIGN.md section 3 (r5)
+# --------------------------------------------------------------------------------------
+def interp_classical(A, S, cf):
+    """Classical (modified) interpolation, distance 1.  C row: 1 at its coarse index.  F row
+    i: C_i = strong C neighbours; d = a_ii + the weak a_ij (row order); num_j = a_ij for
+    j in C_i; then for each strong F neighbour k (row order): s_k = sum of a_km over m in C_i
+    with sign(a_km) = -sign(a_kk) (row k order); s_k = 0 adds a_ik to d, else num_m +=
+    (a_ik a_km) / s_k over those m.  w_ij = -num_j / d (columns ascending)."""
+    R = rows(A)
+    n = len(R)
+    cidx = np.cumsum(cf == 1) - 1
+    diag = {i: dict(zip(*R[i])).get(i, 0.0) for i in range(n)}
+    indptr, indices, data = [0], [], []
+    for i in range(n):
+        if cf[i] == 1:
+            indices.append(int(cidx[i]))
+            data.append(1.0)
+            indptr.append(len(indices))
+            continue
+        Si = set(S[i])
+        cols, vals = R[i]
+        d = diag[i]
+        num = {}
+        for c, v in zip(cols, vals):
+            if c == i:
+                continue
+            if c in Si and cf[c] == 1:
+                num[c] = v
+            elif c not in Si:
+                d = d + v
+        if num:
+            for k, aik in zip(cols, vals):
+                if k == i or k not in Si or cf[k] == 1:
+                    continue
+                kc, kv = R[k]
+                pos = diag[k] > 0.0
+                sel = [(m, v) for m, v in zip(kc, kv) if m in num and ((v < 0.0) if pos else (v > 0.0))]
+                sk = 0.0
+                for _, v in sel:
+                    sk = sk + v
+                if sk == 0.0:
+                    d = d + aik
+                else:
+                    for m, v in sel:
+                        num[m] = num[m] + (aik * v) / sk
+        for c in sorted(num):
+            indices.append(int(cidx[c]))
+            data.append(-num[c] / d)
+        indptr.append(len(indices))
+    return sp.csr_matrix((np.array(data), np.array(indices, np.int64), np.array(indptr, np.int64)),
+                         shape=(n, int((cf == 1).sum())))
+
+
+def sa_prolongator(A, agg, na):
+    """T_{i,agg(i)} = 1 / sqrt(|agg(i)|); rho = max_i sum_k |a_ik| / |a_ii| (row order);
+    P = T - ((4/3) / rho) (1 / a_ii) (A T) on the union pattern."""
+    n = A.shape[0]
+    size = np.bincount(agg, minlength=na)
+    T = sp.csr_matrix((1.0 / np.sqrt(size[agg].astype(np.float64)), agg.astype(np.int64), np.arange(n + 1)),
+                      shape=(n, na))
+    R = rows(A)
+    rho = 0.0
+    for i, (cols, vals) in enumerate(R):
+        s = 0.0
+        for v in vals:
+            s = s + abs(v)
+        r = s / abs(dict(zip(cols, vals))[i])
+        rho = max(rho, r)
+    omega = (4.0 / 3.0) / rho
+    c = omega * (1.0 / A.diagonal())
+    AT = (A @ T).tocsr()
+    return (T - sp.diags(c) @ AT).tocsr()
+
+
+def gauss_jordan_inverse(M):
+    """Dense inverse: for each column c, pivot = first row r >= c of max |M_rc|, swap, scale
+    the pivot row by 1 / M_cc, subtract f = M_rc times it from every other row with f != 0."""
+    M = np.array(M, np.float64, copy=True)
+    n = M.shape[0]
+    inv = np.eye(n)
+    for c in range(n):
+        p = c + int(np.argmax(np.abs(M[c:, c])))
+        if p != c:
+            M[[c, p]] = M[[p, c]]
+            inv[[c, p]] = inv[[p, c]]
+        ip = 1.0 / M[c, c]
+        M[c] = M[c] * ip
+        inv[c] = inv[c] * ip
+        f = M[:, c].copy()
+        f[c] = 0.0
+        rs = np.nonzero(f)[0]
+        M[rs] = M[rs] - f[rs, None] * M[c][None, :]
+        inv[rs] = inv[rs] - f[rs, None] * inv[c][None, :]
+    return inv
+
+
+def coarse_solve(inv, b):
+    """x_i = sum_j inv_ij b_j as 64 partial sums p_l over j = l mod 64 (ascending j, from 0.0)
+    combined by the butterfly p_l <- p_l + p_{l xor m}, m = 32 ... 1; x_i = p_0."""
+    n = b.size
+    x = np.empty(n)
+    lanes = np.arange(64)
+    for i in range(n):
+        p = np.zeros(64)
+        for j in range(n):
+            p[j % 64] = p[j % 64] + inv[i, j] * b[j]
+        m = 32
+        while m >= 1:
+            p = p + p[lanes ^ m]
+            m >>= 1
+        x[i] = p[0]
+    return x
+
+
+def norm2(v):
+    s = 0.0
+    for t in v.tolist():
+        s = s + t * t
+    return float(np.sqrt(s))
+
+
+def canon(M):
+    M = sp.csr_matrix(M)
+    M.eliminate_zeros()
+    M.sort_indices()
+    return M
+
+
+class PyHierarchy:
+    """The setup and V-cycle of DESIGN.md 3 from the restatements above: strength (theta; SA:
+    theta_l = theta 2^-l), RS / PMIS (seed + l) + classical interpolation or MIS(2) (seed + l)
+    + smoothed P; R = P^T; A_c = R (A P) (scipy); stop at n <= max_coarse, n_c = 0, n_c >= n
+    or (n <= 8192 and 5 n_c > 4 n); Gauss-Jordan inverse on the coarsest level.  Cycle: one
+    pre-smooth (Jacobi 2/3 or forward l1 hybrid GS(64)), r = b - A x, b_c = R r, x_c = 0,
+    recurse, x += P x_c, one post-smooth (Jacobi or backward GS)."""
+
+    def __init__(self, A, coarsen, smoother, theta, max_coarse=256, seed=0x5EED, max_levels=25):
+        self.smoother = smoother
+        self.A, self.P, self.R, self.split = [canon(A)], [], [], []
+        while len(self.A) < max_levels and self.A[-1].shape[0] > max_coarse:
+            l = len(self.A) - 1
+            Al = self.A[-1]
+            n = Al.shape[0]
+            if coarsen == "sa":
+                Sv = strength_symmetric(Al, np.ldexp(theta, -l))
+                agg, na = mis2_aggregate(Sv, seed + l)
+                P = sa_prolongator(Al, agg, na)
+                split = agg
+            else:
+                S = strength_classical(Al, theta)
+                cf = rs_split(S) if coarsen == "rs" else pmis_split(S, seed + l)
+                P = interp_classical(Al, S, cf)
+                split = cf
+            nc = P.shape[1]
+            if nc == 0 or nc >= n or (n <= 8192 and 5 * nc > 4 * n):
+                break
+            P = canon(P)
+            R = canon(P.T.tocsr())
+            self.P.append(P)
+            self.R.append(R)
+            self.split.append(np.asarray(split, np.int32))
+            self.A.append(canon(R @ (Al @ P)))
+        self.inv = gauss_jordan_inverse(self.A[-1].toarray())
+
+    def smooth(self, l, x, b, post):
+        A = self.A[l]
+        if self.smoother == "hybrid_gs":
+            return (hybrid_gs_backward if post else hybrid_gs)(A, x, b, 64)
+        return x + (2.0 / 3.0) * ((1.0 / A.diagonal()) * (b - A @ x))
+
+    def cycle(self, x, b, l=0):
+        if l == len(self.A) - 1:
+            return coarse_solve(self.inv, b)
+        x = self.smooth(l, x, b, False)
+        r = b - self.A[l] @ x
+        xc = self.cycle(np.zeros(self.A[l + 1].shape[0]), self.R[l] @ r, l + 1)
+        x = x + self.P[l] @ xc
+        return self.smooth(l, x, b, True)
+
+    def solve(self, b, iters):
+        x = np.zeros(b.size)
+        hist = [norm2(b - self.A[0] @ x)]
+        for _ in range(iters):
+            x = self.cycle(x, b)
+            hist.append(norm2(b - self.A[0] @ x))
+        return x, np.array(hist)
+
+
+# (name, generator, coarsen, smoother, theta, max_coarse)
+SETUP_CASES = [
+    ("p5_32x32_rs_jacobi", lambda: poisson5(32, 32), "rs", "jacobi", 0.25, 256),
+    ("p5_32x32_rs_jacobi_mc16", lambda: poisson5(32, 32), "rs", "jacobi", 0.25, 16),
+    ("p7_10x9x8_pmis_jacobi_mc16", lambda: poisson7(10, 9, 8), "pmis", "jacobi", 0.25, 16),
+    ("fe27_8x7x6_sa_gs_mc16", lambda: fe27(8, 7, 6), "sa", "hybrid_gs", 0.08, 16),
+    ("p7_10x9x8_sa_gs_mc16", lambda: poisson7(10, 9, 8), "sa", "hybrid_gs", 0.08, 16),
+]
+
+
+def gen_setup_case(name, gen, coarsen, smoother, theta, max_coarse):
+    A = gen()
+    H = PyHierarchy(A, coarsen, smoother, theta, max_coarse)
+    n = A.shape[0]
+    b = A @ uniform(n, 42)
+    out = {"nlev": np.array(len(H.A), np.int64), "inv": H.inv, "b": b}
+    for l in range(len(H.A)):
+        out.update(csr_arrays(f"A{l}", H.A[l]))
+        if l + 1 < len(H.A):
+            out.update(csr_arrays(f"P{l}", H.P[l]))
+            out[f"split{l}"] = H.split[l]
+    x = np.zeros(n)
+    for k in range(3):
+        x = H.cycle(x, b)
+        out[f"x{k}"] = x
+    xs, hist = H.solve(b, 8)
+    out["xsolve"] = xs
+    out["hist"] = hist
+    save(f"setup_{name}.npz", **out)
+    print(name, "levels", [M.shape[0] for M in H.A], "hist", hist[0], "->", hist[-1])
+
+
 def save(name, **arrays):
     np.savez_compressed(os.path.join(HERE, name), **arrays)
 
@@ -297,6 +524,8 @@ def main():
         save(f"{name}.npz", **out)
         print(name, n, A.nnz, "C(rs)", int(out["cf_rs"].sum()), "C(pmis)", int(out["cf_pmis"].sum()),
               "aggs", na)
+    for case in SETUP_CASES:
+        gen_setup_case(*case)
     # vector generator at an offset (partition independence of the generator)
     save("uniform.npz", u0=uniform(1000, 42), u_off=uniform(1000, 42, first=123456789),
          u_seed7=uniform(17, 7))

@@ -163,3 +163,57 @@ def test_oracle_pcg_beats_stationary_iteration(oracle):
     assert hp[-1] < 0.1 * hv[-1]
     r = b - A.spmv(x)
     assert abs(np.linalg.norm(r) - hp[-1]) <= 1e-6 * hp[0]  # recursive residual ~ true residual
+
+
+SETUP_CASES = {  # tests/golden/gen_golden.py SETUP_CASES: (generator, coarsen, smoother, theta, max_coarse)
+    "p5_32x32_rs_jacobi": ("p5_32x32", "rs", 256),
+    "p5_32x32_rs_jacobi_mc16": ("p5_32x32", "rs", 16),
+    "p7_10x9x8_pmis_jacobi_mc16": ("p7_10x9x8", "pmis", 16),
+    "fe27_8x7x6_sa_gs_mc16": ("fe27_8x7x6", "sa", 16),
+    "p7_10x9x8_sa_gs_mc16": ("p7_10x9x8", "sa", 16),
+}
+
+
+def _canon(M):
+    M = sp.csr_matrix(M)
+    M.eliminate_zeros()
+    M.sort_indices()
+    return M
+
+
+def _same(a, b):
+    return (a.shape == b.shape and np.array_equal(a.indptr, b.indptr)
+            and np.array_equal(a.indices, b.indices) and np.array_equal(a.data, b.data))
+
+
+@pytest.mark.parametrize("case", list(SETUP_CASES))
+def test_fp_setup_and_cycle_match_restatement(oracle, case):
+    """The oracle's floating-point setup and V-cycle against gen_golden.py's independent
+    restatement: every P_l (classical interpolation weights, or SA's
+    T, rho and smoothed P) and A_{l+1} = R (A P) bit for bit (explicit zeros aside: the oracle
+    keeps them, scipy drops them), the C/F split or aggregates, the Gauss-Jordan coarse
+    inverse bit for bit, three V-cycle iterates (butterfly coarse solve, Jacobi / l1 hybrid GS)
+    bit for bit, and an 8-cycle solve history (sequential norm) bit for bit."""
+    O = oracle
+    prob, coarsen, max_coarse = SETUP_CASES[case]
+    g = load(f"setup_{case}")
+    A = oracle_gen(O, prob)
+    H = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen], max_coarse=max_coarse))
+    nlev = int(g["nlev"])
+    assert H.num_levels == nlev >= 3
+    for l in range(nlev):
+        assert _same(_canon(H.matrix(l, "A")), gold_csr(g, f"A{l}")), ("A", l)
+        if l + 1 < nlev:
+            assert _same(_canon(H.matrix(l, "P")), gold_csr(g, f"P{l}")), ("P", l)
+            assert np.array_equal(H.split(l), g[f"split{l}"]), ("split", l)
+    Ac = O.Csr.from_scipy(H.matrix(nlev - 1, "A"))
+    assert np.array_equal(O.dense_inverse(Ac), g["inv"])
+    b = g["b"]
+    x = np.zeros(b.size)
+    for k in range(3):
+        x = H.cycle(x, b)
+        assert np.array_equal(x, g[f"x{k}"]), ("cycle", k)
+    xs, hist = H.solve(np.zeros(b.size), b, max_iter=8)
+    assert np.array_equal(xs, g["xsolve"])
+    assert np.array_equal(hist, g["hist"])
+    assert hist[-1] < hist[0]
