@@ -136,13 +136,16 @@ def main():
             tr = time.perf_counter()
             A, _ = A.reorder("rcm")
             reorder_s = time.perf_counter() - tr
-    else:
-        boxes = None
+    boxes = None
+    if not g3:
         if args.partition == "boxes" and world > 1:
             boxes = BOXES.get(world) if not args.grid else None
             if boxes is None:  # other rank counts / grids: boxes along z (= slabs)
                 boxes = (1, 1, world)
         A = ra.par_stencil_grid(ctx, "27pt" if sa27 else "7pt", grid, boxes=boxes)
+    part_label = ("one rank" if world == 1 else "even row partition" if g3 else
+                  "boxes " + "x".join(str(v) for v in boxes) + " (grid numbered box by box)"
+                  if boxes and tuple(boxes) != (1, 1, world) else "z-slab row partition")
     log(rank, f"matrix {grid} built in {time.perf_counter() - t0:.1f}s; local rows {A.local_rows}")
     t1 = time.perf_counter()
     graph = False if args.no_graph else None
@@ -190,6 +193,64 @@ def main():
     # the residual faster): the factor over the last 5 cycles is the asymptotic one
     conv_last5 = (float((hist[-1] / hist[-6]) ** 0.2) if len(hist) >= 6 and hist[-6] > 0 else None)
     log(rank, f"{args.steps} V-cycles in {dt * 1e3:.2f} ms -> {iters_per_s:.1f} it/s, conv {conv}")
+
+    def timed_solve(fn):
+        """max over ranks of the wall time of fn() (a collective solve), barrier + device sync
+        on both sides, like the timed region"""
+        x.zero_()
+        ctx.synchronize()
+        barrier()
+        ctx.synchronize()
+        t = time.perf_counter()
+        res = fn()
+        ctx.synchronize()
+        barrier()
+        t = time.perf_counter() - t
+        return (comm.allreduce_max(t) if world > 1 else t), res
+
+    # the other cycle mode, same solve, same process (VERDICT r4 item 6a: at N > 1 graph replay
+    # is the default on an expectation about xGMI; both are measured so a SCALE run decides)
+    modes = None
+    if not args.no_graph:
+        ml.set_graph(False)
+        ml.solve(x, b, max_iter=max(1, args.warmup))
+        t_eager, _ = timed_solve(lambda: ml.solve(x, b, max_iter=args.steps))
+        ml.set_graph(graph_used)
+        ml.solve(x, b, max_iter=max(1, args.warmup))  # recapture
+        modes = {"graph_ms_per_step": round(dt * 1e3 / args.steps, 4) if graph_used else None,
+                 "eager_ms_per_step": round(t_eager * 1e3 / args.steps, 4),
+                 "timed_mode": "graph" if graph_used else "eager"}
+        log(rank, f"eager cycles: {t_eager * 1e3 / args.steps:.4f} ms/step")
+
+    # time to solution (VERDICT r4 item 7): stationary solve and AMG-PCG to 1e-8 relative
+    # residual, setup excluded (reported beside it).  tol > 0 reads the norm back every
+    # iteration (one host wait each); the same iteration count without the check is the
+    # asynchronous figure.
+    tol = 1e-8
+    # each form runs once untimed first: its hipGraphs are captured there, not in the timing
+    # (tol = 1 stops after one cycle, but sizes the device history for 1000 first: a larger
+    # history later would drop the captured graphs)
+    timed_solve(lambda: ml.solve(x, b, max_iter=1000, tol=1.0))
+    timed_solve(lambda: ml.solve(x, b, max_iter=2))
+    t_s, (_, h_s) = timed_solve(lambda: ml.solve(x, b, max_iter=1000, tol=tol))
+    n_s = len(h_s) - 1
+    t_sa, _ = timed_solve(lambda: ml.solve(x, b, max_iter=n_s))
+    timed_solve(lambda: ml.pcg(x, b, max_iter=3))
+    t_p, (_, h_p) = timed_solve(lambda: ml.pcg(x, b, max_iter=1000, tol=tol))
+    n_p = len(h_p) - 1
+    t_pa, _ = timed_solve(lambda: ml.pcg(x, b, max_iter=n_p))
+    time_to_tol = {
+        "tol_rel": tol,
+        "setup_s": round(setup_s, 3),
+        "solve": {"cycles": n_s, "reached": bool(h_s[-1] <= tol * h_s[0]), "seconds": round(t_s, 5),
+                  "seconds_no_check": round(t_sa, 5)},
+        "pcg": {"iterations": n_p, "reached": bool(h_p[-1] <= tol * h_p[0]), "seconds": round(t_p, 5),
+                "seconds_no_check": round(t_pa, 5)},
+        "what": "rel. residual <= tol from x0 = 0; 'seconds' with the per-iteration norm check "
+                "(host wait), 'seconds_no_check' the same iteration count without it; setup "
+                "(hierarchy + device formats) not included",
+    }
+    log(rank, f"time to {tol:g}: solve {n_s} cycles {t_s * 1e3:.1f} ms, pcg {n_p} its {t_p * 1e3:.1f} ms")
 
     # bytes of one V-cycle on all ranks: plain-CSR (SURVEY.md 8(d)) and stored-format (what
     # the kernels stream).  The per-iteration residual norm is fused into the next cycle's
@@ -276,22 +337,27 @@ def main():
         xl, bl, tl = ra.vector_uniform(ctx, nl, 0, 5), ra.vector_uniform(ctx, nl, 0, 6), ctx.empty(nl)
         xc, bc = ra.vector_uniform(ctx, nc, 0, 7), ctx.empty(R.local_rows)
         ai, pi, ri = Al.info, P.info, R.info
+        # per_cycle: launches of the op in one V-cycle (Jacobi: pre + post on level 0; on
+        # coarser levels the pre-sweep from x = 0 is fused into the restriction above)
         if gs:
             Al.hybrid_gs(xl, bl, tl, 64)  # builds the sliced-ELL copy if the cycle has not
             ai = Al._info()
-            ops = [("pre GS (forward)", lambda: Al.hybrid_gs(xl, bl, tl, 64), ai["gs_bytes"]),
-                   ("residual", lambda: Al.residual(xl, bl, tl), ai["residual_bytes"]),
-                   ("restrict R r", lambda: R.mult(tl, bc), ri["spmv_bytes"]),
-                   ("interp x += P e", lambda: P.mult_add(xc, xl), pi["mult_add_bytes"]),
-                   ("post GS (backward)", lambda: Al.hybrid_gs(xl, bl, tl, 64, backward=True), ai["gs_bytes"])]
+            ops = [("pre GS (forward)", lambda: Al.hybrid_gs(xl, bl, tl, 64), ai["gs_bytes"], 1),
+                   ("residual", lambda: Al.residual(xl, bl, tl), ai["residual_bytes"], 1),
+                   ("restrict R r", lambda: R.mult(tl, bc), ri["spmv_bytes"], 1),
+                   ("interp x += P e", lambda: P.mult_add(xc, xl), pi["mult_add_bytes"], 1),
+                   ("post GS (backward)", lambda: Al.hybrid_gs(xl, bl, tl, 64, backward=True), ai["gs_bytes"], 1)]
         else:
-            ops = [("Jacobi", lambda: Al.jacobi(xl, bl, tl), ai["jacobi_bytes"]),
-                   ("residual", lambda: Al.residual(xl, bl, tl), ai["residual_bytes"]),
-                   ("restrict R r", lambda: R.mult(tl, bc), ri["spmv_bytes"]),
-                   ("interp x += P e", lambda: P.mult_add(xc, xl), pi["mult_add_bytes"])]
-        for name, fn, nbytes in ops:
+            ops = [("Jacobi", lambda: Al.jacobi(xl, bl, tl), ai["jacobi_bytes"], 2 if l == 0 else 1),
+                   ("residual", lambda: Al.residual(xl, bl, tl), ai["residual_bytes"], 1),
+                   ("restrict R r", lambda: R.mult(tl, bc), ri["spmv_bytes"], 1),
+                   ("interp x += P e", lambda: P.mult_add(xc, xl), pi["mult_add_bytes"], 1)]
+        for name, fn, nbytes, per in ops:
             ms = timed(fn, 10)
-            table.append({"level": l, "op": name, "us": round(ms * 1e3, 1), "stored_bytes": int(nbytes),
+            M = P if name.startswith("interp") else R if name.startswith("restrict") else Al
+            table.append({"level": l, "op": name, "kernel": kernel_name(M.info, name),
+                          "us": round(ms * 1e3, 1), "per_cycle": per,
+                          "stored_bytes": int(nbytes),
                           "mall_resident": int(nbytes) < MALL_BYTES,
                           "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
                           "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
@@ -317,7 +383,10 @@ def main():
                     row["traffic_stale"] = o is not None
         except (OSError, KeyError, ValueError):
             pass
+    # the dominant kernel: the cycle's longest single launch (the roofline below); the
+    # largest share of a cycle (us x launches per cycle) is named beside it
     dominant = max(table, key=lambda t: t["us"]) if table else None
+    top_share = max(table, key=lambda t: t["us"] * t["per_cycle"]) if table else None
     del fl_src, fl_dst, rd_part
     barrier()
 
@@ -358,13 +427,13 @@ def main():
                 "workload": (f"G3_circuit substitute: graph Laplacian on a {grid[0]}x{grid[1]} lattice "
                              f"({n_global} rows, {infos[0]['nnz_global']} nnz, seed 1), "
                              f"{'random numbering' if args.no_reorder else 'RCM-reordered'}, smoothed "
-                             "aggregation (MIS(2)), hybrid GS(64) 1+1 V-cycle, even row partition")
+                             f"aggregation (MIS(2)), hybrid GS(64) 1+1 V-cycle, {part_label}")
                 if g3 else
                 (f"3D 27-pt Q1 anisotropic diffusion (1,1,1e-3) {grid[0]}x{grid[1]}x{grid[2]}, "
-                             "smoothed aggregation (MIS(2)), hybrid GS(64) 1+1 V-cycle, z-slab row partition")
+                             f"smoothed aggregation (MIS(2)), hybrid GS(64) 1+1 V-cycle, {part_label}")
                 if sa27 else
                 (f"3D 7-pt Poisson {grid[0]}x{grid[1]}x{grid[2]}, PMIS + classical interp, "
-                 "Jacobi(2/3) 1+1 V-cycle, z-slab row partition"),
+                 f"Jacobi(2/3) 1+1 V-cycle, {part_label}"),
                 "grid": list(grid),
                 "global_rows": n_global,
                 "levels": nlev,
@@ -372,10 +441,7 @@ def main():
                 "level_nnz": [i["nnz_global"] for i in infos],
                 "operator_complexity": round(sum(i["nnz_global"] for i in infos) / infos[0]["nnz_global"], 3),
                 "parallelism": f"row-partition x{world}, RCCL halo",
-                "partition": ("one rank" if world == 1 else
-                              "boxes " + "x".join(str(v) for v in BOXES.get(world, (1, 1, world)))
-                              if args.partition == "boxes" and not g3 and not args.grid else
-                              "even rows" if g3 else "z-slabs"),
+                "partition": part_label,
                 "setup_s": round(setup_s, 2),
                 "reorder_s": None if reorder_s is None else round(reorder_s, 2),
                 "hipgraph": graph_used,
@@ -389,7 +455,32 @@ def main():
             "vcycle_stored_bytes": cyc_stored,
             "vcycle_stored_GBps": round(cyc_stored * iters_per_s / 1e9, 1),
             "vcycle_csr_equiv_bytes": cyc_bytes,
-            "roofline": {
+            # roofline: the timed cycle's dominant kernel (its longest single launch), timed
+            # live with HIP events on the context stream (eager launches of the same operation,
+            # rank 0), scored on the bytes its stored format must move;
+            # traffic: PMC 2 x FETCH_SIZE + WRITE_SIZE per launch of the same operation
+            # (profiles/pmc_vcycle_kernels*.json) when taken on this build's format
+            "roofline": None if dominant is None else {
+                "bound": "hbm",
+                "kernel": f"{dominant['kernel']} -- level-{dominant['level']} {dominant['op']}, rank 0",
+                "achieved": dominant["GBps"],
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": dominant["frac"],
+                "traffic": dominant.get("traffic"),
+                "traffic_unit": "bytes per launch",
+                "bytes_per_launch": dominant["stored_bytes"],
+                "bytes_definition": "stored-format HBM bytes per launch (DESIGN.md 4, 8(d) per-unit "
+                                    "figures in the operator's stored format)",
+                "avg_launch_ms": round(dominant["us"] * 1e-3, 5),
+                "stream_copy_GBps": round(copy_gbs, 1),
+                "stream_read_GBps": round(read_gbs, 1),
+                "largest_cycle_share": None if top_share is None else
+                    {k: top_share[k] for k in ("level", "op", "kernel", "us", "per_cycle", "frac")},
+            },
+            # SURVEY.md 8(d)'s SpMV leg (north_star: >= 60 % of the HBM roofline on the 256^3
+            # 7-pt SpMV): the level-0 mult on the plain CSR arrays 8(d) prices
+            "spmv_roofline_csr": {
                 "bound": "hbm",
                 "kernel": "csr_plain_kernel<SPMV> -- level-0 ParCSRMatrix::mult, plain CSR "
                           "(AMG_FORMAT_CSR: int32 row_ptr/col, fp64 val), rank 0",
@@ -434,12 +525,32 @@ def main():
             "runtime": ra.runtime_versions(),
             "vcycle_kernels": table,
             "vcycle_dominant_kernel": dominant,
+            "cycle_modes": modes,
+            "time_to_tol": time_to_tol,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), file=out_stream, flush=True)
     del ml, A
     if world > 1:
         comm.close()
+
+
+def kernel_name(info, op):
+    """The kernel family an operation of a matrix runs, from its format info."""
+    if op.startswith(("pre GS", "post GS")):
+        if info["template_rows"] > 0:
+            return "tpl_gs_acc_kernel + tpl_gs_chain_kernel"
+        return "csr_block_kernel<GSACC> + gs_chain_kernel" if info["gs_split"] else "hybrid_gs_kernel"
+    mode = {"Jacobi": "JACOBI", "residual": "RESID", "restrict R r": "SPMV",
+            "interp x += P e": "SPMV_ADD"}[op]
+    if info["template_rows"] > 0:
+        fam = "tpl_march_kernel" if info["tpl_march_shift"] > 0 else "tpl_kernel"
+        if info["template_rows"] < info["n_local_rows"]:
+            fam += " + csr_block_kernel"
+        return f"{fam}<{mode}>"
+    vi = info["n_vi_blocks"] / max(1, info["n_blocks"])
+    return (f"csr_block_kernel<{mode}> ({info['tile_line_bytes']}-byte x-tile lines, "
+            f"{vi:.0%} value-indexed blocks, {info['n_blocks']} blocks)")
 
 
 def _cpu_model():

@@ -20,8 +20,10 @@ allocated through the C-ABI.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
+import weakref
 
 import numpy as np
 
@@ -71,6 +73,35 @@ def _torch():
     return torch
 
 
+# ---- teardown --------------------------------------------------------------------------
+# Objects left alive at interpreter exit used to be freed by their __del__s during module
+# teardown, after the HIP runtime's (and a profiler tool's) own finalisation had begun: a
+# late hipFree faulted under rocprofv3.  Every live handle is registered
+# here and destroyed by an atexit hook -- Python's atexit runs before the C runtime's exit
+# handlers -- in dependency order: solvers, then matrices, then vectors and events, then
+# contexts.  After it ran, every __del__ is a no-op.
+_live = {k: weakref.WeakSet() for k in ("solver", "matrix", "buffer", "context")}
+_finalized = False
+
+
+def _track(kind: str, obj):
+    _live[kind].add(obj)
+
+
+@atexit.register
+def _teardown():
+    global _finalized
+    if _finalized:
+        return
+    for kind in ("solver", "matrix", "buffer", "context"):
+        for obj in list(_live[kind]):
+            try:
+                obj._release()
+            except Exception:
+                pass
+    _finalized = True
+
+
 class DeviceVector:
     """float64 device vector of a native (torch-free) context, allocated through the C-ABI
     (amg_device_malloc); freed when collected.  ``numpy()`` copies it to the host."""
@@ -80,6 +111,7 @@ class DeviceVector:
         self.n = int(n)
         self.ptr = C.c_void_p()
         check(lib().amg_device_malloc(ctx.h, 8 * self.n, C.byref(self.ptr)))
+        _track("buffer", self)
 
     def numel(self) -> int:
         return self.n
@@ -109,14 +141,18 @@ class DeviceVector:
             check(lib().amg_memset_async(self.ctx.h, self.ptr, 0, 8 * self.n))
         return self
 
-    def __del__(self):
+    def _release(self):
         p = getattr(self, "ptr", None)
-        if p and p.value:
+        self.ptr = None
+        if p and p.value and self.ctx.h:
+            lib().amg_device_free(self.ctx.h, p)
+
+    def __del__(self):
+        if not _finalized:
             try:
-                lib().amg_device_free(self.ctx.h, p)
+                self._release()
             except Exception:
                 pass
-            self.ptr = None
 
 
 class Event:
@@ -126,6 +162,7 @@ class Event:
         self.ctx = ctx
         self.h = C.c_void_p()
         check(lib().amg_event_create(ctx.h, C.byref(self.h)))
+        _track("buffer", self)
 
     def record(self):
         check(lib().amg_event_record(self.h))
@@ -136,14 +173,18 @@ class Event:
         check(lib().amg_event_elapsed_ms(self.h, end.h, C.byref(ms)))
         return ms.value
 
-    def __del__(self):
+    def _release(self):
         h = getattr(self, "h", None)
+        self.h = None
         if h:
+            lib().amg_event_destroy(h)
+
+    def __del__(self):
+        if not _finalized:
             try:
-                lib().amg_event_destroy(h)
+                self._release()
             except Exception:
                 pass
-            self.h = None
 
 
 def _ptr(t):
@@ -182,6 +223,7 @@ class Context:
         self.h = C.c_void_p()
         check(lib().amg_context_create(self.device, C.c_void_p(self.stream.cuda_stream),
                                        C.byref(self.h)))
+        _track("context", self)
         self.rank, self.nranks = 0, 1
         self._keep = []
 
@@ -220,6 +262,7 @@ class Context:
         ctx.stream = None
         ctx.h = C.c_void_p()
         check(lib().amg_context_create(ctx.device, None, C.byref(ctx.h)))
+        _track("context", ctx)
         ctx.rank, ctx.nranks = 0, 1
         ctx._keep = []
         if comm is not None and comm.nranks > 1:
@@ -235,10 +278,12 @@ class Context:
         return ctx
 
     @classmethod
-    def loopback(cls, rank: int, nranks: int, world: str, device: int = 0, stream=None):
+    def loopback(cls, rank: int, nranks: int, world: str, device: int = 0, stream=None,
+                 native: bool = False):
         """In-process virtual rank ``rank`` of ``nranks`` (one thread per rank, shared GPU):
-        the multi-rank path with device-to-device copies in place of RCCL."""
-        ctx = cls(device, stream)
+        the multi-rank path with device-to-device copies in place of RCCL.  native: a
+        torch-free rank (``Context.native``; its own stream, ``DeviceVector``s)."""
+        ctx = cls.native(device) if native else cls(device, stream)
         check(lib().amg_context_set_loopback(ctx.h, int(rank), int(nranks), world.encode()))
         ctx.rank, ctx.nranks = int(rank), int(nranks)
         return ctx
@@ -261,14 +306,18 @@ class Context:
         with torch.cuda.stream(self.stream):
             return torch.zeros(int(n), dtype=torch.float64, device=self.torch_device)
 
-    def __del__(self):
+    def _release(self):
         h = getattr(self, "h", None)
+        self.h = None
         if h:
+            lib().amg_context_destroy(h)
+
+    def __del__(self):
+        if not _finalized:
             try:
-                lib().amg_context_destroy(h)
+                self._release()
             except Exception:
                 pass
-            self.h = None
 
 
 class ParCSRMatrix:
@@ -282,6 +331,8 @@ class ParCSRMatrix:
         self.h = handle
         self._owner = owner  # solver that owns a borrowed level matrix
         self.info = self._info()
+        if owner is None:
+            _track("matrix", self)
 
     # ---- construction -------------------------------------------------------------
     @classmethod
@@ -415,14 +466,18 @@ class ParCSRMatrix:
         check(lib().amg_par_csr_residual_norm(self.h, _ptr(x), _ptr(b), C.byref(out)))
         return out.value
 
-    def __del__(self):
+    def _release(self):
         h = getattr(self, "h", None)
+        self.h = None
         if h and self._owner is None:
+            lib().amg_par_csr_destroy(h)
+
+    def __del__(self):
+        if not _finalized:
             try:
-                lib().amg_par_csr_destroy(h)
+                self._release()
             except Exception:
                 pass
-        self.h = None
 
 
 _STENCILS = {"5pt": AMG_STENCIL_5PT, "7pt": AMG_STENCIL_7PT, "27pt": AMG_STENCIL_27PT}
@@ -547,6 +602,7 @@ class ParMultilevel:
         self.A = A
         self.h = C.c_void_p()
         check(lib().amg_solver_setup(A.h, C.byref(self.options), C.byref(self.h)))
+        _track("solver", self)
         if self.use_graph is not None:
             check(lib().amg_solver_set_graph(self.h, 1 if self.use_graph else 0))
         return self
@@ -574,6 +630,11 @@ class ParMultilevel:
         check(lib().amg_solver_level_split(self.h, int(level),
                                            out.ctypes.data_as(C.POINTER(C.c_int32))))
         return out
+
+    def set_graph(self, enable: bool):
+        """Replay captured hipGraphs (True) or launch cycles eagerly (False).  Collective."""
+        check(lib().amg_solver_set_graph(self.h, 1 if enable else 0))
+        return self
 
     @property
     def graph_enabled(self) -> bool:
@@ -605,14 +666,18 @@ class ParMultilevel:
                                    hist.ctypes.data_as(C.POINTER(C.c_double)), C.byref(it)))
         return x, hist[: it.value + 1]
 
-    def __del__(self):
+    def _release(self):
         h = getattr(self, "h", None)
+        self.h = None
         if h:
+            lib().amg_solver_destroy(h)
+
+    def __del__(self):
+        if not _finalized:
             try:
-                lib().amg_solver_destroy(h)
+                self._release()
             except Exception:
                 pass
-            self.h = None
 
 
 class ParRugeStubenSolver(ParMultilevel):

@@ -7,10 +7,14 @@ barriers / small reductions around timed regions.  ``SocketComm`` provides them 
 importing torch, so the process binds the HIP runtime and RCCL libraptor_amd.so was built
 against (a torch-first process binds torch's bundled copies).
 
-The mesh uses Linux abstract-namespace Unix sockets named after ``key`` (the launcher's
-MASTER_PORT by default), so it is confined to one node -- as the bench is (one node, 1-8 GPUs).
-Rank r listens on ``raptor-amd/<key>/<r>``, connects to every lower rank and accepts every
-higher one; each connection starts with the connecting rank's id."""
+The mesh uses Linux abstract-namespace Unix sockets named after ``key``, so it is confined to
+one node -- as the bench is (one node, 1-8 GPUs).  Rank r listens on ``raptor-amd/<key>/<r>``,
+connects to every lower rank and accepts every higher one; each connection starts with the
+connecting rank's id.  The default key is per job: ``RAPTOR_AMD_MESH_KEY`` if set, else the
+launcher's MASTER_PORT joined with torchrun's TORCHELASTIC_RUN_ID or, without one, the parent
+(launcher) process id -- two jobs on a node never share a name.  Abstract sockets
+carry no file permissions, so both ends check the peer's credentials (SO_PEERCRED): only a
+process of the same user joins the mesh."""
 from __future__ import annotations
 
 import ctypes as C
@@ -27,6 +31,25 @@ from ._lib import ALLTOALLV_FN
 
 def _name(key: str, rank: int) -> str:
     return f"\0raptor-amd/{key}/{rank}"
+
+
+def default_key() -> str:
+    """The per-job mesh name (module docstring)."""
+    k = os.environ.get("RAPTOR_AMD_MESH_KEY")
+    if k:
+        return k
+    run = os.environ.get("TORCHELASTIC_RUN_ID", "")
+    if not run or run == "none":
+        run = f"ppid{os.getppid()}"
+    return f"{os.environ.get('MASTER_PORT', '0')}.{run}"
+
+
+def _check_peer(sock):
+    """The peer runs as this user (SO_PEERCRED: pid, uid, gid)."""
+    cred = sock.getsockopt(socket.SOL_SOCKET, socket.SO_PEERCRED, struct.calcsize("3i"))
+    _, uid, _ = struct.unpack("3i", cred)
+    if uid != os.getuid():
+        raise ConnectionError(f"mesh peer runs as uid {uid}, not {os.getuid()}")
 
 
 def _recv_into(sock, view):
@@ -46,7 +69,7 @@ class SocketComm:
         self.rank, self.nranks = int(rank), int(nranks)
         if not 0 <= self.rank < self.nranks:
             raise ValueError("bad rank / nranks")
-        key = str(key if key is not None else os.environ.get("MASTER_PORT", "0"))
+        key = str(key if key is not None else default_key())
         self.peers: dict[int, socket.socket] = {}
         if self.nranks == 1:
             return
@@ -66,11 +89,13 @@ class SocketComm:
                         if time.monotonic() > deadline:
                             raise TimeoutError(f"rank {self.rank}: rank {q} never listened")
                         time.sleep(0.05)
+                _check_peer(s)
                 s.sendall(struct.pack("<q", self.rank))
                 self.peers[q] = s
             lst.settimeout(max(1.0, deadline - time.monotonic()))
             for _ in range(self.rank + 1, self.nranks):  # accept the higher ranks
                 s, _ = lst.accept()
+                _check_peer(s)
                 s.settimeout(None)
                 hdr = bytearray(8)
                 _recv_into(s, memoryview(hdr))

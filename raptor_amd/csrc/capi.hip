@@ -29,7 +29,7 @@ static thread_local std::string g_err;
 
 template <class F>
 static int guard(F&& f) {
-    omp_quiet_thread();
+    OmpQuiet quiet;  // blocktime 0 for the library's parallel regions, restored on return
     try {
         f();
         return AMG_OK;

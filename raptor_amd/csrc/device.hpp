@@ -493,9 +493,10 @@ struct Solver {
         const double* x = nullptr;
         const double* b = nullptr;
         int64_t fmt_gen = -1;
-    } graphs[3];  // [0] plain cycle, [1] cycle that also appends ||b - A x_in||, [2] the
-                  // residual norm alone (solve's last norm)
-    enum { G_CYCLE = 0, G_CYCLE_NORM = 1, G_NORM = 2 };
+    } graphs[5];  // [0] plain cycle, [1] cycle that also appends ||b - A x_in||, [2] the
+                  // residual norm alone (solve's last norm), [3] / [4] the two halves of a
+                  // PCG iteration (Solver::pcg)
+    enum { G_CYCLE = 0, G_CYCLE_NORM = 1, G_NORM = 2, G_PCG_STEP = 3, G_PCG_PREC = 4 };
     // the graph in `slot` captured for (x, b) -- recaptured by `body` when stale.  Multi-rank
     // with `agree`: the ranks decide together (host allgather of the stale flags, then of the
     // capture / instantiate status), so no rank captures while a peer replays.  false: the
@@ -505,6 +506,7 @@ struct Solver {
     void agree_stale(std::initializer_list<int> slots, const double* x, const double* b);
     void graph_launch(int slot);
     void destroy_graphs();
+    void drop_graph(Graph& G);  // destroy one exec once the stream has drained
 
     DevMatrix& Amat(size_t l) { return l == 0 ? *A0 : *levels[l].A; }
     void setup(DevMatrix& A, const amg_options& o);

@@ -35,9 +35,18 @@ struct Error : std::runtime_error {
 // wins): libomp's default keeps them spinning for 200 ms, and on a CPU-quota'd host two
 // spinning teams -- the setup thread's and the format worker's -- exhausted the quota and
 // stalled the launching thread for 5-10 ms inside timed V-cycles (profiles/r3i_cycle_gaps.txt).
-// Per thread, so the host process's own OpenMP settings and environment are left alone.
-// Called at every C-ABI entry and by the format worker thread.
+// omp_quiet_thread() sets it for good on the library's own threads (the format worker);
+// OmpQuiet, held by every C-ABI entry, sets it on the caller's thread for the call and
+// restores the caller's value on return, so OpenMP teams the host application forks from
+// that thread keep their own blocktime.
 void omp_quiet_thread();
+struct OmpQuiet {
+    int saved = -1;
+    OmpQuiet();
+    ~OmpQuiet();
+    OmpQuiet(const OmpQuiet&) = delete;
+    OmpQuiet& operator=(const OmpQuiet&) = delete;
+};
 #define AMG_CHECK(cond, msg)                                                              \
     do {                                                                                  \
         if (!(cond)) throw ::amg::Error(AMG_ERR_INVALID, std::string(msg));               \

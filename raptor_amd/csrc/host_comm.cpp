@@ -17,16 +17,33 @@
 // LLVM libomp extension (the library links libomp); weak, so a host-only build against
 // another OpenMP runtime (the sanitizer build with libgomp) just skips it
 extern "C" void kmp_set_blocktime(int) __attribute__((weak));
+extern "C" int kmp_get_blocktime(void) __attribute__((weak));
 
 namespace amg {
 
+static bool omp_quiet_wanted() {
+    static const bool on = [] {
+        const char* e = std::getenv("KMP_BLOCKTIME");
+        return !(e && *e) && kmp_set_blocktime && kmp_get_blocktime;
+    }();
+    return on;
+}
+
 void omp_quiet_thread() {
     thread_local bool done = false;
-    if (done) return;
+    if (done || !omp_quiet_wanted()) return;
     done = true;
-    const char* e = std::getenv("KMP_BLOCKTIME");
-    if ((e && *e) || !kmp_set_blocktime) return;
     kmp_set_blocktime(0);
+}
+
+OmpQuiet::OmpQuiet() {
+    if (!omp_quiet_wanted()) return;
+    saved = kmp_get_blocktime();
+    if (saved != 0) kmp_set_blocktime(0);
+}
+
+OmpQuiet::~OmpQuiet() {
+    if (saved > 0) kmp_set_blocktime(saved);
 }
 
 

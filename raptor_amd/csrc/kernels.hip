@@ -2057,7 +2057,7 @@ __global__ __launch_bounds__(64) void tpl_gs_chain_kernel(TplGsChainArgs a) {
     // 64-byte lane stride and a 16-way conflict on every read of the walk
     constexpr int kSt = 65;
     __shared__ __attribute__((aligned(16))) double sacc[kSt * U], sx[kSt * U];
-    __shared__ unsigned sid[64 * (U / 4)];
+    __shared__ __attribute__((aligned(16))) unsigned sid[64 * (U / 4)];
     const int lane = threadIdx.x;
     constexpr int kBit = BACK ? 2 : 1;
     for (int k = lane; k < a.ntpl; k += 64) {

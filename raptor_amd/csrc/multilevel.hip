@@ -393,12 +393,19 @@ bool Solver::can_fuse_norm() const {
            opt.pre_sweeps >= 1 && levels.size() >= 2;
 }
 
+// An exec is destroyed only once the stream has drained: a replay enqueued without a host
+// wait (graph_launch) may still be running, and HIP does not document a deferred free of an
+// executing graph the way CUDA does.  Recaptures are rare, so one wait is cheap.
+void Solver::drop_graph(Graph& G) {
+    if (!G.exec) return;
+    if (!ctx->capturing) HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->graph_inflight = false;
+    HIP_CHECK(hipGraphExecDestroy(G.exec));
+    G.exec = nullptr;
+}
+
 void Solver::destroy_graphs() {
-    for (auto& g : graphs)
-        if (g.exec) {
-            HIP_CHECK(hipGraphExecDestroy(g.exec));
-            g.exec = nullptr;
-        }
+    for (auto& g : graphs) drop_graph(g);
 }
 
 // Capture `body` (enqueues on ctx->stream, RCCL groups included) into graphs[slot] unless the
@@ -421,8 +428,7 @@ bool Solver::graph_ready(int slot, const double* x, const double* b, const std::
         stale = any;
     }
     if (!stale) return true;
-    if (G.exec) HIP_CHECK(hipGraphExecDestroy(G.exec));
-    G.exec = nullptr;
+    drop_graph(G);
     hipStream_t s = ctx->stream;
     static const bool trace = std::getenv("AMG_TRACE_RCCL") != nullptr;
     if (trace) std::fprintf(stderr, "[amg] rank %d capture begin (slot %d)\n", comm.rank, slot);
@@ -433,10 +439,14 @@ bool Solver::graph_ready(int slot, const double* x, const double* b, const std::
     if (multi) ctx->eager_rccl_fence();
     hipGraph_t g = nullptr;
     std::string err;
+    int err_code = AMG_ERR_INTERNAL;  // the amg::Error code of a failing body, rethrown below
     HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     ctx->capturing = true;
     try {
         body();
+    } catch (const Error& e) {
+        err = e.what();
+        err_code = e.code;
     } catch (const std::exception& e) {
         err = e.what();
     }
@@ -459,8 +469,10 @@ bool Solver::graph_ready(int slot, const double* x, const double* b, const std::
     if (worst == -1) {
         destroy_graphs();
         use_graph = false;
-        throw Error(AMG_ERR_INTERNAL, "V-cycle capture failed" + (err.empty() ? std::string(" on another rank")
-                                                                          : ": " + err));
+        // the failing rank keeps its own error code (NOMEM, INVALID, ...); its peers report
+        // the generic failure
+        throw Error(err.empty() ? AMG_ERR_INTERNAL : err_code,
+                    "V-cycle capture failed" + (err.empty() ? std::string(" on another rank") : ": " + err));
     }
     if (worst == 0) {
         // a graph some rank's runtime cannot instantiate: every rank runs eagerly from now on
@@ -493,11 +505,7 @@ void Solver::agree_stale(std::initializer_list<int> slots, const double* x, cons
     for (int64_t v : comm.allgather((int64_t)(stale ? 1 : 0))) any = any || v != 0;
     if (!any) return;
     if (ctx->graph_inflight) ctx->eager_rccl_fence();  // replays of the graphs dropped below
-    for (int slot : slots) {
-        Graph& G = graphs[slot];
-        if (G.exec) HIP_CHECK(hipGraphExecDestroy(G.exec));
-        G.exec = nullptr;
-    }
+    for (int slot : slots) drop_graph(graphs[slot]);
 }
 
 void Solver::graph_launch(int slot) {
@@ -607,32 +615,52 @@ void Solver::dot(const double* a, const double* b, double* dst, bool take_sqrt) 
     }
 }
 
+// With graphs on, an iteration is two captured graphs: G_PCG_STEP (q = A p, p.q, the x / r
+// update, ||r|| appended) and G_PCG_PREC (z = M^-1 r by one V-cycle from z = 0, r.z, the p
+// update).  Multi-rank, their RCCL halo groups and dot allgathers replay inside the graphs, so
+// nothing eager follows a replay inside the loop and Context::eager_rccl_fence never waits
+// there (the eager dot allgathers synchronised the host once per
+// iteration).  The set-up (r = b - A x, ||r||, the first z, r.z) runs eagerly, before any
+// replay.  tol > 0 waits for the norm each iteration anyway.
 int32_t Solver::pcg(double* x, const double* b, int32_t max_iter, double tol, double* hist_host) {
     AMG_CHECK(max_iter >= 0, "max_iter must be >= 0");
     RoctxRange range("ParMultilevel::pcg");
     DevMatrix& A = *A0;
     const int64_t n = A.n_rows;
     hipStream_t s = ctx->stream;
-    if (pcg_vec.n < (size_t)(4 * n + 4)) pcg_vec.alloc((size_t)(4 * n + 4));
     const int g = dot_partial_count(n);
     const size_t need = (size_t)g + g / 4096 + 64 + ctx->host.nranks + 2 + SC_N;
-    if (pcg_scratch.n < need) pcg_scratch.alloc(need);
+    if (pcg_vec.n < (size_t)(4 * n + 4) || pcg_scratch.n < need) {
+        // the captured iteration graphs hold these addresses
+        drop_graph(graphs[G_PCG_STEP]);
+        drop_graph(graphs[G_PCG_PREC]);
+        if (pcg_vec.n < (size_t)(4 * n + 4)) pcg_vec.alloc((size_t)(4 * n + 4));
+        if (pcg_scratch.n < need) pcg_scratch.alloc(need);
+    }
     double* r = pcg_vec.p;
     double* z = r + n;
     double* p = z + n;
     double* q = p + n;
     double* sc = pcg_scratch.p + (need - SC_N);
     ensure_hist(max_iter + 1);
+    if (ctx->host.nranks > 1) ctx->eager_rccl_fence();  // replays of earlier calls
     HIP_CHECK(hipMemsetAsync(hist_counter.p, 0, sizeof(int), s));
     auto record_norm = [&] {
         dot(r, r, sc + SC_RN, true);
         launch_append(s, sc + SC_RN, hist.p, hist_counter.p);
     };
-    bool first = true;
-    auto precondition = [&] {  // z = M^-1 r: one V-cycle from z = 0
+    auto step = [&] {  // q = A p; alpha = rz / pq; x += alpha p; r -= alpha q; ||r||
+        par_apply(A, KM_SPMV, p, nullptr, q, 0.0, nullptr);
+        dot(p, q, sc + SC_PQ, false);
+        launch_pcg_xr(s, n, sc + SC_RZ, sc + SC_PQ, p, q, x, r);
+        record_norm();
+    };
+    auto prec = [&] {  // z = M^-1 r (one V-cycle from z = 0); beta = rz_new / rz; p = z + beta p
         launch_zero(s, n, z);
-        cycle(z, r, false, first);  // z, r stay put: one collective graph decision per pcg
-        first = false;
+        cycle_rec(0, z, r, false, false);
+        dot(r, z, sc + SC_RZN, false);
+        launch_pcg_p(s, n, sc + SC_RZN, sc + SC_RZ, z, p);
+        HIP_CHECK(hipMemcpyAsync(sc + SC_RZ, sc + SC_RZN, sizeof(double), hipMemcpyDeviceToDevice, s));
     };
     par_apply(A, KM_RESID, x, b, r, 0.0, nullptr);
     record_norm();
@@ -641,27 +669,29 @@ int32_t Solver::pcg(double* x, const double* b, int32_t max_iter, double tol, do
         HIP_CHECK(hipMemcpyAsync(&r0, hist.p, sizeof(double), hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipStreamSynchronize(s));
     }
-    precondition();
+    launch_zero(s, n, z);
+    cycle_rec(0, z, r, false, false);
     if (n) HIP_CHECK(hipMemcpyAsync(p, z, n * sizeof(double), hipMemcpyDeviceToDevice, s));
     dot(r, z, sc + SC_RZ, false);
+    // one collective graph decision for both iteration graphs (keyed by the caller's x, b)
+    agree_stale({G_PCG_STEP, G_PCG_PREC}, x, b);
+    auto run = [&](int slot, const std::function<void()>& body) {
+        if (use_graph && graph_ready(slot, x, b, body, false)) graph_launch(slot);
+        else body();
+    };
     int32_t it = 0;
     while (it < max_iter) {
-        par_apply(A, KM_SPMV, p, nullptr, q, 0.0, nullptr);
-        dot(p, q, sc + SC_PQ, false);
-        launch_pcg_xr(s, n, sc + SC_RZ, sc + SC_PQ, p, q, x, r);
-        record_norm();
+        run(G_PCG_STEP, step);
         ++it;
         if (tol > 0.0) {
             double rn = 0.0;
             HIP_CHECK(hipMemcpyAsync(&rn, hist.p + it, sizeof(double), hipMemcpyDeviceToHost, s));
             HIP_CHECK(hipStreamSynchronize(s));
+            ctx->graph_inflight = false;
             if (r0 > 0.0 && rn / r0 < tol) break;
         }
         if (it == max_iter) break;
-        precondition();
-        dot(r, z, sc + SC_RZN, false);
-        launch_pcg_p(s, n, sc + SC_RZN, sc + SC_RZ, z, p);
-        HIP_CHECK(hipMemcpyAsync(sc + SC_RZ, sc + SC_RZN, sizeof(double), hipMemcpyDeviceToDevice, s));
+        run(G_PCG_PREC, prec);
     }
     HIP_CHECK(hipMemcpyAsync(hist_host, hist.p, sizeof(double) * (size_t)(it + 1),
                              hipMemcpyDeviceToHost, s));

@@ -1414,10 +1414,14 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
     // Split sweeps: the old-value couplings as a CSR-block pass (KM_GSACC on A
     // without the sweep's in-chunk new-value couplings -- the same entries in the same order,
     // so acc is bit-identical) and the chain walk on a sliced ELL of the new-value couplings
-    // only.  One rank or a replicated operator (the pass is built as its own matrix), no GS
-    // template rows, and rows of >= AMG_GS_SPLIT_NPR entries on average (default 12: g3sub's
-    // 5.5-entry level 0 ran 60 -> 72 us per sweep split, its 45-entry level 1 121 -> 63 us;
-    // profiles/r3u_split_ab.txt; 0 forces it, tests).
+    // only.  No GS template rows, and rows of >= AMG_GS_SPLIT_NPR entries on average (default
+    // 12: g3sub's 5.5-entry level 0 ran 60 -> 72 us per sweep split, its 45-entry level 1
+    // 121 -> 63 us; profiles/r3u_split_ab.txt; 0 forces it, tests).  On N ranks (r5) the pass
+    // is a distributed matrix of its own: its off-rank columns are A's (chunks never cross a
+    // rank cut, so every in-chunk coupling is local), par_apply exchanges their halo while the
+    // interior blocks run, and the old values across ranks are the Jacobi-across-ranks half of
+    // the oracle's rank-cut definition -- results unchanged.  The pass is built collectively,
+    // so the ranks agree first: all split or none do.
     gs_split = false;
     for (int d = 0; d < 2; ++d) {
         gs_old[d].reset();
@@ -1431,8 +1435,10 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
         const int64_t npr = e ? std::atoll(e) : (int64_t)12;
         const char* off = std::getenv("AMG_GS_SPLIT");
         const bool allow = !(off && std::atoi(off) == 0);
-        if (allow && n_gs_tblk == 0 && n_rows > 0 && nnz >= npr * n_rows &&
-            (ctx->host.nranks == 1 || replicated)) {
+        bool split = allow && n_gs_tblk == 0 && n_rows > 0 && nnz >= npr * n_rows;
+        if (ctx->host.nranks > 1 && !replicated)
+            for (int64_t v : ctx->host.allgather((int64_t)(split ? 1 : 0))) split = split && v != 0;
+        if (split) {
             // in-chunk new-value coupling of row i (local ids): forward cs <= j < i, backward
             // i < j < ce (hybrid_gs_kernel's [lo, hi))
             auto chunk = [&](int64_t i, int64_t& cs, int64_t& ce) {
@@ -1660,7 +1666,7 @@ bool par_restrict_j0(DevMatrix& R, const double* r, double* bc, double* x0c, con
 void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block,
                    bool backward, double* partial) {
     A.ensure_gs_blocks(block);
-    if (A.gs_split && !partial) {  // split sweep: no halo (one rank / replicated)
+    if (A.gs_split && !partial) {  // split sweep: the pass exchanges its halo
         par_apply(*A.gs_old[backward ? 1 : 0], KM_GSACC, x, b, A.gs_acc.p, 0.0, nullptr);
         launch_gs_chain(A.ctx->stream, A, x, A.gs_acc.p, y, backward);
         return;

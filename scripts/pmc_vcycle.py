@@ -64,12 +64,5 @@ ctx.synchronize()
 out = os.environ.get("AMG_PMC_OPS", os.path.join(ROOT, "gpurun_out", "pmc_vcycle_ops.json"))
 json.dump({"grid": [N, N, N], "launches_per_op": 3, "ops": ops}, open(out, "w"), indent=1)
 print(json.dumps(ops))
-# release the library's objects now, in order, while the profiler's tool is still loaded: at
-# interpreter exit the tool is finalized first and a late hipFree in a destructor faults
-del table, Al, P, R, ml, A
-import gc  # noqa: E402
-
-gc.collect()
-ctx.synchronize()
-del ctx
-gc.collect()
+# no explicit teardown: raptor_amd's atexit hook releases the library's objects in order
+# while the runtime and the profiler's tool are still up

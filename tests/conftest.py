@@ -23,6 +23,16 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def ctx():
+    from tests.util import native_mode
+
+    if native_mode():
+        # torch-free (tests/util.py): the ROCm runtime the library was built against
+        import raptor_amd as ra
+
+        try:
+            return ra.Context.native(0)
+        except ra.AmgError as e:
+            pytest.skip(f"no GPU ({e})")
     import torch
 
     if not torch.cuda.is_available():

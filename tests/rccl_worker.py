@@ -121,6 +121,14 @@ def main():
     dx = ctx.zeros(m)
     _, hp = ml.pcg(dx, bb, max_iter=5)
     res["pcg"] = hp
+    if spec.get("trace_pcg"):
+        # a second PCG on the same buffers: its iteration graphs are fresh, so under
+        # AMG_TRACE_RCCL nothing between the markers may capture or wait in the eager fence
+        zero(dx)
+        os.write(2, b"@@pcg2-begin\n")
+        _, hp2 = ml.pcg(dx, bb, max_iter=5)
+        os.write(2, b"@@pcg2-end\n")
+        res["pcg2"] = hp2
     res["graph_used"] = ml.graph_enabled
     np.savez(f"{out}.{rank}.npz", **res)
     del ml, A

@@ -5,6 +5,8 @@ square A_l on the x-tile path, rectangular P_l / R_l on the tile or gather paths
 without value indexing, at one rank and with halo columns (loopback ranks)."""
 import pytest
 
+from tests.util import make_ctx
+
 pytestmark = pytest.mark.gpu
 
 
@@ -33,7 +35,7 @@ def test_device_formats_equal_host_builders(kind, dims, coarsen, smoother, monke
     if kind.endswith("-lines32"):  # 32-byte x-tile lines forced on every tiled operator
         monkeypatch.setenv("AMG_TILE_LINE", "4")
         kind = kind.split("-")[0]
-    ctx = ra.Context(0)
+    ctx = make_ctx(0)
     dev = _digests(ra, ctx, kind, dims, coarsen, smoother, monkeypatch, True)
     host = _digests(ra, ctx, kind, dims, coarsen, smoother, monkeypatch, False)
     assert len(dev) >= 4

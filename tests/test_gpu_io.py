@@ -7,7 +7,7 @@ import pytest
 import scipy.io
 
 from tests.test_gpu_multirank import level_starts, run_ranks, set_oracle_cuts
-from tests.util import same_csr, to_dev, to_host
+from tests.util import loopback_ctx, same_csr, to_dev, to_host
 
 pytestmark = pytest.mark.gpu
 
@@ -88,7 +88,7 @@ def test_multirank_graph_laplacian(oracle, nranks):
     b = O.vec_uniform(n, 8)
 
     def rank(r, nr, world):
-        ctx = ra.Context.loopback(r, nr, world)
+        ctx = loopback_ctx(r, nr, world)
         A = ra.par_graph_laplacian(ctx, 70, 66, seed=5)
         B, perm = A.reorder("rcm")
         ml = ra.ParSmoothedAggregationSolver(replicate_below=400).setup(B)

@@ -8,7 +8,7 @@ import uuid
 import numpy as np
 import pytest
 
-from tests.util import to_dev, to_host
+from tests.util import loopback_ctx, to_dev, to_host
 
 pytestmark = pytest.mark.gpu
 
@@ -73,7 +73,7 @@ def test_slab_kernels_bit_exact(oracle, monkeypatch, nranks, tpl):
     rn_ref = O.norm2(Ao.residual(x, b))
 
     def rank(r, nr, world):
-        ctx = ra.Context.loopback(r, nr, world)
+        ctx = loopback_ctx(r, nr, world)
         A = ra.par_stencil_grid(ctx, "7pt", dims)
         if tpl == "plain":
             A.set_format("csr")
@@ -130,6 +130,19 @@ def test_multirank_boxes_vcycle_bit_exact(oracle, nranks, kind, dims, boxes, coa
     _vcycle_vs_oracle(oracle, nranks, kind, dims, coarsen, smoother, 0, boxes)
 
 
+@pytest.mark.parametrize("nranks,kind,dims", [(2, "27pt", (10, 11, 16)), (4, "27pt", (12, 12, 16)),
+                                              (8, "7pt", (48, 48, 96))])
+def test_multirank_split_gs_bit_exact(oracle, nranks, kind, dims):
+    """Split hybrid-GS sweeps on N ranks: every
+    distributed Galerkin level of the SA hierarchy runs the CSR-block old-value pass (its halo
+    exchanged under the interior blocks) + the chain walk, and the V-cycle iterates stay
+    bit-identical to the oracle's rank-cut hybrid GS."""
+    split = _vcycle_vs_oracle(oracle, nranks, kind, dims, "sa", "hybrid_gs", 0)
+    for per_rank in split:
+        assert len(per_rank) >= 2
+        assert all(per_rank[1:]), per_rank  # every Galerkin level split, on every rank
+
+
 def _vcycle_vs_oracle(oracle, nranks, kind, dims, coarsen, smoother, rep, boxes=None):
     import raptor_amd as ra
 
@@ -144,7 +157,7 @@ def _vcycle_vs_oracle(oracle, nranks, kind, dims, coarsen, smoother, rep, boxes=
     levels = [Ho.matrix(l, "A") for l in range(Ho.num_levels)]
 
     def rank(r, nr, world):
-        ctx = ra.Context.loopback(r, nr, world)
+        ctx = loopback_ctx(r, nr, world)
         A = ra.par_stencil_grid(ctx, kind, dims, boxes=boxes)
         ml = ra.ParMultilevel(coarsen=coarsen, smoother=smoother, replicate_below=rep).setup(A)
         f, m = A.first_row, A.local_rows
@@ -169,20 +182,24 @@ def _vcycle_vs_oracle(oracle, nranks, kind, dims, coarsen, smoother, rep, boxes=
             xs.append(to_host(ctx, dx))
         dx = ctx.zeros(m)
         _, hist = ml.solve(dx, db, max_iter=6)
-        return bad, hist, f, m, xs, level_starts(ml)
+        # distributed levels only (a replicated level is whole on every rank)
+        split = [bool(ml.level_matrix(l, "A").info["gs_split"]) for l in range(ml.num_levels - 1)
+                 if ml.level_matrix(l, "A").local_rows < ml.level_info(l)["n_global"]]
+        return bad, hist, f, m, xs, split, level_starts(ml)
 
     res = run_ranks(nranks, rank)
     set_oracle_cuts(Ho, res)
     xo = np.zeros(n)
     for k in range(3):
         xo = Ho.cycle(xo, b)
-        for _, _, f, m, xs, _ in res:
+        for _, _, f, m, xs, _, _ in res:
             assert np.array_equal(xs[k], xo[f:f + m]), ("cycle", k)
     _, hist_o = Ho.solve(np.zeros(n), b, max_iter=6)
     for bad, hist, *_ in res:
         assert bad == []
         assert np.all(np.abs(hist - hist_o) <= 1e-10 * hist_o)
     assert all(np.array_equal(res[0][1], r[1]) for r in res)  # every rank reports the same
+    return [r[5] for r in res]
 
 
 def test_uneven_partition_from_csr(oracle):
@@ -199,7 +216,7 @@ def test_uneven_partition_from_csr(oracle):
     xo = O.Hierarchy(Ao, **O.DEFAULTS["pmis"]).cycle(np.zeros(n), y_ref)
 
     def rank(r, nr, world):
-        ctx = ra.Context.loopback(r, nr, world)
+        ctx = loopback_ctx(r, nr, world)
         lo, hi = cuts[r], cuts[r + 1]
         A = ra.ParCSRMatrix.from_scipy_local(ctx, M[lo:hi], n, lo)
         out = ctx.empty(hi - lo)
@@ -227,7 +244,7 @@ def test_multirank_pcg(oracle):
     _, hist_o = Ho.pcg(np.zeros(n), b, max_iter=10)
 
     def rank(r, nr, world):
-        ctx = ra.Context.loopback(r, nr, world)
+        ctx = loopback_ctx(r, nr, world)
         A = ra.par_stencil_grid(ctx, "7pt", dims)
         ml = ra.ParRugeStubenSolver(coarsen="pmis", replicate_below=500).setup(A)
         f, m = A.first_row, A.local_rows
@@ -258,7 +275,7 @@ def test_one_row_per_rank(oracle, values):
     ref = {"y": Ao.spmv(x), "r": Ao.residual(x, b), "j": Ao.jacobi(x, b, 2.0 / 3.0)}
 
     def rank(r, nr, world):
-        ctx = ra.Context.loopback(r, nr, world)
+        ctx = loopback_ctx(r, nr, world)
         A = ra.ParCSRMatrix.from_scipy_local(ctx, M[r:r + 1], n, r)
         dx, db, out = to_dev(ctx, x[r:r + 1]), to_dev(ctx, b[r:r + 1]), ctx.empty(1)
         A.mult(dx, out)
@@ -291,7 +308,7 @@ def test_multirank_gs_templates(oracle, monkeypatch, nranks):
     x, b = O.vec_uniform(n, 3), O.vec_uniform(n, 4)
 
     def rank(r, nr, world):
-        ctx = ra.Context.loopback(r, nr, world)
+        ctx = loopback_ctx(r, nr, world)
         A = ra.par_stencil_grid(ctx, "27pt", dims)
         f, m = A.first_row, A.local_rows
         dx, db, out = to_dev(ctx, x[f:f + m]), to_dev(ctx, b[f:f + m]), ctx.empty(m)
@@ -320,7 +337,7 @@ def test_device_setup_equals_host_multirank(nranks, kind, dims, coarsen):
     import raptor_amd as ra
 
     def rank(r, nr, world):
-        ctx = ra.Context.loopback(r, nr, world)
+        ctx = loopback_ctx(r, nr, world)
         A = ra.par_stencil_grid(ctx, kind, dims)
         out = []
         for m in (1, 0):

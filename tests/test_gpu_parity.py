@@ -376,6 +376,46 @@ def test_vcycle_bit_exact(ctx, oracle, kind, dims, coarsen, smoother):
     assert hist[-1] < hist[0]
 
 
+def test_configs0_5pt_256_rs_jacobi(ctx, oracle):
+    """BASELINE.json:7 (configs[0]) at its stated size: 2D 5-pt Poisson 256 x 256 (65,536 rows),
+    Ruge-Stueben coarsening + Jacobi.  The product's hierarchy equals the oracle's own serial
+    setup (O.Hierarchy(gen_5pt(256, 256), COARSEN_RS)) on every level -- A, P, R bit for bit and
+    the C/F split -- and the GPU V-cycle iterates are bit-identical; an 8-cycle solve history
+    within 1e-10 relative (BASELINE.json:5)."""
+    import raptor_amd as ra
+
+    O = oracle
+    Ao = O.gen_5pt(256, 256)
+    A = ra.par_stencil_grid(ctx, "5pt", (256, 256))
+    assert A.local_rows == 65536
+    assert same_csr(A.to_scipy_local(), Ao.to_scipy())
+    ml = ra.ParRugeStubenSolver(coarsen="rs").setup(A)
+    Ho = O.Hierarchy(Ao, **O.DEFAULTS["rs"])
+    assert ml.num_levels == Ho.num_levels >= 3
+    for l in range(ml.num_levels):
+        assert same_csr(ml.level_matrix(l, "A").to_scipy_local(), Ho.matrix(l, "A")), ("A", l)
+        if l + 1 < ml.num_levels:
+            assert same_csr(ml.level_matrix(l, "P").to_scipy_local(), Ho.matrix(l, "P")), ("P", l)
+            assert same_csr(ml.level_matrix(l, "R").to_scipy_local(), Ho.matrix(l, "R")), ("R", l)
+            assert np.array_equal(ml.level_split(l), Ho.split(l)), ("C/F", l)
+    n = Ao.shape[0]
+    b = Ao.spmv(O.vec_uniform(n, 42))
+    db = to_dev(ctx, b)
+    dx = ctx.zeros(n)
+    xo = np.zeros(n)
+    for _ in range(3):
+        ml.cycle(dx, db)
+        xo = Ho.cycle(xo, b)
+        assert np.array_equal(to_host(ctx, dx), xo)
+    dx = ctx.zeros(n)
+    _, hist = ml.solve(dx, db, max_iter=8)
+    xso, hist_o = Ho.solve(np.zeros(n), b, max_iter=8)
+    assert np.array_equal(to_host(ctx, dx), xso)
+    assert hist.shape == hist_o.shape == (9,)
+    assert np.all(np.abs(hist - hist_o) <= 1e-10 * hist_o)
+    assert hist[-1] < 1e-3 * hist[0]  # RS + Jacobi on the 2D Poisson problem converges
+
+
 def test_graph_and_eager_agree(ctx, oracle):
     """hipGraph replay and eager launches: both solves bit-identical to the oracle's iterates
     (and to each other, history included)."""

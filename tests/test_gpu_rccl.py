@@ -30,7 +30,7 @@ def _free_port():
     return p
 
 
-def run_rccl(nranks, spec, tmp_path, timeout=160):
+def run_rccl(nranks, spec, tmp_path, timeout=160, extra_env=None, logs_out=None):
     # (below the GPU runner's 180 s silence limit: a hung rank fails the test with its log)
     port = _free_port()
     out = str(tmp_path / "rank")
@@ -42,6 +42,7 @@ def run_rccl(nranks, spec, tmp_path, timeout=160):
                    NCCL_HOSTID=f"raptor-amd-rank-{r}", NCCL_SOCKET_IFNAME="lo",
                    GLOO_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
                    HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+        env.update(extra_env or {})
         procs.append(subprocess.Popen(
             [sys.executable, os.path.join(ROOT, "tests", "rccl_worker.py"), json.dumps(spec), out],
             env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
@@ -57,6 +58,8 @@ def run_rccl(nranks, spec, tmp_path, timeout=160):
                 p.wait()
     for r, p in enumerate(procs):
         assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{logs[r][-4000:]}"
+    if logs_out is not None:
+        logs_out.extend(logs)
     return [dict(np.load(f"{out}.{r}.npz")) for r in range(nranks)]
 
 
@@ -176,3 +179,28 @@ def test_rccl_graph_policy_follows_runtime(oracle, tmp_path, graph):
                 xo = Ho.cycle(xo, bo)
                 f, m = int(r["f"]), int(r["m"])
                 assert np.array_equal(r[f"x{k}"], xo[f:f + m]), ("cycle", k)
+
+
+def test_rccl_pcg_iterations_replay_without_fence(oracle, tmp_path):
+    """Multi-rank AMG-PCG with both halves of an iteration captured (VERDICT r4
+    item 6b): a second pcg on the same buffers replays the iteration graphs with no capture
+    and no eager-fence wait (AMG_TRACE_RCCL trace between the worker's markers), and repeats
+    the first pcg's history bit for bit; both match the oracle's PCG (1e-9, dot order)."""
+    spec = dict(kind="7pt", dims=[16, 15, 18], coarsen="pmis", smoother="jacobi", rep=0,
+                trace_pcg=True, **MODES["native-graph"])
+    logs = []
+    res = run_rccl(2, spec, tmp_path, extra_env={"AMG_TRACE_RCCL": "1"}, logs_out=logs)
+    O = oracle
+    Ao = O.gen_7pt(*spec["dims"])
+    Ho = O.Hierarchy(Ao, **O.DEFAULTS["pmis"])
+    for l in range(Ho.num_levels):
+        Ho.set_cuts(l, sorted({int(r["starts"][l]) for r in res}))
+    n = Ao.shape[0]
+    _, pcg_o = Ho.pcg(np.zeros(n), Ao.spmv(O.vec_uniform(n, 42)), max_iter=5)
+    for r, log in zip(res, logs):
+        assert bool(r["graph_used"])
+        assert np.array_equal(r["pcg2"], r["pcg"])
+        assert np.all(np.abs(r["pcg"] - pcg_o) <= 1e-9 * pcg_o[0])
+        seg = log.split("@@pcg2-begin", 1)[1].split("@@pcg2-end", 1)[0]
+        assert "eager fence" not in seg and "capture begin" not in seg, seg[-3000:]
+        assert "graph launched (slot 3)" in seg and "graph launched (slot 4)" in seg, seg[-3000:]
