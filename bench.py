@@ -159,6 +159,17 @@ def main():
     log(rank, f"setup {setup_s:.1f}s, levels {nlev}: " +
         " ".join(f"{i['n_global']}/{i['nnz_global']}" for i in infos))
 
+    # hybrid-GS sweep form per level on every rank (1 = split: CSR-block old-value pass + chain
+    # walk; multi-rank since r5)
+    gs_split = None
+    if sa27 or g3:
+        mine = [int(ml.level_matrix(l, "A").info["gs_split"]) for l in range(nlev - 1)]
+        if world > 1:
+            flat = comm.allgather_bytes(bytes(mine))
+            gs_split = [list(v) for v in flat]
+        else:
+            gs_split = [mine]
+
     n = A.local_rows
     xs = ra.vector_uniform(ctx, n, A.first_row, 42)
     b = ctx.empty(n)
@@ -446,6 +457,7 @@ def main():
                 "reorder_s": None if reorder_s is None else round(reorder_s, 2),
                 "hipgraph": graph_used,
                 "hipgraph_all_ranks": graph_all,
+                "gs_split_per_rank_level": gs_split,
             },
             "iters_per_s": round(iters_per_s, 3),
             "convergence_factor": conv,

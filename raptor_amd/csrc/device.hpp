@@ -54,9 +54,7 @@ constexpr int kTplNone = 255;
 constexpr int kTplMax = 255;       // templates per operator
 constexpr int kTplEntries = 1024;  // entries over all templates (staged in LDS per workgroup)
 constexpr int kTplMaxLen = 64;     // entries per template
-#ifndef AMG_CSR_PERSIST_WAVES  // build-time knob: waves/SIMD bound of the persistent x-tile kernel
-#define AMG_CSR_PERSIST_WAVES 6
-#endif
+
 #ifndef AMG_CSR_PRE_TILE  // build-time knob: x-tile blocks issue batch 1 with the header
 #define AMG_CSR_PRE_TILE 1
 #endif
@@ -263,7 +261,6 @@ struct DevMatrix {
     DevBuf<int> gs_tkem, gs_tkep;  // per GS template: index in the row of its -1 / +1 entry (-1)
     DevBuf<double> gs_racc;      // per row: b - old-value couplings (acc kernel -> chain kernel)
     int n_gs_tpl = 0, n_gs_tblk = 0;
-    bool gs_ring = false;  // the template rows' sweep runs fused on the plane ring (4.2d)
     int gs_norm_parts() const { return n_gs_slabs + kNormParts * n_gs_tblk; }
     int64_t gs_bytes = 0;  // sliced-ELL bytes streamed per sweep
     bool gs_wide = false;  // average slab width >= kGsWide: the LDS-chain kernel variant
@@ -320,11 +317,6 @@ struct DevMatrix {
     std::vector<double> tpl_mval;
     double tpl_mpd = 0.0;
     DevBuf<unsigned> tpl_mmask, gs_tmask;
-    // plane ring (variant bit 1024): master offsets o_e = dz_e D + q_e with
-    // dz_e in {-1, 0, 1} and D = tpl_ring_s * kTplRows (0: no such split); a block's slab of
-    // plane p holds x[r0 + p D + tpl_ring_qlo + i], i < tpl_ring_wp; tpl_ring_mq[e] = q_e - qlo
-    int tpl_ring_s = 0, tpl_ring_qlo = 0, tpl_ring_wp = 0;
-    std::vector<int> tpl_ring_dz, tpl_ring_mq;
     int64_t csr_fmt_bytes = 0;  // spmv_fmt_bytes with templates off (AMG_KERNEL_VARIANT)
     // storage format the level kernels use (AMG_FORMAT_*, amg_par_csr_set_format):
     // AUTO = templates + CSR blocks (default), BLOCKS = CSR blocks only, CSR = plain CSR

@@ -79,7 +79,7 @@ struct CsrArgs {
                        // level's first Jacobi sweep from x = 0, fused into the restriction)
     const uint16_t* col16;  // gather operators: 16-bit column codes (C16 kernels), with
     const int4* gband;      // the block's 4 band bases: col = base[code >> 14] + (code & 0x3fff)
-    int nblk;               // blocks of this launch (paired x-tile kernel: 2 per workgroup)
+    int nblk;               // blocks of this launch
 };
 
 // the fused second output of a restriction (CsrArgs::y2): jacobi_zero_kernel's expression;
@@ -182,8 +182,8 @@ __device__ __forceinline__ v2d_t load_pair(const double* base, int q, int n) {
 // are consecutive in it (header diag slot).  VIB: the block's nonzeros take <= 256 distinct
 // values; a 1-byte index per nonzero selects from the table staged in LDS.  NU: lane slots
 // in use (8 = full; the gather path of sparse rectangular blocks uses fewer).
-// Batch 1 of an x-tile block (depends on the block id only): what the persistent kernel
-// prefetches for its next block while the current one runs.
+// Batch 1 of an x-tile block (depends on the block id only): issued with the header, before
+// the loads that depend on it.
 // the x-tile line ids lane `lane` of wave `wv` loads (tile_line_ids) and where lane `lane`
 // finds the line of its 16-byte slot pair j (tile_line_src): 64-byte lines, 4 lanes per line,
 // line 16 wv + (lane >> 2) + 64 j; 32-byte lines, 2 lanes per line, line 32 wv + (lane >> 1) +
@@ -215,14 +215,14 @@ __device__ __forceinline__ void csr_pre_tile(const CsrArgs& a, int bid, CsrPre& 
     if (VI) p.vq = __builtin_nontemporal_load((const v2u_t*)(a.vidx + (size_t)bid * kCAP + (size_t)tid * (kCAP / kTPB)));
 }
 
-// PRE: 0 = load batch 1 here; 1 / 2 = batch 1 comes in *pre, which is then refilled with
-// block nxt's batch 1 (2: with VI indices) unless nxt < 0
+// PRE: 0 = load batch 1 here; 1 / 2 = batch 1 was issued with the header into *pre (2: with
+// VI indices)
 // RPB: rows per lane (gather blocks of rectangular operators hold up to kTPB * kGatherRPB
 // rows; a short-row P block of 256 rows filled a quarter of its 2048-entry stage)
 template <int MODE, bool NORM, bool TILE, bool VIB, int NU, int PRE = 0, int RPB = 1, bool C16 = false,
           int LW = 8>
 __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* stage, double* tabl,
-                                             int* rends, CsrPre* pre = nullptr, int nxt = -1) {
+                                             int* rends, CsrPre* pre = nullptr) {
     constexpr int U = kCAP / kTPB;  // 8 lane slots
     static_assert(NU >= 2 && NU % 2 == 0 && NU <= U && (TILE ? NU == U : true), "slot pairs");
     static_assert(RPB == 1 || (!NORM && (MODE == KM_SPMV || MODE == KM_SPMV_ADD)),
@@ -241,7 +241,6 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
         vq = pre->vq;
         h0 = pre->h0;
         h1 = pre->h1;
-        if (nxt >= 0) csr_pre_tile<PRE == 2, LW>(a, nxt, *pre);  // in flight during this block
     } else {
     if (TILE) {
         // the lines wave w's 16-byte tile slots need (tile_id_index)
@@ -494,44 +493,13 @@ __device__ __forceinline__ void block_partial(const CsrArgs& a, int bid, double 
 // whose blocks hold up to kTPB * kGatherRPB rows; DevMatrix::gather_rpb)
 // C16: gather path with 16-bit column codes (DevMatrix::col16)
 // LW: doubles per x-tile line (8: 256 lines of 64 B, 4: 512 lines of 32 B; DevMatrix::line_w)
-// PAIR (x-tile path, variant bit 2048): each workgroup runs two consecutive blocks, issuing
-// the second block's batch 1 (header, line ids, tile / VI indices) with the first's, so the
-// second block waits on one dependent round of loads instead of two
-template <int MODE, bool NORM, bool XCD, bool TILE, bool VI, int GRPB = 1, bool C16 = false, int LW = 8,
-          bool PAIR = false>
-__global__ __launch_bounds__(kTPB, GRPB > 1 || PAIR ? 7 : 8) void csr_block_kernel(CsrArgs a, int first_block) {
+template <int MODE, bool NORM, bool XCD, bool TILE, bool VI, int GRPB = 1, bool C16 = false, int LW = 8>
+__global__ __launch_bounds__(kTPB, GRPB > 1 ? 7 : 8) void csr_block_kernel(CsrArgs a, int first_block) {
     static_assert(kCAP / kTPB == 8 && (LW == 8 || LW == 4) && kTPB == 256,
                   "lane-major layouts assume 8 entries per lane, 4 waves");
-    static_assert(!PAIR || (TILE && AMG_CSR_PRE_TILE), "paired blocks: x-tile path");
     __shared__ __attribute__((aligned(16))) double stage[kCAP];  // x tile, then products
     __shared__ double tabl[VI ? 256 : 1];
     __shared__ int rends[kTPB * GRPB];
-    if constexpr (PAIR) {
-        constexpr int PV = VI ? 2 : 1;
-        const int w = XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-        const int b0 = first_block + 2 * w, b1 = b0 + 1;
-        const bool has1 = 2 * w + 1 < a.nblk;  // workgroup-uniform
-        CsrPre f0, f1;
-        csr_pre_tile<VI, LW>(a, b0, f0);
-        if (has1) csr_pre_tile<VI, LW>(a, b1, f1);  // in flight during block b0
-        auto run = [&](int bid, CsrPre& f) {
-            const int4 h0 = f.h0, h1 = f.h1;
-            double sq;
-            if (h0.w <= kCAP && (h1.y & 0xffff) <= kCAP / LW && h0.w > 0) {
-                if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f, -1);
-                else sq = block_main<MODE, NORM, true, false, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f, -1);
-            } else {
-                sq = block_long<MODE, NORM>(a, h0, stage);
-            }
-            block_partial<NORM>(a, bid, sq);
-        };
-        run(b0, f0);
-        if (has1) {
-            __syncthreads();  // the stage and row ends are rewritten by block b1
-            run(b1, f1);
-        }
-        return;
-    }
     const int bid = first_block + (XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x);
     if constexpr (TILE && AMG_CSR_PRE_TILE) {
         // square operators: batch 1 (tile line ids, tile / VI indices: fixed offsets from the
@@ -543,8 +511,8 @@ __global__ __launch_bounds__(kTPB, GRPB > 1 || PAIR ? 7 : 8) void csr_block_kern
         const int4 h0 = f.h0, h1 = f.h1;
         double sq;
         if (h0.w <= kCAP && (h1.y & 0xffff) <= kCAP / LW && h0.w > 0) {
-            if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f, -1);
-            else sq = block_main<MODE, NORM, true, false, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f, -1);
+            if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f);
+            else sq = block_main<MODE, NORM, true, false, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f);
         } else {
             sq = block_long<MODE, NORM>(a, h0, stage);
         }
@@ -561,43 +529,6 @@ __global__ __launch_bounds__(kTPB, GRPB > 1 || PAIR ? 7 : 8) void csr_block_kern
         sq = block_long<MODE, NORM>(a, h0, stage);
     }
     block_partial<NORM>(a, bid, sq);
-}
-
-// Persistent form of the x-tile path (variant bit 64): a resident grid (a multiple of 8), XCD
-// x = blockIdx % 8 owning a contiguous 1/8 of the blocks, its workgroups sweeping them side by
-// side.  Each workgroup issues the next block's batch 1 (header, tile line ids, tile and VI
-// indices) before the current block's batch 2, so a block waits on one round of loads
-// instead of two.  Same blocks, same per-block code: bit-identical results and partials.
-template <int MODE, bool NORM, bool VI>
-__global__ __launch_bounds__(kTPB, AMG_CSR_PERSIST_WAVES) void csr_persist_kernel(CsrArgs a, int first_block, int nblk) {
-    __shared__ __attribute__((aligned(16))) double stage[kCAP];
-    __shared__ double tabl[VI ? 256 : 1];
-    __shared__ int rends[kTPB];
-    const int x = blockIdx.x & 7, lw = blockIdx.x >> 3, per = gridDim.x >> 3;
-    const int q = nblk >> 3, rem = nblk & 7;
-    const int b0 = x * q + min(x, rem), b1 = b0 + q + (x < rem ? 1 : 0);
-    int blk = b0 + lw;
-    if (blk >= b1) return;  // workgroup-uniform
-    constexpr int PV = VI ? 2 : 1;
-    CsrPre f;
-    csr_pre_tile<VI>(a, first_block + blk, f);
-    for (;;) {
-        const int bid = first_block + blk, nxt = blk + per;
-        const int nb = nxt < b1 ? first_block + nxt : -1;
-        const int4 h0 = f.h0, h1 = f.h1;
-        double sq;
-        if (h0.w <= kCAP && (h1.y & 0xffff) <= kCAP / 8 && h0.w > 0) {  // 64-byte lines (launch_csr_stream)
-            if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV>(a, bid, stage, tabl, rends, &f, nb);
-            else sq = block_main<MODE, NORM, true, false, 8, PV>(a, bid, stage, tabl, rends, &f, nb);
-        } else {
-            if (nb >= 0) csr_pre_tile<VI>(a, nb, f);
-            sq = block_long<MODE, NORM>(a, h0, stage);
-        }
-        block_partial<NORM>(a, bid, sq);
-        if (nxt >= b1) break;
-        __syncthreads();  // stage / tabl / rends are rewritten by the next block
-        blk = nxt;
-    }
 }
 
 // Plain CSR (AMG_FORMAT_CSR): exactly the arrays SURVEY.md 8(d) prices --
@@ -1384,327 +1315,6 @@ __global__ __launch_bounds__(kTPB, tpl_march_waves(NPL, NORM)) void tpl_march_ke
     }
 }
 
-// ---- ring-marched uniform stencils (variant bit 1024) -------------------
-// A uniform-stencil operator (tpl_mne > 0) whose master offsets split into planes -- o_e =
-// dz_e D + q_e, dz_e in {-1, 0, 1}, D a multiple of kTplRows (one grid plane for the 7- and
-// 27-pt operators) -- is swept by chains of blocks one plane apart (c, c + S, c + 2S, ...,
-// S = D / kTplRows).  Block t of a chain reads three plane slabs: x[(c + S p) kTplRows + qlo +
-// i], i < wp, for p = t - 1, t, t + 1.  They live in a ring of four LDS slots (slab p in slot
-// p & 3), so a step loads ONE new slab (wp doubles for 512 rows: 1.5-2x the rows' own x,
-// where the one-shot kernel loads its whole 3-band window, 6x) and copies nothing inside LDS
-// (tpl_march_kernel copies the reused slots).  Slab t + 2 is loaded into registers while
-// block t is computed and written to its slot at the top of step t + 1 -- the slot of slab
-// t - 2, which no wave reads after the barrier of step t -- so a step has one barrier.  Each
-// row's sum is tpl_rows_master's: the master's products in CSR order, masked entries added as
-// +0.0 -- bit-identical to the oracle.
-struct TplRingArgs {
-    TplArgs t;           // x, b, y, omega, partial, n, ntpl, hdr = entry masks, id, master
-    int S;               // blocks per plane
-    int nblk;            // blocks of the operator
-    int nchunk;          // chains per column
-    int qlo;             // slab slot 0 = row qlo of the block's plane (even)
-    int wp;              // doubles per ring slot (even)
-    // per ring phase (block index t & 3) and master entry: LDS slot of the entry's column
-    // relative to the row, ((t + dz_e) & 3) wp + q_e - qlo (kernel arguments: read with
-    // scalar loads inside the row loop, like tpl_rows_master's mslot)
-    int rslot[4][kTplMasterMax];
-    // fused hybrid-GS sweep (tpl_gs_ring_kernel): per GS template 1 / (a_ii + l1), the chain
-    // coupling's value and presence bit; chunk size; partial offset (hybrid GS layout)
-    const double* dl;
-    const double* cv;
-    const int* cf;
-    int B;
-    int part_off;
-};
-
-template <int NPP>
-struct RingSlab {
-    v2d_t v[NPP];
-    // slab p of column col: pair u of this lane = slots 2 (tid + kTPB u), +1.  Rows before 0 or
-    // past n - 1 load 0 through the buffer bounds (a negative offset is out of range too); a
-    // slab of plane -1 may still hold real rows (the split D need not be a grid plane: a block
-    // of plane 0 can hold rows whose -D neighbours are rows of block 0)
-    __device__ __forceinline__ void load(const TplRingArgs& g, __amdgpu_buffer_rsrc_t xrs, int col, int p) {
-        const int tid = threadIdx.x;
-        const int base = (col + g.S * p) * kTplRows + g.qlo;
-#pragma unroll
-        for (int u = 0; u < NPP; ++u) {
-            const int i = 2 * (tid + kTPB * u);
-            const int vo = i < g.wp ? (base + i) * 8 : -16;
-            v[u] = __builtin_bit_cast(v2d_t, __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, 0, 0));
-        }
-    }
-    __device__ __forceinline__ void store(const TplRingArgs& g, double* win, int p) const {
-        const int tid = threadIdx.x;
-        double* slot = win + (p & 3) * g.wp;
-#pragma unroll
-        for (int u = 0; u < NPP; ++u) {
-            const int i = 2 * (tid + kTPB * u);
-            if (i < g.wp) *(v2d_t*)(slot + i) = v[u];
-        }
-    }
-};
-
-// the block's rows (lane tid's rows tpl_lrow<true>(tid, j)): tpl_rows_master with ring slots
-template <int MODE, bool NORM, int MNE>
-__device__ __forceinline__ double tpl_rows_ring(const TplArgs& a, const double* win, const int* hdr, int r0,
-                                                const int* id, const double* pb, const double* py,
-                                                const int* c, int cdiag) {
-    constexpr int R = kTplRPL;
-    constexpr unsigned kFull = (1u << MNE) - 1u;
-    const int tid = threadIdx.x;
-    unsigned m[R];
-    bool full = true;
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-        m[j] = (unsigned)hdr[id[j]];
-        full = full && m[j] == kFull;
-    }
-    int rs = kTPB;
-#if AMG_TPL_SPLIT_READS
-    asm volatile("" : "+v"(rs));  // two ds_read_b64 per entry, not one ds_read2st64_b64
-#endif
-    const double* w0 = win + tpl_lrow<true>(tid, 0);
-    const double* wr[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j) wr[j] = w0 + j * rs;
-    double s[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j) s[j] = 0.0;
-    tpl_master_sums<MNE, R>(wr, m, __all(full), [&](int e) { return c[e]; }, [&](int e) { return a.mval[e]; }, s);
-    double sq = 0.0;
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-        const bool own = id[j] != kTplNone;
-        double out;
-        if (MODE == KM_SPMV) {
-            out = s[j];
-        } else if (MODE == KM_SPMV_ADD) {
-            out = py[j] + s[j];
-        } else {
-            const double t = pb[j] - s[j];
-            if (NORM) sq += own ? t * t : 0.0;
-            out = MODE == KM_RESID ? t : wr[j][cdiag] + a.omega * (a.mpd * t);
-        }
-        if (own) a.y[r0 + tpl_lrow<true>(tid, j)] = out;
-    }
-    return sq;
-}
-
-// chains ordered (chunk, column); XCD x = blockIdx % 8 takes a contiguous 1/8 of them (the
-// workgroups of one XCD walk neighbouring columns of the same planes: shared L2 lines)
-struct RingChains {
-    int c0, c1, nw, lw, K, per;
-    __device__ __forceinline__ RingChains(const TplRingArgs& g) {
-        K = (g.nblk + g.S - 1) / g.S;
-        per = (K + g.nchunk - 1) / g.nchunk;
-        const int C = g.S * g.nchunk, x = blockIdx.x & 7;
-        lw = blockIdx.x >> 3;
-        nw = gridDim.x >> 3;
-        c0 = x * (C >> 3) + min(x, C & 7);
-        c1 = c0 + (C >> 3) + (x < (C & 7) ? 1 : 0);
-    }
-};
-
-// Per-chain pipeline of the ring kernels: slabs two steps ahead in registers (sA / sB: the
-// slab of step t + 1 is stored at the top of step t, the load of slab t + 3 goes into the same
-// registers after the barrier), row ids two blocks ahead and b / y one block ahead (fA / fB), so
-// a step waits on no load it issued itself.  run_chain calls body(t, blk, r0, f) for each block
-// of the chain with f = that block's ids and operands, one barrier per step.
-template <int MODE, int NPP>
-struct RingPipe {
-    RingSlab<NPP> sA, sB;
-    TplFetch<MODE, 1, true> fA, fB;
-
-    template <class Body>
-    __device__ __forceinline__ void run_chain(const TplRingArgs& g, __amdgpu_buffer_rsrc_t xrs, double* win,
-                                              int col, int t0, int t1, Body&& body) {
-        const TplArgs& a = g.t;
-        auto blk_of = [&](int t) { return col + g.S * t; };
-        auto valid = [&](int t) { return t < t1 && blk_of(t) < g.nblk; };
-        // prologue: slabs t0 - 1, t0 into the ring; t0 + 1, t0 + 2 into registers; ids and
-        // operands of block t0, ids of block t0 + 1
-        sA.load(g, xrs, col, t0 - 1);
-        sA.store(g, win, t0 - 1);
-        sA.load(g, xrs, col, t0);
-        sA.store(g, win, t0);
-        sA.load(g, xrs, col, t0 + 1);
-        if (valid(t0 + 1)) sB.load(g, xrs, col, t0 + 2);
-        fA.issue_ids(a, blk_of(t0) * kTplRows);
-        fA.issue_operands(a);
-        if (valid(t0 + 1)) fB.issue_ids(a, blk_of(t0 + 1) * kTplRows);
-        auto step = [&](int t, RingSlab<NPP>& sn, TplFetch<MODE, 1, true>& fc, TplFetch<MODE, 1, true>& fo) {
-            const int blk = blk_of(t);
-            sn.store(g, win, t + 1);  // slot of slab t - 3: read last in step t - 2
-            __syncthreads();          // slab t + 1 visible; every wave is done with step t - 1
-            if (valid(t + 2)) sn.load(g, xrs, col, t + 3);
-            if (valid(t + 1)) fo.issue_operands(a);
-            body(t, blk, blk * kTplRows, fc);
-            if (valid(t + 2)) fc.issue_ids(a, blk_of(t + 2) * kTplRows);
-        };
-        for (int t = t0;; t += 2) {
-            if (!valid(t)) break;
-            step(t, sA, fA, fB);
-            if (!valid(t + 1)) break;
-            step(t + 1, sB, fB, fA);
-        }
-        __syncthreads();  // the next chain's prologue rewrites the ring
-    }
-};
-
-template <int MODE, bool NORM, int MNE, int NPP>
-__global__ __launch_bounds__(kTPB, 4) void tpl_ring_kernel(TplRingArgs g) {
-    static_assert(MNE > 0 && MNE < 32, "uniform stencils only");
-    const TplArgs& a = g.t;
-    extern __shared__ __attribute__((aligned(16))) double ring_lds[];
-    double* win = ring_lds;
-    int* hdr = (int*)(win + 4 * g.wp);
-    const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
-    const int tid = threadIdx.x;
-    if (tid < a.ntpl) hdr[tid] = a.hdr[tid];
-    if (tid == kTplNone) hdr[kTplNone] = 0;
-    const RingChains rc(g);
-    RingPipe<MODE, NPP> pipe;
-    for (int ch = rc.c0 + rc.lw; ch < rc.c1; ch += rc.nw) {
-        const int col = ch % g.S, t0 = (ch / g.S) * rc.per, t1 = min(rc.K, t0 + rc.per);
-        if (t0 >= t1 || col + g.S * t0 >= g.nblk) continue;  // workgroup-uniform
-        pipe.run_chain(g, xrs, win, col, t0, t1, [&](int t, int blk, int r0, const TplFetch<MODE, 1, true>& f) {
-            const int* c = g.rslot[t & 3];
-            const int cdiag = c[a.mdiag];
-            tpl_partial<NORM>(a, blk, tpl_rows_ring<MODE, NORM, MNE>(a, win, hdr, r0, f.id, f.pb, f.py, c, cdiag));
-        });
-    }
-}
-
-// Fused l1 hybrid-GS sweep on the ring (uniform stencil, every block on the GS template path,
-// n a multiple of kTplRows): per block, acc_i = b_i - the old-value couplings
-// (tpl_gs_acc_kernel's sum, lane = row) goes to LDS; then lane c of wave 0 walks chunk c of the
-// block in sweep order (tpl_gs_chain_kernel's recurrence: acc -= a_i,i-+1 x'_prev; x'_i = x_i +
-// acc * dinv_l1, x_i from the ring's centre slab), eight rows per batch with every LDS read of
-// the batch issued before its dependent chain, and the workgroup stores x' coalesced.  One
-// kernel reads id, b and x and writes x' (25 B per row) where the acc + chain pair moves 50 B.
-template <bool BACK, bool NORM, int MNE, int NPP>
-__global__ __launch_bounds__(kTPB, 4) void tpl_gs_ring_kernel(TplRingArgs g) {
-    static_assert(MNE == 7 || MNE == 27, "chain entry of the instantiated masters");
-    constexpr int R = kTplRPL;
-    constexpr int EC = MNE == 27 ? (BACK ? 14 : 12) : (BACK ? 4 : 2);
-    constexpr unsigned kFull = (1u << MNE) - 1u;
-    const TplArgs& a = g.t;
-    extern __shared__ __attribute__((aligned(16))) double ring_lds[];
-    double* win = ring_lds;
-    const int B = g.B, cpb = kTplRows / B, bs = B + 1;  // chunk stride in the stage (padded)
-    double* stage = win + 4 * g.wp;        // acc, then x' (cpb * (B + 1) doubles)
-    double* sdl = stage + cpb * bs;        // per GS template: 1 / (a_ii + l1)
-    double* scv = sdl + a.ntpl;            // chain coupling value
-    int* hdr = (int*)(scv + a.ntpl);       // entry masks (kTplMax + 1)
-    int* scf = hdr + kTplMax + 1;          // chain coupling present
-    uint8_t* sid = (uint8_t*)(scf + a.ntpl);  // per row of the block: GS template id
-    const __amdgpu_buffer_rsrc_t xrs = tpl_xrs(a);
-    const int tid = threadIdx.x, lane = tid & 63;
-    constexpr int kBit = BACK ? 2 : 1;
-    if (tid < a.ntpl) {
-        hdr[tid] = a.hdr[tid];
-        sdl[tid] = g.dl[tid];
-        scv[tid] = g.cv[tid];
-        scf[tid] = g.cf[tid] & kBit;
-    }
-    if (tid == kTplNone) hdr[kTplNone] = 0;
-    const RingChains rc(g);
-    RingPipe<KM_RESID, NPP> pipe;
-    for (int ch = rc.c0 + rc.lw; ch < rc.c1; ch += rc.nw) {
-        const int col = ch % g.S, t0 = (ch / g.S) * rc.per, t1 = min(rc.K, t0 + rc.per);
-        if (t0 >= t1 || col + g.S * t0 >= g.nblk) continue;  // workgroup-uniform
-        pipe.run_chain(g, xrs, win, col, t0, t1, [&](int t, int blk, int r0, const TplFetch<KM_RESID, 1, true>& f) {
-            const int* c = g.rslot[t & 3];
-            // acc = b - old-value couplings in CSR order (tpl_gs_acc_kernel, MNE > 0 path)
-            bool chain[R];
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                const int i = r0 + tpl_lrow<true>(tid, j), pos = i & (B - 1);
-                chain[j] = BACK ? (pos != B - 1 && i + 1 < a.n) : pos != 0;
-            }
-            unsigned m[R];
-            bool full = true;
-            double acc[R], sold[R];
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                m[j] = (unsigned)hdr[f.id[j]];
-                full = full && m[j] == kFull;
-                acc[j] = f.pb[j];
-                sold[j] = 0.0;
-            }
-            int rs = kTPB;
-#if AMG_TPL_SPLIT_READS
-            asm volatile("" : "+v"(rs));
-#endif
-            const double* w0 = win + tpl_lrow<true>(tid, 0);
-            const double* wr[R];
-#pragma unroll
-            for (int j = 0; j < R; ++j) wr[j] = w0 + j * rs;
-            if (__all(full))
-                tpl_master_gs_sums<MNE, EC, NORM, R>(wr, m, true, chain, [&](int e) { return c[e]; },
-                                                     [&](int e) { return a.mval[e]; }, acc, sold);
-            else
-                tpl_master_gs_sums<MNE, EC, NORM, R>(wr, m, false, chain, [&](int e) { return c[e]; },
-                                                     [&](int e) { return a.mval[e]; }, acc, sold);
-            double sq = 0.0;
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                const int lr = tpl_lrow<true>(tid, j);
-                stage[(lr / B) * bs + (lr & (B - 1))] = acc[j];
-                sid[lr] = (uint8_t)f.id[j];
-                if (NORM && f.id[j] != kTplNone) {
-                    const double rr = f.pb[j] - sold[j];
-                    sq += rr * rr;
-                }
-            }
-            if (NORM) {
-                sq = wave_sum(sq);
-                if (lane == 0) a.partial[g.part_off + 4 * blk + (tid >> 6)] = sq;
-            }
-            __syncthreads();  // acc and ids of the block in LDS
-            // the chain walk: lane c of wave 0 takes chunk c (rows c B .. c B + B - 1), eight rows
-            // per batch (B is a power of two >= 8): the batch's LDS reads first, then its chain
-            if (tid < cpb) {
-                const double* xc = win + (t & 3) * g.wp - g.qlo;  // x of local row lr at xc[lr]
-                double* st = stage + tid * bs;
-                double prev = 0.0;
-                for (int u0 = 0; u0 < B; u0 += 8) {
-                    int kk[8], tp[8];
-                    double ac[8], xv[8], dl[8], cv[8];
-                    bool has[8];
-#pragma unroll
-                    for (int v = 0; v < 8; ++v) {
-                        kk[v] = BACK ? B - 1 - (u0 + v) : u0 + v;
-                        tp[v] = sid[tid * B + kk[v]];
-                        ac[v] = st[kk[v]];
-                        xv[v] = xc[tid * B + kk[v]];
-                    }
-#pragma unroll
-                    for (int v = 0; v < 8; ++v) {
-                        dl[v] = sdl[tp[v]];
-                        cv[v] = scv[tp[v]];
-                        has[v] = (u0 + v > 0) && scf[tp[v]] != 0;
-                    }
-#pragma unroll
-                    for (int v = 0; v < 8; ++v) {
-                        double acv = ac[v];
-                        if (has[v]) acv -= cv[v] * prev;
-                        prev = xv[v] + acv * dl[v];
-                        st[kk[v]] = prev;
-                    }
-                }
-            }
-            __syncthreads();  // x' of the block in LDS
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                const int lr = tpl_lrow<true>(tid, j);
-                if (f.id[j] != kTplNone) a.y[r0 + lr] = stage[(lr / B) * bs + (lr & (B - 1))];
-            }
-        });
-    }
-}
-
 // l1 hybrid Gauss-Seidel (row a5; definition DESIGN.md 3).  One wavefront per slab of <= 64
 // rows (whole GS chunks), lane = row.
 //  phase 1: the lane walks its row in the slab's sliced-ELL layout (entry k of all lanes is
@@ -2389,8 +1999,8 @@ static bool tpl_march_wide() {
 
 int kernel_variant(const DevMatrix& A) {
     // variant bits: 2 = XCD-ordered blocks, 4 = gather path (no x tile), 8 = value-indexed
-    // blocks (when any block qualifies), 32 = row templates (when built), 64 = persistent
-    // x-tile kernel (off by default), 128 = z-marching template windows (default when a
+    // blocks (when any block qualifies), 32 = row templates (when built), 128 = z-marching
+    // template windows (default when a
     // shift with enough reuse exists and the window is <= 2048 doubles: 7-pt level 0 74.5 vs
     // 80.6 us, profiles/r1u_march_ab.txt; the 27-pt window of 3078 doubles ran 204 vs 154 us,
     // profiles/r1u_sa27_kernel_stats.csv against r1t).  Default
@@ -2419,12 +2029,6 @@ int kernel_variant(const DevMatrix& A) {
     // one master's subsequences (DevMatrix::tpl_mne; AMG_TPL_MASTER=0 at build turns it off)
     if (!ev && A.tpl_mne > 0) var |= 512;
     if (A.tpl_mne == 0) var &= ~512;
-    // 1024: plane-ring marching of uniform-stencil rows where the master
-    // splits into planes (DevMatrix::tpl_ring_s, found only with AMG_TPL_RING=1 at matrix
-    // creation: measured slower than the z-march (7-pt) and the one-shot window kernel (27-pt),
-    // profiles/r4_ring_ab.txt)
-    if (!ev && A.tpl_mne > 0 && A.tpl_ring_s > 0) var |= 1024;
-    if (A.tpl_mne == 0 || A.tpl_ring_s == 0 || !(var & 512)) var &= ~1024;
     return var;
 }
 
@@ -2505,51 +2109,6 @@ static void launch_tpl_march(hipStream_t s, const TplArgs& a, int g, size_t lds,
     }
 }
 
-// the ring geometry of A into g (uniform stencil with a plane split)
-static void ring_args(const DevMatrix& A, TplRingArgs& g) {
-    AMG_ASSERT(A.tpl_ring_s > 0 && (int)A.tpl_ring_dz.size() == A.tpl_mne && (int)A.tpl_ring_mq.size() == A.tpl_mne);
-    g.S = A.tpl_ring_s;
-    g.nblk = A.tpl_blocks();
-    g.qlo = A.tpl_ring_qlo;
-    g.wp = A.tpl_ring_wp;
-    for (int ph = 0; ph < 4; ++ph)
-        for (int e = 0; e < A.tpl_mne; ++e) g.rslot[ph][e] = ((ph + A.tpl_ring_dz[e]) & 3) * g.wp + A.tpl_ring_mq[e];
-    AMG_ASSERT(g.wp % 2 == 0 && g.wp <= 3 * 2 * kTPB && g.qlo % 2 == 0);
-}
-
-// a resident grid of chains (S columns x nchunk chunks of planes; XCD-contiguous, RingChains)
-template <class KernelT>
-static int ring_grid(KernelT kern, size_t lds, int S, int& nchunk) {
-    thread_local int ncu = 0;
-    if (ncu == 0) {
-        int dev = 0;
-        HIP_CHECK(hipGetDevice(&dev));
-        HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    int occ = 0;
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kTPB, lds));
-    const int res = std::max(8, std::max(1, occ) * ncu / 8 * 8);
-    nchunk = std::max(1, res / S);
-    const int cap = tpl_march_chunk_cap();
-    if (cap > 0) nchunk = std::min(nchunk, cap);
-    return std::max(8, std::min(res, (S * nchunk + 7) / 8 * 8));
-}
-
-template <int M, bool N, int K, int NPP>
-static void launch_ring_t(hipStream_t s, TplRingArgs& g, size_t lds) {
-    if constexpr (K > 0) {
-        thread_local int grid = 0, nchunk = 0, last_s = -1, last_cap = -1;
-        thread_local size_t last_lds = 0;
-        const int cap = tpl_march_chunk_cap();
-        if (last_s != g.S || last_lds != lds || last_cap != cap) {
-            grid = ring_grid(tpl_ring_kernel<M, N, K, NPP>, lds, g.S, nchunk);
-            last_s = g.S, last_lds = lds, last_cap = cap;
-        }
-        g.nchunk = nchunk;
-        hipLaunchKernelGGL((tpl_ring_kernel<M, N, K, NPP>), dim3(grid), dim3(kTPB), lds, s, g);
-    }
-}
-
 void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const double* x,
                 const double* b, double* y, double omega, double* partial) {
     const int g = A.tpl_blocks();
@@ -2591,41 +2150,6 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
         a.mdiag = A.tpl_mdiag;
         a.mpd = A.tpl_mpd;
         for (int e = 0; e < mne; ++e) a.mslot[e] = A.tpl_mslot[e], a.mval[e] = A.tpl_mval[e];
-    }
-    if (mne > 0 && (kernel_variant(A) & 1024)) {
-        // plane ring: one slab per block from x, nothing copied in LDS
-        TplRingArgs g{};
-        g.t = a;
-        ring_args(A, g);
-        const int npp = (g.wp / 2 + kTPB - 1) / kTPB;
-        const size_t lds = 8 * (size_t)4 * g.wp + 4 * (size_t)(kTplMax + 1);
-#define AMG_R3(M, N, K)                                         \
-    do {                                                        \
-        if (npp <= 2) launch_ring_t<M, N, K, 2>(s, g, lds);     \
-        else launch_ring_t<M, N, K, 3>(s, g, lds);              \
-    } while (0)
-#define AMG_R(M, N)                                \
-    do {                                           \
-        if (mne == 7) AMG_R3(M, N, 7);             \
-        else AMG_R3(M, N, 27);                     \
-    } while (0)
-        switch (mode) {
-            case KM_SPMV: AMG_R(KM_SPMV, false); break;
-            case KM_SPMV_ADD: AMG_R(KM_SPMV_ADD, false); break;
-            case KM_RESID:
-                if (norm) AMG_R(KM_RESID, true);
-                else AMG_R(KM_RESID, false);
-                break;
-            case KM_JACOBI:
-                if (norm) AMG_R(KM_JACOBI, true);
-                else AMG_R(KM_JACOBI, false);
-                break;
-            default: throw Error(AMG_ERR_INTERNAL, "bad kernel mode");
-        }
-#undef AMG_R
-#undef AMG_R3
-        HIP_CHECK(hipGetLastError());
-        return;
     }
     const int npl = !win ? 0 : a.win <= 4 * kTPB ? 4 : a.win <= 8 * kTPB ? 8 : a.win <= 12 * kTPB ? 12 : 16;
     AMG_ASSERT(a.win <= npl * kTPB && a.win <= kTplWin);
@@ -2672,57 +2196,8 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
     HIP_CHECK(hipGetLastError());
 }
 
-template <int M, bool N, bool V>
-static void launch_csr_persist_t(hipStream_t s, const CsrArgs& a, int first_block, int nb) {
-    static int occ = 0;  // resident workgroups per CU (same for every operator)
-    if (occ == 0) HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, csr_persist_kernel<M, N, V>, kTPB, 0));
-    int dev = 0, ncu = 0;
-    HIP_CHECK(hipGetDevice(&dev));
-    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    const int g = std::max(8, std::min(nb, std::max(1, occ) * ncu) / 8 * 8);
-    hipLaunchKernelGGL((csr_persist_kernel<M, N, V>), dim3(g), dim3(kTPB), 0, s, a, first_block, nb);
-}
-
-static void launch_csr_persist(hipStream_t s, int mode, bool norm, const CsrArgs& a, int first_block,
-                               int nb, bool vi) {
-#define AMG_P(M, N)                                              \
-    do {                                                         \
-        if (vi) launch_csr_persist_t<M, N, true>(s, a, first_block, nb);  \
-        else launch_csr_persist_t<M, N, false>(s, a, first_block, nb);    \
-    } while (0)
-    switch (mode) {
-        case KM_SPMV: AMG_P(KM_SPMV, false); break;
-        case KM_SPMV_ADD: AMG_P(KM_SPMV_ADD, false); break;
-        case KM_RESID:
-            if (norm) AMG_P(KM_RESID, true);
-            else AMG_P(KM_RESID, false);
-            break;
-        case KM_JACOBI:
-            if (norm) AMG_P(KM_JACOBI, true);
-            else AMG_P(KM_JACOBI, false);
-            break;
-        default: throw Error(AMG_ERR_INTERNAL, "bad kernel mode");
-    }
-#undef AMG_P
-    HIP_CHECK(hipGetLastError());
-}
-
-// AMG_CSR_PAIR=1: square x-tile operators run two blocks per workgroup (A/B)
-static bool csr_pair() {
-    const char* e = std::getenv("AMG_CSR_PAIR");  // read per launch (tests flip it in-process)
-    return e && *e && std::atoi(e) != 0;
-}
-
 template <int M, bool N, bool X, bool T, bool V>
 static void launch_block(hipStream_t s, dim3 g, const CsrArgs& a, int first_block, bool rpb4, int lw) {
-    if constexpr (T && AMG_CSR_PRE_TILE) {
-        if (a.nblk >= 2 && !rpb4 && csr_pair()) {
-            const dim3 gp((unsigned)((a.nblk + 1) / 2));
-            if (lw == 4) hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, 1, false, 4, true>), gp, dim3(kTPB), 0, s, a, first_block);
-            else hipLaunchKernelGGL((csr_block_kernel<M, N, X, T, V, 1, false, 8, true>), gp, dim3(kTPB), 0, s, a, first_block);
-            return;
-        }
-    }
     if constexpr (T) {
         if (lw == 4) {  // 32-byte x-tile lines
             if constexpr (!N && (M == KM_SPMV || M == KM_SPMV_ADD)) {
@@ -2762,10 +2237,6 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
     const dim3 g(n_blocks);
     const int var = kernel_variant(A);
     if (var & 256) a.col16 = A.col16.p;
-    if ((var & 64) && !(var & 4) && A.square && A.line_w == 8 && mode != KM_GSACC) {  // persistent x-tile kernel: square operators, 64-byte lines
-        launch_csr_persist(s, mode, norm, a, first_block, n_blocks, (var & 8) != 0);
-        return;
-    }
     const bool rpb4 = A.gather_rpb > 1;
 #define AMG_L1(M, N, X, T, V) launch_block<M, N, X, T, V>(s, g, a, first_block, rpb4, A.line_w)
 #define AMG_L2(M, N, V)                                               \
@@ -2910,52 +2381,6 @@ static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, co
         for (int e = 0; e < mne; ++e) a.mslot[e] = A.tpl_mslot[e], a.mval[e] = A.tpl_mval[e];
     }
     const bool norm = partial != nullptr;
-    if (mne > 0 && A.gs_ring && (kernel_variant(A) & 1024)) {
-        // fused sweep on the plane ring: acc and the chain walk in one kernel
-        TplRingArgs r{};
-        r.t = a;
-        r.t.y = y;
-        ring_args(A, r);
-        r.dl = A.gs_tdl.p;
-        r.cv = backward ? A.gs_tcvp.p : A.gs_tcvm.p;
-        r.cf = A.gs_tcf.p;
-        r.B = (int)A.gs_block;
-        r.part_off = A.n_gs_slabs;
-        const int npp = (r.wp / 2 + kTPB - 1) / kTPB;
-        const int cpb = kTplRows / r.B;
-        const size_t lds = 8 * ((size_t)4 * r.wp + (size_t)cpb * (r.B + 1) + 2 * (size_t)a.ntpl) +
-                           4 * ((size_t)kTplMax + 1 + a.ntpl) + kTplRows;
-#define AMG_GR3(BK, NM, K, P)                                                               \
-    do {                                                                                    \
-        thread_local int grid = 0, nchunk = 0, last_s = -1, last_cap = -1;                  \
-        thread_local size_t last_lds = 0;                                                   \
-        const int cap = tpl_march_chunk_cap();                                              \
-        if (last_s != r.S || last_lds != lds || last_cap != cap) {                          \
-            grid = ring_grid(tpl_gs_ring_kernel<BK, NM, K, P>, lds, r.S, nchunk);           \
-            last_s = r.S, last_lds = lds, last_cap = cap;                                   \
-        }                                                                                   \
-        r.nchunk = nchunk;                                                                  \
-        hipLaunchKernelGGL((tpl_gs_ring_kernel<BK, NM, K, P>), dim3(grid), dim3(kTPB), lds, s, r); \
-    } while (0)
-#define AMG_GR2(BK, NM, K)                 \
-    do {                                   \
-        if (npp <= 2) AMG_GR3(BK, NM, K, 2); \
-        else AMG_GR3(BK, NM, K, 3);        \
-    } while (0)
-#define AMG_GR(BK, NM)                      \
-    do {                                    \
-        if (mne == 7) AMG_GR2(BK, NM, 7);   \
-        else AMG_GR2(BK, NM, 27);           \
-    } while (0)
-        if (backward) AMG_GR(true, false);
-        else if (norm) AMG_GR(false, true);
-        else AMG_GR(false, false);
-#undef AMG_GR
-#undef AMG_GR2
-#undef AMG_GR3
-        HIP_CHECK(hipGetLastError());
-        return;
-    }
     const int npl = a.win <= 4 * kTPB ? 4 : a.win <= 8 * kTPB ? 8 : a.win <= 12 * kTPB ? 12 : 16;
     AMG_ASSERT(a.win <= npl * kTPB && a.win <= kTplWin);
     const size_t lds = tpl_gs_lds_bytes(a.win, a.nent, a.ntpl);
@@ -3099,8 +2524,7 @@ void launch_gs_chain(hipStream_t s, const DevMatrix& A, const double* x, const d
              ns, nullptr, nullptr, nullptr, 0, 0};
     AMG_ASSERT(A.gs_cmaxw[d] <= 64);  // <= 63: in-chunk couplings of a <= 64-row chunk
     AMG_ASSERT(A.gs_cbucket[d][kGsChainBuckets] == ns);
-    // one launch per non-empty width bucket (DevMatrix::gs_cbucket: by default every slab is
-    // in the widest slab's bucket, one launch; AMG_GS_CHAIN_BUCKETS=1 sorts them by width)
+    // one launch, at the widest slab's width bucket (DevMatrix::gs_cbucket)
     for (int q = 0; q < kGsChainBuckets; ++q) {
         const int b0 = A.gs_cbucket[d][q], b1 = A.gs_cbucket[d][q + 1];
         if (b1 <= b0) continue;

@@ -551,59 +551,6 @@ static TplBuild build_templates(const std::vector<int>& rp, const hvec<int>& col
     return T;
 }
 
-// Plane ring: a split of the master offsets into o = dz D + q, dz in {-1, 0,
-// 1}, D a multiple of kTplRows (one grid plane of a 3D stencil), with the narrowest slab
-// [qlo, kTplRows + qhi) -- what tpl_ring_kernel loads per block.  Candidates D are the multiples
-// of kTplRows around each |o|; each offset takes the nearest plane.  Slabs of more than 3
-// pairs per lane (1536 doubles) are not taken.
-static void find_plane_ring(DevMatrix& D, const std::vector<int>& moff) {
-    D.tpl_ring_s = D.tpl_ring_qlo = D.tpl_ring_wp = 0;
-    D.tpl_ring_dz.clear();
-    D.tpl_ring_mq.clear();
-    const char* env = std::getenv("AMG_TPL_RING");  // opt-in (kernel_variant: r4_ring_ab.txt)
-    if (!(env && std::atoi(env) == 1)) return;
-    if (D.n_rows % 2 != 0) return;  // 16-byte pair loads never straddle the end of x
-    int64_t best_wp = INT64_MAX, best_d = 0;
-    std::vector<int64_t> cand;
-    for (int o : moff) {
-        const int64_t a = std::abs((int64_t)o);
-        if (a < kTplRows) continue;
-        cand.push_back(a / kTplRows * kTplRows);
-        cand.push_back((a / kTplRows + 1) * kTplRows);
-    }
-    for (int64_t d : cand) {
-        if (d <= 0 || d / kTplRows > (1 << 24)) continue;
-        int64_t qlo = INT64_MAX, qhi = INT64_MIN;
-        bool ok = true, planes = false;
-        for (int o : moff) {
-            const int64_t dz = o >= 0 ? (o + d / 2) / d : -((-o + d / 2) / d);
-            if (dz < -1 || dz > 1) ok = false;
-            planes = planes || dz != 0;
-            const int64_t q = o - dz * d;
-            if (2 * std::abs(q) >= d) ok = false;
-            qlo = std::min(qlo, q);
-            qhi = std::max(qhi, q);
-        }
-        if (!ok || !planes) continue;
-        qlo &= ~(int64_t)1;  // even: slab pairs are 16-byte aligned
-        const int64_t wp = (kTplRows + qhi - qlo + 1) & ~(int64_t)1;  // slots qlo .. kTplRows - 1 + qhi
-        if (wp < best_wp) best_wp = wp, best_d = d;
-    }
-    if (best_d == 0 || best_wp > 3 * 2 * kTPB) return;
-    const int64_t d = best_d;
-    int64_t qlo = INT64_MAX;
-    for (int o : moff) {
-        const int64_t dz = o >= 0 ? (o + d / 2) / d : -((-o + d / 2) / d);
-        qlo = std::min(qlo, o - dz * d);
-        D.tpl_ring_dz.push_back((int)dz);
-    }
-    qlo &= ~(int64_t)1;
-    for (size_t e = 0; e < moff.size(); ++e) D.tpl_ring_mq.push_back((int)(moff[e] - D.tpl_ring_dz[e] * d - qlo));
-    D.tpl_ring_s = (int)(d / kTplRows);
-    D.tpl_ring_qlo = (int)qlo;
-    D.tpl_ring_wp = (int)best_wp;
-}
-
 // Uniform stencil: a constant-coefficient stencil's boundary templates are
 // its interior template with entries removed.  When the longest template (the master) has a
 // kernel instantiation (7 or 27 entries) and every template's (offset, value bits) entries are
@@ -613,7 +560,6 @@ static void find_plane_ring(DevMatrix& D, const std::vector<int>& moff) {
 // order are the row's own, so results are unchanged (bit-identical).
 static void find_master_template(DevMatrix& D, const TplBuild& tb, const std::vector<int>& ldo) {
     D.tpl_mne = 0;
-    D.tpl_ring_s = 0;
     D.tpl_mdiag = D.tpl_mem = D.tpl_mep = -1;
     D.tpl_mslot.clear();
     D.tpl_mval.clear();
@@ -659,7 +605,6 @@ static void find_master_template(DevMatrix& D, const TplBuild& tb, const std::ve
         if (tb.off[sm + e] == 1) D.tpl_mep = e;
     }
     D.tpl_mmask.upload(mask.data(), mask.size());
-    find_plane_ring(D, std::vector<int>(tb.off.begin() + sm, tb.off.begin() + sm + ne));
 }
 
 void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
@@ -934,7 +879,6 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         }
         if (tpl_win == 0) {
             tpl_mne = 0;
-            tpl_ring_s = 0;
             tpl_mmask.reset();
         }
         tm.lap("    build: template window / march");
@@ -1397,18 +1341,9 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
     int64_t ell_rows = 0;
     for (const int4& sl : slabs) ell_rows += sl.y;
     gs_bytes = (gs_ndict > 0 ? 5 : 12) * 64 * cells + 16 * (int64_t)slabs.size() + 32 * ell_rows;
-    // the fused plane-ring sweep (AMG_GS_RING=1): a uniform 3D stencil whose
-    // every block is on the GS template path, whole 512-row blocks, chunks of 8..512 rows;
-    // otherwise the acc + chain kernel pair
-    {
-        const char* e = std::getenv("AMG_GS_RING");  // opt-in: slower than the pair (r4_ring_ab.txt)
-        gs_ring = (e && *e && std::atoi(e) == 1) && n_gs_tblk > 0 && n_gs_tblk == tpl_blocks() && tpl_mne > 0 &&
-                  tpl_ring_s > 0 && gs_tmask.p && n_rows % kTplRows == 0 && B >= 8 && kTplRows % B == 0;
-    }
-    // template rows: acc kernel 1 B id + b + x (window) + acc out; chain kernel acc + x + id + y;
-    // fused ring sweep: id + b + x in, y out
+    // template rows: acc kernel 1 B id + b + x (window) + acc out; chain kernel acc + x + id + y
     if (n_gs_tblk > 0)
-        gs_bytes += (gs_ring ? 25 : 50) * (n_rows - ell_rows) + 16 * (int64_t)n_tpl_ent + 12 * (int64_t)n_gs_tpl;
+        gs_bytes += 50 * (n_rows - ell_rows) + 16 * (int64_t)n_tpl_ent + 12 * (int64_t)n_gs_tpl;
     gs_wide = !slabs.empty() && cells >= (int64_t)kGsWide * (int64_t)slabs.size();
 
     // Split sweeps: the old-value couplings as a CSR-block pass (KM_GSACC on A
@@ -1519,22 +1454,13 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
                         }
                     }
                 }
-                // AMG_GS_CHAIN_BUCKETS=1: slabs grouped by the LDS queue their width needs
-                // (kGsChainW buckets), one chain launch per bucket, so one wide slab does not
-                // size every wave's queue.  Measured slower (g3sub 1560 -> 1360 V-cycles/s:
-                // the sweeps were not faster and the coarse levels paid the extra launches,
-                // profiles/r4f_g3sub_buckets.txt), so by default every slab sits in the
-                // widest slab's bucket: one launch.  The order of the slabs is free.
-                const char* be = std::getenv("AMG_GS_CHAIN_BUCKETS");
-                const bool by_width = be && *be && std::atoi(be) == 1;
-                if (by_width)
-                    std::stable_sort(cs.begin(), cs.end(), [](const int4& a, const int4& b) {
-                        return gs_chain_bucket(a.w) < gs_chain_bucket(b.w);
-                    });
+                // one chain launch: every slab in the widest slab's width bucket (one launch per
+                // bucket measured slower, g3sub 1560 -> 1360 V-cycles/s: the coarse levels pay
+                // the extra launches, profiles/r4f_g3sub_buckets.txt)
                 int wmax = 0;
                 for (const int4& sl : cs) wmax = std::max(wmax, sl.w);
                 for (int q = 0; q <= kGsChainBuckets; ++q) gs_cbucket[d][q] = 0;
-                for (const int4& sl : cs) ++gs_cbucket[d][gs_chain_bucket(by_width ? sl.w : wmax) + 1];
+                gs_cbucket[d][gs_chain_bucket(wmax) + 1] = (int)cs.size();
                 for (int q = 0; q < kGsChainBuckets; ++q) gs_cbucket[d][q + 1] += gs_cbucket[d][q];
                 gs_cslabs[d].upload(cs.data(), cs.size());
                 gs_ccol[d].upload(ccol.data(), ccol.size());

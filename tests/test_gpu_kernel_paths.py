@@ -103,29 +103,21 @@ WIDE = [("27pt", (200, 8, 8), 12), ("27pt", (260, 8, 8), 16), ("27pt", (256, 16,
         ("27pt", (40, 40, 40), 8), ("7pt", (40, 40, 40), 8), ("5pt", (200, 60), 4)]
 
 
-@pytest.mark.parametrize("path", ["ring", "window", "march", "generic", "generic_march"])
+@pytest.mark.parametrize("path", ["window", "march", "generic", "generic_march"])
 @pytest.mark.parametrize("kind,dims,npl", WIDE, ids=[f"{k}-{'x'.join(map(str, d))}" for k, d, _ in WIDE])
 def test_template_window_lanes(ctx, oracle, monkeypatch, kind, dims, npl, path):
     """tpl_kernel<*, *, NPL, MNE> (window) and tpl_march_kernel<*, *, NPL, MNE> (forced by
     variant bit 128, chains capped at one per column so every block after a chain's first
     copies its reused slots inside LDS) at every lanes-per-row instantiation, all modes + norm,
     with uniform-stencil rows (MNE = 7 / 27: every template a subsequence of the master, bit
-    512) and with the per-template tables (generic); and the plane ring (tpl_ring_kernel,
-    bit 1024, opt-in with AMG_TPL_RING=1 for uniform 3D stencils: DESIGN.md 4.0 r4)."""
+    512) and with the per-template tables (generic)."""
     import raptor_amd as ra
 
     O = oracle
     if path.endswith("march") and npl == 4:
         pytest.skip("a window of <= 1024 doubles is one band: no reusing shift exists")
-    if path == "ring" and kind == "5pt":
-        pytest.skip("a 2D stencil has no plane split")
     gen = {"7pt": O.gen_7pt, "27pt": O.gen_27pt, "5pt": O.gen_5pt}[kind]
     Ao = gen(*dims)
-    if path == "window":
-        monkeypatch.setenv("AMG_TPL_RING", "0")
-    if path == "ring":
-        monkeypatch.setenv("AMG_TPL_RING", "1")
-        monkeypatch.setenv("AMG_TPL_MARCH_CHUNKS", "2")  # long chains: every ring phase
     if path.endswith("march"):
         monkeypatch.setenv("AMG_KERNEL_VARIANT", "170" if path == "generic_march" else str(170 | 512))
         monkeypatch.setenv("AMG_TPL_MARCH_CHUNKS", "1")
@@ -142,32 +134,7 @@ def test_template_window_lanes(ctx, oracle, monkeypatch, kind, dims, npl, path):
         assert S > 0, "no reusing shift found"
         blocks = -(-Ao.shape[0] // 512)
         assert blocks >= 2 * S, "chains of one block: the reuse branch would not run"
-    assert bool(inf["kernel_variant"] & 1024) == (path == "ring"), inf["kernel_variant"]
     all_modes_equal(ctx, O, A, Ao)
-
-
-RING = [("7pt", (64, 64, 24)), ("7pt", (40, 40, 40)), ("27pt", (40, 40, 40)), ("27pt", (72, 40, 30)),
-        ("7pt", (256, 8, 12)), ("27pt", (96, 32, 19)), ("7pt", (30, 30, 7))]
-
-
-@pytest.mark.parametrize("chunks", ["0", "1", "3"])
-@pytest.mark.parametrize("kind,dims", RING, ids=[f"{k}-{'x'.join(map(str, d))}" for k, d in RING])
-def test_template_plane_ring(ctx, oracle, monkeypatch, kind, dims, chunks):
-    """tpl_ring_kernel on shapes whose plane is a whole number of 512-row
-    blocks and on shapes whose split D is the nearest block multiple instead (the chain then
-    steps D rows, not a grid plane: the split is algebraic), with partial last blocks and
-    partial last planes; chains of every length (AMG_TPL_MARCH_CHUNKS: 1 = one chain per
-    column).  All modes + norm bit-identical to the oracle."""
-    import raptor_amd as ra
-
-    O = oracle
-    monkeypatch.setenv("AMG_TPL_RING", "1")
-    if chunks != "0":
-        monkeypatch.setenv("AMG_TPL_MARCH_CHUNKS", chunks)
-    Ao = (O.gen_7pt if kind == "7pt" else O.gen_27pt)(*dims)
-    A = _dev(ra, ctx, Ao)
-    assert A.info["kernel_variant"] & 1024, A.info
-    all_modes_equal(ctx, O, A, Ao, seed=41)
 
 
 @pytest.mark.parametrize("kind,dims", [("7pt", (128, 128, 80)), ("27pt", (80, 120, 120))])
@@ -206,21 +173,19 @@ def test_march_reuse_shapes(ctx, oracle, monkeypatch, kind, dims):
 
 
 # ---- V-cycles on forced paths, against the oracle ----------------------------------------
-VPATHS = {"persist_csr": {"AMG_KERNEL_VARIANT": "106", "AMG_TILE_LINE": "8"},
-          "lines64": {"AMG_TILE_LINE": "8"},
+VPATHS = {"lines64": {"AMG_TILE_LINE": "8"},
           "lines32": {"AMG_TILE_LINE": "4"},
           "march_chained": {"AMG_KERNEL_VARIANT": "170", "AMG_TPL_MARCH_CHUNKS": "1"},
           "blocks_only": {"AMG_KERNEL_VARIANT": "10"},
           "gather_int32": {"AMG_GATHER_C16": "0"},
           "rect_tile": {"AMG_RECT_TILE": "1"},
-          "paired_blocks": {"AMG_CSR_PAIR": "1"},
           "eager": {}}
 
 
 @pytest.mark.parametrize("path", list(VPATHS))
 def test_vcycle_paths_vs_oracle(ctx, oracle, monkeypatch, path):
-    """PMIS V-cycles with the level kernels forced onto one path (persistent x-tile kernel,
-    chained march, CSR blocks only, eager launches instead of the hipGraph): iterates
+    """PMIS V-cycles with the level kernels forced onto one path (x-tile line widths, chained
+    march, CSR blocks only, eager launches instead of the hipGraph): iterates
     bit-identical to the oracle's cycle on the product's own operators, history <= 1e-10."""
     import raptor_amd as ra
 
@@ -363,7 +328,7 @@ GS_SHAPES = [("27pt", (260, 8, 8)), ("27pt", (40, 40, 40)), ("7pt", (37, 41, 29)
              ("27pt", (64, 32, 16)), ("7pt", (32, 32, 24))]
 
 
-@pytest.mark.parametrize("tpl_gs", ["templates", "ring", "generic", "ell", "split", "split_buckets"])
+@pytest.mark.parametrize("tpl_gs", ["templates", "generic", "ell", "split"])
 @pytest.mark.parametrize("kind,dims", GS_SHAPES, ids=[f"{k}-{'x'.join(map(str, d))}" for k, d in GS_SHAPES])
 def test_hybrid_gs_template_kernel(ctx, oracle, monkeypatch, kind, dims, tpl_gs):
     """l1 hybrid GS, forward / backward, block sizes 64, 32, 8, 1 (the template kernel needs B
@@ -371,21 +336,14 @@ def test_hybrid_gs_template_kernel(ctx, oracle, monkeypatch, kind, dims, tpl_gs)
     (NPL 16, 8 and 4 windows; a last partial block), with the template kernel on -- uniform-
     stencil masks (7-pt, 27-pt) or per-template tables (generic) -- and off: the one-kernel
     sliced-ELL sweep (ell) or the split sweep (KM_GSACC block pass + chain walk, 4.2c).
-    templates: the acc + chain pair (the default); ring: the fused plane-ring sweep
-    (tpl_gs_ring_kernel, AMG_TPL_RING=1 AMG_GS_RING=1) where it applies (uniform 3D stencil, n
-    a multiple of 512 rows, 8 <= B | 512), else the pair."""
+    templates: the acc + chain pair (the default)."""
     import raptor_amd as ra
 
     O = oracle
-    if tpl_gs == "ring":
-        monkeypatch.setenv("AMG_TPL_RING", "1")
-        monkeypatch.setenv("AMG_GS_RING", "1")
-    if tpl_gs in ("ell", "split", "split_buckets"):
+    if tpl_gs in ("ell", "split"):
         monkeypatch.setenv("AMG_GS_TEMPLATES", "0")
     if tpl_gs.startswith("split"):
         monkeypatch.setenv("AMG_GS_SPLIT_NPR", "0")
-        if tpl_gs == "split_buckets":  # chain walk launched per width bucket
-            monkeypatch.setenv("AMG_GS_CHAIN_BUCKETS", "1")
     else:
         monkeypatch.setenv("AMG_GS_SPLIT", "0")
     if tpl_gs == "generic":
