@@ -428,6 +428,8 @@ void par_apply(DevMatrix& A, int mode, const double* x, const double* b, double*
 // partial (forward only): per-slab sums of (b - A x)^2 for a fused residual norm
 void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, int64_t block,
                    bool backward = false, double* partial = nullptr);
+// the forward sweep from x0 = 0 (zeroed by the caller): the split form skips its old-value pass
+void par_hybrid_gs_from_zero(DevMatrix& A, const double* x0, const double* b, double* y, int64_t block);
 // Norm plumbing: a mode-NORM level kernel leaves per-block partial sums of (b - Ax)^2 in
 // NormSink::partial; norm_finish() reduces them (fixed order), combines ranks (RCCL
 // allgather, rank order) and appends sqrt to hist[*counter] -- all on the device.

@@ -14,11 +14,37 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "device.hpp"
 
 namespace amg {
+
+// Phase trace of the x-tile block kernel (diagnostic build only: make EXTRA=-DAMG_CSR_PHASES=1;
+// scripts/csr_phase_trace.py).  Thread 0 of each block waits for its own outstanding loads at
+// fixed points and stamps s_memtime there: [0] entry, [1] batch 1 in (header, line ids, tile /
+// VI indices), [2] batch 2 in (x tile, value table, row operands), [3] x tile in LDS (first
+// barrier passed), [4] products in LDS (second barrier), [5] row sums stored; [6] / [7]
+// s_memrealtime (100 MHz) at entry and exit.  The waits serialise thread 0's loads a little.
+#ifndef AMG_CSR_PHASES
+#define AMG_CSR_PHASES 0
+#endif
+#if AMG_CSR_PHASES
+__device__ unsigned long long* g_csr_phase;
+#define AMG_PHASE(k)                                                   \
+    do {                                                               \
+        if (threadIdx.x == 0) {                                        \
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+            csr_ph[k] = __builtin_amdgcn_s_memtime();                  \
+        }                                                              \
+    } while (0)
+#else
+#define AMG_PHASE(k) \
+    do {             \
+    } while (0)
+#endif
 
 namespace {
 
@@ -222,7 +248,8 @@ __device__ __forceinline__ void csr_pre_tile(const CsrArgs& a, int bid, CsrPre& 
 template <int MODE, bool NORM, bool TILE, bool VIB, int NU, int PRE = 0, int RPB = 1, bool C16 = false,
           int LW = 8>
 __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* stage, double* tabl,
-                                             int* rends, CsrPre* pre = nullptr) {
+                                             int* rends, CsrPre* pre = nullptr,
+                                             unsigned long long* csr_ph = nullptr) {
     constexpr int U = kCAP / kTPB;  // 8 lane slots
     static_assert(NU >= 2 && NU % 2 == 0 && NU <= U && (TILE ? NU == U : true), "slot pairs");
     static_assert(RPB == 1 || (!NORM && (MODE == KM_SPMV || MODE == KM_SPMV_ADD)),
@@ -363,6 +390,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
                 }
             }
         }
+        if constexpr (PRE > 0) AMG_PHASE(2);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             *(v2d_t*)(stage + 2 * tid + 512 * j) = v2d_t{xs[2 * j], xs[2 * j + 1]};
@@ -372,6 +400,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
     }
     if (VIB) tabl[tid] = tv;
     if (TILE || VIB) __syncthreads();
+    if constexpr (PRE > 0) AMG_PHASE(3);
     constexpr int LS = LW == 8 ? 3 : 2;
     if (px_tile) px = stage[(h1.x + (rr >> LS) - (r0 >> LS)) * LW + (rr & (LW - 1))];
     // 1 / a_ii from the table: the same correctly rounded division the host does for dinv
@@ -404,6 +433,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
         for (int u = 0; u < NU; ++u) stage[tid + u * kTPB] = pr[u];
     }
     __syncthreads();
+    if constexpr (PRE > 0) AMG_PHASE(4);
     if constexpr (RPB > 1) {
 #pragma unroll
         for (int j = 1; j < RPB; ++j) {
@@ -432,6 +462,7 @@ __device__ __forceinline__ double block_main(const CsrArgs& a, int bid, double* 
         a.y[r] = out;
         store_y2<MODE>(a, r, out, pd);
     }
+    if constexpr (PRE > 0) AMG_PHASE(5);
     return sq;
 }
 
@@ -506,17 +537,34 @@ __global__ __launch_bounds__(kTPB, GRPB > 1 ? 7 : 8) void csr_block_kernel(CsrAr
         // block id) issued together with the header instead of after it -- one dependent
         // round of loads less per block
         constexpr int PV = VI ? 2 : 1;
+        unsigned long long* csr_ph = nullptr;
+#if AMG_CSR_PHASES
+        __shared__ unsigned long long ph_lds[8];
+        csr_ph = ph_lds;
+        if (threadIdx.x == 0) csr_ph[6] = __builtin_amdgcn_s_memrealtime();
+        AMG_PHASE(0);
+#endif
         CsrPre f;
         csr_pre_tile<VI, LW>(a, bid, f);
+#if AMG_CSR_PHASES
+        if (threadIdx.x == 0) asm volatile("" ::"v"(f.tid_line), "v"(f.lq.x), "v"(f.vq.x), "s"(f.h0.x), "s"(f.h1.x));
+        AMG_PHASE(1);
+#endif
         const int4 h0 = f.h0, h1 = f.h1;
         double sq;
         if (h0.w <= kCAP && (h1.y & 0xffff) <= kCAP / LW && h0.w > 0) {
-            if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f);
-            else sq = block_main<MODE, NORM, true, false, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f);
+            if (VI && h1.z >= 0) sq = block_main<MODE, NORM, true, true, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f, csr_ph);
+            else sq = block_main<MODE, NORM, true, false, 8, PV, GRPB, false, LW>(a, bid, stage, tabl, rends, &f, csr_ph);
         } else {
             sq = block_long<MODE, NORM>(a, h0, stage);
         }
         block_partial<NORM>(a, bid, sq);
+#if AMG_CSR_PHASES
+        if (threadIdx.x == 0 && g_csr_phase) {
+            csr_ph[7] = __builtin_amdgcn_s_memrealtime();
+            for (int k = 0; k < 8; ++k) g_csr_phase[(size_t)(bid - first_block) * 8 + k] = csr_ph[k];
+        }
+#endif
         return;
     }
     const int4 h0 = a.hdr[2 * bid], h1 = a.hdr[2 * bid + 1];
@@ -1177,6 +1225,7 @@ __device__ __forceinline__ void tpl_partial(const TplArgs& a, int blk, double sq
         if ((threadIdx.x & 63) == 0) a.partial[blk * kNormParts + (threadIdx.x >> 6)] = sq;
     }
 }
+
 
 // waves per SIMD the persistent and marching forms are compiled for: windows of more than
 // 8 slots per lane (27-pt: 3084 doubles, ~34 KiB of LDS with the table) fit 4 workgroups per
@@ -2252,6 +2301,19 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
         if (var & 8) AMG_L2(M, N, true);                              \
         else AMG_L2(M, N, false);                                     \
     } while (0)
+#if AMG_CSR_PHASES
+    // diagnostic build: every launch of a tiled operator dumps its blocks' stamps
+    const char* phase_file = A.tiled ? std::getenv("AMG_CSR_PHASES_FILE") : nullptr;
+    // never freed: a static's hipFree at exit would run after the runtime's teardown
+    static DevBuf<unsigned long long>& phase_buf = *new DevBuf<unsigned long long>();
+    if (phase_file) {
+        if (phase_buf.n < (size_t)n_blocks * 8) phase_buf.alloc((size_t)n_blocks * 8);
+        HIP_CHECK(hipMemsetAsync(phase_buf.p, 0, sizeof(unsigned long long) * n_blocks * 8, s));
+        unsigned long long* p = phase_buf.p;
+        HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_csr_phase), &p, sizeof(p), 0, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+    }
+#endif
     switch (mode) {
         case KM_SPMV: AMG_L(KM_SPMV, false); break;
         case KM_SPMV_ADD: AMG_L(KM_SPMV_ADD, false); break;
@@ -2269,6 +2331,21 @@ void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, i
             break;
         default: throw Error(AMG_ERR_INTERNAL, "bad kernel mode");
     }
+#if AMG_CSR_PHASES
+    if (phase_file) {
+        HIP_CHECK(hipStreamSynchronize(s));
+        std::vector<unsigned long long> h((size_t)n_blocks * 8);
+        HIP_CHECK(hipMemcpy(h.data(), phase_buf.p, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+        unsigned long long* z = nullptr;
+        HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_csr_phase), &z, sizeof(z)));
+        if (FILE* fp = std::fopen(phase_file, "ab")) {
+            const long long hdr[4] = {mode, n_blocks, (long long)A.n_rows, (long long)A.nnz};
+            std::fwrite(hdr, sizeof(hdr), 1, fp);
+            std::fwrite(h.data(), sizeof(unsigned long long), h.size(), fp);
+            std::fclose(fp);
+        }
+    }
+#endif
 #undef AMG_L
 #undef AMG_L2
 #undef AMG_L1
@@ -2381,10 +2458,10 @@ static void launch_tpl_gs(hipStream_t s, const DevMatrix& A, const double* x, co
         for (int e = 0; e < mne; ++e) a.mslot[e] = A.tpl_mslot[e], a.mval[e] = A.tpl_mval[e];
     }
     const bool norm = partial != nullptr;
+    const dim3 grid(g.nblk), blk(kTPB);
     const int npl = a.win <= 4 * kTPB ? 4 : a.win <= 8 * kTPB ? 8 : a.win <= 12 * kTPB ? 12 : 16;
     AMG_ASSERT(a.win <= npl * kTPB && a.win <= kTplWin);
     const size_t lds = tpl_gs_lds_bytes(a.win, a.nent, a.ntpl);
-    const dim3 grid(g.nblk), blk(kTPB);
 #define AMG_G3(BK, NM, P, K) hipLaunchKernelGGL((tpl_gs_acc_kernel<BK, NM, P, K>), grid, blk, lds, s, g)
 #define AMG_G2(BK, NM, P)                          \
     do {                                           \

@@ -302,7 +302,8 @@ void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_
         norm_finish(A, sink);
     } else if (opt.smoother == AMG_SMOOTH_HYBRID_GS) {
         if (x_zero) launch_zero(ctx->stream, A.n_rows, x);
-        par_hybrid_gs(A, x, b, tmp, opt.gs_block, post);
+        if (x_zero && !post) par_hybrid_gs_from_zero(A, x, b, tmp, opt.gs_block);
+        else par_hybrid_gs(A, x, b, tmp, opt.gs_block, post);
     } else if (x_zero) {
         launch_jacobi_zero(ctx->stream, A.n_rows, b, A.dinv.p, tmp, opt.jacobi_omega);
     } else {
@@ -747,9 +748,11 @@ int64_t Solver::stored_bytes_per_cycle(size_t l) const {
     const DevMatrix* Rup = l > 0 ? levels[l - 1].R.get() : nullptr;
     const bool j0 = !gs && Rup && (int)l != rep_level && fuse_restrict_j0() && Rup->format != AMG_FORMAT_CSR &&
                     !Rup->tpl_on();
+    // a split GS sweep from zero is its chain walk alone (par_hybrid_gs_from_zero)
+    const int64_t sweep0 = gs && A.gs_split ? sweep - A.gs_old[0]->mode_bytes(KM_RESID) - 8 * n : sweep;
     for (int k = 0; k < opt.pre_sweeps; ++k, ++sweeps) {
         if (zero && !gs) b += (j0 ? 16 : 24) * n;  // omega * dinv * b
-        else b += sweep + (zero ? 8 * n : 0);      // (zero fill of x first)
+        else b += (zero ? sweep0 : sweep) + (zero ? 8 * n : 0);  // (zero fill of x first)
         zero = false;
     }
     if (zero) b += 8 * n;

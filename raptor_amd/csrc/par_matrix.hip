@@ -1605,6 +1605,19 @@ void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, in
     launch_hybrid_gs(s, A, x, b, y, backward, partial, A.n_gs_slabs_int, A.n_gs_slabs, false);
 }
 
+// Forward sweep from x = 0 (the first pre-smoothing sweep of a coarse level): every old-value
+// term is a_ij * 0.0 = +-0.0, so acc = b bit for bit (b - (+-0.0) == b, and where b is -0.0
+// the new x_i = 0.0 + acc * d is +0.0 either way) -- the split sweep's old-value pass and its
+// halo exchange are skipped and the chain walk starts from acc = b.  Other forms sweep as usual.
+void par_hybrid_gs_from_zero(DevMatrix& A, const double* x0, const double* b, double* y, int64_t block) {
+    A.ensure_gs_blocks(block);
+    if (A.gs_split) {
+        launch_gs_chain(A.ctx->stream, A, x0, b, y, false);
+        return;
+    }
+    par_hybrid_gs(A, x0, b, y, block, false);
+}
+
 void norm_finish(DevMatrix& A, const NormSink& ns, int nparts) {
     Context* c = A.ctx;
     const int nb = nparts >= 0 ? nparts : A.norm_parts();

@@ -458,3 +458,4 @@ def test_full_size_sa27_split_sweeps_and_cycle_256(ctx, oracle, capfd, say):
     say("oracle cycle")
     xo = H.cycle(np.zeros(n), b)
     assert np.array_equal(to_host(ctx, dx), xo)
+

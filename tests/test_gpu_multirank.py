@@ -130,7 +130,7 @@ def test_multirank_boxes_vcycle_bit_exact(oracle, nranks, kind, dims, boxes, coa
     _vcycle_vs_oracle(oracle, nranks, kind, dims, coarsen, smoother, 0, boxes)
 
 
-@pytest.mark.parametrize("nranks,kind,dims", [(2, "27pt", (10, 11, 16)), (4, "27pt", (12, 12, 16)),
+@pytest.mark.parametrize("nranks,kind,dims", [(2, "27pt", (24, 24, 32)), (4, "27pt", (24, 24, 32)),
                                               (8, "7pt", (48, 48, 96))])
 def test_multirank_split_gs_bit_exact(oracle, nranks, kind, dims):
     """Split hybrid-GS sweeps on N ranks: every
