@@ -64,6 +64,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--quick", action="store_true",
+                    help="the timed solve only (no mode comparison, time to tolerance, kernel "
+                         "table or CPU baseline): rehearsals and attribution runs")
     ap.add_argument("--config", choices=["7pt", "sa27", "g3sub"], default="7pt",
                     help="7pt: the metric workload (default); sa27: BASELINE.json configs[2], "
                          "27-pt anisotropic Q1 diffusion, smoothed aggregation + hybrid GS; "
@@ -178,6 +181,141 @@ def main():
     y = ctx.empty(n)
     ctx.synchronize()
 
+    # ---- measurement legs first: level kernels, roofline legs, copy / read ceilings ----------
+    # (timed live with HIP events on the context stream).  They run before the warmup and the
+    # timed solve so the timed cycles see a GPU in its steady working state: the first solve
+    # after an idle setup ran ~3 % slower than the same solve repeated later in the process
+    # (profiles/r5/r5d_bench_7pt.json: 1.254 vs 1.212-1.213 ms per cycle).
+    if not args.quick:
+        # ---- level kernels, timed live with HIP events on the context stream -----------------
+        n = A.local_rows
+
+        e0, e1 = ra.Event(ctx), ra.Event(ctx)
+
+        def timed(fn, reps, flush=None):
+            """avg ms per launch of fn() over reps (HIP events recorded on the context stream, the
+            stream the kernels run on).  flush: run before each launch and excluded (cache-cold
+            timing: a 1 GiB copy evicts the 256 MiB Infinity Cache and the L2s)."""
+            for _ in range(3):
+                fn()
+            if flush is None:
+                e0.record()
+                for _ in range(reps):
+                    fn()
+                e1.record()
+                return e0.elapsed_ms(e1) / reps
+            tot = 0.0
+            for _ in range(reps):
+                flush()
+                e0.record()
+                fn()
+                e1.record()
+                tot += e0.elapsed_ms(e1)
+            return tot / reps
+
+        fl_src = ra.vector_uniform(ctx, 1 << 27, 0, 9)
+        fl_dst = ctx.empty(1 << 27)
+
+        def flush():
+            ra.vector_copy(ctx, fl_src, fl_dst)
+
+        barrier()
+        # roofline (SURVEY.md 8(d)): level-0 ParCSRMatrix::mult on the plain CSR format -- int32
+        # row_ptr, int32 col, fp64 val, exactly the arrays 8(d) prices -- scored on 8(d)'s
+        # algorithmic bytes 12 nnz + 4 (n+1) + 8 (cols + halo) + 8 n
+        A.set_format("csr")
+        csr_bytes = int(A.info["csr_bytes"])
+        csr_warm_ms = timed(lambda: A.mult(x, y), args.spmv_reps)
+        csr_cold_ms = timed(lambda: A.mult(x, y), 10, flush)
+        A.set_format("auto")
+        # an operator whose plain-CSR stream fits the 256 MiB Infinity Cache (the G3 substitute)
+        # is scored on cache-cold launches (a 1 GiB copy between them), so the HBM roofline is
+        # not credited with MALL hits; larger ones on back-to-back launches
+        mall = csr_bytes < MALL_BYTES
+        csr_ms = csr_cold_ms if mall else csr_warm_ms
+        # the product's default format on the same operator (row templates / CSR-VI blocks),
+        # scored on the bytes that format streams
+        spmv_bytes = int(A.info["spmv_bytes"])
+        spmv_ms = timed(lambda: A.mult(x, y), args.spmv_reps)
+        spmv_cold_ms = timed(lambda: A.mult(x, y), 10, flush)
+        # measured STREAM-copy ceiling (SURVEY.md 8d): the 16-byte nontemporal copy kernel, 1 GiB
+        copy_ms = timed(flush, 10)
+        copy_gbs = 2 * fl_src.numel() * 8 / (copy_ms * 1e-3) / 1e9
+        # read ceiling: the same 16-byte loads without the stores (the level kernels read 5-20x
+        # what they write, so this, not the copy rate, is the rate they can approach)
+        rd_part = ctx.empty(4 * ((fl_src.numel() // 2 + 1023) // 1024))
+        read_ms = timed(lambda: ra.vector_read(ctx, fl_src, rd_part), 10)
+        read_gbs = fl_src.numel() * 8 / (read_ms * 1e-3) / 1e9
+        barrier()
+
+        # per-level V-cycle kernels (rank 0's share; eager launches of the ops the cycle runs, on
+        # levels whose kernels outlast the launch overhead).  The in-graph durations are in the
+        # rocprofv3 summary committed under profiles/.
+        table = []
+        gs = sa27 or g3
+        for l in range(nlev - 1):
+            if infos[l]["n_global"] // world < 100000:  # same decision on every rank
+                break
+            Al = A if l == 0 else ml.level_matrix(l, "A")
+            nl = Al.local_rows
+            P, R = ml.level_matrix(l, "P"), ml.level_matrix(l, "R")
+            nc = P.local_cols
+            xl, bl, tl = ra.vector_uniform(ctx, nl, 0, 5), ra.vector_uniform(ctx, nl, 0, 6), ctx.empty(nl)
+            xc, bc = ra.vector_uniform(ctx, nc, 0, 7), ctx.empty(R.local_rows)
+            ai, pi, ri = Al.info, P.info, R.info
+            # per_cycle: launches of the op in one V-cycle (Jacobi: pre + post on level 0; on
+            # coarser levels the pre-sweep from x = 0 is fused into the restriction above)
+            if gs:
+                Al.hybrid_gs(xl, bl, tl, 64)  # builds the sliced-ELL copy if the cycle has not
+                ai = Al._info()
+                ops = [("pre GS (forward)", lambda: Al.hybrid_gs(xl, bl, tl, 64), ai["gs_bytes"], 1),
+                       ("residual", lambda: Al.residual(xl, bl, tl), ai["residual_bytes"], 1),
+                       ("restrict R r", lambda: R.mult(tl, bc), ri["spmv_bytes"], 1),
+                       ("interp x += P e", lambda: P.mult_add(xc, xl), pi["mult_add_bytes"], 1),
+                       ("post GS (backward)", lambda: Al.hybrid_gs(xl, bl, tl, 64, backward=True), ai["gs_bytes"], 1)]
+            else:
+                ops = [("Jacobi", lambda: Al.jacobi(xl, bl, tl), ai["jacobi_bytes"], 2 if l == 0 else 1),
+                       ("residual", lambda: Al.residual(xl, bl, tl), ai["residual_bytes"], 1),
+                       ("restrict R r", lambda: R.mult(tl, bc), ri["spmv_bytes"], 1),
+                       ("interp x += P e", lambda: P.mult_add(xc, xl), pi["mult_add_bytes"], 1)]
+            for name, fn, nbytes, per in ops:
+                ms = timed(fn, 10)
+                M = P if name.startswith("interp") else R if name.startswith("restrict") else Al
+                table.append({"level": l, "op": name, "kernel": kernel_name(M.info, name),
+                              "us": round(ms * 1e3, 1), "per_cycle": per,
+                              "stored_bytes": int(nbytes),
+                              "mall_resident": int(nbytes) < MALL_BYTES,
+                              "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                              "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+            del xl, bl, tl, xc, bc
+        # PMC-measured traffic of the same operations (scripts/gpu_pmc_vcycle.sh, 7-pt 256^3):
+        # 2 x FETCH_SIZE + WRITE_SIZE per launch beside the stored-format byte model; a ratio
+        # above 1.1 is wasted traffic (re-reads), below 1 means cache hits served part of the model
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_vcycle_kernels.json" if args.config == "7pt"
+                                else f"pmc_vcycle_kernels_{args.config}.json")
+        if args.config in ("7pt", "sa27") and grid == (256, 256, 256) and world == 1 and os.path.exists(pmc_path):
+            try:
+                pm = {(o["level"], o["op"]): o for o in json.load(open(pmc_path))["ops"]}
+                for row in table:
+                    o = pm.get((row["level"], row["op"]))
+                    if o and o["stored_bytes"] == row["stored_bytes"]:
+                        row["traffic"] = int(o["traffic_bytes"])
+                        row["traffic_over_stored"] = o["traffic_over_stored"]
+                        row["traffic_GBps"] = round(o["traffic_bytes"] / (row["us"] * 1e-6) / 1e9, 1)
+                    else:
+                        # no counters for this library's format of the operation (the file was
+                        # taken on another build): said so, not silently dropped
+                        row["traffic"] = None
+                        row["traffic_stale"] = o is not None
+            except (OSError, KeyError, ValueError):
+                pass
+        # the dominant kernel: the cycle's longest single launch (the roofline below); the
+        # largest share of a cycle (us x launches per cycle) is named beside it
+        dominant = max(table, key=lambda t: t["us"]) if table else None
+        top_share = max(table, key=lambda t: t["us"] * t["per_cycle"]) if table else None
+        del fl_src, fl_dst, rd_part
+        barrier()
+
     # warmup (captures the cycle and norm hipGraphs, on every rank)
     if args.warmup > 0:
         ml.solve(x, b, max_iter=args.warmup)
@@ -219,19 +357,38 @@ def main():
         t = time.perf_counter() - t
         return (comm.allreduce_max(t) if world > 1 else t), res
 
+    if args.quick:
+        if rank == 0:
+            print(json.dumps({"metric": "V-cycle iters/sec (quick rehearsal line)", "value": round(value, 3),
+                              "n_gpus": world, "steps": args.steps, "ms_per_step": round(dt * 1e3 / args.steps, 4),
+                              "grid": list(grid), "hipgraph_all_ranks": graph_all, "partition": part_label,
+                              "setup_s": round(setup_s, 2)}), file=out_stream, flush=True)
+        del ml, A
+        if world > 1:
+            comm.close()
+        return
+
     # the other cycle mode, same solve, same process (at N > 1 graph replay
     # is the default on an expectation about xGMI; both are measured so a SCALE run decides)
     modes = None
     if not args.no_graph:
-        ml.set_graph(False)
-        ml.solve(x, b, max_iter=max(1, args.warmup))
-        t_eager, _ = timed_solve(lambda: ml.solve(x, b, max_iter=args.steps))
+        # alternating repetitions (the first timed region above is not reused: order effects)
+        reps = {"graph": [], "eager": []}
+        for _ in range(3):
+            for mode in ("eager", "graph"):
+                ml.set_graph(mode == "graph" and graph_used)
+                ml.solve(x, b, max_iter=max(1, args.warmup))  # (re)capture outside the timing
+                t_m, _ = timed_solve(lambda: ml.solve(x, b, max_iter=args.steps))
+                reps[mode].append(round(t_m * 1e3 / args.steps, 4))
         ml.set_graph(graph_used)
-        ml.solve(x, b, max_iter=max(1, args.warmup))  # recapture
-        modes = {"graph_ms_per_step": round(dt * 1e3 / args.steps, 4) if graph_used else None,
-                 "eager_ms_per_step": round(t_eager * 1e3 / args.steps, 4),
-                 "timed_mode": "graph" if graph_used else "eager"}
-        log(rank, f"eager cycles: {t_eager * 1e3 / args.steps:.4f} ms/step")
+        ml.solve(x, b, max_iter=max(1, args.warmup))
+        med = {k: sorted(v)[1] for k, v in reps.items()}
+        modes = {"graph_ms_per_step": med["graph"] if graph_used else None,
+                 "eager_ms_per_step": med["eager"],
+                 "repetitions_ms_per_step": reps,
+                 "timed_mode": "graph" if graph_used else "eager",
+                 "what": "median of 3 alternating timed solves of --steps cycles per mode, same process"}
+        log(rank, f"cycle modes (median of 3): graph {med['graph']} eager {med['eager']} ms/step")
 
     # time to solution: stationary solve and AMG-PCG to 1e-8 relative
     # residual, setup excluded (reported beside it).  tol > 0 reads the norm back every
@@ -272,134 +429,6 @@ def main():
     cyc_bytes = allsum(ml.bytes_per_cycle())
     cyc_stored = allsum(sum(i["stored_bytes_per_cycle_local"] for i in infos))
 
-    # ---- level kernels, timed live with HIP events on the context stream -----------------
-    n = A.local_rows
-
-    e0, e1 = ra.Event(ctx), ra.Event(ctx)
-
-    def timed(fn, reps, flush=None):
-        """avg ms per launch of fn() over reps (HIP events recorded on the context stream, the
-        stream the kernels run on).  flush: run before each launch and excluded (cache-cold
-        timing: a 1 GiB copy evicts the 256 MiB Infinity Cache and the L2s)."""
-        for _ in range(3):
-            fn()
-        if flush is None:
-            e0.record()
-            for _ in range(reps):
-                fn()
-            e1.record()
-            return e0.elapsed_ms(e1) / reps
-        tot = 0.0
-        for _ in range(reps):
-            flush()
-            e0.record()
-            fn()
-            e1.record()
-            tot += e0.elapsed_ms(e1)
-        return tot / reps
-
-    fl_src = ra.vector_uniform(ctx, 1 << 27, 0, 9)
-    fl_dst = ctx.empty(1 << 27)
-
-    def flush():
-        ra.vector_copy(ctx, fl_src, fl_dst)
-
-    barrier()
-    # roofline (SURVEY.md 8(d)): level-0 ParCSRMatrix::mult on the plain CSR format -- int32
-    # row_ptr, int32 col, fp64 val, exactly the arrays 8(d) prices -- scored on 8(d)'s
-    # algorithmic bytes 12 nnz + 4 (n+1) + 8 (cols + halo) + 8 n
-    A.set_format("csr")
-    csr_bytes = int(A.info["csr_bytes"])
-    csr_warm_ms = timed(lambda: A.mult(x, y), args.spmv_reps)
-    csr_cold_ms = timed(lambda: A.mult(x, y), 10, flush)
-    A.set_format("auto")
-    # an operator whose plain-CSR stream fits the 256 MiB Infinity Cache (the G3 substitute)
-    # is scored on cache-cold launches (a 1 GiB copy between them), so the HBM roofline is
-    # not credited with MALL hits; larger ones on back-to-back launches
-    mall = csr_bytes < MALL_BYTES
-    csr_ms = csr_cold_ms if mall else csr_warm_ms
-    # the product's default format on the same operator (row templates / CSR-VI blocks),
-    # scored on the bytes that format streams
-    spmv_bytes = int(A.info["spmv_bytes"])
-    spmv_ms = timed(lambda: A.mult(x, y), args.spmv_reps)
-    spmv_cold_ms = timed(lambda: A.mult(x, y), 10, flush)
-    # measured STREAM-copy ceiling (SURVEY.md 8d): the 16-byte nontemporal copy kernel, 1 GiB
-    copy_ms = timed(flush, 10)
-    copy_gbs = 2 * fl_src.numel() * 8 / (copy_ms * 1e-3) / 1e9
-    # read ceiling: the same 16-byte loads without the stores (the level kernels read 5-20x
-    # what they write, so this, not the copy rate, is the rate they can approach)
-    rd_part = ctx.empty(4 * ((fl_src.numel() // 2 + 1023) // 1024))
-    read_ms = timed(lambda: ra.vector_read(ctx, fl_src, rd_part), 10)
-    read_gbs = fl_src.numel() * 8 / (read_ms * 1e-3) / 1e9
-    barrier()
-
-    # per-level V-cycle kernels (rank 0's share; eager launches of the ops the cycle runs, on
-    # levels whose kernels outlast the launch overhead).  The in-graph durations are in the
-    # rocprofv3 summary committed under profiles/.
-    table = []
-    gs = sa27 or g3
-    for l in range(nlev - 1):
-        if infos[l]["n_global"] // world < 100000:  # same decision on every rank
-            break
-        Al = A if l == 0 else ml.level_matrix(l, "A")
-        nl = Al.local_rows
-        P, R = ml.level_matrix(l, "P"), ml.level_matrix(l, "R")
-        nc = P.local_cols
-        xl, bl, tl = ra.vector_uniform(ctx, nl, 0, 5), ra.vector_uniform(ctx, nl, 0, 6), ctx.empty(nl)
-        xc, bc = ra.vector_uniform(ctx, nc, 0, 7), ctx.empty(R.local_rows)
-        ai, pi, ri = Al.info, P.info, R.info
-        # per_cycle: launches of the op in one V-cycle (Jacobi: pre + post on level 0; on
-        # coarser levels the pre-sweep from x = 0 is fused into the restriction above)
-        if gs:
-            Al.hybrid_gs(xl, bl, tl, 64)  # builds the sliced-ELL copy if the cycle has not
-            ai = Al._info()
-            ops = [("pre GS (forward)", lambda: Al.hybrid_gs(xl, bl, tl, 64), ai["gs_bytes"], 1),
-                   ("residual", lambda: Al.residual(xl, bl, tl), ai["residual_bytes"], 1),
-                   ("restrict R r", lambda: R.mult(tl, bc), ri["spmv_bytes"], 1),
-                   ("interp x += P e", lambda: P.mult_add(xc, xl), pi["mult_add_bytes"], 1),
-                   ("post GS (backward)", lambda: Al.hybrid_gs(xl, bl, tl, 64, backward=True), ai["gs_bytes"], 1)]
-        else:
-            ops = [("Jacobi", lambda: Al.jacobi(xl, bl, tl), ai["jacobi_bytes"], 2 if l == 0 else 1),
-                   ("residual", lambda: Al.residual(xl, bl, tl), ai["residual_bytes"], 1),
-                   ("restrict R r", lambda: R.mult(tl, bc), ri["spmv_bytes"], 1),
-                   ("interp x += P e", lambda: P.mult_add(xc, xl), pi["mult_add_bytes"], 1)]
-        for name, fn, nbytes, per in ops:
-            ms = timed(fn, 10)
-            M = P if name.startswith("interp") else R if name.startswith("restrict") else Al
-            table.append({"level": l, "op": name, "kernel": kernel_name(M.info, name),
-                          "us": round(ms * 1e3, 1), "per_cycle": per,
-                          "stored_bytes": int(nbytes),
-                          "mall_resident": int(nbytes) < MALL_BYTES,
-                          "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
-                          "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
-        del xl, bl, tl, xc, bc
-    # PMC-measured traffic of the same operations (scripts/gpu_pmc_vcycle.sh, 7-pt 256^3):
-    # 2 x FETCH_SIZE + WRITE_SIZE per launch beside the stored-format byte model; a ratio
-    # above 1.1 is wasted traffic (re-reads), below 1 means cache hits served part of the model
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_vcycle_kernels.json" if args.config == "7pt"
-                            else f"pmc_vcycle_kernels_{args.config}.json")
-    if args.config in ("7pt", "sa27") and grid == (256, 256, 256) and world == 1 and os.path.exists(pmc_path):
-        try:
-            pm = {(o["level"], o["op"]): o for o in json.load(open(pmc_path))["ops"]}
-            for row in table:
-                o = pm.get((row["level"], row["op"]))
-                if o and o["stored_bytes"] == row["stored_bytes"]:
-                    row["traffic"] = int(o["traffic_bytes"])
-                    row["traffic_over_stored"] = o["traffic_over_stored"]
-                    row["traffic_GBps"] = round(o["traffic_bytes"] / (row["us"] * 1e-6) / 1e9, 1)
-                else:
-                    # no counters for this library's format of the operation (the file was
-                    # taken on another build): said so, not silently dropped
-                    row["traffic"] = None
-                    row["traffic_stale"] = o is not None
-        except (OSError, KeyError, ValueError):
-            pass
-    # the dominant kernel: the cycle's longest single launch (the roofline below); the
-    # largest share of a cycle (us x launches per cycle) is named beside it
-    dominant = max(table, key=lambda t: t["us"]) if table else None
-    top_share = max(table, key=lambda t: t["us"] * t["per_cycle"]) if table else None
-    del fl_src, fl_dst, rd_part
-    barrier()
 
     traffic = None
     traffic_src = None

@@ -245,6 +245,13 @@ struct DevMatrix {
     // row is a coalesced stream.  gs_dinv = 1 / (a_ii + sum of |a_ij| outside the chunk).
     DevBuf<int4> gs_slabs;  // {first row, rows, offset / 64, width}
     DevBuf<int> gs_col;
+    // the slabs on the host and their cell count (the sliced ELL is built by ensure_gs_ell, on
+    // first use for split operators)
+    std::vector<int4> gs_slabs_host;
+    int64_t gs_cells = 0;
+    bool gs_ell_built = false;
+    void ensure_gs_ell();
+    void ensure_gs_pass(int d);  // gs_old[d], built on first use (ensure_gs_blocks: d = 1)
     DevBuf<double> gs_val, gs_dinv;
     int n_gs_slabs = 0;
     int n_gs_slabs_int = 0;  // slabs [0, n_gs_slabs_int) touch no halo column (run before the wait)

@@ -214,6 +214,11 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         max_blocks = std::max(max_blocks, (size_t)Al.norm_parts_max());
         if (opt.smoother == AMG_SMOOTH_HYBRID_GS) {
             Al.ensure_gs_blocks(opt.gs_block);
+            // level 0's norm-carrying forward sweep runs the one-kernel form, inside captured
+            // cycles: its sliced ELL is built now even where the other sweeps run split
+            if (l == 0) Al.ensure_gs_ell();
+            // a forward split sweep on x != 0: level 0's (tol > 0 solves), a second pre-sweep
+            if (Al.gs_split && (l == 0 || opt.pre_sweeps >= 2)) Al.ensure_gs_pass(0);
             tm.lap("L" + std::to_string(l) + " GS sliced-ELL build");
             max_blocks = std::max(max_blocks, (size_t)Al.gs_norm_parts());
         }
@@ -749,7 +754,7 @@ int64_t Solver::stored_bytes_per_cycle(size_t l) const {
     const bool j0 = !gs && Rup && (int)l != rep_level && fuse_restrict_j0() && Rup->format != AMG_FORMAT_CSR &&
                     !Rup->tpl_on();
     // a split GS sweep from zero is its chain walk alone (par_hybrid_gs_from_zero)
-    const int64_t sweep0 = gs && A.gs_split ? sweep - A.gs_old[0]->mode_bytes(KM_RESID) - 8 * n : sweep;
+    const int64_t sweep0 = gs && A.gs_split ? sweep - A.gs_old[1]->mode_bytes(KM_RESID) - 8 * n : sweep;
     for (int k = 0; k < opt.pre_sweeps; ++k, ++sweeps) {
         if (zero && !gs) b += (j0 ? 16 : 24) * n;  // omega * dinv * b
         else b += (zero ? sweep0 : sweep) + (zero ? 8 * n : 0);  // (zero fill of x first)

@@ -1080,14 +1080,143 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         loopback_register(*ctx, seq, send_buf.p, plan.send_procs, plan.send_ptr);
 }
 
+// The one-kernel sweep's sliced ELL (hybrid_gs_kernel): every entry of the ELL slabs, with a
+// value dictionary when the local operator takes <= 256 distinct values.  Built with the GS
+// blocks unless the operator runs split sweeps (4.2c), whose passes never read it; then on
+// first use (a norm-carrying forward sweep: Solver::setup builds it for level 0).  r5: sa27's
+// level-1 / level-2 GS builds spent ~1.9 s of an 8.1 s setup mostly here.
+// The split sweep's old-value pass for direction d (0 forward, 1 backward): this operator
+// without the sweep's in-chunk new-value couplings, as a CSR-block matrix of its own (4.2c).
+// Collective on N ranks (its halo plan); never inside a graph capture (Solver::setup builds
+// what the cycle needs).
+void DevMatrix::ensure_gs_pass(int d) {
+    if (gs_old[d]) return;
+    AMG_CHECK(gs_split && gs_block > 0, "hybrid GS: no split sweep for this operator");
+    AMG_CHECK(!ctx->capturing, "hybrid GS: split pass requested inside a graph capture");
+    const int64_t B = gs_block, clo = first_col, chi = first_col + n_cols_local;
+    auto is_new = [&](int64_t i, int64_t gc) {
+        if (gc < clo || gc >= chi) return false;
+        const int64_t j = gc - clo, g = first_row + i;
+        const int64_t cs = std::max<int64_t>(0, (g / B) * B - first_row);
+        const int64_t ce = std::min<int64_t>(n_rows, (g / B + 1) * B - first_row);
+        return d == 0 ? (j >= cs && j < i) : (j > i && j < ce);
+    };
+    HostCSR h;
+    h.n_global_rows = host.n_global_rows;
+    h.n_global_cols = host.n_global_cols;
+    h.row_starts = host.row_starts;
+    h.col_starts = host.col_starts;
+    h.rp.assign((size_t)n_rows + 1, 0);
+    for (int64_t i = 0; i < n_rows; ++i) {
+        int64_t c = 0;
+        for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) c += !is_new(i, host.col[k]);
+        h.rp[i + 1] = h.rp[i] + c;
+    }
+    h.col.resize((size_t)h.rp[n_rows]);
+    h.val.resize((size_t)h.rp[n_rows]);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n_rows; ++i) {
+        int64_t o = h.rp[i];
+        for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k)
+            if (!is_new(i, host.col[k])) {
+                h.col[o] = host.col[k];
+                h.val[o] = host.val[k];
+                ++o;
+            }
+    }
+    // CSR blocks only: no row templates (and so no windows, masks or march tables) are built
+    // for the pass's operator, and its format is set before the build -- no
+    // format_generation bump, no captured graph goes stale
+    gs_old[d] = std::make_unique<DevMatrix>();
+    gs_old[d]->blocks_only = true;
+    gs_old[d]->format = AMG_FORMAT_BLOCKS;
+    gs_old[d]->build(ctx, std::move(h), replicated);
+}
+
+void DevMatrix::ensure_gs_ell() {
+    if (gs_ell_built) return;
+    AMG_CHECK(!ctx->capturing, "hybrid GS: sliced ELL requested inside a graph capture");
+    const int64_t clo = first_col, chi = first_col + n_cols_local;
+    auto local_col = [&](int64_t g) -> int {
+        return g >= clo && g < chi ? (int)(g - clo) : (int)(n_cols_local + plan.find(g));
+    };
+    const std::vector<int4>& slabs = gs_slabs_host;
+    const int64_t cells = gs_cells;
+    std::vector<int> sc((size_t)(cells + 4) * 64, -1);
+    std::vector<double> sv(sc.size(), 0.0);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (size_t q = 0; q < slabs.size(); ++q) {
+        const int4 sl = slabs[q];
+        for (int l = 0; l < sl.y; ++l) {
+            const int64_t i = sl.x + l;
+            for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) {
+                const size_t at = ((size_t)sl.z + (size_t)(k - host.rp[i])) * 64 + l;
+                sc[at] = local_col(host.col[k]);
+                sv[at] = host.val[k];
+            }
+        }
+    }
+    // value dictionary: <= 256 distinct values (bit patterns) in the local operator; each
+    // thread scans a chunk into a small set and gives up past 256
+    std::vector<uint64_t> dict;
+    {
+        const int64_t nz = (int64_t)host.val.size();
+        std::atomic<bool> over{false};
+#pragma omp parallel
+        {
+            std::vector<uint64_t> mine;
+#pragma omp for schedule(static) nowait
+            for (int64_t k = 0; k < nz; ++k) {
+                if (over.load(std::memory_order_relaxed)) continue;
+                uint64_t bits;
+                std::memcpy(&bits, &host.val[k], sizeof(bits));
+                if (std::find(mine.begin(), mine.end(), bits) == mine.end()) {
+                    mine.push_back(bits);
+                    if (mine.size() > 256) over.store(true, std::memory_order_relaxed);
+                }
+            }
+#pragma omp critical
+            if (!over.load()) dict.insert(dict.end(), mine.begin(), mine.end());
+        }
+        std::sort(dict.begin(), dict.end());
+        dict.erase(std::unique(dict.begin(), dict.end()), dict.end());
+        if (over.load() || dict.size() > 256) dict.clear();
+    }
+    gs_ndict = (int)dict.size();
+    if (gs_ndict > 0) {
+        std::vector<uint8_t> vid(sc.size(), 0);
+#pragma omp parallel for schedule(dynamic, 64)
+        for (size_t q = 0; q < slabs.size(); ++q) {
+            const int4 sl = slabs[q];
+            for (int l = 0; l < sl.y; ++l)
+                for (int k = 0; k < sl.w; ++k) {
+                    const size_t at = ((size_t)sl.z + (size_t)k) * 64 + (size_t)l;
+                    if (sc[at] < 0) continue;
+                    uint64_t bits;
+                    std::memcpy(&bits, &sv[at], sizeof(bits));
+                    vid[((size_t)sl.z + (size_t)(k & ~3)) * 64 + 4 * (size_t)l + (size_t)(k & 3)] =
+                        (uint8_t)(std::lower_bound(dict.begin(), dict.end(), bits) - dict.begin());
+                }
+        }
+        std::vector<double> tab(dict.size());
+        std::memcpy(tab.data(), dict.data(), sizeof(double) * dict.size());
+        gs_vid.upload(vid.data(), vid.size());
+        gs_vtab.upload(tab.data(), tab.size());
+        gs_val.reset();
+    } else {
+        gs_vid.reset();
+        gs_vtab.reset();
+        gs_val.upload(sv.data(), sv.size());
+    }
+    gs_col.upload(sc.data(), sc.size());
+    gs_ell_built = true;
+}
+
 void DevMatrix::ensure_gs_blocks(int64_t B) {
     AMG_CHECK(square, "hybrid GS needs a square matrix");
     AMG_CHECK(B >= 1 && B <= 64, "hybrid GS block must be in [1, 64]");
     if (gs_block == B) return;
     const int64_t clo = first_col, chi = first_col + n_cols_local;
-    auto local_col = [&](int64_t g) -> int {
-        return g >= clo && g < chi ? (int)(g - clo) : (int)(n_cols_local + plan.find(g));
-    };
     // l1 diagonal of every row: d_i = a_ii + sum of |a_ij| outside the row's chunk (global
     // multiples of B clipped to the rank), summed in CSR order like the oracle
     std::vector<double> di(n_rows);
@@ -1266,74 +1395,15 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
         cells += (sl.w + 3) & ~3;  // slabs start at multiples of 4 cells (dictionary dwords)
     }
     AMG_CHECK((cells + 4) * 64 < INT_MAX, "hybrid GS: sliced-ELL too large for int32 offsets");
-    std::vector<int> sc((size_t)(cells + 4) * 64, -1);
-    std::vector<double> sv(sc.size(), 0.0);
-#pragma omp parallel for schedule(dynamic, 64)
-    for (size_t q = 0; q < slabs.size(); ++q) {
-        const int4 sl = slabs[q];
-        for (int l = 0; l < sl.y; ++l) {
-            const int64_t i = sl.x + l;
-            for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) {
-                const size_t at = ((size_t)sl.z + (size_t)(k - host.rp[i])) * 64 + l;
-                sc[at] = local_col(host.col[k]);
-                sv[at] = host.val[k];
-            }
-        }
-    }
-    // value dictionary: <= 256 distinct values (bit patterns) in the local operator; each
-    // thread scans a chunk into a small set and gives up past 256
-    std::vector<uint64_t> dict;
-    {
-        const int64_t nz = (int64_t)host.val.size();
-        std::atomic<bool> over{false};
-#pragma omp parallel
-        {
-            std::vector<uint64_t> mine;
-#pragma omp for schedule(static) nowait
-            for (int64_t k = 0; k < nz; ++k) {
-                if (over.load(std::memory_order_relaxed)) continue;
-                uint64_t bits;
-                std::memcpy(&bits, &host.val[k], sizeof(bits));
-                if (std::find(mine.begin(), mine.end(), bits) == mine.end()) {
-                    mine.push_back(bits);
-                    if (mine.size() > 256) over.store(true, std::memory_order_relaxed);
-                }
-            }
-#pragma omp critical
-            if (!over.load()) dict.insert(dict.end(), mine.begin(), mine.end());
-        }
-        std::sort(dict.begin(), dict.end());
-        dict.erase(std::unique(dict.begin(), dict.end()), dict.end());
-        if (over.load() || dict.size() > 256) dict.clear();
-    }
-    gs_ndict = (int)dict.size();
-    if (gs_ndict > 0) {
-        std::vector<uint8_t> vid(sc.size(), 0);
-#pragma omp parallel for schedule(dynamic, 64)
-        for (size_t q = 0; q < slabs.size(); ++q) {
-            const int4 sl = slabs[q];
-            for (int l = 0; l < sl.y; ++l)
-                for (int k = 0; k < sl.w; ++k) {
-                    const size_t at = ((size_t)sl.z + (size_t)k) * 64 + (size_t)l;
-                    if (sc[at] < 0) continue;
-                    uint64_t bits;
-                    std::memcpy(&bits, &sv[at], sizeof(bits));
-                    vid[((size_t)sl.z + (size_t)(k & ~3)) * 64 + 4 * (size_t)l + (size_t)(k & 3)] =
-                        (uint8_t)(std::lower_bound(dict.begin(), dict.end(), bits) - dict.begin());
-                }
-        }
-        std::vector<double> tab(dict.size());
-        std::memcpy(tab.data(), dict.data(), sizeof(double) * dict.size());
-        gs_vid.upload(vid.data(), vid.size());
-        gs_vtab.upload(tab.data(), tab.size());
-        gs_val.reset();
-    } else {
-        gs_vid.reset();
-        gs_vtab.reset();
-        gs_val.upload(sv.data(), sv.size());
-    }
     gs_slabs.upload(slabs.data(), slabs.size());
-    gs_col.upload(sc.data(), sc.size());
+    gs_slabs_host = slabs;
+    gs_cells = cells;
+    gs_ell_built = false;
+    gs_col.reset();
+    gs_val.reset();
+    gs_vid.reset();
+    gs_vtab.reset();
+    gs_ndict = 0;
     gs_dinv.upload(di.data(), di.size());
     n_gs_slabs = (int)slabs.size();
     gs_block = B;
@@ -1389,37 +1459,12 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
                 return d == 0 ? (j >= cs && j < i) : (j > i && j < ce);
             };
             int64_t ccells = 0;
+            gs_split = true;  // (ensure_gs_pass checks it)
             for (int d = 0; d < 2; ++d) {
-                HostCSR h;
-                h.n_global_rows = host.n_global_rows;
-                h.n_global_cols = host.n_global_cols;
-                h.row_starts = host.row_starts;
-                h.col_starts = host.col_starts;
-                h.rp.assign((size_t)n_rows + 1, 0);
-                for (int64_t i = 0; i < n_rows; ++i) {
-                    int64_t c = 0;
-                    for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) c += !is_new(d, i, host.col[k]);
-                    h.rp[i + 1] = h.rp[i] + c;
-                }
-                h.col.resize((size_t)h.rp[n_rows]);
-                h.val.resize((size_t)h.rp[n_rows]);
-#pragma omp parallel for schedule(static)
-                for (int64_t i = 0; i < n_rows; ++i) {
-                    int64_t o = h.rp[i];
-                    for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k)
-                        if (!is_new(d, i, host.col[k])) {
-                            h.col[o] = host.col[k];
-                            h.val[o] = host.val[k];
-                            ++o;
-                        }
-                }
-                // CSR blocks only: no row templates (and so no windows, masks or march
-                // tables) are built for the pass's operator, and its format is set before
-                // the build -- no format_generation bump, no captured graph goes stale
-                gs_old[d] = std::make_unique<DevMatrix>();
-                gs_old[d]->blocks_only = true;
-                gs_old[d]->format = AMG_FORMAT_BLOCKS;
-                gs_old[d]->build(ctx, std::move(h), replicated);
+                // the backward pass (post-smoothing) is built now; the forward one on first
+                // use (ensure_gs_pass): a coarse level's forward sweep starts from x = 0 and
+                // skips it (par_hybrid_gs_from_zero)
+                if (d == 1) ensure_gs_pass(1);
                 // the chain ELL: same slabs, only the new-value couplings (CSR order)
                 std::vector<int4> cs = slabs;
                 int64_t cc = 0;
@@ -1473,10 +1518,11 @@ void DevMatrix::ensure_gs_blocks(int64_t B) {
             gs_split = true;
             // bytes per (forward) sweep: the pass (its stored format + b + acc out), then the
             // chain ELL cells + slab headers + acc, x, dinv in and y out
-            gs_bytes = gs_old[0]->mode_bytes(KM_RESID) + 8 * n_rows + 12 * 64 * ccells +
+            gs_bytes = gs_old[1]->mode_bytes(KM_RESID) + 8 * n_rows + 12 * 64 * ccells +
                        16 * (int64_t)slabs.size() + 32 * n_rows;
         }
     }
+    if (!gs_split) ensure_gs_ell();
 }
 
 int64_t DevMatrix::format_generation = 0;
@@ -1593,10 +1639,12 @@ void par_hybrid_gs(DevMatrix& A, const double* x, const double* b, double* y, in
                    bool backward, double* partial) {
     A.ensure_gs_blocks(block);
     if (A.gs_split && !partial) {  // split sweep: the pass exchanges its halo
+        A.ensure_gs_pass(backward ? 1 : 0);
         par_apply(*A.gs_old[backward ? 1 : 0], KM_GSACC, x, b, A.gs_acc.p, 0.0, nullptr);
         launch_gs_chain(A.ctx->stream, A, x, A.gs_acc.p, y, backward);
         return;
     }
+    A.ensure_gs_ell();
     const bool comm = A.halo_begin(x);
     hipStream_t s = A.ctx->stream;
     // template blocks and interior slabs never read the halo: they run while it is in flight

@@ -29,6 +29,14 @@ if [ -n "$AB_CONFIG" ]; then  # in-process A/B of run-time knobs (scripts/ab_env
   timeout -k 10 400 python scripts/ab_env.py $AB_CONFIG "${SETS[@]}" > gpurun_out/${R}_ab_$AB_CONFIG.json 2> gpurun_out/${R}_ab_$AB_CONFIG.err || { tail gpurun_out/${R}_ab_$AB_CONFIG.err; exit 1; }
   cat gpurun_out/${R}_ab_$AB_CONFIG.err | tail -4
 fi
+for spec in $PLAN; do  # per-level RCCL plan of a cycle (scripts/rccl_plan_table.py): cfg:N
+  IFS=':' read -r cfg nr <<< "$spec"
+  timeout -k 10 400 python scripts/rccl_plan_table.py $cfg $nr > gpurun_out/${R}_plan_${cfg}_$nr.json 2> gpurun_out/${R}_plan_${cfg}_$nr.md || { tail gpurun_out/${R}_plan_${cfg}_$nr.md; exit 1; }
+  tail -2 gpurun_out/${R}_plan_${cfg}_$nr.md
+done
+if [ -n "$N2" ]; then
+  CONFIGS="$N2" R=$R bash scripts/r5/gpu_n2_rehearsal.sh || exit 1
+fi
 if [ -n "$PHASES" ]; then  # x-tile block kernel phase trace (diagnostic build)
   RAPTOR_AMD_LIB=raptor_amd/libraptor_amd_phase.so timeout -k 10 300 python scripts/csr_phase_trace.py > gpurun_out/${R}_phases.json 2> gpurun_out/${R}_phases.err || { tail gpurun_out/${R}_phases.err; exit 1; }
   tail -c 300 gpurun_out/${R}_phases.json; echo
