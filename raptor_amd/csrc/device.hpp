@@ -157,6 +157,37 @@ struct Context {
     void allgather(const double* send, double* recv, size_t count);
 };
 
+// Device image of one host CSR of the hierarchy during setup (one rank):
+// the same rows, global column ids, in whichever index widths the consumers need -- int32 for
+// the strength / aggregation / interpolation kernels, the transpose and the left operand of a
+// SpGEMM, int64 for the SpGEMM's right operand (B image) and its row pointers.  A width that
+// is missing is derived on the device from the other (ensure_*).
+struct DevCsr {
+    int64_t n = 0, nnz = 0, ncols = 0;
+    DevBuf<int> rp32, col32;
+    DevBuf<long long> rp64, col64;
+    DevBuf<double> val;
+    void ensure_rp32(hipStream_t s);
+    void ensure_rp64(hipStream_t s);
+    void ensure_col32(hipStream_t s);
+    void ensure_col64(hipStream_t s);
+};
+
+// The device images of one hierarchy setup (Solver::setup, one rank).  A matrix the setup
+// computes on the device (P, R = P^T, A_{l+1} = R (A P)) is registered as it is downloaded,
+// so its consumers in the same level (transpose, Galerkin product, the next level's strength
+// and aggregation) read it where it already is instead of uploading the host copy back; the
+// level-0 operator is uploaded once.  Keyed by the host image's row-pointer buffer, which
+// moves with the HostCSR and is never reallocated; the level loop keeps only the next
+// level's operator when a level is done (keep_only), so no entry outlives its host matrix.
+struct SetupImages {
+    std::vector<std::pair<const int64_t*, std::unique_ptr<DevCsr>>> e;
+    DevCsr* find(const HostCSR& M);
+    DevCsr& get(const HostCSR& M);  // find, or upload rp64 / col64 / val
+    void put(const HostCSR& M, std::unique_ptr<DevCsr> d);  // n / nnz / ncols taken from M
+    void keep_only(const HostCSR& M);
+};
+
 // Galerkin SpGEMM on the device (spgemm.hip); result downloaded as a host image
 HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, const HostCSR& B);
 // formats.hip: the per-nonzero device formats of DevMatrix::build_view built on the GPU
@@ -172,13 +203,28 @@ void build_formats_device(DevMatrix& M, const std::vector<int>& hrp, const hvec<
                           const std::vector<int2>& blocks, const std::vector<int>& tile_ptr,
                           const std::vector<int>& tile_lines, const std::vector<int64_t>& koff, FormatHeaderInfo& out);
 // R (A P), A P kept on the device between the products where it can be (one rank)
+// imgs (one rank, may be null): A, P and R read from their device images, R (A P) registered
 HostCSR galerkin_device(Context& ctx, const HostComm& comm, const HostCSR& R, const HostCSR& A,
-                        const HostCSR& P);
-// device setup of one level (setup_device.hip, single rank): strength, PMIS or MIS(2)
-// aggregation, classical or smoothed-aggregation P; false where it does not apply
+                        const HostCSR& P, SetupImages* imgs = nullptr);
+// device setup of one level (setup_device.hip): strength, PMIS or MIS(2) aggregation,
+// classical or smoothed-aggregation P; false where it does not apply.  imgs: A's device image
+// (any rank count), P registered (one rank)
 bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, const amg_options& opt,
-                        int level, HostCSR& P, std::vector<int32_t>& split);
-bool transpose_device(Context& ctx, const HostComm& comm, const HostCSR& P, HostCSR& R);
+                        int level, HostCSR& P, std::vector<int32_t>& split, SetupImages* imgs = nullptr);
+bool transpose_device(Context& ctx, const HostComm& comm, const HostCSR& P, HostCSR& R,
+                      SetupImages* imgs = nullptr);
+// C = A B with A on the device (DevCsr: rp64, col32, val; one rank, global = local columns)
+// and B's image on the device; C left on the device (rp also on the host)
+struct DevCSR64 {
+    std::vector<long long> rp;  // host copy
+    DevBuf<long long> d_rp, d_col;
+    DevBuf<double> d_val;
+    int64_t nnz() const { return rp.empty() ? 0 : rp.back(); }
+};
+// brp_host: B's row pointers on the host; Bh: B's host image for the rare host-computed rows
+// (null: downloaded from the device image if such a row occurs)
+void spgemm_images(Context& ctx, PhaseTimer& tm, const HostCSR& Ah, DevCsr& A, const long long* brp_host,
+                   const HostCSR* Bh, DevCsr& B, int64_t bncol, DevCSR64& C);
 
 void loopback_join(Context& c, int rank, int nranks, const std::string& world);
 void loopback_leave(Context& c);

@@ -109,21 +109,27 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     LevelSetupFn level_fn = nullptr;
     TransposeFn transpose_fn = nullptr;
     RapFn rap_fn = nullptr;
+    // one rank: the level operators, P and R stay on the device between the setup steps that
+    // read them (SetupImages); only the next level's operator is carried over
+    SetupImages images;
+    SetupImages* im = opt.setup_device && comm.nranks == 1 ? &images : nullptr;
     if (opt.setup_device) {
         galerkin = [this, &comm](const HostCSR& X, const HostCSR& Y) {
             return spgemm_device(*ctx, comm, X, Y);
         };
-        rap_fn = [this, &comm](const HostCSR& R, const HostCSR& Am, const HostCSR& P) {
-            return galerkin_device(*ctx, comm, R, Am, P);
+        rap_fn = [this, &comm, im](const HostCSR& R, const HostCSR& Am, const HostCSR& P) {
+            HostCSR Ac = galerkin_device(*ctx, comm, R, Am, P, im);
+            if (im) im->keep_only(Ac);
+            return Ac;
         };
-        // setup_device == 1: the whole level setup on the GPU where it applies (one rank);
+        // setup_device == 1: the whole level setup on the GPU where it applies;
         // 2: Galerkin products only (the round-1 split, for A/B and tests)
         if (opt.setup_device == 1) {
-            level_fn = [this, &comm](int l, const HostCSR& A, HostCSR& P, std::vector<int32_t>& split) {
-                return level_setup_device(*ctx, comm, A, opt, l, P, split);
+            level_fn = [this, &comm, im](int l, const HostCSR& A, HostCSR& P, std::vector<int32_t>& split) {
+                return level_setup_device(*ctx, comm, A, opt, l, P, split, im);
             };
-            transpose_fn = [this, &comm](const HostCSR& P, HostCSR& R) {
-                return transpose_device(*ctx, comm, P, R);
+            transpose_fn = [this, &comm, im](const HostCSR& P, HostCSR& R) {
+                return transpose_device(*ctx, comm, P, R, im);
             };
         }
     }
@@ -152,6 +158,7 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
             };
         }
         build_hierarchy(comm, A.host, opt, H, galerkin, level_fn, transpose_fn, done, rap_fn);
+        images.e.clear();
         tm.lap("hierarchy (host + SpGEMM)");
         if (worker) worker->finish();
         if (overlap) tm.lap("format builds still running after the hierarchy");

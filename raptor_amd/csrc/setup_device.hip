@@ -641,6 +641,148 @@ int64_t exclusive_scan(hipStream_t s, const int* in, int* out, int n, DevBuf<cha
     return total;
 }
 
+int64_t exclusive_scan64(hipStream_t s, const long long* in, long long* out, int n, DevBuf<char>& tmp) {
+    size_t bytes = 0;
+    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, n + 1, s));
+    if (tmp.n < bytes) tmp.alloc(bytes);
+    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, bytes, in, out, n + 1, s));
+    long long total = 0;
+    HIP_CHECK(hipMemcpyAsync(&total, out + n, sizeof(long long), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    return total;
+}
+
+// index-width conversions of the setup's device images (grid-stride: up to 2^31 entries)
+__global__ void narrow_kernel(long long n, const long long* __restrict__ in, int* __restrict__ out) {
+    for (long long t = (long long)blockIdx.x * kT + threadIdx.x; t < n; t += (long long)gridDim.x * kT)
+        out[t] = (int)in[t];
+}
+
+__global__ void widen_kernel(long long n, const int* __restrict__ in, long long* __restrict__ out) {
+    for (long long t = (long long)blockIdx.x * kT + threadIdx.x; t < n; t += (long long)gridDim.x * kT)
+        out[t] = in[t];
+}
+
+inline unsigned grid_cap(long long n) { return std::min<unsigned>(grid1(n), 1u << 16); }
+
+// P = T - (omega / a_ii) A T on the device, rows merged by column exactly as the host merge in
+// level_setup_device (sa_prolongator): T has one entry per row (aggregate agg_i, value t_i)
+template <bool FILL>
+__global__ void sa_smooth_kernel(int n, const long long* __restrict__ atrp, const long long* __restrict__ atcol,
+                                 const double* __restrict__ atval, const long long* __restrict__ agg,
+                                 const double* __restrict__ tval, const double* __restrict__ d, double omega,
+                                 long long* __restrict__ cnt, const long long* __restrict__ prp,
+                                 long long* __restrict__ pcol, double* __restrict__ pval) {
+    const int i = blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
+    const long long b = atrp[i], e = atrp[i + 1], jt = agg[i];
+    if (!FILL) {
+        long long lo = b, hi = e;
+        while (lo < hi) {
+            const long long m = (lo + hi) >> 1;
+            if (atcol[m] < jt) lo = m + 1;
+            else hi = m;
+        }
+        cnt[i] = (e - b) + ((lo < e && atcol[lo] == jt) ? 0 : 1);
+        return;
+    }
+    const double c = omega * (1.0 / d[i]);
+    long long ka = b, q = prp[i];
+    bool tleft = true;
+    while (ka < e || tleft) {
+        const long long ja = ka < e ? atcol[ka] : LLONG_MAX, jj = tleft ? jt : LLONG_MAX;
+        const long long j = ja < jj ? ja : jj;
+        double tvv = 0.0, av = 0.0;
+        if (jj == j) {
+            tvv = tval[i];
+            tleft = false;
+        }
+        if (ja == j) av = atval[ka++];
+        pcol[q] = j;
+        pval[q++] = tvv - c * av;
+    }
+}
+
+}  // namespace
+
+void DevCsr::ensure_rp32(hipStream_t s) {
+    if (rp32.p) return;
+    AMG_CHECK(rp64.p && nnz < INT_MAX, "device image: row pointers exceed int32 indexing");
+    rp32.alloc((size_t)n + 1);
+    hipLaunchKernelGGL(narrow_kernel, dim3(grid_cap(n + 1)), dim3(kT), 0, s, (long long)n + 1, rp64.p, rp32.p);
+    HIP_CHECK(hipGetLastError());
+}
+
+void DevCsr::ensure_rp64(hipStream_t s) {
+    if (rp64.p) return;
+    AMG_CHECK(rp32.p, "device image without row pointers");
+    rp64.alloc((size_t)n + 1);
+    hipLaunchKernelGGL(widen_kernel, dim3(grid_cap(n + 1)), dim3(kT), 0, s, (long long)n + 1, rp32.p, rp64.p);
+    HIP_CHECK(hipGetLastError());
+}
+
+void DevCsr::ensure_col32(hipStream_t s) {
+    if (col32.p) return;
+    AMG_CHECK(col64.p && ncols < INT_MAX, "device image: columns exceed int32 indexing");
+    col32.alloc((size_t)std::max<int64_t>(nnz, 1));
+    if (nnz)
+        hipLaunchKernelGGL(narrow_kernel, dim3(grid_cap(nnz)), dim3(kT), 0, s, (long long)nnz, col64.p, col32.p);
+    HIP_CHECK(hipGetLastError());
+}
+
+void DevCsr::ensure_col64(hipStream_t s) {
+    if (col64.p) return;
+    AMG_CHECK(col32.p, "device image without columns");
+    col64.alloc((size_t)std::max<int64_t>(nnz, 1));
+    if (nnz)
+        hipLaunchKernelGGL(widen_kernel, dim3(grid_cap(nnz)), dim3(kT), 0, s, (long long)nnz, col32.p, col64.p);
+    HIP_CHECK(hipGetLastError());
+}
+
+DevCsr* SetupImages::find(const HostCSR& M) {
+    for (auto& kv : e)
+        if (kv.first == M.rp.data() && kv.second->n == M.nrows() && kv.second->nnz == M.nnz()) return kv.second.get();
+    return nullptr;
+}
+
+DevCsr& SetupImages::get(const HostCSR& M) {
+    if (DevCsr* d = find(M)) return *d;
+    static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
+    std::unique_ptr<DevCsr> d(new DevCsr());
+    d->rp64.upload(reinterpret_cast<const long long*>(M.rp.data()), M.rp.size());
+    if (M.nnz()) {
+        d->col64.upload(reinterpret_cast<const long long*>(M.col.data()), (size_t)M.nnz());
+        d->val.upload(M.val.data(), (size_t)M.nnz());
+    } else {
+        d->col64.alloc(1);
+        d->val.alloc(1);
+    }
+    DevCsr& r = *d;
+    put(M, std::move(d));
+    return r;
+}
+
+void SetupImages::put(const HostCSR& M, std::unique_ptr<DevCsr> d) {
+    d->n = M.nrows();
+    d->nnz = M.nnz();
+    d->ncols = M.n_global_cols;
+    for (auto& kv : e)
+        if (kv.first == M.rp.data()) {
+            kv.second = std::move(d);
+            return;
+        }
+    e.emplace_back(M.rp.data(), std::move(d));
+}
+
+void SetupImages::keep_only(const HostCSR& M) {
+    std::vector<std::pair<const int64_t*, std::unique_ptr<DevCsr>>> keep;
+    for (auto& kv : e)
+        if (kv.first == M.rp.data()) keep.push_back(std::move(kv));
+    e.swap(keep);
+}
+
+namespace {
+
 // the level operator on the device: this rank's rows, global column ids (int32)
 struct DevLevel {
     DevBuf<int> rp, col;
@@ -740,18 +882,27 @@ struct DevHalo {
 // hierarchy is bit-identical to the host path's at every rank count.  Returns false for
 // Ruge-Stueben (the serial first pass stays on the host).
 bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, const amg_options& opt,
-                        int level, HostCSR& P, std::vector<int32_t>& split) {
+                        int level, HostCSR& P, std::vector<int32_t>& split, SetupImages* imgs) {
     if (opt.coarsen == AMG_COARSEN_RS) return false;
     hipStream_t s = ctx.stream;
     const int n = (int)A.nrows();
     if (comm.nranks == 1 && n == 0) return false;
     PhaseTimer tm(comm);
+    // A on the device: the setup's image (one rank: uploaded once, or left there by the
+    // previous level's Galerkin product), else uploaded for this level
     DevLevel D;
-    upload_level(comm, A, D);
-    const int lo = D.lo;
+    DevCsr* DA = imgs ? &imgs->get(A) : nullptr;
+    if (DA) {
+        AMG_CHECK(n < INT_MAX && A.n_global_cols < INT_MAX, "device setup: level exceeds int32 indexing");
+        DA->ensure_rp32(s);
+        DA->ensure_col32(s);
+    } else {
+        upload_level(comm, A, D);
+    }
+    const int lo = (int)A.row_starts[comm.rank];
     DevBuf<char> tmp;
     DevS S;
-    const DCsr Av = D.view();
+    const DCsr Av = DA ? DCsr{DA->rp32.p, DA->col32.p, DA->val.p, n, lo} : D.view();
     if (opt.coarsen == AMG_COARSEN_PMIS) {
         const double theta = opt.strong_threshold;
         build_strength(
@@ -946,6 +1097,13 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
         P.col.assign(hcol.begin(), hcol.end());
         P.val.resize((size_t)pnnz);
         copy_to_host(P.val.data(), pval.p, sizeof(double) * pnnz, s);
+        if (imgs && !dist) {  // P where it was computed, for the transpose and the Galerkin product
+            std::unique_ptr<DevCsr> d(new DevCsr());
+            d->rp32 = std::move(prp);
+            d->col32 = std::move(pcol);
+            d->val = std::move(pval);
+            imgs->put(P, std::move(d));
+        }
         tm.lap("  device interpolation");
         return true;
     }
@@ -1104,6 +1262,52 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
         T.val[i] = 1.0 / std::sqrt((double)sz);
     }
     tm.lap("  device tentative prolongator");
+    if (DA && !dist) {
+        // one rank: A T, the smoothing and P stay on the device; P is downloaded once and kept
+        // as the setup's image of P (transpose, Galerkin product)
+        static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
+        DevCsr dT;
+        dT.n = n;
+        dT.nnz = n;
+        dT.ncols = na;
+        dT.rp64.upload(reinterpret_cast<const long long*>(T.rp.data()), T.rp.size());
+        dT.col64.upload(reinterpret_cast<const long long*>(T.col.data()), (size_t)std::max(n, 1));
+        dT.val.upload(T.val.data(), (size_t)std::max(n, 1));
+        DevCSR64 AT;
+        spgemm_images(ctx, tm, A, *DA, reinterpret_cast<const long long*>(T.rp.data()), &T, dT, na, AT);
+        tm.lap("  device A*T");
+        DevBuf<long long> pcnt, prp, pcol;
+        DevBuf<double> pval;
+        pcnt.alloc((size_t)n + 1);
+        HIP_CHECK(hipMemsetAsync(pcnt.p, 0, sizeof(long long) * pcnt.n, s));
+        hipLaunchKernelGGL(sa_smooth_kernel<false>, dim3(grid1(n)), dim3(kT), 0, s, n, AT.d_rp.p, AT.d_col.p,
+                           AT.d_val.p, dT.col64.p, dT.val.p, d.p, omega, pcnt.p, nullptr, nullptr, nullptr);
+        prp.alloc((size_t)n + 1);
+        const int64_t pnnz = exclusive_scan64(s, pcnt.p, prp.p, n, tmp);
+        pcol.alloc((size_t)std::max<int64_t>(pnnz, 1));
+        pval.alloc((size_t)std::max<int64_t>(pnnz, 1));
+        hipLaunchKernelGGL(sa_smooth_kernel<true>, dim3(grid1(n)), dim3(kT), 0, s, n, AT.d_rp.p, AT.d_col.p,
+                           AT.d_val.p, dT.col64.p, dT.val.p, d.p, omega, nullptr, prp.p, pcol.p, pval.p);
+        HIP_CHECK(hipGetLastError());
+        P = HostCSR();
+        P.n_global_rows = A.n_global_rows;
+        P.n_global_cols = na;
+        P.row_starts = A.row_starts;
+        P.col_starts = astarts;
+        P.rp.resize((size_t)n + 1);
+        P.col.resize((size_t)pnnz);
+        P.val.resize((size_t)pnnz);
+        copy_to_host(P.rp.data(), prp.p, sizeof(long long) * (n + 1), s);
+        copy_to_host(P.col.data(), pcol.p, sizeof(long long) * pnnz, nullptr);
+        copy_to_host(P.val.data(), pval.p, sizeof(double) * pnnz, nullptr);
+        std::unique_ptr<DevCsr> dp(new DevCsr());
+        dp->rp64 = std::move(prp);
+        dp->col64 = std::move(pcol);
+        dp->val = std::move(pval);
+        imgs->put(P, std::move(dp));
+        tm.lap("  device smoothed prolongator");
+        return true;
+    }
     HostCSR AT = spgemm_device(ctx, comm, A, T);
     tm.lap("  device A*T");
     // P = T - (omega / a_ii) A T, rows merged by column (same as sa_prolongator)
@@ -1144,45 +1348,55 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
 
 // R = P^T on the device for one rank: stable radix sort of the entries by column keeps each
 // R row in ascending fine-row order, like transpose().
-bool transpose_device(Context& ctx, const HostComm& comm, const HostCSR& P, HostCSR& R) {
+bool transpose_device(Context& ctx, const HostComm& comm, const HostCSR& P, HostCSR& R, SetupImages* imgs) {
     if (comm.nranks != 1) return false;
     hipStream_t s = ctx.stream;
     const int64_t n = P.nrows(), nnz = P.nnz(), nc = P.n_global_cols;
     if (nnz == 0 || n >= INT_MAX || nnz >= INT_MAX || nc >= INT_MAX) return false;
-    std::vector<int> rp(n + 1), col(nnz);
-#pragma omp parallel for schedule(static)
-    for (int64_t i = 0; i <= n; ++i) rp[i] = (int)P.rp[i];
-#pragma omp parallel for schedule(static)
-    for (int64_t k = 0; k < nnz; ++k) col[k] = (int)P.col[k];
-    DevBuf<int> drp, dcol, keys_out, idx_in, idx_out, rowof, cnt, rrp;
-    DevBuf<double> dval;
+    DevBuf<int> drp_up, dcol_up, keys_out, idx_in, idx_out, rowof, cnt, rrp;
+    DevBuf<double> dval_up;
     DevBuf<long long> rcol;
     DevBuf<double> rval;
     DevBuf<char> tmp;
-    drp.upload(rp.data(), rp.size());
-    dcol.upload(col.data(), col.size());
-    dval.upload(P.val.data(), P.val.size());
+    const int *drp_p, *dcol_p;
+    const double* dval_p;
+    if (imgs) {  // P's image (left on the device by the level setup)
+        DevCsr& dP = imgs->get(P);
+        dP.ensure_rp32(s);
+        dP.ensure_col32(s);
+        drp_p = dP.rp32.p, dcol_p = dP.col32.p, dval_p = dP.val.p;
+    } else {
+        std::vector<int> rp(n + 1), col(nnz);
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i <= n; ++i) rp[i] = (int)P.rp[i];
+#pragma omp parallel for schedule(static)
+        for (int64_t k = 0; k < nnz; ++k) col[k] = (int)P.col[k];
+        drp_up.upload(rp.data(), rp.size());
+        dcol_up.upload(col.data(), col.size());
+        dval_up.upload(P.val.data(), P.val.size());
+        drp_p = drp_up.p, dcol_p = dcol_up.p, dval_p = dval_up.p;
+    }
     keys_out.alloc(nnz);
     idx_in.alloc(nnz);
     idx_out.alloc(nnz);
     rowof.alloc(nnz);
     hipLaunchKernelGGL(iota_kernel, dim3(grid1(nnz)), dim3(kT), 0, s, (int)nnz, idx_in.p);
-    hipLaunchKernelGGL(expand_rows_kernel, dim3(grid1(n)), dim3(kT), 0, s, drp.p, (int)n, rowof.p);
+    hipLaunchKernelGGL(expand_rows_kernel, dim3(grid1(n)), dim3(kT), 0, s, drp_p, (int)n, rowof.p);
     int bits = 1;
     while (bits < 31 && (1ll << bits) < nc) ++bits;
     size_t bytes = 0;
-    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, dcol.p, keys_out.p, idx_in.p, idx_out.p,
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, dcol_p, keys_out.p, idx_in.p, idx_out.p,
                                                  (int)nnz, 0, bits, s));
     tmp.alloc(bytes);
-    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp.p, bytes, dcol.p, keys_out.p, idx_in.p, idx_out.p,
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp.p, bytes, dcol_p, keys_out.p, idx_in.p, idx_out.p,
                                                  (int)nnz, 0, bits, s));
     rcol.alloc(nnz);
     rval.alloc(nnz);
     hipLaunchKernelGGL(gather_transpose_kernel, dim3(grid1(nnz)), dim3(kT), 0, s, (int)nnz, idx_out.p,
-                       rowof.p, dval.p, rcol.p, rval.p);
+                       rowof.p, dval_p, rcol.p, rval.p);
     cnt.alloc((size_t)nc + 1);
     HIP_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int) * cnt.n, s));
-    hipLaunchKernelGGL(count_cols_kernel, dim3(grid1(nnz)), dim3(kT), 0, s, (int)nnz, dcol.p, cnt.p);
+    hipLaunchKernelGGL(count_cols_kernel, dim3(grid1(nnz)), dim3(kT), 0, s, (int)nnz, dcol_p, cnt.p);
     rrp.alloc((size_t)nc + 1);
     exclusive_scan(s, cnt.p, rrp.p, (int)nc, tmp);
     HIP_CHECK(hipGetLastError());
@@ -1198,6 +1412,13 @@ bool transpose_device(Context& ctx, const HostComm& comm, const HostCSR& P, Host
     static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
     copy_to_host(R.col.data(), rcol.p, sizeof(long long) * nnz, s);
     copy_to_host(R.val.data(), rval.p, sizeof(double) * nnz, nullptr);
+    if (imgs) {  // R where it was computed, for the Galerkin product
+        std::unique_ptr<DevCsr> d(new DevCsr());
+        d->rp32 = std::move(rrp);
+        d->col64 = std::move(rcol);
+        d->val = std::move(rval);
+        imgs->put(R, std::move(d));
+    }
     return true;
 }
 

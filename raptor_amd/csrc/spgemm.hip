@@ -186,13 +186,6 @@ __global__ void unpack_recs_kernel(long long n, const PackRec* __restrict__ in, 
 // acol: A's columns as rows of that image; ub: per row the bound sum_k |B_k|.  C stays on
 // the device (crp also on the host); rows that overflow the largest LDS table are computed on
 // the host (bhost() supplies B's host arrays for them) and uploaded into place.
-struct DevCSR64 {
-    std::vector<long long> rp;  // host copy
-    DevBuf<long long> d_rp, d_col;
-    DevBuf<double> d_val;
-    int64_t nnz() const { return rp.empty() ? 0 : rp.back(); }
-};
-
 struct BImage {
     const long long* brp_host;  // nb + 1 entries
     const long long *d_brp, *d_bcol;
@@ -202,8 +195,33 @@ struct BImage {
     std::function<void(std::function<int64_t(long long)>&, std::function<double(long long)>&)> bhost;
 };
 
-void spgemm_core(Context& ctx, PhaseTimer& tm, const HostCSR& A, const std::vector<int>& acol,
-                 const std::vector<int64_t>& ub, const BImage& B, DevCSR64& C) {
+// the left operand: device arrays (row pointers, B-image row of each entry, values) and the
+// host arrays the fallback rows read (acol_host null: the host columns, one rank)
+struct AOperand {
+    const HostCSR* host;
+    const int* acol_host;
+    const long long* d_rp;
+    const int* d_col;
+    const double* d_val;
+};
+
+struct AUpload {
+    DevBuf<long long> rp;
+    DevBuf<int> col;
+    DevBuf<double> val;
+};
+
+AOperand upload_a(PhaseTimer& tm, const HostCSR& A, const std::vector<int>& acol, AUpload& u) {
+    u.rp.upload(reinterpret_cast<const long long*>(A.rp.data()), A.rp.size());
+    u.col.upload(acol.data(), acol.size());
+    u.val.upload(A.val.data(), A.val.size());
+    tm.lap("    spgemm: uploads of A");
+    return AOperand{&A, acol.data(), u.rp.p, u.col.p, u.val.p};
+}
+
+void spgemm_core(Context& ctx, PhaseTimer& tm, const AOperand& Aop, const std::vector<int64_t>& ub,
+                 const BImage& B, DevCSR64& C) {
+    const HostCSR& A = *Aop.host;
     const int64_t n = A.nrows();
     // bins by table size (load factor <= 1/2 on the upper bound); rows beyond the largest
     // table try it anyway (their distinct columns are usually far fewer than the bound) and
@@ -232,17 +250,12 @@ void spgemm_core(Context& ctx, PhaseTimer& tm, const HostCSR& A, const std::vect
     }
     tm.lap("    spgemm: bins");
     hipStream_t s = ctx.stream;
-    DevBuf<long long> d_arp, d_counts;
-    DevBuf<int> d_acol, d_rows[4];
-    DevBuf<double> d_aval;
-    d_arp.upload(reinterpret_cast<const long long*>(A.rp.data()), A.rp.size());
-    d_acol.upload(acol.data(), acol.size());
-    d_aval.upload(A.val.data(), A.val.size());
+    DevBuf<long long> d_counts;
+    DevBuf<int> d_rows[4];
     d_counts.alloc((size_t)std::max<int64_t>(n, 1));
     HIP_CHECK(hipMemsetAsync(d_counts.p, 0, sizeof(long long) * d_counts.n, s));
-    tm.lap("    spgemm: uploads of A");
 #define AMG_BIN(T, NUM, b)                                                                          \
-    launch_bin<T, NUM>(s, bins[b], d_rows[b], d_arp.p, d_acol.p, d_aval.p, B.d_brp, B.d_bcol,      \
+    launch_bin<T, NUM>(s, bins[b], d_rows[b], Aop.d_rp, Aop.d_col, Aop.d_val, B.d_brp, B.d_bcol,   \
                        B.d_bval, d_counts.p, C.d_rp.p, C.d_col.p, C.d_val.p)
     AMG_BIN(256, false, 0);
     AMG_BIN(1024, false, 1);
@@ -282,7 +295,7 @@ void spgemm_core(Context& ctx, PhaseTimer& tm, const HostCSR& A, const std::vect
                 const int64_t i = host_rows[t];
                 touched.clear();
                 for (int64_t ka = A.rp[i]; ka < A.rp[i + 1]; ++ka) {
-                    const int64_t r = acol[ka];
+                    const int64_t r = Aop.acol_host ? (int64_t)Aop.acol_host[ka] : A.col[ka];
                     for (long long q = B.brp_host[r]; q < B.brp_host[r + 1]; ++q) {
                         const int64_t j = bcol_at(q);
                         if (!seen[j]) seen[j] = 1, touched.push_back(j);
@@ -345,7 +358,59 @@ HostCSR download(Context& ctx, PhaseTimer& tm, const HostCSR& A, const HostCSR& 
     return out;
 }
 
+// B-image row bounds sum_k |B_{acol_k}| per row of A, on the device (the SpGEMM bins)
+__global__ void row_bound_kernel(long long n, const long long* __restrict__ arp, const int* __restrict__ acol,
+                                 const long long* __restrict__ brp, long long* __restrict__ ub) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    long long u = 0;
+    for (long long k = arp[i]; k < arp[i + 1]; ++k) {
+        const int c = acol[k];
+        u += brp[c + 1] - brp[c];
+    }
+    ub[i] = u;
+}
+
 }  // namespace
+
+void spgemm_images(Context& ctx, PhaseTimer& tm, const HostCSR& Ah, DevCsr& A, const long long* brp_host,
+                   const HostCSR* Bh, DevCsr& B, int64_t bncol, DevCSR64& C) {
+    hipStream_t s = ctx.stream;
+    A.ensure_rp64(s);
+    A.ensure_col32(s);
+    B.ensure_rp64(s);
+    B.ensure_col64(s);
+    const int64_t n = A.n;
+    AMG_CHECK(n == Ah.nrows() && A.nnz == Ah.nnz(), "spgemm: device image does not match its host matrix");
+    std::vector<int64_t> ub((size_t)n);
+    if (n) {
+        DevBuf<long long> d_ub;
+        d_ub.alloc((size_t)n);
+        hipLaunchKernelGGL(row_bound_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (long long)n,
+                           A.rp64.p, A.col32.p, B.rp64.p, d_ub.p);
+        HIP_CHECK(hipGetLastError());
+        copy_to_host(ub.data(), d_ub.p, sizeof(long long) * n, s);
+    }
+    tm.lap("    spgemm: row bounds (device)");
+    // host copies of the B image only if some row overflows the LDS tables
+    std::vector<long long> hc;
+    std::vector<double> hv;
+    BImage img{brp_host, B.rp64.p, B.col64.p, B.val.p, bncol,
+               [&](std::function<int64_t(long long)>& ca, std::function<double(long long)>& va) {
+                   if (Bh) {
+                       ca = [Bh](long long q) -> int64_t { return Bh->col[q]; };
+                       va = [Bh](long long q) -> double { return Bh->val[q]; };
+                       return;
+                   }
+                   hc.resize((size_t)B.nnz);
+                   hv.resize((size_t)B.nnz);
+                   copy_to_host(hc.data(), B.col64.p, sizeof(long long) * B.nnz, s);
+                   copy_to_host(hv.data(), B.val.p, sizeof(double) * B.nnz, nullptr);
+                   ca = [&](long long q) -> int64_t { return hc[q]; };
+                   va = [&](long long q) -> double { return hv[q]; };
+               }};
+    spgemm_core(ctx, tm, AOperand{&Ah, nullptr, A.rp64.p, A.col32.p, A.val.p}, ub, img, C);
+}
 
 HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, const HostCSR& B) {
     AMG_CHECK(A.col_starts == B.row_starts, "spgemm: A columns and B rows partitioned differently");
@@ -393,7 +458,8 @@ HostCSR spgemm_device(Context& ctx, const HostComm& comm, const HostCSR& A, cons
                    va = [&](long long q) -> double { return q < bl ? B.val[q] : G.val[q - bl]; };
                }};
     DevCSR64 C;
-    spgemm_core(ctx, tm, A, acol, ub, img, C);
+    AUpload au;
+    spgemm_core(ctx, tm, upload_a(tm, A, acol, au), ub, img, C);
     return download(ctx, tm, A, B, C);
 }
 
@@ -448,7 +514,8 @@ HostCSR galerkin_device_dist(Context& ctx, const HostComm& comm, const HostCSR& 
                        ca = [&](long long q) -> int64_t { return q < bl ? P.col[q] : G.col[q - bl]; };
                        va = [&](long long q) -> double { return q < bl ? P.val[q] : G.val[q - bl]; };
                    }};
-        spgemm_core(ctx, tm, A, acol, ub, img, AP);
+        AUpload au;
+        spgemm_core(ctx, tm, upload_a(tm, A, acol, au), ub, img, AP);
     }
     // ---- ghost rows of A P for R's off-rank columns, gathered on the device
     const int64_t nl = A.nrows(), lo = A.row_starts[comm.rank], hi = A.row_starts[comm.rank + 1];
@@ -537,7 +604,8 @@ HostCSR galerkin_device_dist(Context& ctx, const HostComm& comm, const HostCSR& 
                    va = [&](long long q) -> double { return hv[q]; };
                }};
     DevCSR64 RAP;
-    spgemm_core(ctx, tm, R, rcol, rub, img, RAP);
+    AUpload au;
+    spgemm_core(ctx, tm, upload_a(tm, R, rcol, au), rub, img, RAP);
     return download(ctx, tm, R, P, RAP);
 }
 
@@ -548,7 +616,7 @@ HostCSR galerkin_device_dist(Context& ctx, const HostComm& comm, const HostCSR& 
 // galerkin_device_dist, the ghost rows of A P gathered on the device).  AMG_GALERKIN_DIST=0:
 // several ranks run the two spgemm_device calls (A P through the host), the round-3 form.
 HostCSR galerkin_device(Context& ctx, const HostComm& comm, const HostCSR& R, const HostCSR& A,
-                        const HostCSR& P) {
+                        const HostCSR& P, SetupImages* imgs) {
     if (comm.nranks > 1) {
         const char* e = std::getenv("AMG_GALERKIN_DIST");
         if (e && *e && std::atoi(e) == 0) return spgemm_device(ctx, comm, R, spgemm_device(ctx, comm, A, P));
@@ -556,65 +624,35 @@ HostCSR galerkin_device(Context& ctx, const HostComm& comm, const HostCSR& R, co
     }
     AMG_CHECK(A.col_starts == P.row_starts && R.col_starts == A.row_starts, "galerkin: partitions differ");
     PhaseTimer tm(comm);
-    const int64_t n = A.nrows();
-    // A P: B image = P's rows, A's (global = local) columns index it directly
-    std::vector<int> acol(A.nnz());
-    std::vector<int64_t> ub(n, 0);
-#pragma omp parallel for schedule(static)
-    for (int64_t i = 0; i < n; ++i) {
-        int64_t u = 0;
-        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
-            acol[k] = (int)A.col[k];
-            u += P.rp[A.col[k] + 1] - P.rp[A.col[k]];
-        }
-        ub[i] = u;
-    }
-    static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
-    DevBuf<long long> d_prp, d_pcol;
-    DevBuf<double> d_pval;
-    d_prp.upload(reinterpret_cast<const long long*>(P.rp.data()), P.rp.size());
-    d_pcol.upload(reinterpret_cast<const long long*>(P.col.data()), P.col.size());
-    d_pval.upload(P.val.data(), P.val.size());
-    tm.lap("    galerkin: A column map, upload of P");
-    BImage pimg{reinterpret_cast<const long long*>(P.rp.data()), d_prp.p, d_pcol.p, d_pval.p, P.n_global_cols,
-                [&](std::function<int64_t(long long)>& ca, std::function<double(long long)>& va) {
-                    ca = [&](long long q) -> int64_t { return P.col[q]; };
-                    va = [&](long long q) -> double { return P.val[q]; };
-                }};
+    // one rank: A's (global = local) columns are P's rows, R's are A P's rows; all three
+    // operands are read from their device images (uploaded here unless the setup holds them)
+    SetupImages local;
+    SetupImages& im = imgs ? *imgs : local;
+    DevCsr& dA = im.get(A);
+    DevCsr& dP = im.get(P);
+    DevCsr& dR = im.get(R);
+    tm.lap("    galerkin: device images of A, P, R");
     DevCSR64 AP;
-    spgemm_core(ctx, tm, A, acol, ub, pimg, AP);
-    d_pcol.reset();
-    d_pval.reset();
-    // R (A P): the image is A P on the device
-    const int64_t nr = R.nrows();
-    std::vector<int> rcol(R.nnz());
-    std::vector<int64_t> rub(nr, 0);
-#pragma omp parallel for schedule(static)
-    for (int64_t i = 0; i < nr; ++i) {
-        int64_t u = 0;
-        for (int64_t k = R.rp[i]; k < R.rp[i + 1]; ++k) {
-            rcol[k] = (int)R.col[k];
-            u += AP.rp[R.col[k] + 1] - AP.rp[R.col[k]];
-        }
-        rub[i] = u;
-    }
-    tm.lap("    galerkin: R column map");
-    // host copies of A P only if some row of R (A P) overflows the LDS tables
-    std::vector<long long> apc;
-    std::vector<double> apv;
-    BImage apimg{AP.rp.data(), AP.d_rp.p, AP.d_col.p, AP.d_val.p, P.n_global_cols,
-                 [&](std::function<int64_t(long long)>& ca, std::function<double(long long)>& va) {
-                     const int64_t m = AP.nnz();
-                     apc.resize(m);
-                     apv.resize(m);
-                     copy_to_host(apc.data(), AP.d_col.p, sizeof(long long) * m, ctx.stream);
-                     copy_to_host(apv.data(), AP.d_val.p, sizeof(double) * m, nullptr);
-                     ca = [&](long long q) -> int64_t { return apc[q]; };
-                     va = [&](long long q) -> double { return apv[q]; };
-                 }};
+    spgemm_images(ctx, tm, A, dA, reinterpret_cast<const long long*>(P.rp.data()), &P, dP, P.n_global_cols, AP);
+    DevCsr dAP;  // A P as the B image of the second product, where it was computed
+    dAP.n = A.nrows();
+    dAP.nnz = AP.nnz();
+    dAP.ncols = P.n_global_cols;
+    dAP.rp64 = std::move(AP.d_rp);
+    dAP.col64 = std::move(AP.d_col);
+    dAP.val = std::move(AP.d_val);
     DevCSR64 RAP;
-    spgemm_core(ctx, tm, R, rcol, rub, apimg, RAP);
-    return download(ctx, tm, R, P, RAP);
+    spgemm_images(ctx, tm, R, dR, AP.rp.data(), nullptr, dAP, P.n_global_cols, RAP);
+    dAP = DevCsr();
+    HostCSR out = download(ctx, tm, R, P, RAP);
+    if (imgs) {  // the next level's operator, for its strength / aggregation and products
+        std::unique_ptr<DevCsr> d(new DevCsr());
+        d->rp64 = std::move(RAP.d_rp);
+        d->col64 = std::move(RAP.d_col);
+        d->val = std::move(RAP.d_val);
+        imgs->put(out, std::move(d));
+    }
+    return out;
 }
 
 }  // namespace amg
