@@ -239,6 +239,10 @@ void loopback_halo(Context& c, int64_t seq, const double* x_send_buf, double* ha
 struct DevMatrix {
     Context* ctx = nullptr;
     HostCSR host;              // host image (global column ids), kept for export / setup
+    // while Solver::setup's worker threads build this operator's formats (and its GS
+    // structures) from the hierarchy's CSR in place, before it is moved into `host`
+    const HostCSR* host_view = nullptr;
+    const HostCSR& host_image() const { return host_view ? *host_view : host; }
     int64_t first_row = 0, n_rows = 0, first_col = 0, n_cols_local = 0, nnz = 0;
     bool square = false;
     // stored for the x-tile kernel (tile ids, 16-bit tile indices, kCAP-stride VI indices):

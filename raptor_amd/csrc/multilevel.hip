@@ -138,29 +138,57 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     const bool overlap = comm.nranks == 1 && setup_overlap();
     const size_t maxl = (size_t)std::max(opt.max_levels, 1) + 1;
     std::vector<std::unique_ptr<DevMatrix>> preA(maxl), preP(maxl), preR(maxl);
+    const bool hgs = opt.smoother == AMG_SMOOTH_HYBRID_GS;
+    // a level operator's hybrid-GS structures: l1 diagonals, slabs, templates,
+    // the split sweep's old-value pass (built by ensure_gs_blocks), level 0's sliced ELL
+    auto gs_build = [this](DevMatrix& Al, int l) {
+        Al.ensure_gs_blocks(opt.gs_block);
+        // level 0's norm-carrying forward sweep runs the one-kernel form, inside captured
+        // cycles: its sliced ELL is built now even where the other sweeps run split
+        if (l == 0) Al.ensure_gs_ell();
+        // a forward split sweep on x != 0: level 0's (tol > 0 solves), a second pre-sweep
+        if (Al.gs_split && (l == 0 || opt.pre_sweeps >= 2)) Al.ensure_gs_pass(0);
+    };
     {
         RoctxRange r("setup: hierarchy (strength, split / aggregates, P, R, Galerkin)");
-        std::unique_ptr<FormatWorker> worker;
+        // r5: a second worker builds each operator's GS structures as soon as its formats
+        // exist (level 0 from the start), beside the format worker (sa27: 0.9 s of GS builds
+        // after the hierarchy before)
+        std::unique_ptr<FormatWorker> worker, gs_worker;
         LevelDoneFn done = nullptr;
         if (overlap) {
             worker.reset(new FormatWorker(ctx->device));
+            if (hgs) {
+                gs_worker.reset(new FormatWorker(ctx->device));
+                DevMatrix* a0 = &A;
+                gs_worker->push([gs_build, a0] { gs_build(*a0, 0); });
+            }
             done = [&](int l) {
-                auto job = [this](std::unique_ptr<DevMatrix>& slot, const HostCSR& M) {
-                    return [this, &slot, &M] {
+                auto job = [this, &gs_worker, &gs_build](std::unique_ptr<DevMatrix>& slot, const HostCSR& M,
+                                                         int gs_level) {
+                    return [this, &slot, &M, &gs_worker, &gs_build, gs_level] {
                         std::unique_ptr<DevMatrix> d(new DevMatrix());
                         d->build_view(ctx, M);
+                        if (gs_level >= 0 && gs_worker) {
+                            DevMatrix* dm = d.get();
+                            dm->host_view = &M;
+                            gs_worker->push([gs_build, dm, gs_level] { gs_build(*dm, gs_level); });
+                        }
                         slot = std::move(d);
                     };
                 };
-                worker->push(job(preP[l], H.levels[l].P));
-                worker->push(job(preR[l], H.levels[l].R));
-                worker->push(job(preA[l + 1], H.levels[l + 1].A));
+                // A_{l+1} first: its GS structures start on the second worker while P_l and
+                // R_l are built
+                worker->push(job(preA[l + 1], H.levels[l + 1].A, l + 1));
+                worker->push(job(preP[l], H.levels[l].P, -1));
+                worker->push(job(preR[l], H.levels[l].R, -1));
             };
         }
         build_hierarchy(comm, A.host, opt, H, galerkin, level_fn, transpose_fn, done, rap_fn);
         images.e.clear();
         tm.lap("hierarchy (host + SpGEMM)");
-        if (worker) worker->finish();
+        if (worker) worker->finish();  // before gs_worker: its jobs push GS jobs
+        if (gs_worker) gs_worker->finish();
         if (overlap) tm.lap("format builds still running after the hierarchy");
     }
     // replicated coarse levels (multi-rank): from the first level with <= replicate_below
@@ -182,6 +210,7 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
             std::unique_ptr<DevMatrix> d(std::move(pre));
             if (d) {
                 d->host = std::move(M);  // built from M on the worker
+                d->host_view = nullptr;
                 return d;
             }
             d.reset(new DevMatrix());
@@ -219,14 +248,9 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         levels[l].r.alloc(n);
         levels[l].t.alloc(n);
         max_blocks = std::max(max_blocks, (size_t)Al.norm_parts_max());
-        if (opt.smoother == AMG_SMOOTH_HYBRID_GS) {
-            Al.ensure_gs_blocks(opt.gs_block);
-            // level 0's norm-carrying forward sweep runs the one-kernel form, inside captured
-            // cycles: its sliced ELL is built now even where the other sweeps run split
-            if (l == 0) Al.ensure_gs_ell();
-            // a forward split sweep on x != 0: level 0's (tol > 0 solves), a second pre-sweep
-            if (Al.gs_split && (l == 0 || opt.pre_sweeps >= 2)) Al.ensure_gs_pass(0);
-            tm.lap("L" + std::to_string(l) + " GS sliced-ELL build");
+        if (hgs) {
+            gs_build(Al, (int)l);  // done on the GS worker already where the setup overlaps
+            tm.lap("L" + std::to_string(l) + " GS structures");
             max_blocks = std::max(max_blocks, (size_t)Al.gs_norm_parts());
         }
     }

@@ -172,15 +172,17 @@ struct BlockBuild {
 
 // tplf (optional): per row 1 = handled by the template kernel; blocks then also break where it
 // changes, and all-templated interior blocks come first
+// sample > 1: cut only every sample-th chunk (statistics for the format choices below; no
+// tile indices)
 static BlockBuild build_row_blocks(const std::vector<int>& rp, const hvec<int>& col,
                                    const std::vector<uint8_t>& cls, int64_t ncl, int64_t nhalo,
                                    const std::vector<uint8_t>* tplf = nullptr, int row_cap = kTPB,
-                                   bool line_cap = true, bool want_lcol = true, int lw = 8) {
+                                   bool line_cap = true, bool want_lcol = true, int lw = 8, int sample = 1) {
+    if (sample > 1) want_lcol = false;
     const int n = (int)rp.size() - 1;
     const int sh = lw == 8 ? 3 : 2, tl_cap = kCAP / lw;
     AMG_ASSERT(lw == 8 || lw == 4);
     const int64_t hl0 = (ncl + lw - 1) / lw;
-    const size_t nlines = (size_t)(hl0 + (nhalo + lw - 1) / lw) + 1;
     auto line_of = [&](int c) -> int64_t { return c < ncl ? c >> sh : hl0 + ((c - ncl) >> sh); };
     struct Rec {
         int r0, r1;
@@ -198,49 +200,90 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const hvec<int>& 
     // block at its first row), in parallel: blocks never change the arithmetic (rows never
     // straddle a block), and a fixed chunk count keeps the cut independent of the thread count.
     // Sequential, the cut took 0.4-0.7 s per 256^3-level operator.
-    const int nch = n >= (1 << 16) ? 64 : 1;
+    // (r5: also operators of few but long rows -- sa27's R1, 49,492 rows of ~270 entries, took
+    // 0.45 s in one chunk)
+    const int nch = n >= (1 << 16) || (n >= (1 << 12) && rp.back() >= (1 << 20)) ? 64 : 1;
     std::vector<std::vector<Rec>> recs((size_t)nch);
+    // Each thread keeps the open block's lines (and the current row's new ones) in an
+    // open-addressing table with a generation per slot: a slot of an older generation (block)
+    // reads as empty, so closing a block clears nothing.  Sized for one block's lines (<= its
+    // entries: kCAP, or one longer row) plus one row's.  r5: per-thread arrays indexed by line
+    // id (16 B per line of the column space, filled per call) cost more than the cut itself on
+    // level-0 operators (0.54 s for a 16.7 M-column operator on 16 threads).
+    int max_row = 0;
+#pragma omp parallel for reduction(max : max_row) schedule(static)
+    for (int i = 0; i < n; ++i) max_row = std::max(max_row, rp[i + 1] - rp[i]);
+    int hb = 10;
+    while (((size_t)1 << hb) < 2 * ((size_t)kCAP + 2 * (size_t)max_row)) ++hb;
+    const size_t H = (size_t)1 << hb;
 #pragma omp parallel if (nch > 1)
     {
-        std::vector<int> stamp(nlines, -1), slot(nlines, 0);
-        std::vector<int64_t> tstamp(nlines, -1);
+        std::vector<int64_t> hkey(H), hrow(H);
+        std::vector<int> hgen(H, -1), hpos(H);
+        std::vector<char> hin(H);
         std::vector<int> lines, cand;
-        int blk = 0;  // per thread, never reset: stamp markers stay unique across chunks
+        std::vector<size_t> cslot;
+        int blk = 0;  // per thread, never reset: generations stay unique across chunks
+        size_t used = 0;
+        // the slot of line L in the open block's generation (inserted: not in the block, no row)
+        auto find = [&](int64_t L) -> size_t {
+            size_t h = (size_t)(((uint64_t)L * 0x9E3779B97F4A7C15ull) >> (64 - hb));
+            for (;;) {
+                if (hgen[h] != blk) {
+                    AMG_ASSERT(++used < H);
+                    hgen[h] = blk;
+                    hkey[h] = L;
+                    hin[h] = 0;
+                    hrow[h] = -1;
+                    return h;
+                }
+                if (hkey[h] == L) return h;
+                h = (h + 1) & (H - 1);
+            }
+        };
+        auto next_block = [&] {
+            ++blk;
+            used = 0;
+        };
 #pragma omp for schedule(dynamic, 1)
         for (int ch = 0; ch < nch; ++ch) {
+            if (ch % sample) continue;
             const int ra = (int)((int64_t)n * ch / nch), rb = (int)((int64_t)n * (ch + 1) / nch);
             std::vector<Rec>& rc = recs[(size_t)ch];
             int r0 = ra, nl = 0;
             long long acc = 0;
             lines.clear();
-            ++blk;
+            next_block();
             auto emit = [&](int a, int b) {
                 if (b <= a) return;
                 std::sort(lines.begin(), lines.end());
-                for (size_t q = 0; q < lines.size(); ++q) slot[lines[q]] = (int)q;
+                for (size_t q = 0; q < lines.size(); ++q) hpos[find(lines[q])] = (int)q;
                 const bool tiled = (int)lines.size() <= tl_cap;
                 if (want_lcol)
                     for (int k = rp[a]; k < rp[b]; ++k) {
                         const int c = col[k];
                         // element within its line
                         const int e = c < ncl ? (c & (lw - 1)) : (int)((c - ncl) & (lw - 1));
-                        out.lcol[k] = tiled ? (uint16_t)(slot[line_of(c)] * lw + e) : (uint16_t)0;
+                        out.lcol[k] = tiled ? (uint16_t)(hpos[find(line_of(c))] * lw + e) : (uint16_t)0;
                     }
                 rc.push_back({a, b, tiled ? lines : std::vector<int>(), cls[a] != 0,
                               tplf != nullptr && (*tplf)[a] != 0});
                 if (!tiled) rc.back().lines.assign(tl_cap + 1, 0);  // marker: untiled
                 lines.clear();
-                ++blk;
+                next_block();
             };
             // distinct lines of row r not yet in the open block (marker keeps them distinct
             // per call)
             auto collect = [&](int r, int64_t marker) {
                 cand.clear();
+                cslot.clear();
                 for (int k = rp[r]; k < rp[r + 1]; ++k) {
                     const int64_t L = line_of(col[k]);
-                    if (stamp[L] != blk && tstamp[L] != marker) {
-                        tstamp[L] = marker;
+                    const size_t h = find(L);
+                    if (!hin[h] && hrow[h] != marker) {
+                        hrow[h] = marker;
                         cand.push_back((int)L);
+                        cslot.push_back(h);
                     }
                 }
             };
@@ -250,15 +293,15 @@ static BlockBuild build_row_blocks(const std::vector<int>& rp, const hvec<int>& 
                 if (r > r0 && (cls[r] != cls[r0] || acc + len > kCAP || r - r0 >= row_cap ||
                                (line_cap && nl + (int)cand.size() > tl_cap) ||
                                (tplf && (*tplf)[r] != (*tplf)[r0]))) {
-                    emit(r0, r);  // closes [r0, r); blk advances
+                    emit(r0, r);  // closes [r0, r); a new generation
                     r0 = r;
                     acc = 0;
                     nl = 0;
                     collect(r, 2 * (int64_t)r + 1);  // all of row r's lines are new to the new block
                 }
-                for (int L : cand) {
-                    stamp[L] = blk;
-                    lines.push_back(L);
+                for (size_t q = 0; q < cand.size(); ++q) {
+                    hin[cslot[q]] = 1;
+                    lines.push_back(cand[q]);
                 }
                 nl += (int)cand.size();
                 acc += len;
@@ -636,7 +679,11 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
     tm.lap("    build: halo plan");
 
     std::vector<int> hrp(n_rows + 1);
-    hvec<int> hcol(nnz);  // every entry written below
+    // every entry written below; capacity for the kPad zero entries appended after the
+    // templates, so that resize does not reallocate and copy (0.4 s for a 449 M-entry operator)
+    hvec<int> hcol;
+    hcol.reserve((size_t)nnz + kPad);
+    hcol.resize(nnz);
     std::vector<uint8_t> cls(n_rows, 0);
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i <= n_rows; ++i) hrp[i] = (int)host.rp[i];
@@ -689,11 +736,14 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         // with 7+ entries per row was slower that way: R0 94 -> 106 us, sa27 R0 350 -> 415)
         gather_rpb = !square && nnz <= 4 * n_rows ? kGatherRPB : 1;
         const bool dev_fmt = device_formats();
-        BlockBuild bb = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(),
-                                         tplf.empty() ? nullptr : &tplf, kTPB * gather_rpb, true, !dev_fmt);
-        nb_int = bb.nb_int;
-        nb_bnd = bb.nb_bnd;
-        tm.lap("    build: row blocks + x tiles");
+        // The format choices below (x tile or gather, 64- or 32-byte lines) read statistics of
+        // the 64-byte cut; r5 takes them from every 8th of its 64 row chunks (the whole
+        // operator below 65,536 rows) and cuts the operator once, at the chosen width.  Before,
+        // each choice cut the whole operator again: 0.6 s of sa27's setup.
+        constexpr int kSample = 8;
+        const BlockBuild s8 = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(),
+                                               tplf.empty() ? nullptr : &tplf, kTPB * gather_rpb, true, false, 8,
+                                               kSample);
         // rectangular operators take the x-tile kernel when their blocks reuse x lines: at most
         // 0.5 tile lines per nonzero.  Same-box A/B (profiles/r2y_rtile_*, r2z_rpb_*): 7-pt R0
         // 106 -> 79 us (0.23 lines / nnz), R1 66 -> 53 (0.34), P0 (4 rows per lane, 0.06)
@@ -701,68 +751,69 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         // (0.33), P0 19 -> 15; sa27 R1 122 -> 158 at 0.70 (a 297-entry block loading 210
         // lines) stays on the gather kernel.
         // AMG_RECT_TILE=0 / 1: never / always (A/B runs)
-        int64_t tile_lines_total = 0, tile_full = 0;
-        for (size_t q = 0; q + 1 < bb.tile_ptr.size(); ++q) {
-            const int nt = bb.tile_ptr[q + 1] - bb.tile_ptr[q];
+        int64_t tile_lines_total = 0, tile_full = 0, sample_nnz = 0;
+        for (size_t q = 0; q + 1 < s8.tile_ptr.size(); ++q) {
+            const int nt = s8.tile_ptr[q + 1] - s8.tile_ptr[q];
             tile_lines_total += nt;
             tile_full += nt >= kTileLines;
+            sample_nnz += hrp[s8.blocks[q].y] - hrp[s8.blocks[q].x];
         }
         {
             const char* e = std::getenv("AMG_RECT_TILE");
             const int mode = e ? std::atoi(e) : -1;
-            tiled = square || (mode != 0 && (mode == 1 || 2 * tile_lines_total <= (int64_t)nnz));
+            tiled = square || (mode != 0 && (mode == 1 || 2 * tile_lines_total <= sample_nnz));
         }
         if (std::getenv("AMG_TRACE_BLOCKS")) {
             const int64_t lines = tile_lines_total, full = tile_full;
-            std::fprintf(stderr, "[amg-blocks] %s rows %lld cols %lld nnz %lld blocks %zu lines %lld full %lld rpb %d\n",
+            std::fprintf(stderr, "[amg-blocks] %s rows %lld cols %lld nnz %lld sampled: blocks %zu lines %lld full %lld nnz %lld rpb %d\n",
                          square ? "square" : tiled ? "rect-tiled" : "rect-gather", (long long)n_rows, (long long)n_cols_local, (long long)nnz,
-                         bb.blocks.size(), (long long)lines, (long long)full, gather_rpb);
+                         s8.blocks.size(), (long long)lines, (long long)full, (long long)sample_nnz, gather_rpb);
         }
-        // the gather kernel reads x from global memory: its blocks need only the kCAP-entry
-        // and row caps, not the 256-line tile cap.  sa27's R1 (270 entries per row over ~200
-        // lines each) was cut into blocks of ~1 row by that cap: one lane summing while 255
-        // idled.  AMG_GATHER_LINECAP=1 keeps the cap (A/B)
         // x-tile line width: operators whose blocks, cut at 256 lines of
         // 64 B, run close to the cap (>= 3/4 full on average: Galerkin operators,
-        // restrictions) are cut again at 512 lines of 32 B (the 7-pt 256^3 A2: 40,250 ->
-        // 25,615 blocks; R0: same-box 76 -> 70 us); P-like operators (few lines per block)
-        // keep 64-byte lines and their 1 KiB of line ids per block (sa27 P0: 234 us at 64 B,
-        // 263 at 32 B), and so do square operators the re-cut saves < 20 % of the blocks.
+        // restrictions) are cut at 512 lines of 32 B (the 7-pt 256^3 A2: 40,250 -> 25,615
+        // blocks; R0: same-box 76 -> 70 us); P-like operators (few lines per block) keep
+        // 64-byte lines and their 1 KiB of line ids per block (sa27 P0: 234 us at 64 B, 263 at
+        // 32 B), and so do square operators the 32-byte cut saves < 20 % of the blocks (the
+        // 7-pt A1: 50,573 -> 46,841 blocks ran 144 -> 149 us; A2: 40,281 -> 25,640 ran 125 ->
+        // 102 us); restrictions gain either way (R0 91 -> 88 us at -9 %, R1 61 -> 52 at -33 %).
         // AMG_TILE_LINE=8 / 4 forces the width.
-        line_w = 8;
-        if (tiled && !bb.blocks.empty()) {
+        // The gather kernel reads x from global memory: its blocks need only the kCAP-entry and
+        // row caps, not the 256-line tile cap.  sa27's R1 (270 entries per row over ~200 lines
+        // each) was cut into blocks of ~1 row by that cap: one lane summing while 255 idled.
+        // AMG_GATHER_LINECAP=1 keeps the cap (A/B)
+        int lw = 8;
+        bool line_cap = true;
+        if (tiled && !s8.blocks.empty()) {
             const char* e = std::getenv("AMG_TILE_LINE");
             const int force = e ? std::atoi(e) : 0;
             const bool tryhalf = force == 4 || (force != 8 && 4 * tile_lines_total >= 3 * (int64_t)kTileLines *
-                                                                                         (int64_t)bb.blocks.size());
+                                                                                         (int64_t)s8.blocks.size());
             if (tryhalf) {
-                BlockBuild b4 = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(),
-                                                 tplf.empty() ? nullptr : &tplf, kTPB * gather_rpb, true, !dev_fmt, 4);
-                // square operators must lose >= 20 % of their blocks (the 7-pt A1: 50,573 ->
-                // 46,841 blocks ran 144 -> 149 us; A2: 40,281 -> 25,640 ran 125 -> 102 us);
-                // restrictions gain either way (R0 91 -> 88 us at -9 %, R1 61 -> 52 at -33 %)
-                if (force == 4 || !square || 5 * b4.blocks.size() <= 4 * bb.blocks.size()) {
-                    bb = std::move(b4);
-                    line_w = 4;
-                    nb_int = bb.nb_int;
-                    nb_bnd = bb.nb_bnd;
+                bool take = force == 4 || !square;
+                if (!take) {
+                    const BlockBuild s4 = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(),
+                                                           tplf.empty() ? nullptr : &tplf, kTPB * gather_rpb, true,
+                                                           false, 4, kSample);
+                    take = 5 * s4.blocks.size() <= 4 * s8.blocks.size();
                 }
+                if (take) lw = 4;
             }
-            if (std::getenv("AMG_TRACE_BLOCKS"))
-                std::fprintf(stderr, "[amg-blocks]   x-tile lines of %d B: %zu blocks\n", 8 * line_w, bb.blocks.size());
-            tm.lap("    build: row blocks, 32-byte lines");
         }
         if (!tiled) {
             const char* e = std::getenv("AMG_GATHER_LINECAP");
-            if (!(e && std::atoi(e) != 0)) {
-                bb = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(), nullptr, kTPB * gather_rpb, false,
-                                      !dev_fmt);
-                nb_int = bb.nb_int;
-                nb_bnd = bb.nb_bnd;
-                if (std::getenv("AMG_TRACE_BLOCKS"))
-                    std::fprintf(stderr, "[amg-blocks]   gather blocks without the line cap: %zu\n", bb.blocks.size());
-            }
+            line_cap = e && std::atoi(e) != 0;
         }
+        tm.lap("    build: row blocks, sampled cuts");
+        BlockBuild bb = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(),
+                                         tplf.empty() ? nullptr : &tplf, kTPB * gather_rpb, line_cap, !dev_fmt, lw);
+        line_w = lw;
+        nb_int = bb.nb_int;
+        nb_bnd = bb.nb_bnd;
+        if (std::getenv("AMG_TRACE_BLOCKS"))
+            std::fprintf(stderr, "[amg-blocks]   %s, lines of %d B: %zu blocks\n", tiled ? "x tile" : "gather",
+                         8 * line_w, bb.blocks.size());
+        tm.lap("    build: row blocks + x tiles");
         if (!tb.hdr.empty()) {
             // rows of blocks the CSR kernel still runs are not the template kernel's
             std::vector<char> keep(n_rows, 0);
@@ -1091,6 +1142,7 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
 // what the cycle needs).
 void DevMatrix::ensure_gs_pass(int d) {
     if (gs_old[d]) return;
+    const HostCSR& host = host_image();  // the member, or the CSR a worker builds from
     AMG_CHECK(gs_split && gs_block > 0, "hybrid GS: no split sweep for this operator");
     AMG_CHECK(!ctx->capturing, "hybrid GS: split pass requested inside a graph capture");
     const int64_t B = gs_block, clo = first_col, chi = first_col + n_cols_local;
@@ -1107,11 +1159,13 @@ void DevMatrix::ensure_gs_pass(int d) {
     h.row_starts = host.row_starts;
     h.col_starts = host.col_starts;
     h.rp.assign((size_t)n_rows + 1, 0);
+#pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n_rows; ++i) {
         int64_t c = 0;
         for (int64_t k = host.rp[i]; k < host.rp[i + 1]; ++k) c += !is_new(i, host.col[k]);
-        h.rp[i + 1] = h.rp[i] + c;
+        h.rp[i + 1] = c;
     }
+    for (int64_t i = 0; i < n_rows; ++i) h.rp[i + 1] += h.rp[i];
     h.col.resize((size_t)h.rp[n_rows]);
     h.val.resize((size_t)h.rp[n_rows]);
 #pragma omp parallel for schedule(static)
@@ -1135,6 +1189,7 @@ void DevMatrix::ensure_gs_pass(int d) {
 
 void DevMatrix::ensure_gs_ell() {
     if (gs_ell_built) return;
+    const HostCSR& host = host_image();  // the member, or the CSR a worker builds from
     AMG_CHECK(!ctx->capturing, "hybrid GS: sliced ELL requested inside a graph capture");
     const int64_t clo = first_col, chi = first_col + n_cols_local;
     auto local_col = [&](int64_t g) -> int {
@@ -1213,6 +1268,7 @@ void DevMatrix::ensure_gs_ell() {
 }
 
 void DevMatrix::ensure_gs_blocks(int64_t B) {
+    const HostCSR& host = host_image();  // the member, or the CSR a worker builds from
     AMG_CHECK(square, "hybrid GS needs a square matrix");
     AMG_CHECK(B >= 1 && B <= 64, "hybrid GS block must be in [1, 64]");
     if (gs_block == B) return;
