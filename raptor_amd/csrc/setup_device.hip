@@ -628,6 +628,54 @@ __global__ void count_cols_kernel(int nnz, const int* col, int* cnt) {
     if (t < nnz) atomicAdd(&cnt[col[t]], 1);
 }
 
+// N ranks: the transpose's exchange record (the host transpose's layout: R row j, R column i
+// = global fine row, value)
+struct TRec {
+    long long j, i;
+    double v;
+};
+
+// send side: entries in (column, fine row) order -- the radix sort by column is stable over
+// the row-major entry order -- as records; the owner of column j receives a contiguous range
+__global__ void transpose_records_kernel(int nnz, const int* __restrict__ keys, const int* __restrict__ perm,
+                                        const int* __restrict__ rowof, const double* __restrict__ val,
+                                        long long i0, TRec* __restrict__ out) {
+    const int t = blockIdx.x * kT + threadIdx.x;
+    if (t >= nnz) return;
+    const int k = perm[t];
+    out[t] = TRec{keys[t], i0 + rowof[k], val[k]};
+}
+
+// receive side: the local row of every record (j - lo), the key of a stable sort that keeps
+// rank order, then ascending i, inside each row
+__global__ void record_rows_kernel(int m, const TRec* __restrict__ in, long long lo, int* __restrict__ key) {
+    const int t = blockIdx.x * kT + threadIdx.x;
+    if (t < m) key[t] = (int)(in[t].j - lo);
+}
+
+__global__ void gather_records_kernel(int m, const int* __restrict__ perm, const TRec* __restrict__ in,
+                                      long long* __restrict__ rcol, double* __restrict__ rval) {
+    const int t = blockIdx.x * kT + threadIdx.x;
+    if (t >= m) return;
+    const TRec e = in[perm[t]];
+    rcol[t] = e.i;
+    rval[t] = e.v;
+}
+
+// first sorted position with key >= bound[o], per owner boundary o
+__global__ void owner_bounds_kernel(int m, const int* __restrict__ keys, int nb, const long long* __restrict__ bound,
+                                    long long* __restrict__ out) {
+    const int o = blockIdx.x * kT + threadIdx.x;
+    if (o >= nb) return;
+    int lo = 0, hi = m;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((long long)keys[mid] < bound[o]) lo = mid + 1;
+        else hi = mid;
+    }
+    out[o] = lo;
+}
+
 // ---- helpers ---------------------------------------------------------------------------
 // exclusive scan of n ints into out[0..n] (out[n] = total)
 int64_t exclusive_scan(hipStream_t s, const int* in, int* out, int n, DevBuf<char>& tmp) {
@@ -1346,10 +1394,143 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
     return true;
 }
 
+namespace {
+
+void sort_pairs_stable(hipStream_t s, const int* keys_in, int* keys_out, const int* vals_in, int* vals_out, int m,
+                       int64_t key_range, DevBuf<char>& tmp) {
+    int bits = 1;
+    while (bits < 31 && (1ll << bits) < key_range) ++bits;
+    size_t bytes = 0;
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, keys_in, keys_out, vals_in, vals_out, m, 0, bits, s));
+    if (tmp.n < bytes) tmp.alloc(bytes);
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp.p, bytes, keys_in, keys_out, vals_in, vals_out, m, 0, bits, s));
+}
+
+// R = P^T on N ranks (host_comm.cpp transpose(), the same records and exchange): each rank
+// sorts its entries by global column on the device (stable: fine rows stay ascending), ships
+// each owner its contiguous record range (one all-to-all-v), and the owner sorts what it
+// received by local row, stably -- rank order, then ascending fine row, as the host
+// transpose places them.  Bit-identical to it.
+bool transpose_device_dist(Context& ctx, const HostComm& comm, const HostCSR& P, HostCSR& R) {
+    hipStream_t s = ctx.stream;
+    const int64_t n = P.nrows(), nnz = P.nnz(), nc = P.n_global_cols;
+    const int64_t lo = P.col_starts[comm.rank], m_rows = P.col_starts[comm.rank + 1] - lo;
+    // every rank takes the same path (the exchange is collective)
+    int64_t ok = n < INT_MAX && nnz < INT_MAX && nc < INT_MAX;
+    for (int64_t v : comm.allgather(ok)) ok = ok && v;
+    if (!ok) return false;
+    static_assert(sizeof(TRec) == 24, "record layout");
+    DevBuf<char> tmp;
+    const int nr = comm.nranks, me = comm.rank;
+    // records sorted by column: owner o's range [off[o], off[o + 1]); this rank's own range
+    // stays on the device, only the others' travel through the host exchange
+    std::vector<long long> off((size_t)nr + 1, 0);
+    DevBuf<TRec> recs;
+    std::vector<TRec> sbuf;
+    if (nnz) {
+        SetupImages local;
+        DevCsr& dP = local.get(P);
+        dP.ensure_rp32(s);
+        dP.ensure_col32(s);
+        DevBuf<int> keys_out, idx_in, idx_out, rowof;
+        DevBuf<long long> dbound, doff;
+        keys_out.alloc(nnz);
+        idx_in.alloc(nnz);
+        idx_out.alloc(nnz);
+        rowof.alloc(nnz);
+        recs.alloc(nnz);
+        hipLaunchKernelGGL(iota_kernel, dim3(grid1(nnz)), dim3(kT), 0, s, (int)nnz, idx_in.p);
+        if (n) hipLaunchKernelGGL(expand_rows_kernel, dim3(grid1(n)), dim3(kT), 0, s, dP.rp32.p, (int)n, rowof.p);
+        sort_pairs_stable(s, dP.col32.p, keys_out.p, idx_in.p, idx_out.p, (int)nnz, nc, tmp);
+        hipLaunchKernelGGL(transpose_records_kernel, dim3(grid1(nnz)), dim3(kT), 0, s, (int)nnz, keys_out.p, idx_out.p,
+                           rowof.p, dP.val.p, (long long)P.row_starts[me], recs.p);
+        std::vector<long long> bound(P.col_starts.begin() + 1, P.col_starts.end());
+        dbound.upload(bound.data(), bound.size());
+        doff.alloc((size_t)nr);
+        hipLaunchKernelGGL(owner_bounds_kernel, dim3(grid1(nr)), dim3(kT), 0, s, (int)nnz, keys_out.p, nr, dbound.p,
+                           doff.p);
+        HIP_CHECK(hipGetLastError());
+        copy_to_host(off.data() + 1, doff.p, sizeof(long long) * nr, s);
+        off[nr] = nnz;
+        const int64_t nsend = nnz - (off[me + 1] - off[me]);
+        sbuf.resize((size_t)nsend);
+        copy_to_host(sbuf.data(), recs.p, sizeof(TRec) * off[me], nullptr);
+        copy_to_host(sbuf.data() + off[me], recs.p + off[me + 1], sizeof(TRec) * (nnz - off[me + 1]), nullptr);
+    }
+    std::vector<int64_t> cnt(nr, 0), sb(nr), rb(nr);
+    for (int o = 0; o < nr; ++o) cnt[o] = off[o + 1] - off[o];
+    const std::vector<int64_t> rcnt = comm.alltoall_counts(cnt);
+    int64_t rtot = 0, rfor = 0, before = 0;
+    for (int o = 0; o < nr; ++o) {
+        sb[o] = o == me ? 0 : cnt[o] * (int64_t)sizeof(TRec);
+        rb[o] = o == me ? 0 : rcnt[o] * (int64_t)sizeof(TRec);
+        rtot += rcnt[o];
+        if (o != me) rfor += rcnt[o];
+        if (o < me) before += rcnt[o];
+    }
+    std::vector<TRec> rbuf((size_t)rfor);
+    comm.alltoallv(sbuf.data(), sb, rbuf.data(), rb);
+    std::vector<TRec>().swap(sbuf);
+    AMG_CHECK(rtot < INT_MAX && m_rows < INT_MAX, "device transpose: rows exceed int32 indexing");
+    R = HostCSR();
+    R.n_global_rows = nc;
+    R.n_global_cols = P.n_global_rows;
+    R.row_starts = P.col_starts;
+    R.col_starts = P.row_starts;
+    R.rp.assign((size_t)m_rows + 1, 0);
+    R.col.resize((size_t)rtot);
+    R.val.resize((size_t)rtot);
+    if (rtot) {
+        // received records in rank order: [ranks < me | own range (device to device) | ranks > me]
+        DevBuf<TRec> drec;
+        DevBuf<int> key, key_out, idx_in, idx_out, cntd, rrp;
+        DevBuf<long long> rcol;
+        DevBuf<double> rval;
+        const int64_t own = rtot - rfor;
+        drec.alloc((size_t)rtot);
+        if (before) copy_to_device(drec.p, rbuf.data(), sizeof(TRec) * before);
+        if (own)
+            HIP_CHECK(hipMemcpyAsync(drec.p + before, recs.p + off[me], sizeof(TRec) * own, hipMemcpyDeviceToDevice, s));
+        if (rfor > before)
+            copy_to_device(drec.p + before + own, rbuf.data() + before, sizeof(TRec) * (rfor - before));
+        std::vector<TRec>().swap(rbuf);
+        HIP_CHECK(hipStreamSynchronize(s));
+        recs.reset();
+        key.alloc(rtot);
+        key_out.alloc(rtot);
+        idx_in.alloc(rtot);
+        idx_out.alloc(rtot);
+        hipLaunchKernelGGL(record_rows_kernel, dim3(grid1(rtot)), dim3(kT), 0, s, (int)rtot, drec.p, (long long)lo, key.p);
+        hipLaunchKernelGGL(iota_kernel, dim3(grid1(rtot)), dim3(kT), 0, s, (int)rtot, idx_in.p);
+        sort_pairs_stable(s, key.p, key_out.p, idx_in.p, idx_out.p, (int)rtot, m_rows, tmp);
+        rcol.alloc(rtot);
+        rval.alloc(rtot);
+        hipLaunchKernelGGL(gather_records_kernel, dim3(grid1(rtot)), dim3(kT), 0, s, (int)rtot, idx_out.p, drec.p,
+                           rcol.p, rval.p);
+        cntd.alloc((size_t)m_rows + 1);
+        HIP_CHECK(hipMemsetAsync(cntd.p, 0, sizeof(int) * cntd.n, s));
+        hipLaunchKernelGGL(count_cols_kernel, dim3(grid1(rtot)), dim3(kT), 0, s, (int)rtot, key.p, cntd.p);
+        rrp.alloc((size_t)m_rows + 1);
+        exclusive_scan(s, cntd.p, rrp.p, (int)m_rows, tmp);
+        HIP_CHECK(hipGetLastError());
+        const std::vector<int> hrp = download_ints(s, rrp.p, m_rows + 1);
+        R.rp.assign(hrp.begin(), hrp.end());
+        copy_to_host(R.col.data(), rcol.p, sizeof(long long) * rtot, s);
+        copy_to_host(R.val.data(), rval.p, sizeof(double) * rtot, nullptr);
+    }
+    return true;
+}
+
+}  // namespace
+
 // R = P^T on the device for one rank: stable radix sort of the entries by column keeps each
 // R row in ascending fine-row order, like transpose().
 bool transpose_device(Context& ctx, const HostComm& comm, const HostCSR& P, HostCSR& R, SetupImages* imgs) {
-    if (comm.nranks != 1) return false;
+    if (comm.nranks != 1) {
+        const char* e = std::getenv("AMG_TRANSPOSE_DIST");  // 0: the host transpose (A/B, tests)
+        if (e && *e && std::atoi(e) == 0) return false;
+        return transpose_device_dist(ctx, comm, P, R);
+    }
     hipStream_t s = ctx.stream;
     const int64_t n = P.nrows(), nnz = P.nnz(), nc = P.n_global_cols;
     if (nnz == 0 || n >= INT_MAX || nnz >= INT_MAX || nc >= INT_MAX) return false;
