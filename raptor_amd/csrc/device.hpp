@@ -157,7 +157,7 @@ struct Context {
     void allgather(const double* send, double* recv, size_t count);
 };
 
-// Device image of one host CSR of the hierarchy during setup (one rank):
+// Device image of one host CSR of the hierarchy during setup:
 // the same rows, global column ids, in whichever index widths the consumers need -- int32 for
 // the strength / aggregation / interpolation kernels, the transpose and the left operand of a
 // SpGEMM, int64 for the SpGEMM's right operand (B image) and its row pointers.  A width that
@@ -173,7 +173,7 @@ struct DevCsr {
     void ensure_col64(hipStream_t s);
 };
 
-// The device images of one hierarchy setup (Solver::setup, one rank).  A matrix the setup
+// The device images of one hierarchy setup (Solver::setup; any rank count, r5).  A matrix the setup
 // computes on the device (P, R = P^T, A_{l+1} = R (A P)) is registered as it is downloaded,
 // so its consumers in the same level (transpose, Galerkin product, the next level's strength
 // and aggregation) read it where it already is instead of uploading the host copy back; the
@@ -203,12 +203,12 @@ void build_formats_device(DevMatrix& M, const std::vector<int>& hrp, const hvec<
                           const std::vector<int2>& blocks, const std::vector<int>& tile_ptr,
                           const std::vector<int>& tile_lines, const std::vector<int64_t>& koff, FormatHeaderInfo& out);
 // R (A P), A P kept on the device between the products where it can be (one rank)
-// imgs (one rank, may be null): A, P and R read from their device images, R (A P) registered
+// imgs (may be null): A, P and R read from their device images, R (A P) registered
 HostCSR galerkin_device(Context& ctx, const HostComm& comm, const HostCSR& R, const HostCSR& A,
                         const HostCSR& P, SetupImages* imgs = nullptr);
 // device setup of one level (setup_device.hip): strength, PMIS or MIS(2) aggregation,
-// classical or smoothed-aggregation P; false where it does not apply.  imgs: A's device image
-// (any rank count), P registered (one rank)
+// classical or smoothed-aggregation P; false where it does not apply.  imgs: A's device image,
+// P registered (SA: one rank)
 bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, const amg_options& opt,
                         int level, HostCSR& P, std::vector<int32_t>& split, SetupImages* imgs = nullptr);
 bool transpose_device(Context& ctx, const HostComm& comm, const HostCSR& P, HostCSR& R,

@@ -109,10 +109,10 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     LevelSetupFn level_fn = nullptr;
     TransposeFn transpose_fn = nullptr;
     RapFn rap_fn = nullptr;
-    // one rank: the level operators, P and R stay on the device between the setup steps that
-    // read them (SetupImages); only the next level's operator is carried over
+    // the level operators, P and R stay on the device between the setup steps that read them
+    // (SetupImages); only the next level's operator is carried over
     SetupImages images;
-    SetupImages* im = opt.setup_device && comm.nranks == 1 ? &images : nullptr;
+    SetupImages* im = opt.setup_device ? &images : nullptr;
     if (opt.setup_device) {
         galerkin = [this, &comm](const HostCSR& X, const HostCSR& Y) {
             return spgemm_device(*ctx, comm, X, Y);

@@ -1145,7 +1145,7 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
         P.col.assign(hcol.begin(), hcol.end());
         P.val.resize((size_t)pnnz);
         copy_to_host(P.val.data(), pval.p, sizeof(double) * pnnz, s);
-        if (imgs && !dist) {  // P where it was computed, for the transpose and the Galerkin product
+        if (imgs) {  // P where it was computed, for the transpose and the Galerkin product
             std::unique_ptr<DevCsr> d(new DevCsr());
             d->rp32 = std::move(prp);
             d->col32 = std::move(pcol);
@@ -1411,7 +1411,7 @@ void sort_pairs_stable(hipStream_t s, const int* keys_in, int* keys_out, const i
 // each owner its contiguous record range (one all-to-all-v), and the owner sorts what it
 // received by local row, stably -- rank order, then ascending fine row, as the host
 // transpose places them.  Bit-identical to it.
-bool transpose_device_dist(Context& ctx, const HostComm& comm, const HostCSR& P, HostCSR& R) {
+bool transpose_device_dist(Context& ctx, const HostComm& comm, const HostCSR& P, HostCSR& R, SetupImages* imgs) {
     hipStream_t s = ctx.stream;
     const int64_t n = P.nrows(), nnz = P.nnz(), nc = P.n_global_cols;
     const int64_t lo = P.col_starts[comm.rank], m_rows = P.col_starts[comm.rank + 1] - lo;
@@ -1429,7 +1429,7 @@ bool transpose_device_dist(Context& ctx, const HostComm& comm, const HostCSR& P,
     std::vector<TRec> sbuf;
     if (nnz) {
         SetupImages local;
-        DevCsr& dP = local.get(P);
+        DevCsr& dP = (imgs ? *imgs : local).get(P);
         dP.ensure_rp32(s);
         dP.ensure_col32(s);
         DevBuf<int> keys_out, idx_in, idx_out, rowof;
@@ -1517,6 +1517,13 @@ bool transpose_device_dist(Context& ctx, const HostComm& comm, const HostCSR& P,
         R.rp.assign(hrp.begin(), hrp.end());
         copy_to_host(R.col.data(), rcol.p, sizeof(long long) * rtot, s);
         copy_to_host(R.val.data(), rval.p, sizeof(double) * rtot, nullptr);
+        if (imgs) {  // R where it was computed, for the Galerkin product
+            std::unique_ptr<DevCsr> d(new DevCsr());
+            d->rp32 = std::move(rrp);
+            d->col64 = std::move(rcol);
+            d->val = std::move(rval);
+            imgs->put(R, std::move(d));
+        }
     }
     return true;
 }
@@ -1529,7 +1536,7 @@ bool transpose_device(Context& ctx, const HostComm& comm, const HostCSR& P, Host
     if (comm.nranks != 1) {
         const char* e = std::getenv("AMG_TRANSPOSE_DIST");  // 0: the host transpose (A/B, tests)
         if (e && *e && std::atoi(e) == 0) return false;
-        return transpose_device_dist(ctx, comm, P, R);
+        return transpose_device_dist(ctx, comm, P, R, imgs);
     }
     hipStream_t s = ctx.stream;
     const int64_t n = P.nrows(), nnz = P.nnz(), nc = P.n_global_cols;

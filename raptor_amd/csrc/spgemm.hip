@@ -195,11 +195,11 @@ struct BImage {
     std::function<void(std::function<int64_t(long long)>&, std::function<double(long long)>&)> bhost;
 };
 
-// the left operand: device arrays (row pointers, B-image row of each entry, values) and the
-// host arrays the fallback rows read (acol_host null: the host columns, one rank)
+// the left operand: device arrays (row pointers, B-image row of each entry, values) and what
+// the host fallback rows read (the host rows and values, and each entry's B-image row)
 struct AOperand {
     const HostCSR* host;
-    const int* acol_host;
+    std::function<int64_t(int64_t)> acol_at;  // B-image row of entry k (null: host->col[k])
     const long long* d_rp;
     const int* d_col;
     const double* d_val;
@@ -216,7 +216,8 @@ AOperand upload_a(PhaseTimer& tm, const HostCSR& A, const std::vector<int>& acol
     u.col.upload(acol.data(), acol.size());
     u.val.upload(A.val.data(), A.val.size());
     tm.lap("    spgemm: uploads of A");
-    return AOperand{&A, acol.data(), u.rp.p, u.col.p, u.val.p};
+    const int* ac = acol.data();
+    return AOperand{&A, [ac](int64_t k) -> int64_t { return ac[k]; }, u.rp.p, u.col.p, u.val.p};
 }
 
 void spgemm_core(Context& ctx, PhaseTimer& tm, const AOperand& Aop, const std::vector<int64_t>& ub,
@@ -295,7 +296,7 @@ void spgemm_core(Context& ctx, PhaseTimer& tm, const AOperand& Aop, const std::v
                 const int64_t i = host_rows[t];
                 touched.clear();
                 for (int64_t ka = A.rp[i]; ka < A.rp[i + 1]; ++ka) {
-                    const int64_t r = Aop.acol_host ? (int64_t)Aop.acol_host[ka] : A.col[ka];
+                    const int64_t r = Aop.acol_at ? Aop.acol_at(ka) : A.col[ka];
                     for (long long q = B.brp_host[r]; q < B.brp_host[r + 1]; ++q) {
                         const int64_t j = bcol_at(q);
                         if (!seen[j]) seen[j] = 1, touched.push_back(j);
@@ -369,6 +370,52 @@ __global__ void row_bound_kernel(long long n, const long long* __restrict__ arp,
         u += brp[c + 1] - brp[c];
     }
     ub[i] = u;
+}
+
+// N ranks: the B-image row of every entry of A (global column c): c - lo for B's local rows,
+// n_local + (position of c among the sorted halo ids) for its ghost rows
+__global__ void bimage_rows_kernel(long long nnz, const int* __restrict__ col, long long lo, long long hi,
+                                   long long n_local, const long long* __restrict__ halo, int nh, int* __restrict__ out) {
+    for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < nnz; k += (long long)gridDim.x * 256) {
+        const long long c = col[k];
+        if (c >= lo && c < hi) {
+            out[k] = (int)(c - lo);
+        } else {
+            int a = 0, b = nh;
+            while (a < b) {
+                const int m = (a + b) >> 1;
+                if (halo[m] < c) a = m + 1;
+                else b = m;
+            }
+            out[k] = (int)(n_local + a);
+        }
+    }
+}
+
+// A's B-image rows and per-row bounds on the device (N ranks); returns the bounds on the host
+std::vector<int64_t> device_column_map(hipStream_t s, DevCsr& A, const HaloPlan& plan, int64_t lo, int64_t hi,
+                                       int64_t n_local, const long long* d_brp, DevBuf<int>& acol) {
+    A.ensure_rp64(s);
+    A.ensure_col32(s);
+    DevBuf<long long> dh;
+    std::vector<long long> hg(plan.halo_gid.begin(), plan.halo_gid.end());
+    dh.upload(hg.data(), std::max<size_t>(hg.size(), 1));
+    acol.alloc((size_t)std::max<int64_t>(A.nnz, 1));
+    if (A.nnz)
+        hipLaunchKernelGGL(bimage_rows_kernel, dim3((unsigned)std::min<int64_t>((A.nnz + 255) / 256, 1 << 16)), dim3(256),
+                           0, s, (long long)A.nnz, A.col32.p, (long long)lo, (long long)hi, (long long)n_local, dh.p,
+                           (int)plan.n_halo(), acol.p);
+    std::vector<int64_t> ub((size_t)A.n);
+    if (A.n) {
+        DevBuf<long long> d_ub;
+        d_ub.alloc((size_t)A.n);
+        hipLaunchKernelGGL(row_bound_kernel, dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, s, (long long)A.n,
+                           A.rp64.p, acol.p, d_brp, d_ub.p);
+        HIP_CHECK(hipGetLastError());
+        copy_to_host(ub.data(), d_ub.p, sizeof(long long) * A.n, s);
+    }
+    HIP_CHECK(hipStreamSynchronize(s));  // dh is freed on return
+    return ub;
 }
 
 }  // namespace
@@ -471,51 +518,55 @@ namespace {
 // this rank's own rows, which are copied device to device into the B image of R (A P).  Same
 // products and order as the two spgemm_device calls it replaces: bit-identical.
 HostCSR galerkin_device_dist(Context& ctx, const HostComm& comm, const HostCSR& R, const HostCSR& A,
-                             const HostCSR& P) {
+                             const HostCSR& P, SetupImages* imgs) {
     AMG_CHECK(A.col_starts == P.row_starts && R.col_starts == A.row_starts, "galerkin: partitions differ");
     PhaseTimer tm(comm);
     hipStream_t s = ctx.stream;
     static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
+    // A, P and R from the setup's device images (r5; uploaded here without them); their
+    // columns mapped to B-image rows on the device
+    SetupImages local;
+    SetupImages& im = imgs ? *imgs : local;
     // ---- A P: B image = [P's rows | ghost rows of P] (spgemm_device's first product)
     DevCSR64 AP;
     {
         HaloPlan plan = halo_plan_for_cols(comm, A);
         GhostRows G = fetch_rows(comm, plan, P);
-        const int64_t n = A.nrows(), nbl = P.nrows(), lo = P.row_starts[comm.rank], hi = P.row_starts[comm.rank + 1];
+        const int64_t nbl = P.nrows(), lo = P.row_starts[comm.rank], hi = P.row_starts[comm.rank + 1];
         std::vector<long long> brp(nbl + plan.n_halo() + 1);
         for (int64_t r = 0; r <= nbl; ++r) brp[r] = P.rp[r];
         for (int64_t t = 0; t < plan.n_halo(); ++t) brp[nbl + t + 1] = P.rp[nbl] + G.rp[t + 1];
-        std::vector<int> acol(A.nnz());
-        std::vector<int64_t> ub(n, 0);
-#pragma omp parallel for schedule(static)
-        for (int64_t i = 0; i < n; ++i) {
-            int64_t u = 0;
-            for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
-                const int64_t c = A.col[k];
-                const int64_t r = (c >= lo && c < hi) ? c - lo : nbl + plan.find(c);
-                acol[k] = (int)r;
-                u += brp[r + 1] - brp[r];
-            }
-            ub[i] = u;
-        }
         const int64_t bl = P.nnz(), bnnz = brp.back();
         DevBuf<long long> d_brp, d_bcol;
         DevBuf<double> d_bval;
         d_brp.upload(brp.data(), brp.size());
         d_bcol.alloc((size_t)std::max<int64_t>(bnnz, 1));
         d_bval.alloc((size_t)std::max<int64_t>(bnnz, 1));
-        copy_to_device(d_bcol.p, P.col.data(), sizeof(long long) * bl);
-        copy_to_device(d_bval.p, P.val.data(), sizeof(double) * bl);
+        DevCsr& dP = im.get(P);
+        dP.ensure_col64(s);
+        if (bl) {
+            HIP_CHECK(hipMemcpyAsync(d_bcol.p, dP.col64.p, sizeof(long long) * bl, hipMemcpyDeviceToDevice, s));
+            HIP_CHECK(hipMemcpyAsync(d_bval.p, dP.val.p, sizeof(double) * bl, hipMemcpyDeviceToDevice, s));
+        }
+        HIP_CHECK(hipStreamSynchronize(s));
         copy_to_device(d_bcol.p + bl, G.col.data(), sizeof(long long) * (bnnz - bl));
         copy_to_device(d_bval.p + bl, G.val.data(), sizeof(double) * (bnnz - bl));
-        tm.lap("    galerkin: A P column map, P image");
+        DevCsr& dA = im.get(A);
+        DevBuf<int> acol;
+        const std::vector<int64_t> ub = device_column_map(s, dA, plan, lo, hi, nbl, d_brp.p, acol);
+        tm.lap("    galerkin: A P column map (device), P image");
         BImage img{brp.data(), d_brp.p, d_bcol.p, d_bval.p, P.n_global_cols,
                    [&](std::function<int64_t(long long)>& ca, std::function<double(long long)>& va) {
                        ca = [&](long long q) -> int64_t { return q < bl ? P.col[q] : G.col[q - bl]; };
                        va = [&](long long q) -> double { return q < bl ? P.val[q] : G.val[q - bl]; };
                    }};
-        AUpload au;
-        spgemm_core(ctx, tm, upload_a(tm, A, acol, au), ub, img, AP);
+        const AOperand aop{&A,
+                           [&](int64_t k) -> int64_t {
+                               const int64_t c = A.col[k];
+                               return (c >= lo && c < hi) ? c - lo : nbl + plan.find(c);
+                           },
+                           dA.rp64.p, acol.p, dA.val.p};
+        spgemm_core(ctx, tm, aop, ub, img, AP);
     }
     // ---- ghost rows of A P for R's off-rank columns, gathered on the device
     const int64_t nl = A.nrows(), lo = A.row_starts[comm.rank], hi = A.row_starts[comm.rank + 1];
@@ -574,20 +625,9 @@ HostCSR galerkin_device_dist(Context& ctx, const HostComm& comm, const HostCSR& 
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipStreamSynchronize(s));  // d_in is freed at the end of this scope
     }
-    const int64_t nr = R.nrows();
-    std::vector<int> rcol(R.nnz());
-    std::vector<int64_t> rub(nr, 0);
-#pragma omp parallel for schedule(static)
-    for (int64_t i = 0; i < nr; ++i) {
-        int64_t u = 0;
-        for (int64_t k = R.rp[i]; k < R.rp[i + 1]; ++k) {
-            const int64_t c = R.col[k];
-            const int64_t r = (c >= lo && c < hi) ? c - lo : nl + rplan.find(c);
-            rcol[k] = (int)r;
-            u += brp[r + 1] - brp[r];
-        }
-        rub[i] = u;
-    }
+    DevCsr& dR = im.get(R);
+    DevBuf<int> rcol;
+    const std::vector<int64_t> rub = device_column_map(s, dR, rplan, lo, hi, nl, d_brp.p, rcol);
     AP.d_col.reset();
     AP.d_val.reset();
     tm.lap("    galerkin: R column map, A P image");
@@ -604,9 +644,22 @@ HostCSR galerkin_device_dist(Context& ctx, const HostComm& comm, const HostCSR& 
                    va = [&](long long q) -> double { return hv[q]; };
                }};
     DevCSR64 RAP;
-    AUpload au;
-    spgemm_core(ctx, tm, upload_a(tm, R, rcol, au), rub, img, RAP);
-    return download(ctx, tm, R, P, RAP);
+    const AOperand rop{&R,
+                       [&](int64_t k) -> int64_t {
+                           const int64_t c = R.col[k];
+                           return (c >= lo && c < hi) ? c - lo : nl + rplan.find(c);
+                       },
+                       dR.rp64.p, rcol.p, dR.val.p};
+    spgemm_core(ctx, tm, rop, rub, img, RAP);
+    HostCSR out = download(ctx, tm, R, P, RAP);
+    if (imgs) {  // the next level's operator (its strength / splitting and products)
+        std::unique_ptr<DevCsr> d(new DevCsr());
+        d->rp64 = std::move(RAP.d_rp);
+        d->col64 = std::move(RAP.d_col);
+        d->val = std::move(RAP.d_val);
+        imgs->put(out, std::move(d));
+    }
+    return out;
 }
 
 }  // namespace
@@ -620,7 +673,7 @@ HostCSR galerkin_device(Context& ctx, const HostComm& comm, const HostCSR& R, co
     if (comm.nranks > 1) {
         const char* e = std::getenv("AMG_GALERKIN_DIST");
         if (e && *e && std::atoi(e) == 0) return spgemm_device(ctx, comm, R, spgemm_device(ctx, comm, A, P));
-        return galerkin_device_dist(ctx, comm, R, A, P);
+        return galerkin_device_dist(ctx, comm, R, A, P, imgs);
     }
     AMG_CHECK(A.col_starts == P.row_starts && R.col_starts == A.row_starts, "galerkin: partitions differ");
     PhaseTimer tm(comm);
