@@ -229,26 +229,33 @@ void spgemm_core(Context& ctx, PhaseTimer& tm, const AOperand& Aop, const std::v
     // fall back to the host only when it overflows.  Chunks bin in parallel and concatenate
     // in chunk order: each bin lists its rows ascending, as a serial pass would.
     static constexpr int kBins[] = {256, 1024, 4096, 8192};
-    std::vector<int> bins[4];
-    {
+    // rows binned in parallel chunks, concatenated in chunk order (each bin lists its rows
+    // ascending, as a serial pass would)
+    auto bin_rows = [n](std::vector<int>(&bins)[4], const std::function<int(int64_t)>& bin_of) {
         const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(256, n / 65536));
         std::vector<std::array<std::vector<int>, 4>> part((size_t)nch);
 #pragma omp parallel for schedule(dynamic, 1)
         for (int c = 0; c < nch; ++c) {
             const int64_t r0 = n * c / nch, r1 = n * (c + 1) / nch;
             for (int64_t i = r0; i < r1; ++i) {
-                int b = 0;
-                while (b < 3 && 2 * ub[i] > kBins[b]) ++b;
-                part[(size_t)c][b].push_back((int)i);
+                const int b = bin_of(i);
+                if (b >= 0) part[(size_t)c][b].push_back((int)i);
             }
         }
         for (int b = 0; b < 4; ++b) {
             size_t tot = 0;
             for (auto& pc : part) tot += pc[b].size();
+            bins[b].clear();
             bins[b].reserve(tot);
             for (auto& pc : part) bins[b].insert(bins[b].end(), pc[b].begin(), pc[b].end());
         }
-    }
+    };
+    // symbolic: rows whose bound fits 256 slots there, every other row first in the 1024-slot
+    // table (r5: a row's distinct columns are usually far fewer than its bound -- sa27's
+    // R0 (A0 P0) rows bound ~7,000, hold a few hundred -- and a 128 KiB table of 8192 slots runs
+    // one workgroup per CU), the rows that overflow it again in 8192 slots
+    std::vector<int> bins[4];
+    bin_rows(bins, [&](int64_t i) { return 2 * ub[i] > kBins[0] ? 1 : 0; });
     tm.lap("    spgemm: bins");
     hipStream_t s = ctx.stream;
     DevBuf<long long> d_counts;
@@ -260,22 +267,35 @@ void spgemm_core(Context& ctx, PhaseTimer& tm, const AOperand& Aop, const std::v
                        B.d_bval, d_counts.p, C.d_rp.p, C.d_col.p, C.d_val.p)
     AMG_BIN(256, false, 0);
     AMG_BIN(1024, false, 1);
-    AMG_BIN(4096, false, 2);
-    AMG_BIN(8192, false, 3);
     std::vector<long long> counts((size_t)n);
     if (n) HIP_CHECK(hipMemcpyAsync(counts.data(), d_counts.p, sizeof(long long) * n, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    {
+        std::vector<int> retry;
+        for (int i : bins[1])
+            if (counts[i] < 0) retry.push_back(i);
+        if (!retry.empty()) {
+            bins[3].swap(retry);
+            AMG_BIN(8192, false, 3);
+            HIP_CHECK(hipMemcpyAsync(counts.data(), d_counts.p, sizeof(long long) * n, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+        }
+    }
     tm.lap("    spgemm: symbolic");
     // rows that overflowed the largest table: host, same canonical order, a dense
     // accumulator per thread (acc_j in k order, then the touched columns sorted)
     std::vector<int64_t> host_rows;
-    {
-        std::vector<int> keep;
-        for (int i : bins[3])
-            if (counts[i] < 0) host_rows.push_back(i);
-            else keep.push_back(i);
-        bins[3].swap(keep);
-    }
+    for (int64_t i = 0; i < n; ++i)
+        if (counts[i] < 0) host_rows.push_back(i);
+    // numeric: the table each row's exact count fits at load <= 1/2 (the 8192-slot table
+    // above that: the symbolic pass found the row fits it)
+    bin_rows(bins, [&](int64_t i) {
+        const long long c = counts[i];
+        if (c < 0) return -1;
+        int b = 0;
+        while (b < 3 && 2 * c > kBins[b]) ++b;
+        return b;
+    });
     std::vector<std::vector<std::pair<int64_t, double>>> hostout(host_rows.size());
     if (!host_rows.empty()) {
         std::function<int64_t(long long)> bcol_at;
