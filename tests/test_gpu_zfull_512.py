@@ -160,3 +160,62 @@ def test_512cubed_one_rank_vs_eight_loopback_ranks(capfd, monkeypatch, partition
         with open(os.path.join(rep_dir, f"test_512_{partition}_report.json"), "w") as fh:
             json.dump(report, fh)
     say(f"done: {report}")
+
+
+@pytest.mark.skipif(os.environ.get("AMG_TEST_RCCL_512") != "1",
+                    reason="opt-in (AMG_TEST_RCCL_512=1): eight RCCL processes of 512^3 on one GPU")
+def test_512cubed_rccl_eight_processes_vs_one_rank(tmp_path, capfd):
+    """configs[3] at its size over the product's RCCL transport: eight
+    torch-free processes, 2 x 2 x 2 boxes of 256^3 (the bench's --gpus 8 partition), device
+    setup, RCCL halo exchange and captured cycles -- on one GPU, each process its own RCCL
+    "host" (tests/test_gpu_rccl.py) -- against one rank of the same box-numbered problem: every
+    rank's slice of the first V-cycle iterate bit-identical, and the same hierarchy."""
+    import raptor_amd as ra
+
+    from tests.test_gpu_rccl import run_rccl
+
+    t_start = time.perf_counter()
+
+    def say(msg):
+        with capfd.disabled():
+            print(f"[512^3 rccl {time.perf_counter() - t_start:7.1f}s] {msg}", flush=True)
+
+    n = DIMS[0] * DIMS[1] * DIMS[2]
+    report = {}
+    ctx = ra.Context.native(0)
+    A = ra.par_stencil_grid(ctx, "7pt", DIMS, boxes=(2, 2, 2))
+    t = time.perf_counter()
+    ml = ra.ParMultilevel(coarsen="pmis", smoother="jacobi", replicate_below=65536, use_graph=True).setup(A)
+    report["setup_1rank_s"] = time.perf_counter() - t
+    sizes1 = [[ml.level_info(l)["n_global"], ml.level_info(l)["nnz_global"]] for l in range(ml.num_levels)]
+    xs = ra.vector_uniform(ctx, n, 0, 42)
+    b = ctx.empty(n)
+    A.mult(xs, b)
+    x = ctx.zeros(n)
+    ml.cycle(x, b)
+    ctx.synchronize()
+    x1 = x.numpy()
+    assert np.all(np.isfinite(x1))
+    say(f"1 rank: setup {report['setup_1rank_s']:.1f}s, levels {sizes1}")
+    del ml, A, xs, b, x
+    ctx.synchronize()
+    del ctx
+
+    spec = dict(kind="7pt", dims=list(DIMS), boxes=[2, 2, 2], coarsen="pmis", smoother="jacobi", rep=65536,
+                native=True, graph=True, big=True)
+    res = run_rccl(NRANKS, spec, tmp_path, timeout=900)
+    say(f"{NRANKS} RCCL processes: setup {max(float(r['setup_s']) for r in res):.1f}s, "
+        f"cycle {max(float(r['cycle_ms']) for r in res):.1f} ms (one shared GPU, socket transport)")
+    assert [int(r["f"]) for r in res] == [q * n // NRANKS for q in range(NRANKS)]
+    for r in res:
+        assert r["levels"].tolist() == sizes1, "hierarchy differs between 1 rank and 8 RCCL ranks"
+        f, m = int(r["f"]), int(r["m"])
+        assert np.array_equal(r["x1"], x1[f:f + m]), f"rank slice [{f}, {f + m}) of the first V-cycle differs"
+        assert bool(r["graph_used"])
+    report.update(setup_8proc_s=max(float(r["setup_s"]) for r in res),
+                  cycle_8proc_ms=max(float(r["cycle_ms"]) for r in res), levels=sizes1)
+    rep_dir = os.environ.get("AMG_TEST_REPORT_DIR")
+    if rep_dir:
+        with open(os.path.join(rep_dir, "test_512_rccl_report.json"), "w") as fh:
+            json.dump(report, fh)
+    say(f"done: {report}")
