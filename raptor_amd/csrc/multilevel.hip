@@ -154,10 +154,11 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         // r5: a second worker builds each operator's GS structures as soon as its formats
         // exist (level 0 from the start), beside the format worker (sa27: 0.9 s of GS builds
         // after the hierarchy before)
-        std::unique_ptr<FormatWorker> worker, gs_worker;
+        std::unique_ptr<FormatWorker> worker, worker2, gs_worker;
         LevelDoneFn done = nullptr;
         if (overlap) {
             worker.reset(new FormatWorker(ctx->device));
+            worker2.reset(new FormatWorker(ctx->device));
             if (hgs) {
                 gs_worker.reset(new FormatWorker(ctx->device));
                 DevMatrix* a0 = &A;
@@ -179,15 +180,17 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
                 };
                 // A_{l+1} first: its GS structures start on the second worker while P_l and
                 // R_l are built
+                // (r5: P_l and R_l on a second format worker beside A_{l+1})
                 worker->push(job(preA[l + 1], H.levels[l + 1].A, l + 1));
-                worker->push(job(preP[l], H.levels[l].P, -1));
-                worker->push(job(preR[l], H.levels[l].R, -1));
+                worker2->push(job(preP[l], H.levels[l].P, -1));
+                worker2->push(job(preR[l], H.levels[l].R, -1));
             };
         }
         build_hierarchy(comm, A.host, opt, H, galerkin, level_fn, transpose_fn, done, rap_fn);
         images.e.clear();
         tm.lap("hierarchy (host + SpGEMM)");
         if (worker) worker->finish();  // before gs_worker: its jobs push GS jobs
+        if (worker2) worker2->finish();
         if (gs_worker) gs_worker->finish();
         if (overlap) tm.lap("format builds still running after the hierarchy");
     }
