@@ -1126,9 +1126,13 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
     send_idx.upload(sidx.data(), sidx.size());
     send_buf.alloc(sidx.size());
     halo.alloc(plan.n_halo());
-    seq = ctx->mat_seq++;  // collective order: the same id on every rank
-    if (ctx->transport == TR_LOOPBACK && !replicated)
+    // collective order: the same id on every rank.  Only the loopback transport matches
+    // matrices by it, and only one rank's setup builds formats on worker threads (several at
+    // once), so the counter is touched where it is used
+    if (ctx->transport == TR_LOOPBACK && !replicated) {
+        seq = ctx->mat_seq++;
         loopback_register(*ctx, seq, send_buf.p, plan.send_procs, plan.send_ptr);
+    }
 }
 
 // The one-kernel sweep's sliced ELL (hybrid_gs_kernel): every entry of the ELL slabs, with a
