@@ -321,6 +321,35 @@ def main():
         ml.solve(x, b, max_iter=args.warmup)
     x.zero_()
     ctx.synchronize()
+    graph_avail = ml.graph_enabled
+    # N > 1: graph replay or eager cycles, decided on this machine before the timed region
+    # (the one-GPU socket rehearsal favoured eager, xGMI is expected to
+    # favour replay): --steps cycles per mode, twice, alternating, max over ranks -- every rank
+    # sees the same times and takes the same mode; the faster is timed below, both are reported
+    mode_probe = None
+    if world > 1 and graph_avail and not args.no_graph:
+        pr = {"eager": [], "graph": []}
+        for _ in range(2):
+            for mode in ("eager", "graph"):
+                ml.set_graph(mode == "graph")
+                ml.solve(x, b, max_iter=max(1, args.warmup))  # (re)capture outside the timing
+                x.zero_()
+                ctx.synchronize()
+                barrier()
+                t = time.perf_counter()
+                ml.solve(x, b, max_iter=args.steps)
+                ctx.synchronize()
+                barrier()
+                pr[mode].append(round(comm.allreduce_max(time.perf_counter() - t) * 1e3 / args.steps, 4))
+        use_graph = min(pr["graph"]) <= min(pr["eager"])
+        ml.set_graph(use_graph)
+        ml.solve(x, b, max_iter=max(1, args.warmup))
+        x.zero_()
+        ctx.synchronize()
+        mode_probe = {"ms_per_step": pr, "chosen": "graph" if use_graph else "eager",
+                      "what": "before the timed region: --steps cycles per mode, twice, alternating; "
+                              "the mode with the smaller minimum is timed"}
+        log(rank, f"mode probe {pr}: timing {mode_probe['chosen']}")
 
     barrier()
     ctx.synchronize()
@@ -376,17 +405,18 @@ def main():
         reps = {"graph": [], "eager": []}
         for _ in range(3):
             for mode in ("eager", "graph"):
-                ml.set_graph(mode == "graph" and graph_used)
+                ml.set_graph(mode == "graph" and graph_avail)
                 ml.solve(x, b, max_iter=max(1, args.warmup))  # (re)capture outside the timing
                 t_m, _ = timed_solve(lambda: ml.solve(x, b, max_iter=args.steps))
                 reps[mode].append(round(t_m * 1e3 / args.steps, 4))
         ml.set_graph(graph_used)
         ml.solve(x, b, max_iter=max(1, args.warmup))
         med = {k: sorted(v)[1] for k, v in reps.items()}
-        modes = {"graph_ms_per_step": med["graph"] if graph_used else None,
+        modes = {"graph_ms_per_step": med["graph"] if graph_avail else None,
                  "eager_ms_per_step": med["eager"],
                  "repetitions_ms_per_step": reps,
                  "timed_mode": "graph" if graph_used else "eager",
+                 "mode_probe": mode_probe,
                  "what": "median of 3 alternating timed solves of --steps cycles per mode, same process"}
         log(rank, f"cycle modes (median of 3): graph {med['graph']} eager {med['eager']} ms/step")
 
