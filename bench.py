@@ -390,7 +390,8 @@ def main():
         if rank == 0:
             print(json.dumps({"metric": "V-cycle iters/sec (quick rehearsal line)", "value": round(value, 3),
                               "n_gpus": world, "steps": args.steps, "ms_per_step": round(dt * 1e3 / args.steps, 4),
-                              "grid": list(grid), "hipgraph_all_ranks": graph_all, "partition": part_label,
+                              "grid": list(grid), "hipgraph_all_ranks": graph_all, "graph_available": graph_avail,
+                              "mode_probe": mode_probe, "partition": part_label,
                               "setup_s": round(setup_s, 2)}), file=out_stream, flush=True)
         del ml, A
         if world > 1:
@@ -515,7 +516,8 @@ def main():
                 "setup_s": round(setup_s, 2),
                 "reorder_s": None if reorder_s is None else round(reorder_s, 2),
                 "hipgraph": graph_used,
-                "hipgraph_all_ranks": graph_all,
+                "hipgraph_all_ranks": graph_all,  # the timed mode (the probe's choice at N > 1)
+                "graph_available": graph_avail,
                 "gs_split_per_rank_level": gs_split,
             },
             "iters_per_s": round(iters_per_s, 3),
