@@ -602,6 +602,17 @@ __global__ void sa_rho_kernel(DCsr A, const double* d, double* rho) {
     rho[i] = s / fabs(d[i]);
 }
 
+// MIS(2) roots: flags for the exclusive scan that numbers them, then each root's aggregate id
+__global__ void root_flag_kernel(int n, const int* st, int* flag) {
+    const int i = blockIdx.x * kT + threadIdx.x;
+    if (i < n) flag[i] = st[i] == M_IN;
+}
+
+__global__ void root_id_kernel(int n, const int* st, const int* pos, int base, int* aggr) {
+    const int i = blockIdx.x * kT + threadIdx.x;
+    if (i < n) aggr[i] = st[i] == M_IN ? base + pos[i] : -1;
+}
+
 // ---- transpose: R = P^T, rows of R sorted by fine index (stable radix sort on columns) ---
 __global__ void iota_kernel(int n, int* v) {
     const int i = blockIdx.x * kT + threadIdx.x;
@@ -1221,9 +1232,13 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
         if ((dist ? comm.allreduce_sum((int64_t)left) : (int64_t)left) == 0) break;
     }
     // roots numbered in global row order (ranks in order); aggr = a root's aggregate id, -1
-    const std::vector<int32_t> hst = download_ints(s, st.p, n);
-    int64_t nroot = 0;
-    for (int32_t v : hst) nroot += v == M_IN;
+    // (r5: an exclusive scan of the root flags on the device, not a host pass over the states)
+    DevBuf<int> rflag, rpos;
+    rflag.alloc(nn + 1);
+    rpos.alloc(nn + 1);
+    HIP_CHECK(hipMemsetAsync(rflag.p, 0, sizeof(int) * rflag.n, s));
+    if (n) hipLaunchKernelGGL(root_flag_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, st.p, rflag.p);
+    const int64_t nroot = exclusive_scan(s, rflag.p, rpos.p, n, tmp);
     std::vector<int64_t> astarts(comm.nranks + 1, 0);
     {
         const std::vector<int64_t> counts = comm.allgather(nroot);
@@ -1231,11 +1246,11 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
     }
     const int64_t na = astarts[comm.nranks];
     AMG_CHECK(na < INT_MAX, "device setup: coarse level exceeds int32 indexing");
-    std::vector<int> haggr(nn, -1);
-    for (int i = 0, c = (int)astarts[comm.rank]; i < n; ++i)
-        if (hst[i] == M_IN) haggr[i] = c++;
     DevBuf<int> aggr, haggr_d, a1, ha1, agg;
-    aggr.upload(haggr.data(), haggr.size());
+    aggr.alloc(nn);
+    if (n)
+        hipLaunchKernelGGL(root_id_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, st.p, rpos.p,
+                           (int)astarts[comm.rank], aggr.p);
     haggr_d.alloc(1);
     ha1.alloc(1);
     a1.alloc(nn);
@@ -1259,13 +1274,21 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
     std::vector<int64_t> size((size_t)(ahi - alo), 0);
     std::vector<std::vector<int64_t>> sendc(comm.nranks);
     std::vector<int64_t> needa;
-    for (int i = 0; i < n; ++i) {
-        const int64_t a = split[i];
-        if (a >= alo && a < ahi) {
-            size[a - alo]++;
-        } else {
-            sendc[owner_of(astarts, a)].push_back(a);
-            needa.push_back(a);
+    if (!dist) {  // every aggregate is this rank's: counted in parallel (integer counts)
+#pragma omp parallel for schedule(static)
+        for (int i = 0; i < n; ++i) {
+#pragma omp atomic
+            size[split[i] - alo]++;
+        }
+    } else {
+        for (int i = 0; i < n; ++i) {
+            const int64_t a = split[i];
+            if (a >= alo && a < ahi) {
+                size[a - alo]++;
+            } else {
+                sendc[owner_of(astarts, a)].push_back(a);
+                needa.push_back(a);
+            }
         }
     }
     if (dist) {
@@ -1284,13 +1307,14 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
     rho.alloc(nn);
     if (n) hipLaunchKernelGGL(sa_rho_kernel, dim3(grid1(n)), dim3(kT), 0, s, Av, d.p, rho.p);
     HIP_CHECK(hipGetLastError());
-    std::vector<double> hrho(nn), hdiag(nn);
+    const bool host_merge = dist || !DA;  // the smoothing below on the host reads a_ii there
+    std::vector<double> hrho(nn), hdiag(host_merge ? nn : 0);
     HIP_CHECK(hipMemcpyAsync(hrho.data(), rho.p, sizeof(double) * nn, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipMemcpyAsync(hdiag.data(), d.p, sizeof(double) * nn, hipMemcpyDeviceToHost, s));
+    if (host_merge) HIP_CHECK(hipMemcpyAsync(hdiag.data(), d.p, sizeof(double) * nn, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    double r = 0.0;
-    for (int i = 0; i < n; ++i)
-        if (hrho[i] > r) r = hrho[i];
+    double r = 0.0;  // a maximum: the same value in any order
+#pragma omp parallel for schedule(static) reduction(max : r)
+    for (int i = 0; i < n; ++i) r = std::max(r, hrho[i]);
     if (dist) r = comm.allreduce_max(r);
     const double omega = (4.0 / 3.0) / r;
     const std::vector<double>& hd_loc = hdiag;
@@ -1302,7 +1326,9 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
     T.rp.resize((size_t)n + 1);
     T.col.resize(n);
     T.val.resize(n);
+#pragma omp parallel for schedule(static)
     for (int i = 0; i <= n; ++i) T.rp[i] = i;
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < n; ++i) {
         const int64_t a = split[i];
         const int64_t sz = (a >= alo && a < ahi) ? size[a - alo] : hsize[splan.find(a)];
