@@ -234,6 +234,7 @@ int amg_par_csr_create(amg_context ctx, int64_t n_global, int64_t first_row, int
         std::unique_ptr<amg_matrix_s> m(new amg_matrix_s());
         m->own.reset(new DevMatrix());
         m->m = m->own.get();
+        m->m->keep_setup_csr = true;  // the level-0 operator of a later solver setup
         m->m->build(&c, std::move(h));
         *out = m.release();
     });
@@ -251,6 +252,7 @@ int amg_par_stencil_create(amg_context ctx, int kind, int64_t nx, int64_t ny, in
         std::unique_ptr<amg_matrix_s> m(new amg_matrix_s());
         m->own.reset(new DevMatrix());
         m->m = m->own.get();
+        m->m->keep_setup_csr = true;  // the level-0 operator of a later solver setup
         m->m->build(&c, std::move(h));
         *out = m.release();
     });
@@ -268,6 +270,7 @@ int amg_par_stencil_create_boxes(amg_context ctx, int kind, int64_t nx, int64_t 
         std::unique_ptr<amg_matrix_s> m(new amg_matrix_s());
         m->own.reset(new DevMatrix());
         m->m = m->own.get();
+        m->m->keep_setup_csr = true;  // the level-0 operator of a later solver setup
         m->m->build(&c, std::move(h));
         *out = m.release();
     });
@@ -277,6 +280,7 @@ static void upload(Context& c, HostCSR&& h, amg_matrix* out) {
     std::unique_ptr<amg_matrix_s> m(new amg_matrix_s());
     m->own.reset(new DevMatrix());
     m->m = m->own.get();
+    m->m->keep_setup_csr = true;  // the level-0 operator of a later solver setup
     m->m->build(&c, std::move(h));
     *out = m.release();
 }

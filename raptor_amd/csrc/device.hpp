@@ -334,6 +334,12 @@ struct DevMatrix {
     // gs_ccol / gs_cval[0 / 1] = the same slabs' sliced ELL holding only those couplings, in
     // consumption order (backward: descending column) for gs_chain_kernel
     std::unique_ptr<DevMatrix> gs_old[2];
+    // r5: an operator the caller created (C-ABI constructors) keeps, on one rank, the CSR the
+    // device format build uploaded (row pointers, columns, values in row order) until a solver
+    // setup takes it as its level-0 image (SetupImages) instead of uploading the operator
+    // again; 12 B per nonzero while it is held
+    bool keep_setup_csr = false;
+    std::unique_ptr<DevCsr> setup_csr;
     DevBuf<int4> gs_cslabs[2];
     DevBuf<int> gs_ccol[2];
     DevBuf<double> gs_cval[2];

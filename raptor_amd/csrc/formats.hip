@@ -324,6 +324,17 @@ void build_formats_device(DevMatrix& M, const std::vector<int>& hrp, const hvec<
     HIP_CHECK(hipMemsetAsync(M.rend.p, 0, M.rend.n * sizeof(uint16_t), s));
     if (nbk) hipLaunchKernelGGL(row_end_kernel, dim3(nbk), dim3(kT), 0, s, M.blocks.p, M.rp.p, M.rend.p);
     HIP_CHECK(hipGetLastError());
+    // one rank, square, no halo: the local columns are the global ones -- the uploaded CSR is
+    // the solver setup's level-0 image (DevMatrix::setup_csr)
+    if (M.keep_setup_csr && M.square && !M.replicated && M.ctx->host.nranks == 1 && M.first_col == 0 &&
+        M.plan.n_halo() == 0) {
+        std::unique_ptr<DevCsr> d(new DevCsr());
+        d->rp32.alloc((size_t)M.n_rows + 1);
+        HIP_CHECK(hipMemcpyAsync(d->rp32.p, M.rp.p, sizeof(int) * (M.n_rows + 1), hipMemcpyDeviceToDevice, s));
+        d->col32 = std::move(dcol);
+        d->val = std::move(dval);
+        M.setup_csr = std::move(d);
+    }
     HIP_CHECK(hipStreamSynchronize(s));
 }
 

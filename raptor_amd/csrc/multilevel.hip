@@ -113,6 +113,8 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     // (SetupImages); only the next level's operator is carried over
     SetupImages images;
     SetupImages* im = opt.setup_device ? &images : nullptr;
+    // the level-0 operator's CSR left on the device by its format build (one rank)
+    if (im && A.setup_csr) images.put(A.host, std::move(A.setup_csr));
     if (opt.setup_device) {
         galerkin = [this, &comm](const HostCSR& X, const HostCSR& Y) {
             return spgemm_device(*ctx, comm, X, Y);
