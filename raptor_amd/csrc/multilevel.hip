@@ -114,7 +114,9 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     SetupImages images;
     SetupImages* im = opt.setup_device ? &images : nullptr;
     // the level-0 operator's CSR left on the device by its format build (one rank)
+    // (a host-side setup has no use for it: freed here either way)
     if (im && A.setup_csr) images.put(A.host, std::move(A.setup_csr));
+    A.setup_csr.reset();
     if (opt.setup_device) {
         galerkin = [this, &comm](const HostCSR& X, const HostCSR& Y) {
             return spgemm_device(*ctx, comm, X, Y);
