@@ -8,6 +8,7 @@
 #include <initializer_list>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "host.hpp"
@@ -143,6 +144,8 @@ struct Context {
     ncclComm_t nccl = nullptr;
     std::shared_ptr<LoopbackWorld> lb;
     void* lb_user = nullptr;  // host-exchange callback state for the loopback world
+    int lb_omp_threads = 0;   // the joining thread's OpenMP team size before the loopback share
+    std::thread::id lb_thread;
     int64_t mat_seq = 0;      // collective creation counter: matches matrices across ranks
     // RCCL ordering between graph-launched and eager work on this communicator:
     // `capturing` while a V-cycle is captured; `graph_inflight` from a multi-rank replay until

@@ -9,9 +9,11 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 
 #include <cstdio>
 #include <cstdlib>
+#include <omp.h>
 
 #include "device.hpp"
 
@@ -119,11 +121,17 @@ void loopback_join(Context& c, int rank, int nranks, const std::string& name) {
     c.host.fn = lb_alltoallv;
     c.host.user = c.lb_user;
     c.transport = TR_LOOPBACK;
+    // the ranks' host loops share the process's cores: each rank thread forks teams of
+    // 1/nranks of them (this thread's OpenMP setting only), not nranks full teams
+    c.lb_omp_threads = omp_get_max_threads();
+    c.lb_thread = std::this_thread::get_id();
+    omp_set_num_threads(std::max(1, c.lb_omp_threads / nranks));
     w->barrier();  // every rank's events exist before anyone waits on them
 }
 
 void loopback_leave(Context& c) {
     if (!c.lb) return;
+    if (c.lb_omp_threads > 0 && c.lb_thread == std::this_thread::get_id()) omp_set_num_threads(c.lb_omp_threads);
     delete static_cast<LbUser*>(c.lb_user);
     c.lb_user = nullptr;
     c.lb.reset();
