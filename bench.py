@@ -256,9 +256,9 @@ def main():
         for l in range(nlev - 1):
             if infos[l]["n_global"] // world < 100000:  # same decision on every rank
                 break
-            Al = A if l == 0 else ml.level_matrix(l, "A")
+            Al = A if l == 0 else ml.level_matrix(l, "A_cycle")
             nl = Al.local_rows
-            P, R = ml.level_matrix(l, "P"), ml.level_matrix(l, "R")
+            P, R = ml.level_matrix(l, "P_cycle"), ml.level_matrix(l, "R_cycle")
             nc = P.local_cols
             xl, bl, tl = ra.vector_uniform(ctx, nl, 0, 5), ra.vector_uniform(ctx, nl, 0, 6), ctx.empty(nl)
             xc, bc = ra.vector_uniform(ctx, nc, 0, 7), ctx.empty(R.local_rows)

@@ -236,7 +236,10 @@ typedef struct amg_level_info {
                                               stream (templates, CSR-VI blocks, sliced ELL) */
 } amg_level_info;
 int amg_solver_level_info(amg_solver S, int32_t level, amg_level_info* info);
-/* which: 0 = A_l, 1 = P_l, 2 = R_l.  Borrowed handle, valid while S lives. */
+/* which: 0 = A_l, 1 = P_l, 2 = R_l; 3, 4, 5 = the same operators as the V-cycle runs them
+   (a Jacobi level of a grid-built hierarchy runs its points in a private brick order on one
+   rank, DESIGN.md 4.1 r5: these operators then apply to vectors in that order; elsewhere they
+   are 0, 1, 2).  Borrowed handle, valid while S lives. */
 int amg_solver_level_matrix(amg_solver S, int32_t level, int32_t which, amg_matrix* out);
 /* Integer setup result of level l for the local rows: C/F marker (1 = C, 0 = F) for
  * RS/PMIS, global aggregate id for SA.  Bit-exact against the oracle. */

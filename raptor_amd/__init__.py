@@ -620,7 +620,10 @@ class ParMultilevel:
 
     def level_matrix(self, level: int, which: str = "A") -> ParCSRMatrix:
         h = C.c_void_p()
-        check(lib().amg_solver_level_matrix(self.h, int(level), {"A": 0, "P": 1, "R": 2}[which],
+        # "A" / "P" / "R": the hierarchy's operators; "A_cycle" / "P_cycle" / "R_cycle": the same
+        # operators as the V-cycle runs them (a private brick order on Jacobi levels)
+        check(lib().amg_solver_level_matrix(self.h, int(level), {"A": 0, "P": 1, "R": 2, "A_cycle": 3,
+                                                                 "P_cycle": 4, "R_cycle": 5}[which],
                                             C.byref(h)))
         return ParCSRMatrix(self.A.ctx, h, owner=self)
 

@@ -253,6 +253,9 @@ int amg_par_stencil_create(amg_context ctx, int kind, int64_t nx, int64_t ny, in
         m->own.reset(new DevMatrix());
         m->m = m->own.get();
         m->m->keep_setup_csr = true;  // the level-0 operator of a later solver setup
+        m->m->grid_local[0] = nx;     // a z-slab of whole (nx, ny) planes
+        m->m->grid_local[1] = ny;
+        m->m->grid_local[2] = (h.nrows() + nx * ny - 1) / (nx * ny);
         m->m->build(&c, std::move(h));
         *out = m.release();
     });
@@ -271,6 +274,12 @@ int amg_par_stencil_create_boxes(amg_context ctx, int kind, int64_t nx, int64_t 
         m->own.reset(new DevMatrix());
         m->m = m->own.get();
         m->m->keep_setup_csr = true;  // the level-0 operator of a later solver setup
+        if (bx * by * bz == c.host.nranks) {  // one box per rank: its extents (stencil_boxes' split)
+            const int64_t b = c.host.rank, ix = b % bx, iy = (b / bx) % by, iz = b / (bx * by);
+            m->m->grid_local[0] = nx * (ix + 1) / bx - nx * ix / bx;
+            m->m->grid_local[1] = ny * (iy + 1) / by - ny * iy / by;
+            m->m->grid_local[2] = nz * (iz + 1) / bz - nz * iz / bz;
+        }
         m->m->build(&c, std::move(h));
         *out = m.release();
     });
@@ -327,6 +336,13 @@ int amg_par_csr_reorder(amg_matrix A, int method, amg_matrix* out, int64_t* new_
 int amg_par_csr_info(amg_matrix A, amg_matrix_info* info) {
     return guard([&] {
         AMG_CHECK(A && info, "null argument");
+        // a level operator the cycle runs as a cycle-order copy: built here on one rank; on N
+        // ranks the build is collective (halo plan), so info reports its shape only (format
+        // fields 0) and the first compute call, which every rank makes, builds it
+        if (A->m->deferred && A->m->ctx->host.nranks == 1) {
+            set_device(*A->m->ctx);
+            A->m->ensure_built();
+        }
         const DevMatrix& m = *A->m;
         info->n_global_rows = m.host.n_global_rows;
         info->n_global_cols = m.host.n_global_cols;
@@ -368,6 +384,7 @@ int amg_par_csr_set_format(amg_matrix A, int32_t format) {
         AMG_CHECK(A, "null matrix");
         set_device(*A->m->ctx);
         HIP_CHECK(hipStreamSynchronize(A->m->ctx->stream));
+        A->m->ensure_built();
         A->m->set_format(format);
     });
 }
@@ -378,6 +395,7 @@ int amg_par_csr_format_digest(amg_matrix A, uint64_t* digest) {
         DevMatrix& M = *A->m;
         set_device(*M.ctx);
         HIP_CHECK(hipStreamSynchronize(M.ctx->stream));
+        M.ensure_built();
         uint64_t h = 1469598103934665603ull;
         auto mix = [&](const void* p, size_t bytes) {
             std::vector<unsigned char> b(bytes);
@@ -417,6 +435,7 @@ static int apply(amg_matrix A, int mode, const double* x, const double* b, doubl
         AMG_CHECK(A, "null matrix");
         AMG_CHECK((x || A->m->n_cols_local == 0) && (y || A->m->n_rows == 0), "null vector");
         set_device(*A->m->ctx);
+        A->m->ensure_built();
         par_apply(*A->m, mode, x, b, y, w, nullptr);
     });
 }
@@ -437,6 +456,7 @@ int amg_par_csr_hybrid_gs(amg_matrix A, const double* x, const double* b, double
         AMG_CHECK(A, "null matrix");
         AMG_CHECK(x != xo, "hybrid GS is out of place: x and x_out must differ");
         set_device(*A->m->ctx);
+        A->m->ensure_built();
         par_hybrid_gs(*A->m, x, b, xo, block);
     });
 }
@@ -447,6 +467,7 @@ int amg_par_csr_hybrid_gs_backward(amg_matrix A, const double* x, const double* 
         AMG_CHECK(A, "null matrix");
         AMG_CHECK(x != xo, "hybrid GS is out of place: x and x_out must differ");
         set_device(*A->m->ctx);
+        A->m->ensure_built();
         par_hybrid_gs(*A->m, x, b, xo, block, true);
     });
 }
@@ -471,6 +492,7 @@ int amg_par_csr_residual_norm(amg_matrix A, const double* x, const double* b, do
         AMG_CHECK(A && out, "null argument");
         Context& c = *A->m->ctx;
         set_device(c);
+        A->m->ensure_built();
         const size_t nb = (size_t)A->m->norm_parts_max(), tmpn = nb / 4096 + 64;
         DevBuf<double> r, buf;
         DevBuf<int> cnt;
@@ -531,6 +553,7 @@ int amg_solver_setup(amg_matrix A, const amg_options* opt, amg_solver* out) {
     return guard([&] {
         AMG_CHECK(A && opt && out, "null argument");
         set_device(*A->m->ctx);
+        A->m->ensure_built();
         auto* s = new amg_solver_s();
         try {
             s->s.setup(*A->m, *opt);
@@ -573,9 +596,14 @@ int amg_solver_level_matrix(amg_solver S, int32_t l, int32_t which, amg_matrix* 
     return guard([&] {
         AMG_CHECK(S && out, "null argument");
         AMG_CHECK(l >= 0 && l < (int32_t)S->s.levels.size(), "level out of range");
-        AMG_CHECK(which >= 0 && which <= 2, "which must be 0 (A), 1 (P) or 2 (R)");
-        DevMatrix* m = which == 0 ? &S->s.Amat(l)
-                                  : which == 1 ? S->s.levels[l].P.get() : S->s.levels[l].R.get();
+        AMG_CHECK(which >= 0 && which <= 5, "which must be 0 (A), 1 (P), 2 (R), or 3-5 (their cycle-order forms)");
+        Solver& s = S->s;
+        const bool coarsest = l + 1 == (int32_t)s.levels.size();
+        AMG_CHECK(which % 3 == 0 || !coarsest, "no such matrix on this level (the coarsest level has no P/R)");
+        DevMatrix* m = which == 0 ? &s.Amat(l)
+                     : which == 1 ? s.levels[l].P.get()
+                     : which == 2 ? s.levels[l].R.get()
+                     : which == 3 ? &s.CA(l) : which == 4 ? &s.CP(l) : &s.CR(l);
         AMG_CHECK(m, "no such matrix on this level (the coarsest level has no P/R)");
         std::unique_ptr<amg_matrix_s> v(new amg_matrix_s());
         v->m = m;

@@ -390,6 +390,12 @@ struct DevMatrix {
     // the format is first selected: local | halo column numbering, 2 padding entries)
     int format = AMG_FORMAT_AUTO;
     bool blocks_only = false;  // build only the CSR-block formats (the split-GS pass operators)
+    // local rows as a lexicographic box (x fastest) of these extents, when the operator came
+    // from a grid (stencil constructors); 0: unknown.  Only a locality hint (cycle order)
+    int64_t grid_local[3] = {0, 0, 0};
+    // build-time only: this rank's send lists index its column level through this map (old
+    // local position -> new; the cycle-order copies)
+    const std::vector<int64_t>* send_map = nullptr;
     DevBuf<int> pcol;
     DevBuf<double> pval;
     int plain_blocks() const { return (int)((n_rows + kTPB - 1) / kTPB); }
@@ -419,6 +425,11 @@ struct DevMatrix {
     // replicated: a whole matrix held by every rank (one-rank view, no halo, no exchange)
     bool replicated = false;
     void build(Context* c, HostCSR&& h, bool replicated_view = false);
+    // host CSR and shape only; the device formats wait for ensure_built() (a level operator
+    // the V-cycle runs as a cycle-order copy: built when a caller asks for it)
+    bool deferred = false;
+    void defer(Context* c, HostCSR&& h);
+    void ensure_built();
     // the same formats from a CSR that stays the caller's (moved into `host` afterwards)
     void build_view(Context* c, const HostCSR& h, bool replicated_view = false);
     void ensure_gs_blocks(int64_t block);
@@ -519,6 +530,10 @@ void par_residual_norm(DevMatrix& A, const double* x, const double* b, double* r
 
 struct Level {
     std::unique_ptr<DevMatrix> A, P, R;
+    // cycle-order copies: the same operators with this level's points (and
+    // the next level's) in a private brick order, entries of each row in the hierarchy's order;
+    // null where the cycle runs the operator above as it is
+    std::unique_ptr<DevMatrix> Ac, Pc, Rc;
     std::vector<int32_t> split;  // C/F or aggregate id (local rows)
     DevBuf<double> x, b, r, t;
 };
@@ -569,6 +584,10 @@ struct Solver {
     void drop_graph(Graph& G);  // destroy one exec once the stream has drained
 
     DevMatrix& Amat(size_t l) { return l == 0 ? *A0 : *levels[l].A; }
+    // the operators the cycle runs (cycle-order copies where they exist)
+    DevMatrix& CA(size_t l) { return l > 0 && levels[l].Ac ? *levels[l].Ac : Amat(l); }
+    DevMatrix& CP(size_t l) { return levels[l].Pc ? *levels[l].Pc : *levels[l].P; }
+    DevMatrix& CR(size_t l) { return levels[l].Rc ? *levels[l].Rc : *levels[l].R; }
     void setup(DevMatrix& A, const amg_options& o);
     // one V-cycle; with_norm: the first level-0 Jacobi sweep also appends ||b - A x_in||
     // to the device history (falls back to a separate residual when it cannot).  agree: the

@@ -88,6 +88,123 @@ class FormatWorker {
 
 }  // namespace
 
+// Cycle order.  A Jacobi-smoothed level's kernels form each row's products
+// and sum them in the row's stored order; neither depends on where the row sits or on the
+// numbering of its columns.  So the cycle may run a level's points in any order Pi, as long as
+// every operator touching the level carries the same Pi: A_l (rows and columns), P_l (rows),
+// R_l (columns), R_{l-1} (rows) and P_{l-1} (columns).  Each row keeps its entries in the
+// hierarchy's order, so every sum is the hierarchy's, bit for bit.  The order chosen is 8x8x8
+// bricks of the fine grid: a level point sits at the fine point of its restriction row's
+// first local column (for PMIS / RS its C point; for SA a fine point at its aggregate).  A
+// block of consecutive rows is then a compact piece of space, and its x tile holds fewer
+// lines than a block of a lexicographic slab (tests/analysis_brick_cut.py).  Grid-built
+// operators (stencil constructors: each rank knows its box or slab), Jacobi levels only
+// (hybrid-GS chunks are defined on the hierarchy's order), distributed levels only (not the
+// coarsest, not replicated ones).  On N ranks each rank orders its own points; its send lists
+// index its vectors through that order (DevMatrix::send_map), halo columns keep their global
+// ids.  AMG_CYCLE_ORDER=0 turns it off.
+namespace {
+// rows: new row -> old row, cols: old local column -> new (either empty: identity); halo
+// columns (other ranks' points) keep their global ids
+HostCSR permuted_csr(const HostCSR& M, int rank, const std::vector<int64_t>& rows, const std::vector<int64_t>& cols) {
+    const int64_t clo = M.col_starts[rank], chi = M.col_starts[rank + 1];
+    HostCSR B;
+    B.n_global_rows = M.n_global_rows;
+    B.n_global_cols = M.n_global_cols;
+    B.row_starts = M.row_starts;
+    B.col_starts = M.col_starts;
+    const int64_t n = M.nrows();
+    B.rp.assign((size_t)n + 1, 0);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t o = rows.empty() ? i : rows[i];
+        B.rp[i + 1] = M.rp[o + 1] - M.rp[o];
+    }
+    for (int64_t i = 0; i < n; ++i) B.rp[i + 1] += B.rp[i];
+    B.col.resize((size_t)M.nnz());
+    B.val.resize((size_t)M.nnz());
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t o = rows.empty() ? i : rows[i];
+        int64_t d = B.rp[i];
+        for (int64_t k = M.rp[o]; k < M.rp[o + 1]; ++k, ++d) {
+            const int64_t c = M.col[k];
+            B.col[d] = cols.empty() || c < clo || c >= chi ? c : clo + cols[c - clo];
+            B.val[d] = M.val[k];
+        }
+    }
+    return B;
+}
+
+// the brick orders of a hierarchy's levels, one level at a time as the setup produces them
+struct CycleOrder {
+    static constexpr int64_t kB = 8, kMinRows = 4096;
+    bool open = false;                             // the next level may still be permuted
+    int64_t g[3] = {0, 0, 0};                      // level-0 local grid extents
+    std::vector<char> on;                          // per level: permuted (the same on every rank)
+    std::vector<std::vector<int64_t>> perm, inv;   // this rank's points: new -> old, old -> new
+    std::vector<int64_t> at;                       // fine point of each point of the last level seen
+
+    void init(const DevMatrix& A, const amg_options& opt, const HostComm& comm, size_t maxl) {
+        const char* e = std::getenv("AMG_CYCLE_ORDER");  // read per setup (tests compare both)
+        std::copy(A.grid_local, A.grid_local + 3, g);
+        const bool mine = g[0] > 0 && g[1] > 0 && g[0] * g[1] * std::max<int64_t>(g[2], 1) >= A.n_rows;
+        open = !(e && std::atoi(e) == 0) && opt.smoother == AMG_SMOOTH_JACOBI &&
+               comm.allreduce_sum(mine ? 0 : 1) == 0;  // every rank's operator came from a grid
+        on.assign(maxl, 0);
+        perm.assign(maxl, {});
+        inv.assign(maxl, {});
+        if (!open) return;
+        at.resize((size_t)A.n_rows);
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < A.n_rows; ++i) at[i] = i;
+    }
+    bool any(size_t l) const { return l < on.size() && on[l]; }
+    // level l + 1's order, from R_l (its rows are level l + 1's points, ascending fine columns)
+    void next(size_t l, const HostCSR& R, const amg_options& opt, const HostComm& comm) {
+        if (!open) return;
+        const int64_t n = R.nrows(), ng = R.n_global_rows;
+        const int64_t flo = R.col_starts[comm.rank], fhi = R.col_starts[comm.rank + 1];
+        // large enough, not the coarsest level (dense-solved in the hierarchy's order) and not
+        // replicated (multi-rank coarse levels held whole on every rank)
+        if (ng < kMinRows || ng <= opt.max_coarse || (int)l + 2 >= opt.max_levels || l + 1 >= perm.size() ||
+            (comm.nranks > 1 && opt.replicate_below > 0 && ng <= opt.replicate_below)) {
+            open = false;
+            return;
+        }
+        on[l + 1] = 1;
+        std::vector<int64_t> up((size_t)n), key((size_t)n);
+        const int64_t nbx = (g[0] + kB - 1) / kB, nby = (g[1] + kB - 1) / kB, nbz = (g[2] + kB - 1) / kB;
+#pragma omp parallel for schedule(static)
+        for (int64_t c = 0; c < n; ++c) {
+            int64_t f = 0;  // the fine point of the row's first local column
+            for (int64_t k = R.rp[c]; k < R.rp[c + 1]; ++k)
+                if (R.col[k] >= flo && R.col[k] < fhi) {
+                    f = at[R.col[k] - flo];
+                    break;
+                }
+            const int64_t x = f % g[0], y = (f / g[0]) % g[1], z = f / (g[0] * g[1]);
+            up[c] = f;
+            key[c] = ((z / kB) * nby + y / kB) * nbx + x / kB;
+        }
+        at.swap(up);
+        // stable counting sort by brick
+        std::vector<int64_t> cnt((size_t)(nbx * nby * nbz) + 1, 0);
+        for (int64_t c = 0; c < n; ++c) ++cnt[key[c] + 1];
+        for (size_t b = 1; b < cnt.size(); ++b) cnt[b] += cnt[b - 1];
+        std::vector<int64_t>& p = perm[l + 1];
+        std::vector<int64_t>& q = inv[l + 1];
+        p.resize((size_t)n);
+        q.resize((size_t)n);
+        for (int64_t c = 0; c < n; ++c) {
+            const int64_t t = cnt[key[c]]++;
+            p[t] = c;
+            q[c] = t;
+        }
+    }
+};
+}  // namespace
+
 Solver::~Solver() {
     for (auto& g : graphs)
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
@@ -141,8 +258,22 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     // device formats of finished levels, built on a worker thread during the hierarchy
     const bool overlap = comm.nranks == 1 && setup_overlap();
     const size_t maxl = (size_t)std::max(opt.max_levels, 1) + 1;
-    std::vector<std::unique_ptr<DevMatrix>> preA(maxl), preP(maxl), preR(maxl);
+    std::vector<std::unique_ptr<DevMatrix>> preA(maxl), preP(maxl), preR(maxl), preAc(maxl), prePc(maxl), preRc(maxl);
     const bool hgs = opt.smoother == AMG_SMOOTH_HYBRID_GS;
+    // cycle order: the brick order of level l + 1 is fixed once R_l exists; the operators that
+    // touch a permuted level are built as cycle-order copies (their hierarchy-order formats wait
+    // for a caller that asks for them: DevMatrix::defer)
+    CycleOrder co;
+    co.init(A, opt, comm, maxl);
+    auto copy = [this, &comm](const HostCSR& M, const std::vector<int64_t>& rows, const std::vector<int64_t>& cols) {
+        std::unique_ptr<DevMatrix> d(new DevMatrix());
+        d->blocks_only = true;  // row templates assume ascending offsets
+        // what this rank sends of its column level: positions in that level's order
+        d->send_map = cols.empty() ? nullptr : &cols;
+        d->build(ctx, permuted_csr(M, comm.rank, rows, cols));
+        d->send_map = nullptr;
+        return d;
+    };
     // a level operator's hybrid-GS structures: l1 diagonals, slabs, templates,
     // the split sweep's old-value pass (built by ensure_gs_blocks), level 0's sliced ELL
     auto gs_build = [this](DevMatrix& Al, int l) {
@@ -185,9 +316,22 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
                 // A_{l+1} first: its GS structures start on the second worker while P_l and
                 // R_l are built
                 // (r5: P_l and R_l on a second format worker beside A_{l+1})
-                worker->push(job(preA[l + 1], H.levels[l + 1].A, l + 1));
-                worker2->push(job(preP[l], H.levels[l].P, -1));
-                worker2->push(job(preR[l], H.levels[l].R, -1));
+                co.next((size_t)l, H.levels[l].R, opt, comm);
+                const size_t a = (size_t)l + 1, p = (size_t)l;
+                if (co.any(a)) {
+                    const HostCSR* M = &H.levels[a].A;
+                    worker->push([&, a, M] { preAc[a] = copy(*M, co.perm[a], co.inv[a]); });
+                } else {
+                    worker->push(job(preA[a], H.levels[a].A, (int)a));
+                }
+                if (co.any(p) || co.any(a)) {
+                    const HostCSR *Ph = &H.levels[p].P, *Rh = &H.levels[p].R;
+                    worker2->push([&, a, p, Ph] { prePc[p] = copy(*Ph, co.perm[p], co.inv[a]); });
+                    worker2->push([&, a, p, Rh] { preRc[p] = copy(*Rh, co.perm[a], co.inv[p]); });
+                } else {
+                    worker2->push(job(preP[p], H.levels[p].P, -1));
+                    worker2->push(job(preR[p], H.levels[p].R, -1));
+                }
             };
         }
         build_hierarchy(comm, A.host, opt, H, galerkin, level_fn, transpose_fn, done, rap_fn);
@@ -207,13 +351,15 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
                 rep_level = (int)l;
                 break;
             }
+    if (!overlap)  // the brick orders (overlapped setups fixed them level by level)
+        for (size_t l = 0; l + 1 < H.levels.size(); ++l) co.next(l, H.levels[l].R, opt, comm);
     levels.clear();
     levels.resize(H.levels.size());
     RoctxRange rbuild("setup: device level formats");
     for (size_t l = 0; l < H.levels.size(); ++l) {
         HostLevel& hl = H.levels[l];
         const bool rep = rep_level >= 0 && (int)l >= rep_level;
-        auto make = [&](HostCSR& M, std::unique_ptr<DevMatrix>& pre) {
+        auto make = [&](HostCSR& M, std::unique_ptr<DevMatrix>& pre, bool cycle_copy) {
             std::unique_ptr<DevMatrix> d(std::move(pre));
             if (d) {
                 d->host = std::move(M);  // built from M on the worker
@@ -222,17 +368,37 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
             }
             d.reset(new DevMatrix());
             if (rep) d->build(ctx, gather_global(comm, M), true);
+            else if (cycle_copy) d->defer(ctx, std::move(M));  // the cycle runs its copy
             else d->build(ctx, std::move(M));
             return d;
         };
-        if (l > 0) levels[l].A = make(hl.A, preA[l]);
+        const bool pa = l > 0 && co.any(l), pr = co.any(l) || co.any(l + 1);
+        if (l > 0) levels[l].A = make(hl.A, preA[l], pa);
         if (!overlap) tm.lap("L" + std::to_string(l) + " device A build");
         if (l + 1 < H.levels.size()) {
             levels[l].split = std::move(hl.split);
-            levels[l].P = make(hl.P, preP[l]);
-            levels[l].R = make(hl.R, preR[l]);
+            levels[l].P = make(hl.P, preP[l], pr);
+            levels[l].R = make(hl.R, preR[l], pr);
             if (!overlap) tm.lap("L" + std::to_string(l) + " device P/R build");
         }
+    }
+    // cycle-order copies (built on the workers where the setup overlaps, here otherwise)
+    if (co.any(levels.size() - 1)) {
+        // the coarsening stalled on a permuted level, which became the (dense-solved) coarsest:
+        // the cycle runs the hierarchy's order
+        for (auto& L : levels)
+            for (DevMatrix* m : {L.A.get(), L.P.get(), L.R.get()})
+                if (m) m->ensure_built();
+    } else {
+        for (size_t l = 0; l < levels.size(); ++l) {
+            const bool pa = l > 0 && co.any(l), pr = l + 1 < levels.size() && (co.any(l) || co.any(l + 1));
+            if (pa) levels[l].Ac = preAc[l] ? std::move(preAc[l]) : copy(levels[l].A->host, co.perm[l], co.inv[l]);
+            if (pr) {
+                levels[l].Pc = prePc[l] ? std::move(prePc[l]) : copy(levels[l].P->host, co.perm[l], co.inv[l + 1]);
+                levels[l].Rc = preRc[l] ? std::move(preRc[l]) : copy(levels[l].R->host, co.perm[l + 1], co.inv[l]);
+            }
+        }
+        if (!overlap) tm.lap("cycle-order copies");
     }
     if (rep_level > 0) {  // transition: distributed R output -> whole vector on every rank
         const HostCSR& Rh = levels[rep_level - 1].R->host;
@@ -254,7 +420,7 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         }
         levels[l].r.alloc(n);
         levels[l].t.alloc(n);
-        max_blocks = std::max(max_blocks, (size_t)Al.norm_parts_max());
+        max_blocks = std::max({max_blocks, (size_t)Al.norm_parts_max(), (size_t)CA(l).norm_parts_max()});
         if (hgs) {
             gs_build(Al, (int)l);  // done on the GS worker already where the setup overlaps
             tm.lap("L" + std::to_string(l) + " GS structures");
@@ -333,7 +499,7 @@ void Solver::ensure_hist(int32_t n) {
 // the V-cycle is then a symmetric operator, as CG requires (oracle smooth()).
 void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_zero,
                     bool with_norm, bool post) {
-    DevMatrix& A = Amat(l);
+    DevMatrix& A = CA(l);
     if (with_norm && opt.smoother == AMG_SMOOTH_HYBRID_GS) {
         // forward GS sweep that also leaves the partials of ||b - A x|| (old x)
         AMG_ASSERT(!x_zero && !post);
@@ -365,7 +531,7 @@ static bool fuse_restrict_j0() {
 }
 
 void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool with_norm, bool x0_in_t) {
-    DevMatrix& A = Amat(l);
+    DevMatrix& A = CA(l);
     hipStream_t s = ctx->stream;
     const HostComm& comm = ctx->host;
     if (l + 1 == levels.size()) {
@@ -405,7 +571,7 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
         // distributed R output -> whole b_{l+1} on every rank (padded allgather + unpad)
         const int64_t cmax = rep_cmax, me = comm.rank;
         double* slot = rep_pad.p + cmax * comm.nranks;
-        par_apply(*L.R, KM_SPMV, L.r.p, nullptr, slot, 0.0, nullptr);
+        par_apply(CR(l), KM_SPMV, L.r.p, nullptr, slot, 0.0, nullptr);
         ctx->allgather(slot, rep_pad.p, (size_t)cmax);
         for (int q = 0; q < comm.nranks; ++q) {
             const int64_t cnt = rep_starts[q + 1] - rep_starts[q];
@@ -416,16 +582,16 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
         (void)me;
         cycle_rec(l + 1, C.x.p, C.b.p, true, false);
         // this rank's slice of the whole correction feeds the distributed interpolation
-        par_apply(*L.P, KM_SPMV_ADD, C.x.p + L.P->first_col, nullptr, cur, 0.0, nullptr);
+        par_apply(CP(l), KM_SPMV_ADD, C.x.p + L.P->first_col, nullptr, cur, 0.0, nullptr);
     } else {
         // Jacobi: the coarse level's first sweep from x = 0 (omega dinv b) rides along with
         // the restriction that produces b (one pass over b and a launch fewer per level)
         const bool j0 = opt.smoother == AMG_SMOOTH_JACOBI && opt.pre_sweeps >= 1 && l + 2 < levels.size() &&
                         fuse_restrict_j0() &&
-                        par_restrict_j0(*L.R, L.r.p, C.b.p, C.t.p, Amat(l + 1).dinv.p, opt.jacobi_omega);
-        if (!j0) par_apply(*L.R, KM_SPMV, L.r.p, nullptr, C.b.p, 0.0, nullptr);
+                        par_restrict_j0(CR(l), L.r.p, C.b.p, C.t.p, CA(l + 1).dinv.p, opt.jacobi_omega);
+        if (!j0) par_apply(CR(l), KM_SPMV, L.r.p, nullptr, C.b.p, 0.0, nullptr);
         cycle_rec(l + 1, C.x.p, C.b.p, true, false, j0);
-        par_apply(*L.P, KM_SPMV_ADD, C.x.p, nullptr, cur, 0.0, nullptr);
+        par_apply(CP(l), KM_SPMV_ADD, C.x.p, nullptr, cur, 0.0, nullptr);
     }
     for (int k = 0; k < opt.post_sweeps; ++k) smooth(l, cur, b, tmp, false, false, true);
     if (cur != x)
@@ -749,7 +915,8 @@ static int64_t spmv_bytes(const DevMatrix& M) {
 }
 
 int64_t Solver::bytes_per_cycle(size_t l) const {
-    const DevMatrix& A = const_cast<Solver*>(this)->Amat(l);
+    Solver& me = *const_cast<Solver*>(this);
+    const DevMatrix& A = me.CA(l);
     const int64_t n = A.n_rows;
     if (l + 1 == levels.size()) return 8 * coarse_n * n + 8 * coarse_n + 8 * n;
     const int64_t base = 12 * A.nnz + 4 * (n + 1);
@@ -764,8 +931,8 @@ int64_t Solver::bytes_per_cycle(size_t l) const {
     }
     if (zero) b += 8 * n;
     b += base + 24 * n;                                   // residual
-    b += spmv_bytes(*levels[l].R);                        // restriction
-    b += spmv_bytes(*levels[l].P) + 8 * n;                // interpolation (reads x)
+    b += spmv_bytes(me.CR(l));                            // restriction
+    b += spmv_bytes(me.CP(l)) + 8 * n;                    // interpolation (reads x)
     b += opt.post_sweeps * jac;
     sweeps += opt.post_sweeps;
     if (sweeps % 2 == 1) b += 16 * n;                     // copy back
@@ -779,7 +946,8 @@ namespace amg {
 // Mirrors cycle_rec(): per operation the stored-format bytes of the kernel that runs it
 // (DevMatrix::mode_bytes, the sliced-ELL stream for hybrid GS), plus the vector-only passes.
 int64_t Solver::stored_bytes_per_cycle(size_t l) const {
-    const DevMatrix& A = const_cast<Solver*>(this)->Amat(l);
+    Solver& me = *const_cast<Solver*>(this);
+    const DevMatrix& A = me.CA(l);  // the operators the cycle runs
     const int64_t n = A.n_rows;
     if (l + 1 == levels.size()) return 8 * coarse_n * n + 8 * coarse_n + 8 * n;
     const bool gs = opt.smoother == AMG_SMOOTH_HYBRID_GS;
@@ -788,7 +956,7 @@ int64_t Solver::stored_bytes_per_cycle(size_t l) const {
     bool zero = l > 0;
     int64_t sweeps = 0;
     // the sweep from zero fused into the restriction above (cycle_rec): dinv read + x write
-    const DevMatrix* Rup = l > 0 ? levels[l - 1].R.get() : nullptr;
+    const DevMatrix* Rup = l > 0 ? &me.CR(l - 1) : nullptr;
     const bool j0 = !gs && Rup && (int)l != rep_level && fuse_restrict_j0() && Rup->format != AMG_FORMAT_CSR &&
                     !Rup->tpl_on();
     // a split GS sweep from zero is its chain walk alone (par_hybrid_gs_from_zero)
@@ -800,8 +968,8 @@ int64_t Solver::stored_bytes_per_cycle(size_t l) const {
     }
     if (zero) b += 8 * n;
     b += A.mode_bytes(KM_RESID);
-    b += levels[l].R->mode_bytes(KM_SPMV);
-    b += levels[l].P->mode_bytes(KM_SPMV_ADD);
+    b += me.CR(l).mode_bytes(KM_SPMV);
+    b += me.CP(l).mode_bytes(KM_SPMV_ADD);
     b += opt.post_sweeps * sweep;
     sweeps += opt.post_sweeps;
     if (sweeps % 2 == 1) b += 16 * n;  // copy back

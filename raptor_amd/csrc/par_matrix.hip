@@ -655,6 +655,26 @@ void DevMatrix::build(Context* c, HostCSR&& h, bool replicated_view) {
     host = std::move(h);
 }
 
+void DevMatrix::defer(Context* c, HostCSR&& h) {
+    ctx = c;
+    replicated = false;
+    host = std::move(h);
+    const HostComm& comm = ctx->host;
+    first_row = host.row_starts[comm.rank];
+    n_rows = host.nrows();
+    first_col = host.col_starts[comm.rank];
+    n_cols_local = host.col_starts[comm.rank + 1] - first_col;
+    nnz = host.nnz();
+    square = host.n_global_rows == host.n_global_cols && host.row_starts == host.col_starts;
+    deferred = true;
+}
+
+void DevMatrix::ensure_built() {
+    if (!deferred) return;
+    build_view(ctx, host);
+    deferred = false;
+}
+
 // Every device format from a CSR the caller keeps (the member `host` is shadowed by the
 // argument): Solver::setup runs this on a worker thread while the hierarchy thread still
 // reads the same CSR, and moves it into `host` after both are done.
@@ -675,6 +695,8 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
     AMG_CHECK(nnz < INT_MAX && n_rows < INT_MAX, "local matrix exceeds int32 indexing");
     square = host.n_global_rows == host.n_global_cols && host.row_starts == host.col_starts;
     plan = halo_plan_for_cols(comm, host);
+    if (send_map && !replicated)
+        for (int64_t& v : plan.send_idx) v = (*send_map)[v];
     AMG_CHECK(n_cols_local + plan.n_halo() < INT_MAX, "too many columns for int32");
     tm.lap("    build: halo plan");
 

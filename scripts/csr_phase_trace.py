@@ -70,7 +70,7 @@ def main():
     ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
     report = {"grid": N, "ops": []}
     for l in (1, 2):
-        Al = ml.level_matrix(l, "A")
+        Al = ml.level_matrix(l, "A_cycle")
         n = Al.local_rows
         x, b, t = ra.vector_uniform(ctx, n, 0, 5), ra.vector_uniform(ctx, n, 0, 6), ctx.empty(n)
         for name, fn in (("residual", lambda: Al.residual(x, b, t)), ("Jacobi", lambda: Al.jacobi(x, b, t))):
