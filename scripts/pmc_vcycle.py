@@ -33,8 +33,9 @@ def marker(idx):
 for l in range(ml.num_levels - 1):
     if ml.level_info(l)["n_global"] < 100000:
         break
-    Al = A if l == 0 else ml.level_matrix(l, "A")
-    P, R = ml.level_matrix(l, "P"), ml.level_matrix(l, "R")
+    # the operators as the cycle runs them (cycle-order copies on Jacobi levels)
+    Al = A if l == 0 else ml.level_matrix(l, "A_cycle")
+    P, R = ml.level_matrix(l, "P_cycle"), ml.level_matrix(l, "R_cycle")
     nl, nc = Al.local_rows, P.local_cols
     xl, bl, tl = ra.vector_uniform(ctx, nl, 0, 5), ra.vector_uniform(ctx, nl, 0, 6), ctx.empty(nl)
     xc, bc = ra.vector_uniform(ctx, nc, 0, 7), ctx.empty(R.local_rows)
