@@ -55,6 +55,19 @@ def test_cycle_order_bit_identical(ctx, oracle, monkeypatch, case):
     e1, e1c = A1.export(), A1c.export()
     assert not (np.array_equal(e1[1], e1c[1]) and np.array_equal(e1[0], e1c[0])), "no cycle order"
     assert _is_brick_copy(A1, A1c)
+    # the hierarchy-order operator's formats wait for a caller (DevMatrix::defer): its first
+    # compute call builds them, and it applies in the hierarchy's order
+    m1 = A1.local_rows
+    x1h, b1h = O.vec_uniform(m1, 5), O.vec_uniform(m1, 6)
+    r1 = ctx.empty(m1)
+    A1.residual(to_dev(ctx, x1h), to_dev(ctx, b1h), r1)
+    A1o = O.Csr.from_arrays(m1, m1, *e1)
+    assert np.array_equal(to_host(ctx, r1), A1o.residual(x1h, b1h))
+    P0 = ml.level_matrix(0, "P")
+    e = ctx.empty(n)
+    P0.mult(to_dev(ctx, x1h), e)
+    rp, col, val = P0.export()
+    assert np.array_equal(to_host(ctx, e), O.Csr.from_arrays(n, m1, rp, col, val).spmv(x1h))
     b = O.vec_uniform(n, 31)
     db = to_dev(ctx, b)
     xs = _cycles(ctx, ml, db, n, 3)
