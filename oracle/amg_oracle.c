@@ -398,7 +398,13 @@ orc_csr* orc_strength_classical(const orc_csr* A, double theta) {
     return S;
 }
 
-/* symmetric (SA): j != i strong iff |a_ij| >= theta * sqrt(|a_ii * a_jj|) */
+/* symmetric, signed (SA, r6): j != i strong iff -a_ij >= theta * sqrt(|a_ii * a_jj|).
+ * Positive couplings are never strong: the 27-pt Q1 operator's +16 z couplings (eps_z = 1e-3)
+ * made |a_ij| aggregates span the weakly coupled direction. */
+static int sa_strong(double aij, double di, double dj, double theta) {
+    return -aij >= theta * sqrt(fabs(di * dj));
+}
+
 orc_csr* orc_strength_symmetric(const orc_csr* A, double theta) {
     int64_t n = A->n_rows, nnz = 0;
     double* d = XMALLOC(double, n);
@@ -409,7 +415,7 @@ orc_csr* orc_strength_symmetric(const orc_csr* A, double theta) {
         for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
             int64_t j = A->col[k];
             if (j == i) continue;
-            if (fabs(A->val[k]) >= theta * sqrt(fabs(d[i] * d[j]))) {
+            if (sa_strong(A->val[k], d[i], d[j], theta)) {
                 S->col[nnz] = j;
                 S->val[nnz++] = A->val[k];
             }
@@ -717,10 +723,73 @@ int64_t orc_mis2_aggregate(const orc_csr* S, uint64_t seed, int32_t* agg) {
     return na;
 }
 
-/* Smoothed prolongator (row a9): T_i,agg(i) = 1/sqrt(|agg|);  rho = max_i
- * (sum_k |a_ik|) / |a_ii|;  omega = (4/3)/rho;  P_ij = T_ij - (omega * dinv_i) * (AT)_ij
- * over the union pattern. */
-orc_csr* orc_sa_prolongator(const orc_csr* A, const int32_t* agg, int64_t n_agg) {
+double orc_sa_theta_next(double theta) { return theta * 0.75; }
+
+/* Filtered operator of SA smoothing (row a9, r6): the diagonal and the strong off-diagonals
+ * (sa_strong, the strength test above) in CSR order; the diagonal value becomes
+ * f_i = a_ii + the weak off-diagonal a_ij, added in row order.  Row sums are kept. */
+orc_csr* orc_sa_filter(const orc_csr* A, double theta) {
+    int64_t n = A->n_rows, nnz = 0;
+    double* d = XMALLOC(double, n);
+    for (int64_t i = 0; i < n; ++i) d[i] = diag_of(A, i);
+    orc_csr* F = csr_alloc(n, A->n_cols, orc_csr_nnz(A));
+    F->rp[0] = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        double f = d[i];
+        for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
+            int64_t j = A->col[k];
+            if (j != i && !sa_strong(A->val[k], d[i], d[j], theta)) f += A->val[k];
+        }
+        for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
+            int64_t j = A->col[k];
+            if (j == i) {
+                F->col[nnz] = j;
+                F->val[nnz++] = f;
+            } else if (sa_strong(A->val[k], d[i], d[j], theta)) {
+                F->col[nnz] = j;
+                F->val[nnz++] = A->val[k];
+            }
+        }
+        F->rp[i + 1] = nnz;
+    }
+    free(d);
+    return F;
+}
+
+/* rho(D^-1 A_F), D = diag(A) (row a9, r6): ORC_SA_RHO_ITERS power steps normalised in the max
+ * norm, which is exact in any order (so the same on every partition): x = u / max|u| with
+ * u = vec_uniform(seed); per step y_i = (A_F x)_i / a_ii (row_dot order), lam = max|y_i|,
+ * stop if lam = 0, else x = y / lam.  Returns the last lam. */
+double orc_sa_rho(const orc_csr* F, const double* d, uint64_t seed) {
+    int64_t n = F->n_rows;
+    double* x = XMALLOC(double, n);
+    double* y = XMALLOC(double, n);
+    orc_vec_uniform(n, 0, seed, x);
+    double m = 0.0;
+    for (int64_t i = 0; i < n; ++i) m = fabs(x[i]) > m ? fabs(x[i]) : m;
+    if (m > 0.0)
+        for (int64_t i = 0; i < n; ++i) x[i] = x[i] / m;
+    double lam = 0.0;
+    for (int it = 0; it < ORC_SA_RHO_ITERS; ++it) {
+        lam = 0.0;
+        for (int64_t i = 0; i < n; ++i) {
+            y[i] = row_dot(F, i, x) / d[i];
+            lam = fabs(y[i]) > lam ? fabs(y[i]) : lam;
+        }
+        if (lam == 0.0) break;
+        for (int64_t i = 0; i < n; ++i) x[i] = y[i] / lam;
+    }
+    free(x);
+    free(y);
+    return lam;
+}
+
+/* Smoothed prolongator (row a9; r6 definition): T_i,agg(i) = 1/sqrt(|agg|); A_F =
+ * orc_sa_filter(A, theta); rho = orc_sa_rho(A_F, diag A, seed); omega = (4/3)/rho (0 if
+ * rho = 0); P_ij = T_ij - (omega * (1/a_ii)) * (A_F T)_ij over the union pattern (A_F T by
+ * orc_spgemm: each entry summed from 0.0 over A_F's row in order). */
+orc_csr* orc_sa_prolongator(const orc_csr* A, const int32_t* agg, int64_t n_agg, double theta,
+                            uint64_t seed) {
     int64_t n = A->n_rows;
     int64_t* size = XMALLOC(int64_t, n_agg);
     for (int64_t a = 0; a < n_agg; ++a) size[a] = 0;
@@ -732,20 +801,17 @@ orc_csr* orc_sa_prolongator(const orc_csr* A, const int32_t* agg, int64_t n_agg)
         T->val[i] = 1.0 / sqrt((double)size[agg[i]]);
         T->rp[i + 1] = i + 1;
     }
-    double rho = 0.0;
-    for (int64_t i = 0; i < n; ++i) {
-        double s = 0.0;
-        for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) s += fabs(A->val[k]);
-        double r = s / fabs(diag_of(A, i));
-        if (r > rho) rho = r;
-    }
-    double omega = (4.0 / 3.0) / rho;
-    orc_csr* AT = orc_spgemm(A, T);
+    double* d = XMALLOC(double, n);
+    for (int64_t i = 0; i < n; ++i) d[i] = diag_of(A, i);
+    orc_csr* F = orc_sa_filter(A, theta);
+    double rho = orc_sa_rho(F, d, seed);
+    double omega = rho > 0.0 ? (4.0 / 3.0) / rho : 0.0;
+    orc_csr* AT = orc_spgemm(F, T);
     orc_csr* P = csr_alloc(n, n_agg, orc_csr_nnz(AT) + n);
     int64_t nnz = 0;
     P->rp[0] = 0;
     for (int64_t i = 0; i < n; ++i) {
-        double c = omega * (1.0 / diag_of(A, i));
+        double c = omega * (1.0 / d[i]);
         int64_t ka = AT->rp[i], ea = AT->rp[i + 1], kt = T->rp[i], et = T->rp[i + 1];
         while (ka < ea || kt < et) {
             int64_t ja = ka < ea ? AT->col[ka] : INT64_MAX, jt = kt < et ? T->col[kt] : INT64_MAX;
@@ -759,7 +825,9 @@ orc_csr* orc_sa_prolongator(const orc_csr* A, const int32_t* agg, int64_t n_agg)
         P->rp[i + 1] = nnz;
     }
     orc_csr_free(AT);
+    orc_csr_free(F);
     orc_csr_free(T);
+    free(d);
     free(size);
     return P;
 }
@@ -835,16 +903,17 @@ orc_hier* orc_hier_setup(const orc_csr* A0, const orc_options* opt) {
     H->A[0] = orc_csr_new(A0->n_rows, A0->n_cols, A0->rp, A0->col, A0->val);
     int32_t l = 0;
     int32_t maxl = opt->max_levels < ORC_MAX_LEVELS ? opt->max_levels : ORC_MAX_LEVELS;
-    while (l + 1 < maxl && H->A[l]->n_rows > opt->max_coarse) {
+    double theta = opt->strong_threshold;
+    for (; l + 1 < maxl && H->A[l]->n_rows > opt->max_coarse; theta = orc_sa_theta_next(theta)) {
         orc_csr* A = H->A[l];
         int64_t n = A->n_rows;
         int32_t* split = XMALLOC(int32_t, n);
         orc_csr* P;
         if (opt->coarsen == ORC_COARSEN_SA) {
-            /* Vanek-Mandel-Brezina: theta_l = theta_0 * (1/2)^l */
-            orc_csr* S = orc_strength_symmetric(A, ldexp(opt->strong_threshold, -l));
+            /* theta_l = theta_{l-1} * 3/4 (r6; rounded per level) */
+            orc_csr* S = orc_strength_symmetric(A, theta);
             int64_t na = orc_mis2_aggregate(S, opt->seed + (uint64_t)l, split);
-            P = orc_sa_prolongator(A, split, na);
+            P = orc_sa_prolongator(A, split, na, theta, opt->seed + (uint64_t)l);
             orc_csr_free(S);
         } else {
             orc_csr* S = orc_strength_classical(A, opt->strong_threshold);

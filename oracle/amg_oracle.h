@@ -72,7 +72,14 @@ void orc_rs_split(const orc_csr* S, int32_t* cf);   /* cf: 1 = C, 0 = F */
 void orc_pmis_split(const orc_csr* S, uint64_t seed, int32_t* cf);
 orc_csr* orc_interp_classical(const orc_csr* A, const orc_csr* S, const int32_t* cf);
 int64_t orc_mis2_aggregate(const orc_csr* S, uint64_t seed, int32_t* agg);
-orc_csr* orc_sa_prolongator(const orc_csr* A, const int32_t* agg, int64_t n_agg);
+/* SA smoothing (r6): filtered operator, max-norm power-iteration rho, smoothed P */
+#define ORC_SA_RHO_ITERS 10
+orc_csr* orc_sa_filter(const orc_csr* A, double theta);
+double orc_sa_rho(const orc_csr* F, const double* d, uint64_t seed);
+orc_csr* orc_sa_prolongator(const orc_csr* A, const int32_t* agg, int64_t n_agg, double theta,
+                            uint64_t seed);
+/* SA strength threshold of the next level: theta * 0.75 */
+double orc_sa_theta_next(double theta);
 void orc_dense_inverse(int64_t n, const orc_csr* A, double* inv); /* row-major n*n */
 
 /* unstructured inputs (io_oracle.c, row f2; specs in DESIGN.md 8) */

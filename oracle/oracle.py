@@ -86,7 +86,10 @@ def lib():
             "orc_pmis_split": (None, [vp, C.c_uint64, _i32p]),
             "orc_interp_classical": (vp, [vp, vp, _i32p]),
             "orc_mis2_aggregate": (C.c_int64, [vp, C.c_uint64, _i32p]),
-            "orc_sa_prolongator": (vp, [vp, _i32p, C.c_int64]),
+            "orc_sa_prolongator": (vp, [vp, _i32p, C.c_int64, C.c_double, C.c_uint64]),
+            "orc_sa_filter": (vp, [vp, C.c_double]),
+            "orc_sa_rho": (C.c_double, [vp, _f64p, C.c_uint64]),
+            "orc_sa_theta_next": (C.c_double, [C.c_double]),
             "orc_dense_inverse": (None, [C.c_int64, vp, _f64p]),
             "orc_hier_setup": (vp, [vp, C.POINTER(_Opt)]),
             "orc_hier_free": (None, [vp]),
@@ -291,9 +294,23 @@ def mis2_aggregate(S, seed):
     return agg, na
 
 
-def sa_prolongator(A, agg, n_agg):
+def sa_prolongator(A, agg, n_agg, theta, seed):
     agg = np.ascontiguousarray(agg, np.int32)
-    return Csr(lib().orc_sa_prolongator(A.h, _p(agg, _i32p), n_agg))
+    return Csr(lib().orc_sa_prolongator(A.h, _p(agg, _i32p), n_agg, theta, seed))
+
+
+def sa_filter(A, theta):
+    """SA smoothing's filtered operator."""
+    return Csr(lib().orc_sa_filter(A.h, theta))
+
+
+def sa_rho(F, d, seed):
+    d = np.ascontiguousarray(d, np.float64)
+    return lib().orc_sa_rho(F.h, _p(d, _f64p), seed)
+
+
+def sa_theta_next(theta):
+    return lib().orc_sa_theta_next(theta)
 
 
 def dense_inverse(A):

@@ -10,6 +10,7 @@
 // C-ABI, torch.distributed/gloo in the Python host layer); the solve-time data path never
 // touches it (RCCL, see device.hpp).
 #pragma once
+#include <cmath>
 #include <cstdint>
 #include <deque>
 #include <functional>
@@ -171,8 +172,21 @@ HostCSR interp_classical(const HostComm& comm, const HostCSR& A, const HostCSR& 
 // returns global aggregate id per local row; *n_agg_global receives the count
 std::vector<int64_t> mis2_aggregate(const HostComm& comm, const HostCSR& S, uint64_t seed,
                                     int64_t* n_agg_global, std::vector<int64_t>* agg_starts);
+// SA: the signed strength test; theta of level l (theta_0 * 0.75 per level,
+// rounded per level); the filtered operator; rho(D^-1 A_F) by kSaRhoIters max-norm power
+// steps; P = T - (4/3 rho) (1/a_ii) A_F T
+constexpr int kSaRhoIters = 10;
+inline bool sa_strong(double aij, double di, double dj, double theta) {
+    return -aij >= theta * std::sqrt(std::fabs(di * dj));
+}
+inline double sa_theta(double theta0, int level) {
+    double t = theta0;
+    for (int l = 0; l < level; ++l) t = t * 0.75;
+    return t;
+}
+HostCSR sa_filter(const HostComm& comm, const HostCSR& A, double theta);
 HostCSR sa_prolongator(const HostComm& comm, const HostCSR& A, const std::vector<int64_t>& agg,
-                       int64_t n_agg, const std::vector<int64_t>& agg_starts);
+                       int64_t n_agg, const std::vector<int64_t>& agg_starts, double theta, uint64_t seed);
 // every rank receives the whole matrix (rows in global order); the result is a one-rank
 // matrix (row_starts {0, n}, col_starts {0, n_cols}) for replicated coarse levels
 HostCSR gather_global(const HostComm& comm, const HostCSR& M);

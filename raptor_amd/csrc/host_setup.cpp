@@ -86,7 +86,7 @@ HostCSR strength_classical(const HostComm& comm, const HostCSR& A, double theta)
     });
 }
 
-// symmetric: |a_ij| >= theta * sqrt(|a_ii * a_jj|), j != i
+// SA, signed (r6): -a_ij >= theta * sqrt(|a_ii * a_jj|), j != i (sa_strong)
 HostCSR strength_symmetric(const HostComm& comm, const HostCSR& A, double theta) {
     int64_t lo = A.row_starts[comm.rank], hi = A.row_starts[comm.rank + 1];
     std::vector<double> d = diagonal(comm, A);
@@ -97,8 +97,34 @@ HostCSR strength_symmetric(const HostComm& comm, const HostCSR& A, double theta)
         int64_t j = A.col[k];
         if (j == lo + i) return false;
         double dj = (j >= lo && j < hi) ? d[j - lo] : hd[plan.find(j)];
-        return std::fabs(A.val[k]) >= theta * std::sqrt(std::fabs(d[i] * dj));
+        return sa_strong(A.val[k], d[i], dj, theta);
     });
+}
+
+// SA's filtered operator (r6; oracle orc_sa_filter): the diagonal and the strong off-diagonals
+// in row order; the diagonal value becomes a_ii + the weak off-diagonals (row order)
+HostCSR sa_filter(const HostComm& comm, const HostCSR& A, double theta) {
+    int64_t lo = A.row_starts[comm.rank], hi = A.row_starts[comm.rank + 1];
+    std::vector<double> d = diagonal(comm, A);
+    HaloPlan plan = halo_plan_for_cols(comm, A);
+    std::vector<double> hd(plan.n_halo());
+    plan.forward(comm, d.data(), hd.data());
+    auto strong = [&](int64_t i, int64_t k) {
+        int64_t j = A.col[k];
+        double dj = (j >= lo && j < hi) ? d[j - lo] : hd[plan.find(j)];
+        return sa_strong(A.val[k], d[i], dj, theta);
+    };
+    HostCSR F = filter_rows(A, [&](int64_t i, int64_t k) { return A.col[k] == lo + i || strong(i, k); });
+    const int64_t n = A.nrows();
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        double f = d[i];
+        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k)
+            if (A.col[k] != lo + i && !strong(i, k)) f += A.val[k];
+        for (int64_t k = F.rp[i]; k < F.rp[i + 1]; ++k)
+            if (F.col[k] == lo + i) F.val[k] = f;
+    }
+    return F;
 }
 
 // local transpose pattern of the local-local part of S (row i -> local j with i in S_j)
@@ -482,8 +508,9 @@ std::vector<int64_t> mis2_aggregate(const HostComm& comm, const HostCSR& S, uint
 }
 
 HostCSR sa_prolongator(const HostComm& comm, const HostCSR& A, const std::vector<int64_t>& agg,
-                       int64_t n_agg, const std::vector<int64_t>& agg_starts) {
+                       int64_t n_agg, const std::vector<int64_t>& agg_starts, double theta, uint64_t seed) {
     int64_t n = A.nrows(), alo = agg_starts[comm.rank], ahi = agg_starts[comm.rank + 1];
+    int64_t lo = A.row_starts[comm.rank], hi = A.row_starts[comm.rank + 1];
     // aggregate sizes: owners sum member counts
     std::vector<int64_t> size(ahi - alo, 0);
     std::vector<std::vector<int64_t>> sendc(comm.nranks);
@@ -517,16 +544,43 @@ HostCSR sa_prolongator(const HostComm& comm, const HostCSR& A, const std::vector
         T.rp[i + 1] = i + 1;
     }
     std::vector<double> d = diagonal(comm, A);
-    double rho = 0.0;
-    for (int64_t i = 0; i < n; ++i) {
-        double s = 0.0;
-        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) s += std::fabs(A.val[k]);
-        double r = s / std::fabs(d[i]);
-        if (r > rho) rho = r;
+    HostCSR F = sa_filter(comm, A, theta);
+    // rho(D^-1 A_F): power steps in the max norm from x = u / max|u| (u = the seeded uniform
+    // vector of the global ids); maxima are exact in any order, so every partition agrees
+    HaloPlan fplan = halo_plan_for_cols(comm, F);
+    std::vector<int64_t> where(F.nnz());  // >= 0 local index, < 0: -(halo index + 1)
+    for (int64_t k = 0; k < F.nnz(); ++k) {
+        int64_t j = F.col[k];
+        where[k] = (j >= lo && j < hi) ? j - lo : -(fplan.find(j) + 1);
     }
-    rho = comm.allreduce_max(rho);
-    double omega = (4.0 / 3.0) / rho;
-    HostCSR AT = spgemm(comm, A, T);
+    std::vector<double> x(n), y(n), hx(fplan.n_halo());
+    for (int64_t i = 0; i < n; ++i) {
+        uint64_t u = mix64(seed * 0xD1B54A32D192ED03ull + (uint64_t)(lo + i));
+        x[i] = (double)(u >> 11) * 0x1.0p-52 - 1.0;
+    }
+    double m = 0.0;
+    for (int64_t i = 0; i < n; ++i) m = std::max(m, std::fabs(x[i]));
+    m = comm.allreduce_max(m);
+    if (m > 0.0)
+        for (int64_t i = 0; i < n; ++i) x[i] = x[i] / m;
+    double rho = 0.0;
+    for (int it = 0; it < kSaRhoIters; ++it) {
+        fplan.forward(comm, x.data(), hx.data());
+        double lam = 0.0;
+#pragma omp parallel for schedule(static) reduction(max : lam)
+        for (int64_t i = 0; i < n; ++i) {
+            double s = 0.0;
+            for (int64_t k = F.rp[i]; k < F.rp[i + 1]; ++k)
+                s += F.val[k] * (where[k] >= 0 ? x[where[k]] : hx[-where[k] - 1]);
+            y[i] = s / d[i];
+            lam = std::max(lam, std::fabs(y[i]));
+        }
+        rho = comm.allreduce_max(lam);
+        if (rho == 0.0) break;
+        for (int64_t i = 0; i < n; ++i) x[i] = y[i] / rho;
+    }
+    double omega = rho > 0.0 ? (4.0 / 3.0) / rho : 0.0;
+    HostCSR AT = spgemm(comm, F, T);
     HostCSR P;
     P.n_global_rows = A.n_global_rows;
     P.n_global_cols = n_agg;
@@ -623,14 +677,15 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
         if (level_fn && level_fn(l, A, P, split)) {
             tm.lap(L + "device strength + split / aggregates + P");
         } else if (opt.coarsen == AMG_COARSEN_SA) {
-            HostCSR S = strength_symmetric(comm, A, std::ldexp(opt.strong_threshold, -l));
+            const double theta = sa_theta(opt.strong_threshold, l);
+            HostCSR S = strength_symmetric(comm, A, theta);
             tm.lap(L + "strength");
             int64_t na = 0;
             std::vector<int64_t> astarts;
             std::vector<int64_t> agg = mis2_aggregate(comm, S, opt.seed + (uint64_t)l, &na, &astarts);
             for (size_t i = 0; i < agg.size(); ++i) split[i] = (int32_t)agg[i];
             tm.lap(L + "aggregate");
-            P = sa_prolongator(comm, A, agg, na, astarts);
+            P = sa_prolongator(comm, A, agg, na, astarts, theta, opt.seed + (uint64_t)l);
             tm.lap(L + "prolongator");
         } else if (opt.coarsen == AMG_COARSEN_RS || opt.coarsen == AMG_COARSEN_PMIS) {
             HostCSR S = strength_classical(comm, A, opt.strong_threshold);

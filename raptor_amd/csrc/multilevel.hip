@@ -289,7 +289,10 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         // r5: a second worker builds each operator's GS structures as soon as its formats
         // exist (level 0 from the start), beside the format worker (sa27: 0.9 s of GS builds
         // after the hierarchy before)
-        std::unique_ptr<FormatWorker> worker, worker2, gs_worker;
+        // gs_worker first: members are destroyed in reverse order, so when build_hierarchy
+        // throws, worker and worker2 drain (their A_{l+1} jobs push onto gs_worker) before
+        // gs_worker itself is joined and freed
+        std::unique_ptr<FormatWorker> gs_worker, worker, worker2;
         LevelDoneFn done = nullptr;
         if (overlap) {
             worker.reset(new FormatWorker(ctx->device));

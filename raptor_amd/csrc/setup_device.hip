@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstring>
 
 #include "device.hpp"
 
@@ -132,8 +133,12 @@ __global__ void diagonal_kernel(DCsr A, double* d) {
     d[i] = v;
 }
 
-// symmetric: |a_ij| >= theta sqrt(|a_ii a_jj|), j != i
+// SA strength, signed (r6; host_setup.cpp sa_strong): -a_ij >= theta sqrt(|a_ii a_jj|), j != i
 // (a_jj of another rank's column through D: the forwarded diagonal hd)
+__device__ __forceinline__ bool dsa_strong(double aij, double di, double dj, double theta) {
+    return -aij >= theta * sqrt(fabs(di * dj));
+}
+
 template <bool FILL>
 __global__ void strength_symmetric_kernel(DCsr A, Dist D, const double* d, const double* hd, double theta,
                                           int* cnt, const int* srp, int* scol, double* sval) {
@@ -143,7 +148,7 @@ __global__ void strength_symmetric_kernel(DCsr A, Dist D, const double* d, const
     for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) {
         const int j = A.col[k];
         if (j == A.lo + i) continue;
-        if (!(fabs(A.val[k]) >= theta * sqrt(fabs(d[i] * D.get(d, hd, j))))) continue;
+        if (!dsa_strong(A.val[k], d[i], D.get(d, hd, j), theta)) continue;
         if (FILL) {
             scol[q] = j;
             sval[q++] = A.val[k];
@@ -593,13 +598,124 @@ __global__ void mis2_pass2_kernel(DCsr S, Dist D, const int* a1, const int* ha1,
     if (ba < 0) atomicAdd(orphans, 1ull);
 }
 
-// rho_i = sum_k |a_ik| / |a_ii| (row order)
-__global__ void sa_rho_kernel(DCsr A, const double* d, double* rho) {
+// ---- SA smoothing (r6; host_setup.cpp sa_filter / sa_rho / sa_prolongator) ------------------
+// the filtered operator: the diagonal and the strong off-diagonals in row order; the diagonal
+// value f_i = a_ii + the weak off-diagonals (row order).  Pass 0 counts, pass 1 fills.
+template <bool FILL>
+__global__ void sa_filter_kernel(DCsr A, Dist D, const double* d, const double* hd, double theta, int* cnt,
+                                 const int* frp, int* fcol, double* fval) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i >= A.n) return;
+    const int gi = A.lo + i;
+    if (!FILL) {
+        int c = 0;
+        for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+            const int j = A.col[k];
+            c += j == gi || dsa_strong(A.val[k], d[i], D.get(d, hd, j), theta);
+        }
+        cnt[i] = c;
+        return;
+    }
+    double f = d[i];
+    for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+        const int j = A.col[k];
+        if (j != gi && !dsa_strong(A.val[k], d[i], D.get(d, hd, j), theta)) f += A.val[k];
+    }
+    int q = frp[i];
+    for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+        const int j = A.col[k];
+        if (j == gi) {
+            fcol[q] = j;
+            fval[q++] = f;
+        } else if (dsa_strong(A.val[k], d[i], D.get(d, hd, j), theta)) {
+            fcol[q] = j;
+            fval[q++] = A.val[k];
+        }
+    }
+}
+
+// the largest |v_i|: non-negative doubles order like their bit patterns, so an integer
+// atomicMax is exact in any order
+__device__ __forceinline__ void dmax_abs(unsigned long long* m, double v) {
+    atomicMax(m, (unsigned long long)__double_as_longlong(fabs(v)));
+}
+
+__global__ void max_abs_kernel(int n, const double* __restrict__ x, unsigned long long* m) {
+    const int i = blockIdx.x * kT + threadIdx.x;
+    if (i < n) dmax_abs(m, x[i]);
+}
+
+__global__ void div_scalar_kernel(int n, const double* __restrict__ y, double lam, double* __restrict__ x) {
+    const int i = blockIdx.x * kT + threadIdx.x;
+    if (i < n) x[i] = y[i] / lam;
+}
+
+// one power step: y_i = (A_F x)_i / a_ii (row order from 0.0), max |y_i|
+__global__ void sa_power_kernel(DCsr F, Dist D, const double* __restrict__ x, const double* __restrict__ hx,
+                                const double* __restrict__ d, double* __restrict__ y, unsigned long long* m) {
+    const int i = blockIdx.x * kT + threadIdx.x;
+    if (i >= F.n) return;
     double s = 0.0;
-    for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) s += fabs(A.val[k]);
-    rho[i] = s / fabs(d[i]);
+    for (int k = F.rp[i]; k < F.rp[i + 1]; ++k) s += F.val[k] * D.get(x, hx, F.col[k]);
+    const double v = s / d[i];
+    y[i] = v;
+    dmax_abs(m, v);
+}
+
+// P = T - (omega / a_ii) (A_F T): row i's products (agg_k, f_ik t_k) in A_F's row order,
+// insertion-sorted by aggregate (stable: row order kept inside an aggregate) into the row's
+// slice of the scratch; pass 0 sorts and counts the distinct aggregates with T's (agg_i);
+// pass 1 sums each aggregate's products from 0.0 in that order and merges T's entry
+template <bool FILL>
+__global__ void sa_smooth_kernel(DCsr F, Dist D, const int* __restrict__ agg, const int* __restrict__ hagg,
+                                 const double* __restrict__ t, const double* __restrict__ ht,
+                                 const double* __restrict__ d, double omega, int* __restrict__ skey,
+                                 double* __restrict__ sval, long long* __restrict__ cnt,
+                                 const long long* __restrict__ prp, long long* __restrict__ pcol,
+                                 double* __restrict__ pval) {
+    const int i = blockIdx.x * kT + threadIdx.x;
+    if (i >= F.n) return;
+    const int b = F.rp[i], e = F.rp[i + 1], ai = agg[i];
+    if (!FILL) {
+        for (int k = b; k < e; ++k) {
+            const int g = F.col[k];
+            const int key = D.get(agg, hagg, g);
+            const double v = F.val[k] * D.get(t, ht, g);
+            int p = k;
+            while (p > b && skey[p - 1] > key) {
+                skey[p] = skey[p - 1];
+                sval[p] = sval[p - 1];
+                --p;
+            }
+            skey[p] = key;
+            sval[p] = v;
+        }
+        long long c = 0;
+        bool tin = false;
+        for (int k = b; k < e; ++k) {
+            if (k == b || skey[k] != skey[k - 1]) ++c;
+            tin = tin || skey[k] == ai;
+        }
+        cnt[i] = c + (tin ? 0 : 1);
+        return;
+    }
+    const double c = omega * (1.0 / d[i]);
+    long long q = prp[i];
+    bool tleft = true;
+    int k = b;
+    while (k < e || tleft) {
+        const long long ja = k < e ? (long long)skey[k] : LLONG_MAX, jj = tleft ? (long long)ai : LLONG_MAX;
+        const long long j = ja < jj ? ja : jj;
+        double tvv = 0.0, av = 0.0;
+        if (jj == j) {
+            tvv = t[i];
+            tleft = false;
+        }
+        if (ja == j)
+            for (; k < e && skey[k] == j; ++k) av += sval[k];
+        pcol[q] = j;
+        pval[q++] = tvv - c * av;
+    }
 }
 
 // MIS(2) roots: flags for the exclusive scan that numbers them, then each root's aggregate id
@@ -867,10 +983,11 @@ void upload_level(const HostComm& comm, const HostCSR& A, DevLevel& D) {
     else D.val.alloc(1);
 }
 
-struct DevS {  // strength graph (this rank's rows, global column ids)
+struct DevS {  // strength graph / SA's filtered operator (this rank's rows, global column ids)
     DevBuf<int> rp, col;
     DevBuf<double> val;
     int n = 0, lo = 0;
+    int64_t nnz = 0;
     DCsr view() const { return DCsr{rp.p, col.p, val.p, n, lo}; }
 };
 
@@ -882,6 +999,7 @@ void build_strength(hipStream_t s, int n, int lo, DevS& S, DevBuf<char>& tmp, Co
     count(cnt.p);
     S.rp.alloc((size_t)n + 1);
     const int64_t nnz = exclusive_scan(s, cnt.p, S.rp.p, n, tmp);
+    S.nnz = nnz;
     S.col.alloc((size_t)std::max<int64_t>(nnz, 1));
     S.val.alloc((size_t)std::max<int64_t>(nnz, 1));
     S.n = n;
@@ -1169,7 +1287,7 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
     // smoothed aggregation (host_setup.cpp strength_symmetric, mis2_aggregate, sa_prolongator)
     AMG_CHECK(opt.coarsen == AMG_COARSEN_SA, "unknown coarsening");
     const bool dist = comm.nranks > 1;
-    const double theta = std::ldexp(opt.strong_threshold, -level);
+    const double theta = sa_theta(opt.strong_threshold, level);
     // A's halo: a_jj of other ranks' columns, then the MIS(2) tuples and aggregate ids of the
     // strong neighbours (S is a subset of A's pattern)
     HaloPlan aplan;
@@ -1269,7 +1387,7 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
     split = download_ints(s, agg.p, n);
     tm.lap("  device aggregation");
     // aggregate sizes (owners count their members, members elsewhere report in), T = 1 /
-    // sqrt(|aggregate|), rho = max_i sum_k |a_ik| / |a_ii| over every rank
+    // sqrt(|aggregate|)
     const int64_t alo = astarts[comm.rank], ahi = astarts[comm.rank + 1];
     std::vector<int64_t> size((size_t)(ahi - alo), 0);
     std::vector<std::vector<int64_t>> sendc(comm.nranks);
@@ -1303,118 +1421,109 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
         hsize.resize(splan.n_halo());
         splan.forward(comm, size.data(), hsize.data());
     }
-    DevBuf<double> rho;
-    rho.alloc(nn);
-    if (n) hipLaunchKernelGGL(sa_rho_kernel, dim3(grid1(n)), dim3(kT), 0, s, Av, d.p, rho.p);
-    HIP_CHECK(hipGetLastError());
-    const bool host_merge = dist || !DA;  // the smoothing below on the host reads a_ii there
-    std::vector<double> hrho(nn), hdiag(host_merge ? nn : 0);
-    HIP_CHECK(hipMemcpyAsync(hrho.data(), rho.p, sizeof(double) * nn, hipMemcpyDeviceToHost, s));
-    if (host_merge) HIP_CHECK(hipMemcpyAsync(hdiag.data(), d.p, sizeof(double) * nn, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    double r = 0.0;  // a maximum: the same value in any order
-#pragma omp parallel for schedule(static) reduction(max : r)
-    for (int i = 0; i < n; ++i) r = std::max(r, hrho[i]);
-    if (dist) r = comm.allreduce_max(r);
-    const double omega = (4.0 / 3.0) / r;
-    const std::vector<double>& hd_loc = hdiag;
-    HostCSR T;
-    T.n_global_rows = A.n_global_rows;
-    T.n_global_cols = na;
-    T.row_starts = A.row_starts;
-    T.col_starts = astarts;
-    T.rp.resize((size_t)n + 1);
-    T.col.resize(n);
-    T.val.resize(n);
-#pragma omp parallel for schedule(static)
-    for (int i = 0; i <= n; ++i) T.rp[i] = i;
+    std::vector<double> tv((size_t)std::max(n, 1));
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < n; ++i) {
         const int64_t a = split[i];
         const int64_t sz = (a >= alo && a < ahi) ? size[a - alo] : hsize[splan.find(a)];
-        T.col[i] = a;
-        T.val[i] = 1.0 / std::sqrt((double)sz);
+        tv[i] = 1.0 / std::sqrt((double)sz);
     }
+    DevBuf<double> dt, hdt;
+    dt.upload(tv.data(), tv.size());
+    hdt.alloc(1);
+    if (dist) AH.forward(s, comm, dt.p, hdt);  // t of the halo columns (A_F T)
     tm.lap("  device tentative prolongator");
-    if (DA && !dist) {
-        // one rank: A T, the smoothing and P stay on the device; P is downloaded once and kept
-        // as the setup's image of P (transpose, Galerkin product)
-        static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
-        DevCsr dT;
-        dT.n = n;
-        dT.nnz = n;
-        dT.ncols = na;
-        dT.rp64.upload(reinterpret_cast<const long long*>(T.rp.data()), T.rp.size());
-        dT.col64.upload(reinterpret_cast<const long long*>(T.col.data()), (size_t)std::max(n, 1));
-        dT.val.upload(T.val.data(), (size_t)std::max(n, 1));
-        DevCSR64 AT;
-        spgemm_images(ctx, tm, A, *DA, reinterpret_cast<const long long*>(T.rp.data()), &T, dT, na, AT);
-        tm.lap("  device A*T");
-        DevBuf<long long> pcnt, prp, pcol;
-        DevBuf<double> pval;
-        pcnt.alloc((size_t)n + 1);
-        HIP_CHECK(hipMemsetAsync(pcnt.p, 0, sizeof(long long) * pcnt.n, s));
-        hipLaunchKernelGGL(sa_smooth_kernel<false>, dim3(grid1(n)), dim3(kT), 0, s, n, AT.d_rp.p, AT.d_col.p,
-                           AT.d_val.p, dT.col64.p, dT.val.p, d.p, omega, pcnt.p, nullptr, nullptr, nullptr);
-        prp.alloc((size_t)n + 1);
-        const int64_t pnnz = exclusive_scan64(s, pcnt.p, prp.p, n, tmp);
-        pcol.alloc((size_t)std::max<int64_t>(pnnz, 1));
-        pval.alloc((size_t)std::max<int64_t>(pnnz, 1));
-        hipLaunchKernelGGL(sa_smooth_kernel<true>, dim3(grid1(n)), dim3(kT), 0, s, n, AT.d_rp.p, AT.d_col.p,
-                           AT.d_val.p, dT.col64.p, dT.val.p, d.p, omega, nullptr, prp.p, pcol.p, pval.p);
-        HIP_CHECK(hipGetLastError());
-        P = HostCSR();
-        P.n_global_rows = A.n_global_rows;
-        P.n_global_cols = na;
-        P.row_starts = A.row_starts;
-        P.col_starts = astarts;
-        P.rp.resize((size_t)n + 1);
-        P.col.resize((size_t)pnnz);
-        P.val.resize((size_t)pnnz);
-        copy_to_host(P.rp.data(), prp.p, sizeof(long long) * (n + 1), s);
-        copy_to_host(P.col.data(), pcol.p, sizeof(long long) * pnnz, nullptr);
-        copy_to_host(P.val.data(), pval.p, sizeof(double) * pnnz, nullptr);
-        std::unique_ptr<DevCsr> dp(new DevCsr());
-        dp->rp64 = std::move(prp);
-        dp->col64 = std::move(pcol);
-        dp->val = std::move(pval);
-        imgs->put(P, std::move(dp));
-        tm.lap("  device smoothed prolongator");
-        return true;
+    // the filtered operator A_F (r6): the diagonal + the strong couplings, weak ones lumped
+    DevS F;
+    build_strength(
+        s, n, lo, F, tmp,
+        [&](int* cnt) {
+            if (n)
+                hipLaunchKernelGGL(sa_filter_kernel<false>, dim3(grid1(n)), dim3(kT), 0, s, Av, Da, d.p, hd.p, theta,
+                                   cnt, nullptr, nullptr, nullptr);
+        },
+        [&](const int* frp, int* fcol, double* fval) {
+            if (n)
+                hipLaunchKernelGGL(sa_filter_kernel<true>, dim3(grid1(n)), dim3(kT), 0, s, Av, Da, d.p, hd.p, theta,
+                                   nullptr, frp, fcol, fval);
+        });
+    const DCsr Fv = F.view();
+    // rho(D^-1 A_F): power steps in the max norm (exact maxima, the same on every partition)
+    double rho = 0.0;
+    {
+        DevBuf<double> x, y, hx;
+        DevBuf<unsigned long long> mx;
+        x.alloc((size_t)std::max(n, 1));
+        y.alloc((size_t)std::max(n, 1));
+        hx.alloc(1);
+        mx.alloc(1);
+        auto global_max = [&]() {
+            unsigned long long bits = 0;
+            HIP_CHECK(hipMemcpyAsync(&bits, mx.p, sizeof(bits), hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            double m;
+            std::memcpy(&m, &bits, sizeof(m));
+            return dist ? comm.allreduce_max(m) : m;
+        };
+        launch_uniform(s, n, lo, opt.seed + (uint64_t)level, x.p);
+        HIP_CHECK(hipMemsetAsync(mx.p, 0, sizeof(unsigned long long), s));
+        if (n) hipLaunchKernelGGL(max_abs_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, x.p, mx.p);
+        const double m0 = global_max();
+        if (m0 > 0.0 && n) hipLaunchKernelGGL(div_scalar_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, x.p, m0, x.p);
+        for (int it = 0; it < kSaRhoIters; ++it) {
+            if (dist) AH.forward(s, comm, x.p, hx);
+            HIP_CHECK(hipMemsetAsync(mx.p, 0, sizeof(unsigned long long), s));
+            if (n) hipLaunchKernelGGL(sa_power_kernel, dim3(grid1(n)), dim3(kT), 0, s, Fv, Da, x.p, hx.p, d.p, y.p, mx.p);
+            HIP_CHECK(hipGetLastError());
+            rho = global_max();
+            if (rho == 0.0) break;
+            if (n) hipLaunchKernelGGL(div_scalar_kernel, dim3(grid1(n)), dim3(kT), 0, s, n, y.p, rho, x.p);
+        }
     }
-    HostCSR AT = spgemm_device(ctx, comm, A, T);
-    tm.lap("  device A*T");
-    // P = T - (omega / a_ii) A T, rows merged by column (same as sa_prolongator)
+    const double omega = rho > 0.0 ? (4.0 / 3.0) / rho : 0.0;
+    tm.lap("  device filtered operator + rho");
+    // P = T - (omega / a_ii) A_F T on the device, on any number of ranks; kept as the setup's
+    // image of P where there is one (transpose, Galerkin product)
+    static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
+    DevBuf<int> hagg, skey;
+    DevBuf<double> sval;
+    hagg.alloc(1);
+    if (dist) AH.forward(s, comm, agg.p, hagg);
+    const int64_t fnnz = F.nnz;
+    skey.alloc((size_t)std::max<int64_t>(fnnz, 1));
+    sval.alloc((size_t)std::max<int64_t>(fnnz, 1));
+    DevBuf<long long> pcnt, prp, pcol;
+    DevBuf<double> pval;
+    pcnt.alloc((size_t)n + 1);
+    HIP_CHECK(hipMemsetAsync(pcnt.p, 0, sizeof(long long) * pcnt.n, s));
+    if (n)
+        hipLaunchKernelGGL(sa_smooth_kernel<false>, dim3(grid1(n)), dim3(kT), 0, s, Fv, Da, agg.p, hagg.p, dt.p,
+                           hdt.p, d.p, omega, skey.p, sval.p, pcnt.p, nullptr, nullptr, nullptr);
+    prp.alloc((size_t)n + 1);
+    const int64_t pnnz = exclusive_scan64(s, pcnt.p, prp.p, n, tmp);
+    pcol.alloc((size_t)std::max<int64_t>(pnnz, 1));
+    pval.alloc((size_t)std::max<int64_t>(pnnz, 1));
+    if (n)
+        hipLaunchKernelGGL(sa_smooth_kernel<true>, dim3(grid1(n)), dim3(kT), 0, s, Fv, Da, agg.p, hagg.p, dt.p,
+                           hdt.p, d.p, omega, skey.p, sval.p, nullptr, prp.p, pcol.p, pval.p);
+    HIP_CHECK(hipGetLastError());
     P = HostCSR();
     P.n_global_rows = A.n_global_rows;
     P.n_global_cols = na;
     P.row_starts = A.row_starts;
     P.col_starts = astarts;
-    P.rp.assign((size_t)n + 1, 0);
-    std::vector<int64_t> len(n);
-#pragma omp parallel for schedule(static)
-    for (int i = 0; i < n; ++i) {
-        int64_t c = AT.rp[i + 1] - AT.rp[i];
-        const int64_t jt = T.col[i];
-        if (!std::binary_search(AT.col.begin() + AT.rp[i], AT.col.begin() + AT.rp[i + 1], jt)) ++c;
-        len[i] = c;
-    }
-    for (int i = 0; i < n; ++i) P.rp[i + 1] = P.rp[i] + len[i];
-    P.col.resize(P.rp[n]);
-    P.val.resize(P.rp[n]);
-#pragma omp parallel for schedule(static)
-    for (int i = 0; i < n; ++i) {
-        const double c = omega * (1.0 / hd_loc[i]);
-        int64_t ka = AT.rp[i], ea = AT.rp[i + 1], kt = T.rp[i], et = T.rp[i + 1], q = P.rp[i];
-        while (ka < ea || kt < et) {
-            const int64_t ja = ka < ea ? AT.col[ka] : INT64_MAX, jt = kt < et ? T.col[kt] : INT64_MAX;
-            const int64_t j = ja < jt ? ja : jt;
-            double tvv = 0.0, av = 0.0;
-            if (jt == j) tvv = T.val[kt++];
-            if (ja == j) av = AT.val[ka++];
-            P.col[q] = j;
-            P.val[q++] = tvv - c * av;
-        }
+    P.rp.resize((size_t)n + 1);
+    P.col.resize((size_t)pnnz);
+    P.val.resize((size_t)pnnz);
+    copy_to_host(P.rp.data(), prp.p, sizeof(long long) * (n + 1), s);
+    copy_to_host(P.col.data(), pcol.p, sizeof(long long) * pnnz, nullptr);
+    copy_to_host(P.val.data(), pval.p, sizeof(double) * pnnz, nullptr);
+    if (imgs) {
+        std::unique_ptr<DevCsr> dp(new DevCsr());
+        dp->rp64 = std::move(prp);
+        dp->col64 = std::move(pcol);
+        dp->val = std::move(pval);
+        imgs->put(P, std::move(dp));
     }
     tm.lap("  device smoothed prolongator");
     return true;

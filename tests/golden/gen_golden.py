@@ -9,7 +9,8 @@ oracle is pinned here by implementations that share no code with it:
     (small sizes only), written from DESIGN.md section 3, not from the C code;
   * (r5) the floating-point setup and the cycle, restated the same way:
     classical (modified) interpolation weights, SA's tentative prolongator T, rho and smoothed
-    P = T - (4/3 rho) (D^-1 A T), the Gauss-Jordan coarse inverse (numpy row operations), the
+    P = T - (4/3 rho) (D^-1 A_F T) (r6: signed strength, filtered A_F, max-norm power rho),
+    the Gauss-Jordan coarse inverse (numpy row operations), the
     64-way interleaved butterfly coarse solve, and whole hierarchies + V-cycles built from
     these restatements, scipy's Galerkin products and the loop smoothers only
     (setup_<case>.npz).
@@ -61,6 +62,26 @@ def fe27(nx, ny, nz, ex=1.0, ey=1.0, ez=1e-3):
     return ((t1 + t2) + t3).tocsr()
 
 
+def mixed_graph(n, deg, seed):
+    """Unstructured SPD test matrix (r6): a symmetric random graph (deg random partners per
+    node, numpy Generator(PCG64(seed))), couplings -U(0.5, 1.5) with one in eight positive
+    +U(0.05, 0.6), diagonal sum |a_ij| + 0.01 -- positive couplings and weak entries
+    exercise SA's signed strength and the filtered operator."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    i = np.repeat(np.arange(n), deg)
+    j = rng.integers(0, n, size=n * deg)
+    keep = i != j
+    i, j = i[keep], j[keep]
+    w = -rng.uniform(0.5, 1.5, size=i.size)
+    pos = rng.integers(0, 8, size=i.size) == 0
+    w[pos] = rng.uniform(0.05, 0.6, size=int(pos.sum()))
+    W = sp.coo_matrix((w, (i, j)), shape=(n, n)).tocsr()
+    W = ((W + W.T) * 0.5).tocsr()
+    W.sum_duplicates()
+    d = np.asarray(abs(W).sum(axis=1)).ravel() + 0.01
+    return (W + sp.diags(d)).tocsr()
+
+
 # --------------------------------------------------------------------------------------
 # splitmix64 in numpy uint64
 # --------------------------------------------------------------------------------------
@@ -109,11 +130,16 @@ def strength_classical(A, theta):
     return out
 
 
+def sa_strong(v, di, dc, theta):
+    """SA strength, signed (r6): -a_ij >= theta sqrt(|a_ii a_jj|); positive couplings never."""
+    return -v >= theta * np.sqrt(abs(di * dc))
+
+
 def strength_symmetric(A, theta):
     R = rows(A)
     d = A.diagonal()
     return [[(c, v) for c, v in zip(cols, vals)
-             if c != i and abs(v) >= theta * np.sqrt(abs(d[i] * d[c]))] for i, (cols, vals) in enumerate(R)]
+             if c != i and sa_strong(v, d[i], d[c], theta)] for i, (cols, vals) in enumerate(R)]
 
 
 def transpose_lists(S, n):
@@ -312,25 +338,61 @@ def interp_classical(A, S, cf):
                          shape=(n, int((cf == 1).sum())))
 
 
-def sa_prolongator(A, agg, na):
-    """T_{i,agg(i)} = 1 / sqrt(|agg(i)|); rho = max_i sum_k |a_ik| / |a_ii| (row order);
-    P = T - ((4/3) / rho) (1 / a_ii) (A T) on the union pattern."""
+def sa_filter(A, theta):
+    """Filtered operator (r6): the diagonal and the strong off-diagonals in row order; the
+    diagonal value f_i = a_ii + the weak off-diagonal a_ij (row order).  Explicit zeros kept."""
+    R = rows(A)
+    d = A.diagonal()
+    n = len(R)
+    indptr, indices, data = [0], [], []
+    for i, (cols, vals) in enumerate(R):
+        f = d[i]
+        for c, v in zip(cols, vals):
+            if c != i and not sa_strong(v, d[i], d[c], theta):
+                f = f + v
+        for c, v in zip(cols, vals):
+            if c == i:
+                indices.append(c)
+                data.append(f)
+            elif sa_strong(v, d[i], d[c], theta):
+                indices.append(c)
+                data.append(v)
+        indptr.append(len(indices))
+    return sp.csr_matrix((np.array(data, np.float64), np.array(indices, np.int64), np.array(indptr, np.int64)),
+                         shape=A.shape)
+
+
+def sa_rho(F, d, seed, iters=10):
+    """rho(D^-1 A_F) by power steps in the max norm: x = u / max|u| (u = uniform(seed));
+    y = (A_F x) / a_ii, lam = max|y|, stop at lam = 0, x = y / lam."""
+    x = uniform(F.shape[0], seed)
+    m = float(np.max(np.abs(x))) if x.size else 0.0
+    if m > 0.0:
+        x = x / m
+    lam = 0.0
+    for _ in range(iters):
+        y = (F @ x) / d
+        lam = float(np.max(np.abs(y))) if y.size else 0.0
+        if lam == 0.0:
+            break
+        x = y / lam
+    return lam
+
+
+def sa_prolongator(A, agg, na, theta, seed):
+    """T_{i,agg(i)} = 1 / sqrt(|agg(i)|); A_F = sa_filter(A, theta); rho = sa_rho(A_F, diag A,
+    seed); P = T - ((4/3) / rho) (1 / a_ii) (A_F T) on the union pattern (r6)."""
     n = A.shape[0]
     size = np.bincount(agg, minlength=na)
     T = sp.csr_matrix((1.0 / np.sqrt(size[agg].astype(np.float64)), agg.astype(np.int64), np.arange(n + 1)),
                       shape=(n, na))
-    R = rows(A)
-    rho = 0.0
-    for i, (cols, vals) in enumerate(R):
-        s = 0.0
-        for v in vals:
-            s = s + abs(v)
-        r = s / abs(dict(zip(cols, vals))[i])
-        rho = max(rho, r)
-    omega = (4.0 / 3.0) / rho
-    c = omega * (1.0 / A.diagonal())
-    AT = (A @ T).tocsr()
-    return (T - sp.diags(c) @ AT).tocsr()
+    d = A.diagonal()
+    F = sa_filter(A, theta)
+    rho = sa_rho(F, d, seed)
+    omega = (4.0 / 3.0) / rho if rho > 0.0 else 0.0
+    c = omega * (1.0 / d)
+    FT = (F @ T).tocsr()
+    return (T - sp.diags(c) @ FT).tocsr()
 
 
 def gauss_jordan_inverse(M):
@@ -389,7 +451,7 @@ def canon(M):
 
 class PyHierarchy:
     """The setup and V-cycle of DESIGN.md 3 from the restatements above: strength (theta; SA:
-    theta_l = theta 2^-l), RS / PMIS (seed + l) + classical interpolation or MIS(2) (seed + l)
+    signed, theta_l = theta (3/4)^l rounded per level), RS / PMIS (seed + l) + classical interpolation or MIS(2) (seed + l)
     + smoothed P; R = P^T; A_c = R (A P) (scipy); stop at n <= max_coarse, n_c = 0, n_c >= n
     or (n <= 8192 and 5 n_c > 4 n); Gauss-Jordan inverse on the coarsest level.  Cycle: one
     pre-smooth (Jacobi 2/3 or forward l1 hybrid GS(64)), r = b - A x, b_c = R r, x_c = 0,
@@ -398,14 +460,15 @@ class PyHierarchy:
     def __init__(self, A, coarsen, smoother, theta, max_coarse=256, seed=0x5EED, max_levels=25):
         self.smoother = smoother
         self.A, self.P, self.R, self.split = [canon(A)], [], [], []
+        th = theta
         while len(self.A) < max_levels and self.A[-1].shape[0] > max_coarse:
             l = len(self.A) - 1
             Al = self.A[-1]
             n = Al.shape[0]
             if coarsen == "sa":
-                Sv = strength_symmetric(Al, np.ldexp(theta, -l))
+                Sv = strength_symmetric(Al, th)
                 agg, na = mis2_aggregate(Sv, seed + l)
-                P = sa_prolongator(Al, agg, na)
+                P = sa_prolongator(Al, agg, na, th, seed + l)
                 split = agg
             else:
                 S = strength_classical(Al, theta)
@@ -421,6 +484,7 @@ class PyHierarchy:
             self.R.append(R)
             self.split.append(np.asarray(split, np.int32))
             self.A.append(canon(R @ (Al @ P)))
+            th = th * 0.75  # SA: theta_{l+1} = theta_l * 3/4 (r6)
         self.inv = gauss_jordan_inverse(self.A[-1].toarray())
 
     def smooth(self, l, x, b, post):
@@ -454,6 +518,7 @@ SETUP_CASES = [
     ("p7_10x9x8_pmis_jacobi_mc16", lambda: poisson7(10, 9, 8), "pmis", "jacobi", 0.25, 16),
     ("fe27_8x7x6_sa_gs_mc16", lambda: fe27(8, 7, 6), "sa", "hybrid_gs", 0.08, 16),
     ("p7_10x9x8_sa_gs_mc16", lambda: poisson7(10, 9, 8), "sa", "hybrid_gs", 0.08, 16),
+    ("mixed_600_sa_gs_mc16", lambda: mixed_graph(600, 2, 11), "sa", "hybrid_gs", 0.08, 16),
 ]
 
 
@@ -463,6 +528,11 @@ def gen_setup_case(name, gen, coarsen, smoother, theta, max_coarse):
     n = A.shape[0]
     b = A @ uniform(n, 42)
     out = {"nlev": np.array(len(H.A), np.int64), "inv": H.inv, "b": b}
+    out.update(csr_arrays("Ain", canon(A)))  # the input (the unstructured case has no C generator)
+    if coarsen == "sa":  # level 0's filtered operator and rho, for the oracle's pieces
+        F = sa_filter(canon(A), theta)
+        out.update(csr_arrays("F0", F))
+        out["rho0"] = np.array(sa_rho(F, canon(A).diagonal(), seed=0x5EED))
     for l in range(len(H.A)):
         out.update(csr_arrays(f"A{l}", H.A[l]))
         if l + 1 < len(H.A):

@@ -322,6 +322,24 @@ def test_bad_arguments_fail_loudly(ctx):
         A.hybrid_gs(x, x, ctx.zeros(16), 1000)  # block > 256
 
 
+def test_setup_failure_with_overlapped_gs_builds_is_an_error(ctx):
+    """a setup that throws while the format workers still hold jobs that
+    push GS builds (hybrid GS, overlapped setup) comes back as AmgError -- the workers drain
+    before the GS worker is freed -- and the context stays usable."""
+    import raptor_amd as ra
+
+    # 44^3 PMIS: the first coarse level has ~27 k rows > the dense-solve limit (20000), so
+    # max_levels=2 throws after level 0 was handed to the workers
+    A = ra.par_stencil_grid(ctx, "7pt", (44, 44, 44))
+    for _ in range(2):
+        with pytest.raises(ra.AmgError, match="coarsest level too large"):
+            ra.ParMultilevel(coarsen="pmis", smoother="hybrid_gs", max_levels=2).setup(A)
+    ml = ra.ParMultilevel(coarsen="pmis", smoother="hybrid_gs").setup(A)
+    n = A.local_rows
+    _, hist = ml.solve(ctx.zeros(n), to_dev(ctx, np.ones(n)), max_iter=3)
+    assert hist[-1] < hist[0]
+
+
 CASES = [
     ("7pt", (24, 24, 24), "pmis", "jacobi"),
     ("5pt", (48, 40), "rs", "jacobi"),

@@ -171,6 +171,7 @@ SETUP_CASES = {  # tests/golden/gen_golden.py SETUP_CASES: (generator, coarsen, 
     "p7_10x9x8_pmis_jacobi_mc16": ("p7_10x9x8", "pmis", 16),
     "fe27_8x7x6_sa_gs_mc16": ("fe27_8x7x6", "sa", 16),
     "p7_10x9x8_sa_gs_mc16": ("p7_10x9x8", "sa", 16),
+    "mixed_600_sa_gs_mc16": ("mixed", "sa", 16),
 }
 
 
@@ -197,7 +198,8 @@ def test_fp_setup_and_cycle_match_restatement(oracle, case):
     O = oracle
     prob, coarsen, max_coarse = SETUP_CASES[case]
     g = load(f"setup_{case}")
-    A = oracle_gen(O, prob)
+    A = O.Csr.from_scipy(gold_csr(g, "Ain")) if prob == "mixed" else oracle_gen(O, prob)
+    assert _same(_canon(A.to_scipy()), gold_csr(g, "Ain"))
     H = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen], max_coarse=max_coarse))
     nlev = int(g["nlev"])
     assert H.num_levels == nlev >= 3
@@ -217,3 +219,26 @@ def test_fp_setup_and_cycle_match_restatement(oracle, case):
     assert np.array_equal(xs, g["xsolve"])
     assert np.array_equal(hist, g["hist"])
     assert hist[-1] < hist[0]
+
+
+@pytest.mark.parametrize("case", [c for c, v in SETUP_CASES.items() if v[1] == "sa"])
+def test_sa_filter_and_rho_match_restatement(oracle, case):
+    """SA smoothing's pieces at level 0: the filtered operator (diagonal +
+    signed-strong couplings, weak ones lumped onto the diagonal in row order) and the
+    max-norm power-iteration rho, bit for bit against gen_golden.py's restatement."""
+    O = oracle
+    g = load(f"setup_{case}")
+    A = O.Csr.from_scipy(gold_csr(g, "Ain"))
+    F = O.sa_filter(A, 0.08)
+    Fs = F.to_scipy()
+    G = gold_csr(g, "F0")
+    assert np.array_equal(Fs.indptr, G.indptr) and np.array_equal(Fs.indices, G.indices)
+    assert np.array_equal(Fs.data, G.data)
+    # row sums are kept by the lumping (up to rounding)
+    assert np.allclose(np.asarray(Fs.sum(axis=1)).ravel(), np.asarray(A.to_scipy().sum(axis=1)).ravel(),
+                       rtol=0, atol=1e-12 * abs(A.to_scipy()).max())
+    rho = O.sa_rho(F, A.to_scipy().diagonal(), 0x5EED)
+    assert rho == float(g["rho0"]) and rho > 0.5
+    # no positive coupling is ever strong
+    S = O.strength_symmetric(A, 0.08).to_scipy()
+    assert S.nnz == 0 or S.data.max() < 0.0
