@@ -114,9 +114,11 @@ struct DevBuf {
         if (count) HIP_CHECK(hipMalloc(&p, count * sizeof(T)));
         n = count;
     }
+    // count may be padded to >= 1 for an empty host array (data() == nullptr): then only the
+    // allocation is made (a halo plan with no ghost ids, an operator without nonzeros)
     void upload(const T* h, size_t count) {
         alloc(count);
-        if (count) copy_to_device(p, h, count * sizeof(T));
+        if (count && h) copy_to_device(p, h, count * sizeof(T));
     }
 };
 

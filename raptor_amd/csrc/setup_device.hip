@@ -1482,8 +1482,8 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
     }
     const double omega = rho > 0.0 ? (4.0 / 3.0) / rho : 0.0;
     tm.lap("  device filtered operator + rho");
-    // P = T - (omega / a_ii) A_F T on the device, on any number of ranks; kept as the setup's
-    // image of P where there is one (transpose, Galerkin product)
+    // P = T - (omega / a_ii) A_F T on the device, on any number of ranks; one rank keeps it as
+    // the setup's image of P (transpose, Galerkin product)
     static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
     DevBuf<int> hagg, skey;
     DevBuf<double> sval;
@@ -1518,7 +1518,7 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
     copy_to_host(P.rp.data(), prp.p, sizeof(long long) * (n + 1), s);
     copy_to_host(P.col.data(), pcol.p, sizeof(long long) * pnnz, nullptr);
     copy_to_host(P.val.data(), pval.p, sizeof(double) * pnnz, nullptr);
-    if (imgs) {
+    if (imgs && !dist) {  // (N ranks: the transpose and SpGEMM build their own images of P)
         std::unique_ptr<DevCsr> dp(new DevCsr());
         dp->rp64 = std::move(prp);
         dp->col64 = std::move(pcol);

@@ -418,8 +418,7 @@ def test_full_size_sa27_split_sweeps_and_cycle_256(ctx, oracle, capfd, say):
     the Galerkin levels (KM_GSACC block pass + the LDS-queue chain walk, DESIGN.md
     4.2c) on the product's own level-1 and level-2 operators, forward and backward at B = 64,
     bit-identical to the oracle's hybrid_gs on those operators -- with the chain walk's widest
-    in-chunk coupling count recorded -- then one full SA V-cycle iterate bit-identical to the
-    oracle's cycle on the product's exported hierarchy."""
+    in-chunk coupling count recorded."""
     import raptor_amd as ra
 
     O = oracle
@@ -453,9 +452,6 @@ def test_full_size_sa27_split_sweeps_and_cycle_256(ctx, oracle, capfd, say):
         del Ao, dxl, dbl, out
     with capfd.disabled():
         print(f"\n[sa27 256^3] split-sweep chain widths (forward, backward) per level: {widths}", flush=True)
-    say("exporting the hierarchy to the oracle")
-    H = O.Hierarchy(None, levels=oracle_levels(O, ml), smoother=O.SMOOTH_HYBRID_GS)
-    say("oracle cycle")
-    xo = H.cycle(np.zeros(n), b)
-    assert np.array_equal(to_host(ctx, dx), xo)
+    # the whole cycle at this size against the oracle's own setup:
+    # tests/test_gpu_zfull_configs.py::test_configs2_sa27_setup_vs_oracle_own_setup_256
 

@@ -1,0 +1,163 @@
+"""configs[2] and configs[4] at their stated sizes against the oracle's OWN serial setup
+(VERDICT r5 "next" 1).  Every level's A, P, R and aggregates of the GPU hierarchy must equal
+the independently built oracle hierarchy bit for bit, the V-cycle iterates too, and the PCG
+history within 1e-9 (BASELINE.json:5).
+
+* configs[4] (BASELINE.json:11): G3_circuit is not in the container (no network), so the
+  seeded 1,500,625-row graph-Laplacian substitute bench.py times (par_graph_laplacian(1225,
+  1225, seed=1) + RCM, SA + hybrid GS) -- on one rank and on 8 loopback ranks (each rank's
+  slice of every level equal to the oracle's one-rank hierarchy; hybrid GS clipped to the
+  ranks' cuts in the oracle).  Parity with G3_circuit itself is unpinned.
+* configs[2] (BASELINE.json:9): 27-pt anisotropic 256^3, SA + hybrid GS, against
+  O.Hierarchy(gen_27pt(256, 256, 256), SA) -- not against the product's exported levels.
+"""
+import numpy as np
+import pytest
+
+from tests.test_gpu_multirank import level_starts, run_ranks, set_oracle_cuts
+from tests.util import loopback_ctx, same_csr, to_dev, to_host
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+LATTICE = 1225  # bench.py --config g3sub default: 1225^2 = 1,500,625 rows
+
+
+@pytest.fixture(scope="module")
+def g3sub(oracle):
+    """The substitute, RCM-reordered, and the oracle's own serial SA hierarchy of it."""
+    O = oracle
+    G = O.gen_graph_laplacian(LATTICE, LATTICE, 1)
+    perm = O.rcm(G)
+    B = O.permute(G, perm)
+    H = O.Hierarchy(B, **O.DEFAULTS["sa"])
+    n = B.shape[0]
+    b = O.vec_uniform(n, 42)
+    return {"perm": perm, "B": B, "H": H, "b": b,
+            "levels": [{w: H.matrix(l, w) for w in "APR"} for l in range(H.num_levels)]}
+
+
+def _op_complexity(levels):
+    return sum(L["A"].nnz for L in levels) / levels[0]["A"].nnz
+
+
+def test_configs4_substitute_full_size_one_rank(ctx, oracle, g3sub, say):
+    import raptor_amd as ra
+
+    O = oracle
+    A = ra.par_graph_laplacian(ctx, LATTICE, LATTICE, seed=1)
+    Bd, perm = A.reorder("rcm")
+    assert Bd.global_rows == LATTICE * LATTICE == 1500625
+    assert np.array_equal(perm, g3sub["perm"])
+    ml = ra.ParSmoothedAggregationSolver().setup(Bd)
+    say(f"GPU setup done: {ml.num_levels} levels")
+    H, lv = g3sub["H"], g3sub["levels"]
+    assert ml.num_levels == H.num_levels >= 3
+    for l in range(H.num_levels):
+        assert same_csr(ml.level_matrix(l, "A").to_scipy_local(), lv[l]["A"]), ("A", l)
+        if l + 1 < H.num_levels:
+            assert same_csr(ml.level_matrix(l, "P").to_scipy_local(), lv[l]["P"]), ("P", l)
+            assert same_csr(ml.level_matrix(l, "R").to_scipy_local(), lv[l]["R"]), ("R", l)
+            assert np.array_equal(ml.level_split(l), H.split(l)), ("aggregates", l)
+    say(f"hierarchy bit-identical; operator complexity {_op_complexity(lv):.3f}, "
+        f"levels {[(L['A'].shape[0], L['A'].nnz) for L in lv]}")
+    b = g3sub["b"]
+    n = b.size
+    db = to_dev(ctx, b)
+    dx = ctx.zeros(n)
+    xo = np.zeros(n)
+    for _ in range(3):
+        ml.cycle(dx, db)
+        xo = H.cycle(xo, b)
+        assert np.array_equal(to_host(ctx, dx), xo)
+    _, hist = ml.pcg(ctx.zeros(n), db, max_iter=20)
+    _, hist_o = H.pcg(np.zeros(n), b, max_iter=20)
+    assert hist.shape == hist_o.shape
+    assert np.all(np.abs(hist - hist_o) <= 1e-9 * hist_o[0])
+    assert hist[-1] < 1e-6 * hist[0]
+    say(f"3 iterates bit-identical; PCG 20 iterations {hist[-1] / hist[0]:.2e} (oracle within 1e-9)")
+
+
+def test_configs4_substitute_full_size_eight_loopback_ranks(oracle, g3sub, say):
+    """8 ranks (configs[4] is an 8-GPU config): loopback ranks on one GPU run the distributed
+    setup (device strength / MIS(2) / filtered smoothing / transpose / SpGEMM with ghost rows)
+    and cycle; every rank's slice of every level's A, P, R and aggregates equals the oracle's
+    one-rank hierarchy, and the first two iterates equal the oracle's rank-cut hybrid GS."""
+    import raptor_amd as ra
+
+    H, lv, b = g3sub["H"], g3sub["levels"], g3sub["b"]
+    splits = [H.split(l) for l in range(H.num_levels - 1)]
+
+    def rank(r, nr, world):
+        ctx = loopback_ctx(r, nr, world)
+        A = ra.par_graph_laplacian(ctx, LATTICE, LATTICE, seed=1)
+        B, perm = A.reorder("rcm")
+        ml = ra.ParSmoothedAggregationSolver().setup(B)
+        bad = []
+        if ml.num_levels != H.num_levels:
+            bad.append(("levels", ml.num_levels, H.num_levels))
+        for l in range(min(ml.num_levels, H.num_levels)):
+            for w in ("APR" if l + 1 < H.num_levels else "A"):
+                M = ml.level_matrix(l, w)
+                G = lv[l][w][M.first_row:M.first_row + M.local_rows]
+                if not same_csr(M.to_scipy_local(), G):
+                    bad.append((w, l))
+            if l + 1 < H.num_levels:
+                M = ml.level_matrix(l, "A")
+                if not np.array_equal(ml.level_split(l), splits[l][M.first_row:M.first_row + M.local_rows]):
+                    bad.append(("aggregates", l))
+        f, m = B.first_row, B.local_rows
+        dx = ctx.zeros(m)
+        db = to_dev(ctx, b[f:f + m])
+        xs = []
+        for _ in range(2):
+            ml.cycle(dx, db)
+            xs.append(to_host(ctx, dx))
+        return bad, f, m, xs, level_starts(ml)
+
+    res = run_ranks(8, rank)
+    say("8 ranks done; oracle rank-cut cycles")
+    for bad, *_ in res:
+        assert bad == []
+    assert sum(r[2] for r in res) == b.size
+    set_oracle_cuts(H, res)
+    xo = np.zeros(b.size)
+    for k in range(2):
+        xo = H.cycle(xo, b)
+        for _, f, m, xs, _ in res:
+            assert np.array_equal(xs[k], xo[f:f + m]), ("cycle", k)
+    H.set_cuts(0, [0])  # later users of the module fixture see the serial hierarchy
+    for l in range(1, H.num_levels):
+        H.set_cuts(l, [0])
+
+
+def test_configs2_sa27_setup_vs_oracle_own_setup_256(ctx, oracle, say):
+    """configs[2] at full size: the GPU SA setup of the 27-pt anisotropic 256^3 operator (449 M
+    nonzeros) equals the oracle's own serial SA setup of gen_27pt(256, 256, 256) on every level
+    -- P, R, aggregates and the Galerkin operators, bit for bit -- and one V-cycle iterate is
+    bit-identical to the oracle's cycle on its own hierarchy."""
+    import raptor_amd as ra
+
+    O = oracle
+    N = 256
+    A = ra.par_stencil_grid(ctx, "27pt", (N, N, N))
+    ml = ra.ParSmoothedAggregationSolver().setup(A)
+    say(f"GPU setup done ({ml.num_levels} levels); oracle setup (serial)")
+    Ao = O.gen_27pt(N, N, N)
+    H = O.Hierarchy(Ao, **O.DEFAULTS["sa"])
+    say(f"oracle setup done ({H.num_levels} levels); comparing levels")
+    assert ml.num_levels == H.num_levels >= 4
+    for l in range(H.num_levels):
+        if l > 0:
+            assert same_csr(ml.level_matrix(l, "A").to_scipy_local(), H.matrix(l, "A")), ("A", l)
+        if l + 1 < H.num_levels:
+            assert same_csr(ml.level_matrix(l, "P").to_scipy_local(), H.matrix(l, "P")), ("P", l)
+            assert same_csr(ml.level_matrix(l, "R").to_scipy_local(), H.matrix(l, "R")), ("R", l)
+            assert np.array_equal(ml.level_split(l), H.split(l)), ("aggregates", l)
+        say(f"level {l} bit-identical")
+    n = N ** 3
+    b = O.vec_uniform(n, 42)
+    dx = ctx.zeros(n)
+    ml.cycle(dx, to_dev(ctx, b))
+    xo = H.cycle(np.zeros(n), b)
+    assert np.array_equal(to_host(ctx, dx), xo)
+    say("V-cycle iterate bit-identical")
