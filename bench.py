@@ -309,10 +309,37 @@ def main():
                         row["traffic_stale"] = o is not None
             except (OSError, KeyError, ValueError):
                 pass
-        # the dominant kernel: the cycle's longest single launch (the roofline below); the
-        # largest share of a cycle (us x launches per cycle) is named beside it
-        dominant = max(table, key=lambda t: t["us"]) if table else None
-        top_share = max(table, key=lambda t: t["us"] * t["per_cycle"]) if table else None
+        # in-graph durations: one rank captures the cycle with a timing
+        # event after every operation and replays it (amg_solver_cycle_timeline); each table
+        # row gets its operation's in-graph time where the cycle runs it on the same bytes
+        # (level 0's pre-smoothing carries the norm in the timed solve, coarse levels' first
+        # sweep rides with the restriction above: those rows keep their eager time only)
+        timeline = None
+        if world == 1 and ml.graph_enabled:
+            ops, in_graph = ml.cycle_timeline(x, b, reps=max(5, args.steps))
+            timeline = {"in_graph": in_graph, "reps": max(5, args.steps),
+                        "ops": [{"op": lab, "us": round(us, 1)} for lab, us in ops],
+                        "sum_us": round(sum(us for _, us in ops), 1),
+                        "what": "median event-to-event time of each operation of one V-cycle, the "
+                                "cycle captured with a timing event after every operation and "
+                                "replayed (includes the gap before each operation)"}
+            tl = {lab: us for lab, us in ops} if in_graph else {}
+            for row in table:
+                lab = {"residual": "residual", "interp x += P e": "interp", "restrict R r": "restrict",
+                       "Jacobi": "post-smooth", "post GS (backward)": "post-smooth",
+                       "pre GS (forward)": "pre-smooth"}.get(row["op"])
+                us = tl.get(f"L{row['level']} {lab}") if lab else None
+                if us is not None:
+                    row["in_graph_us"] = round(us, 1)
+                    row["in_graph_frac"] = round(row["stored_bytes"] / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+        # the dominant kernel: the cycle's longest single launch (the roofline below; in-graph
+        # where the timeline has it); the largest share of a cycle (us x launches per cycle) is
+        # named beside it
+        def launch_us(t):
+            return t.get("in_graph_us", t["us"])
+
+        dominant = max(table, key=launch_us) if table else None
+        top_share = max(table, key=lambda t: launch_us(t) * t["per_cycle"]) if table else None
         del fl_src, fl_dst, rd_part
         barrier()
 
@@ -536,20 +563,25 @@ def main():
             "roofline": None if dominant is None else {
                 "bound": "hbm",
                 "kernel": f"{dominant['kernel']} -- level-{dominant['level']} {dominant['op']}, rank 0",
-                "achieved": dominant["GBps"],
+                "achieved": round(dominant["stored_bytes"] / (launch_us(dominant) * 1e-6) / 1e9, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": dominant["frac"],
+                "frac": round(dominant["stored_bytes"] / (launch_us(dominant) * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                "timing": ("in-graph: median over replays of the captured cycle, timing events "
+                           "around the operation (amg_solver_cycle_timeline)" if "in_graph_us" in dominant
+                           else "eager back-to-back launches, HIP events"),
+                "eager": {"avg_launch_ms": round(dominant["us"] * 1e-3, 5), "achieved": dominant["GBps"],
+                          "frac": dominant["frac"]},
                 "traffic": dominant.get("traffic"),
                 "traffic_unit": "bytes per launch",
                 "bytes_per_launch": dominant["stored_bytes"],
                 "bytes_definition": "stored-format HBM bytes per launch (DESIGN.md 4, 8(d) per-unit "
                                     "figures in the operator's stored format)",
-                "avg_launch_ms": round(dominant["us"] * 1e-3, 5),
+                "avg_launch_ms": round(launch_us(dominant) * 1e-3, 5),
                 "stream_copy_GBps": round(copy_gbs, 1),
                 "stream_read_GBps": round(read_gbs, 1),
                 "largest_cycle_share": None if top_share is None else
-                    {k: top_share[k] for k in ("level", "op", "kernel", "us", "per_cycle", "frac")},
+                    {k: top_share.get(k) for k in ("level", "op", "kernel", "us", "in_graph_us", "per_cycle", "frac")},
             },
             # SURVEY.md 8(d)'s SpMV leg (north_star: >= 60 % of the HBM roofline on the 256^3
             # 7-pt SpMV): the level-0 mult on the plain CSR arrays 8(d) prices
@@ -598,6 +630,7 @@ def main():
             "runtime": ra.runtime_versions(),
             "vcycle_kernels": table,
             "vcycle_dominant_kernel": dominant,
+            "cycle_timeline": timeline,
             "cycle_modes": modes,
             "time_to_tol": time_to_tol,
             "cpu_baseline": cpu,

@@ -74,7 +74,11 @@ int amg_context_destroy(amg_context ctx);
 /* ---- ParCSRMatrix ------------------------------------------ */
 /* Rank-local rows [first_row, first_row + n_local) of an n_global x n_global matrix;
  * row_ptr[n_local+1], col_global[nnz] (global column ids; sorted per row on entry or
- * sorted by the call), val[nnz].  Collective over the ranks of the context.             */
+ * sorted by the call), val[nnz].  Collective over the ranks of the context.
+ * Memory: on one rank a square matrix also keeps its uploaded CSR on the device (int32
+ * row_ptr / col + fp64 val, 4 (n+1) + 12 nnz bytes: ~5 GB for a 256^3 27-point operator) as
+ * the level-0 image of a later amg_solver_setup, which takes it over; a matrix that is never
+ * set up holds it until amg_par_csr_destroy.                                               */
 int amg_par_csr_create(amg_context ctx, int64_t n_global, int64_t first_row, int64_t n_local,
                        const int64_t* row_ptr, const int64_t* col_global, const double* val,
                        amg_matrix* out);
@@ -151,6 +155,9 @@ typedef struct amg_matrix_info {
                               * old-value couplings + the in-chunk chain walk (4.2c)     */
     int32_t gs_chain_maxw;   /* split sweeps: most in-chunk couplings of one row, forward |  *
                               * backward << 16 (the chain walk's widest LDS-queue bucket) */
+    int32_t deferred;        /* 1: a level operator whose device formats are not built yet (the  *
+                              * V-cycle runs a cycle-order copy): shape fields     *
+                              * are valid, format fields 0 until the first compute call builds it */
 } amg_matrix_info;
 int amg_par_csr_info(amg_matrix A, amg_matrix_info* info);
 
@@ -266,6 +273,17 @@ int amg_solver_set_graph(amg_solver S, int32_t enable);
 /* 1 while cycles replay a hipGraph (0 after set_graph(0), or if the runtime refused to
  * instantiate a multi-rank graph and the solver fell back to eager launches). */
 int amg_solver_get_graph(amg_solver S, int32_t* enabled);
+/* In-graph time of every operation of one V-cycle (one rank; measurement, no reference
+ * counterpart): the cycle is captured with a timing event after each operation (smoothing
+ * sweep, residual, restriction, coarse solve, interpolation) and replayed `reps` times; us[k]
+ * is the median event-to-event time of operation k in microseconds (so it includes the gap
+ * before the operation), labels + k * label_bytes its NUL-terminated name "L<level> <op>".
+ * *n_ops receives the operation count (only the first n_max are written); *in_graph is 1 when
+ * the cycles replayed a captured graph, 0 when they ran eagerly (graphs off).  x is updated
+ * by the reps cycles like amg_solver_cycle. */
+int amg_solver_cycle_timeline(amg_solver S, double* x, const double* b, int32_t reps, int32_t n_max,
+                              double* us, char* labels, int32_t label_bytes, int32_t* n_ops,
+                              int32_t* in_graph);
 int amg_solver_destroy(amg_solver S);
 
 /* ---- host-only hierarchy (no GPU needed) ------------------------------------------ */

@@ -330,9 +330,16 @@ class ParCSRMatrix:
         self.ctx = ctx
         self.h = handle
         self._owner = owner  # solver that owns a borrowed level matrix
-        self.info = self._info()
         if owner is None:
             _track("matrix", self)
+
+    @property
+    def info(self) -> dict:
+        """amg_par_csr_info, read on every access (formats change with set_format and with the
+        first compute call).  A borrowed level operator the V-cycle runs as a cycle-order copy
+        reports deferred = 1 and zero format fields until a compute call builds it (info never
+        builds it: ADVICE r5)."""
+        return self._info()
 
     # ---- construction -------------------------------------------------------------
     @classmethod
@@ -422,7 +429,6 @@ class ParCSRMatrix:
         "blocks" (CSR blocks with x tiles / value indexing on every row) or "csr" (plain
         row_ptr / col / val, the SURVEY.md 8(d) format).  Results are identical."""
         check(lib().amg_par_csr_set_format(self.h, self._FORMATS[fmt]))
-        self.info = self._info()
         return self
 
     def format_digest(self) -> int:
@@ -645,6 +651,21 @@ class ParMultilevel:
         v = C.c_int32()
         check(lib().amg_solver_get_graph(self.h, C.byref(v)))
         return bool(v.value)
+
+    def cycle_timeline(self, x, b, reps=20):
+        """In-graph time of each operation of one V-cycle (one rank): ([(label, us), ...],
+        in_graph).  Runs `reps` cycles on x (amg_solver_cycle_timeline)."""
+        nmax, lb = 256, 64
+        us = np.zeros(nmax)
+        buf = C.create_string_buffer(nmax * lb)
+        n, g = C.c_int32(), C.c_int32()
+        check(lib().amg_solver_cycle_timeline(self.h, _ptr(x), _ptr(b), int(reps), nmax,
+                                              us.ctypes.data_as(C.POINTER(C.c_double)), buf, lb,
+                                              C.byref(n), C.byref(g)))
+        raw = buf.raw
+        ops = [(raw[k * lb:(k + 1) * lb].split(b"\0", 1)[0].decode(), float(us[k]))
+               for k in range(min(n.value, nmax))]
+        return ops, bool(g.value)
 
     def bytes_per_cycle(self) -> int:
         """Algorithmic HBM bytes of one V-cycle on this rank."""

@@ -75,6 +75,7 @@ class MatrixInfo(C.Structure):
         ("tile_line_bytes", C.c_int32),
         ("gs_split", C.c_int32),
         ("gs_chain_maxw", C.c_int32),
+        ("deferred", C.c_int32),
     ]
 
 
@@ -145,6 +146,8 @@ SIGNATURES = {
     "amg_solver_pcg": (C.c_int, [_vp, _vp, _vp, _i32, _f64, _pf64, C.POINTER(_i32)]),
     "amg_solver_set_graph": (C.c_int, [_vp, _i32]),
     "amg_solver_get_graph": (C.c_int, [_vp, C.POINTER(_i32)]),
+    "amg_solver_cycle_timeline": (C.c_int, [_vp, _vp, _vp, _i32, _i32, C.POINTER(C.c_double), C.c_char_p, _i32,
+                                            C.POINTER(_i32), C.POINTER(_i32)]),
     "amg_solver_destroy": (C.c_int, [_vp]),
     "amg_vector_uniform": (C.c_int, [_vp, _i64, _i64, C.c_uint64, _vp]),
     "amg_vector_copy": (C.c_int, [_vp, _i64, _vp, _vp]),

@@ -5,6 +5,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -336,14 +337,11 @@ int amg_par_csr_reorder(amg_matrix A, int method, amg_matrix* out, int64_t* new_
 int amg_par_csr_info(amg_matrix A, amg_matrix_info* info) {
     return guard([&] {
         AMG_CHECK(A && info, "null argument");
-        // a level operator the cycle runs as a cycle-order copy: built here on one rank; on N
-        // ranks the build is collective (halo plan), so info reports its shape only (format
-        // fields 0) and the first compute call, which every rank makes, builds it
-        if (A->m->deferred && A->m->ctx->host.nranks == 1) {
-            set_device(*A->m->ctx);
-            A->m->ensure_built();
-        }
+        // a level operator the cycle runs as a cycle-order copy is not built by info (that
+        // would undo the deferral and double the level's device memory): its shape
+        // fields are valid, its format fields 0 with deferred = 1, until the first compute call
         const DevMatrix& m = *A->m;
+        info->deferred = m.deferred ? 1 : 0;
         info->n_global_rows = m.host.n_global_rows;
         info->n_global_cols = m.host.n_global_cols;
         info->first_row = m.first_row;
@@ -661,6 +659,24 @@ int amg_solver_set_graph(amg_solver S, int32_t enable) {
         if (enable && S->s.ctx->host.nranks > 1) AMG_CHECK(Solver::rccl_graph_allowed(&why), why);
         S->s.use_graph = enable != 0;
         S->s.destroy_graphs();
+    });
+}
+
+int amg_solver_cycle_timeline(amg_solver S, double* x, const double* b, int32_t reps, int32_t n_max,
+                              double* us, char* labels, int32_t label_bytes, int32_t* n_ops, int32_t* in_graph) {
+    return guard([&] {
+        AMG_CHECK(S && us && labels && n_ops && in_graph, "null argument");
+        AMG_CHECK(n_max >= 0 && label_bytes >= 2, "bad buffer sizes");
+        set_device(*S->s.ctx);
+        std::vector<std::string> lab;
+        std::vector<double> t;
+        *in_graph = S->s.cycle_timeline(x, b, reps, lab, t) ? 1 : 0;
+        *n_ops = (int32_t)t.size();
+        for (size_t k = 0; k < t.size() && (int32_t)k < n_max; ++k) {
+            us[k] = t[k];
+            char* dst = labels + k * (size_t)label_bytes;
+            std::snprintf(dst, (size_t)label_bytes, "%s", lab[k].c_str());
+        }
     });
 }
 

@@ -610,6 +610,18 @@ struct Solver {
     int32_t pcg(double* x, const double* b, int32_t max_iter, double tol, double* hist_host);
     DevBuf<double> pcg_vec, pcg_scratch;  // r | z | p | q ; dot partials | tmp | gathered | scalars
     void dot(const double* a, const double* b, double* dst, bool take_sqrt);
+    // in-graph time of every operation of a cycle (amg_solver_cycle_timeline, one rank): while
+    // tl_on, cycle_rec records a timing event after each operation -- inside a capture these
+    // become event-record nodes of the graph, so a replay timestamps its own kernels
+    bool tl_on = false;
+    std::vector<hipEvent_t> tl_ev;
+    std::vector<std::string> tl_label;
+    size_t tl_n = 0;
+    void mark(size_t l, const char* what);
+    // reps replays (eager cycles where graphs are off); per operation the median of the
+    // event-to-event times in microseconds; returns true if the cycles replayed a graph
+    bool cycle_timeline(double* x, const double* b, int reps, std::vector<std::string>& labels,
+                        std::vector<double>& us);
     int64_t bytes_per_cycle(size_t l) const;
     // the bytes level l's share of a cycle streams in the stored formats (<= what HBM can
     // move in the measured time)

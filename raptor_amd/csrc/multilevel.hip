@@ -1,6 +1,7 @@
 // multilevel.hip -- ParMultilevel: hierarchy setup (host, distributed) and the GPU V-cycle.
 // SURVEY.md 8a rows a6-a10.  The cycle mirrors oracle/amg_oracle.c cycle_rec() operation
 // for operation, so the iterates are bit-identical to the oracle's.
+#include <algorithm>
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
@@ -208,6 +209,7 @@ struct CycleOrder {
 Solver::~Solver() {
     for (auto& g : graphs)
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    for (hipEvent_t e : tl_ev) (void)hipEventDestroy(e);
 }
 
 void Solver::setup(DevMatrix& A, const amg_options& o) {
@@ -522,6 +524,83 @@ void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_
         par_apply(A, KM_JACOBI, x, b, tmp, opt.jacobi_omega, nullptr);
     }
     std::swap(x, tmp);
+    mark(l, post ? "post-smooth" : with_norm ? "pre-smooth + norm" : x_zero ? "pre-smooth from 0" : "pre-smooth");
+}
+
+void Solver::mark(size_t l, const char* what) {
+    if (!tl_on) return;
+    if (tl_n == tl_ev.size()) {
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreate(&e));  // timing enabled
+        tl_ev.push_back(e);
+        tl_label.emplace_back();
+    }
+    tl_label[tl_n] = "L" + std::to_string(l) + " " + what;
+    HIP_CHECK(hipEventRecord(tl_ev[tl_n], ctx->stream));
+    ++tl_n;
+}
+
+bool Solver::cycle_timeline(double* x, const double* b, int reps, std::vector<std::string>& labels,
+                            std::vector<double>& us) {
+    AMG_CHECK(ctx->host.nranks == 1, "cycle timeline: one rank");
+    AMG_CHECK(reps >= 1, "cycle timeline: reps must be >= 1");
+    hipStream_t s = ctx->stream;
+    hipGraphExec_t exec = nullptr;
+    auto record = [&] {
+        tl_on = true;
+        tl_n = 0;
+        try {
+            mark(0, "begin");
+            cycle_rec(0, x, b, false, false);
+        } catch (...) {
+            tl_on = false;
+            throw;
+        }
+        tl_on = false;
+    };
+    if (use_graph) {
+        hipGraph_t g = nullptr;
+        HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        ctx->capturing = true;
+        std::string err;
+        try {
+            record();
+        } catch (const std::exception& e) {
+            err = e.what();
+        }
+        ctx->capturing = false;
+        const hipError_t ce = hipStreamEndCapture(s, &g);
+        AMG_CHECK(err.empty(), "cycle timeline capture: " + err);
+        HIP_CHECK(ce);
+        const hipError_t ie = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (ie != hipSuccess) {
+            (void)hipGetLastError();
+            exec = nullptr;
+        }
+    }
+    const size_t n = tl_n;
+    std::vector<std::vector<float>> t(n > 0 ? n - 1 : 0);
+    for (int r = 0; r < reps; ++r) {
+        if (exec) HIP_CHECK(hipGraphLaunch(exec, s));
+        else record();
+        HIP_CHECK(hipStreamSynchronize(s));
+        for (size_t k = 1; k < n; ++k) {
+            float ms = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&ms, tl_ev[k - 1], tl_ev[k]));
+            t[k - 1].push_back(ms);
+        }
+    }
+    if (exec) {
+        HIP_CHECK(hipGraphExecDestroy(exec));
+    }
+    labels.assign(tl_label.begin() + 1, tl_label.begin() + (n > 0 ? n : 1));
+    us.clear();
+    for (auto& v : t) {
+        std::sort(v.begin(), v.end());
+        us.push_back(1e3 * (double)v[v.size() / 2]);
+    }
+    return exec != nullptr;
 }
 
 // AMG_FUSE_RESTRICT_J0=0: separate jacobi_zero launches (A/B)
@@ -556,6 +635,7 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
         } else {
             launch_dense_gemv(s, A.n_rows, coarse_n, invT.p, bf, x);
         }
+        mark(l, "coarse solve");
         return;
     }
     Level& L = levels[l];
@@ -569,6 +649,7 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
     }
     if (zero) launch_zero(s, A.n_rows, cur);
     par_apply(A, KM_RESID, cur, b, L.r.p, 0.0, nullptr);
+    mark(l, "residual");
     Level& C = levels[l + 1];
     if ((int)l + 1 == rep_level) {
         // distributed R output -> whole b_{l+1} on every rank (padded allgather + unpad)
@@ -583,6 +664,7 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
                                          cnt * sizeof(double), hipMemcpyDeviceToDevice, s));
         }
         (void)me;
+        mark(l, "restrict + allgather");
         cycle_rec(l + 1, C.x.p, C.b.p, true, false);
         // this rank's slice of the whole correction feeds the distributed interpolation
         par_apply(CP(l), KM_SPMV_ADD, C.x.p + L.P->first_col, nullptr, cur, 0.0, nullptr);
@@ -593,12 +675,16 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
                         fuse_restrict_j0() &&
                         par_restrict_j0(CR(l), L.r.p, C.b.p, C.t.p, CA(l + 1).dinv.p, opt.jacobi_omega);
         if (!j0) par_apply(CR(l), KM_SPMV, L.r.p, nullptr, C.b.p, 0.0, nullptr);
+        mark(l, j0 ? "restrict + next pre-smooth from 0" : "restrict");
         cycle_rec(l + 1, C.x.p, C.b.p, true, false, j0);
         par_apply(CP(l), KM_SPMV_ADD, C.x.p, nullptr, cur, 0.0, nullptr);
     }
+    mark(l, "interp");
     for (int k = 0; k < opt.post_sweeps; ++k) smooth(l, cur, b, tmp, false, false, true);
-    if (cur != x)
+    if (cur != x) {
         HIP_CHECK(hipMemcpyAsync(x, cur, A.n_rows * sizeof(double), hipMemcpyDeviceToDevice, s));
+        mark(l, "copy");
+    }
 }
 
 bool Solver::can_fuse_norm() const {

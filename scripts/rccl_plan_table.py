@@ -55,7 +55,7 @@ def main():
                 for w in "APR":
                     if w != "A" and l == ml.num_levels - 1:
                         continue
-                    inf = ml.level_matrix(l, w).info
+                    inf = ml.level_matrix(l, w + "_cycle").info  # the operators the cycle runs
                     e[w] = {"peers": inf["n_neighbors"], "recv": inf["n_halo"], "send": inf["n_send"]}
                 out.append(e)
             res[r] = out

@@ -340,6 +340,35 @@ def test_setup_failure_with_overlapped_gs_builds_is_an_error(ctx):
     assert hist[-1] < hist[0]
 
 
+@pytest.mark.parametrize("coarsen,smoother", [("pmis", "jacobi"), ("sa", "hybrid_gs")])
+def test_cycle_timeline(ctx, oracle, coarsen, smoother):
+    """amg_solver_cycle_timeline (the bench's in-graph durations): one labelled, positive time
+    per operation of the cycle, replayed from a captured graph, and the reps cycles it ran
+    leave x exactly where as many ordinary cycles do."""
+    import raptor_amd as ra
+
+    O = oracle
+    dims = (28, 26, 24)
+    A = ra.par_stencil_grid(ctx, "7pt", dims)
+    ml = ra.ParMultilevel(coarsen=coarsen, smoother=smoother).setup(A)
+    n = A.local_rows
+    b = to_dev(ctx, O.vec_uniform(n, 42))
+    x = ctx.zeros(n)
+    ops, in_graph = ml.cycle_timeline(x, b, reps=5)
+    assert in_graph
+    labels = [lab for lab, _ in ops]
+    L = ml.num_levels
+    for l in range(L - 1):
+        for op in ("residual", "interp", "post-smooth"):
+            assert f"L{l} {op}" in labels, (l, op, labels)
+    assert "L0 pre-smooth" in labels and f"L{L - 1} coarse solve" in labels
+    assert all(us > 0.0 for _, us in ops)
+    x2 = ctx.zeros(n)
+    for _ in range(5):
+        ml.cycle(x2, b)
+    assert np.array_equal(to_host(ctx, x), to_host(ctx, x2))
+
+
 CASES = [
     ("7pt", (24, 24, 24), "pmis", "jacobi"),
     ("5pt", (48, 40), "rs", "jacobi"),

@@ -42,7 +42,13 @@ def boundary_faces(torch, n, dims, device):
     return faces.to(torch.float64)
 
 
-@pytest.mark.parametrize("partition", ["slabs", "boxes"])
+# the z-slab form is opt-in since r6 (AMG_TEST_512_SLABS=1; ~50 s): the -m gpu step keeps its
+# time for the full-size configs[2] / configs[4] checks (test_gpu_zfull_configs.py); boxes are
+# the partition bench.py --gpus 8 runs
+@pytest.mark.parametrize("partition", [
+    pytest.param("slabs", marks=pytest.mark.skipif(os.environ.get("AMG_TEST_512_SLABS") != "1",
+                                                   reason="opt-in: AMG_TEST_512_SLABS=1")),
+    "boxes"])
 def test_512cubed_one_rank_vs_eight_loopback_ranks(capfd, monkeypatch, partition):
     import torch
 
