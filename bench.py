@@ -320,9 +320,10 @@ def main():
             timeline = {"in_graph": in_graph, "reps": max(5, args.steps),
                         "ops": [{"op": lab, "us": round(us, 1)} for lab, us in ops],
                         "sum_us": round(sum(us for _, us in ops), 1),
-                        "what": "median event-to-event time of each operation of one V-cycle, the "
-                                "cycle captured with a timing event after every operation and "
-                                "replayed (includes the gap before each operation)"}
+                        "what": "median event-to-event time of each operation of one V-cycle: the "
+                                "cycle captured as one graph per operation, replayed back to back "
+                                "with timing events between them (each time includes the "
+                                "graph-launch gap before the operation)"}
             tl = {lab: us for lab, us in ops} if in_graph else {}
             for row in table:
                 lab = {"residual": "residual", "interp x += P e": "interp", "restrict R r": "restrict",
@@ -567,8 +568,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(dominant["stored_bytes"] / (launch_us(dominant) * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                "timing": ("in-graph: median over replays of the captured cycle, timing events "
-                           "around the operation (amg_solver_cycle_timeline)" if "in_graph_us" in dominant
+                "timing": ("in-graph: median over replays of the cycle captured one graph per "
+                           "operation, timing events between them (amg_solver_cycle_timeline)" if "in_graph_us" in dominant
                            else "eager back-to-back launches, HIP events"),
                 "eager": {"avg_launch_ms": round(dominant["us"] * 1e-3, 5), "achieved": dominant["GBps"],
                           "frac": dominant["frac"]},

@@ -274,10 +274,11 @@ int amg_solver_set_graph(amg_solver S, int32_t enable);
  * instantiate a multi-rank graph and the solver fell back to eager launches). */
 int amg_solver_get_graph(amg_solver S, int32_t* enabled);
 /* In-graph time of every operation of one V-cycle (one rank; measurement, no reference
- * counterpart): the cycle is captured with a timing event after each operation (smoothing
- * sweep, residual, restriction, coarse solve, interpolation) and replayed `reps` times; us[k]
- * is the median event-to-event time of operation k in microseconds (so it includes the gap
- * before the operation), labels + k * label_bytes its NUL-terminated name "L<level> <op>".
+ * counterpart): the cycle is captured as one graph per operation (smoothing sweep, residual,
+ * restriction, coarse solve, interpolation), the graphs are replayed back to back `reps`
+ * times with a timing event between consecutive ones; us[k] is the median event-to-event
+ * time of operation k in microseconds (its kernels plus the graph-launch gap before them),
+ * labels + k * label_bytes its NUL-terminated name "L<level> <op>".
  * *n_ops receives the operation count (only the first n_max are written); *in_graph is 1 when
  * the cycles replayed a captured graph, 0 when they ran eagerly (graphs off).  x is updated
  * by the reps cycles like amg_solver_cycle. */

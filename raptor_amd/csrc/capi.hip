@@ -337,11 +337,22 @@ int amg_par_csr_reorder(amg_matrix A, int method, amg_matrix* out, int64_t* new_
 int amg_par_csr_info(amg_matrix A, amg_matrix_info* info) {
     return guard([&] {
         AMG_CHECK(A && info, "null argument");
+        std::memset(info, 0, sizeof(*info));
         // a level operator the cycle runs as a cycle-order copy is not built by info (that
         // would undo the deferral and double the level's device memory): its shape
         // fields are valid, its format fields 0 with deferred = 1, until the first compute call
         const DevMatrix& m = *A->m;
         info->deferred = m.deferred ? 1 : 0;
+        if (m.deferred) {  // shape only
+            info->n_global_rows = m.host.n_global_rows;
+            info->n_global_cols = m.host.n_global_cols;
+            info->first_row = m.first_row;
+            info->n_local_rows = m.n_rows;
+            info->first_col = m.first_col;
+            info->n_local_cols = m.n_cols_local;
+            info->nnz_local = m.nnz;
+            return;
+        }
         info->n_global_rows = m.host.n_global_rows;
         info->n_global_cols = m.host.n_global_cols;
         info->first_row = m.first_row;

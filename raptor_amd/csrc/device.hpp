@@ -82,8 +82,8 @@ constexpr int kTplMasterMax = 27;
 
 // Host <-> device copies of large pageable buffers (setup: operator uploads, Galerkin and
 // P / R downloads) through pinned staging: OpenMP threads fill one 32 MiB buffer while the
-// DMA engine drains the other.  Synchronous for the host.  Below 4 MiB, or with
-// AMG_STAGED_COPY=0, plain hipMemcpy.  copy_to_host waits for `after` (the producing stream).
+// DMA engine drains the other.  Synchronous for the host.  Below 4 MiB, plain hipMemcpy.
+// copy_to_host waits for `after` (the producing stream).
 void copy_to_device(void* dst, const void* src, size_t bytes);
 void copy_to_host(void* dst, const void* src, size_t bytes, hipStream_t after);
 
@@ -611,11 +611,12 @@ struct Solver {
     DevBuf<double> pcg_vec, pcg_scratch;  // r | z | p | q ; dot partials | tmp | gathered | scalars
     void dot(const double* a, const double* b, double* dst, bool take_sqrt);
     // in-graph time of every operation of a cycle (amg_solver_cycle_timeline, one rank): while
-    // tl_on, cycle_rec records a timing event after each operation -- inside a capture these
-    // become event-record nodes of the graph, so a replay timestamps its own kernels
+    // tl_on, cycle_rec marks the end of each operation -- a timing event when eager, the end of
+    // a captured segment (one graph per operation, replayed back to back) when capturing
     bool tl_on = false;
     std::vector<hipEvent_t> tl_ev;
     std::vector<std::string> tl_label;
+    std::vector<hipGraph_t> tl_graphs;  // the timeline's captured segments (one per operation)
     size_t tl_n = 0;
     void mark(size_t l, const char* what);
     // reps replays (eager cycles where graphs are off); per operation the median of the

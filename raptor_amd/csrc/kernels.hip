@@ -2037,15 +2037,6 @@ void launch_append(hipStream_t s, const double* v, double* hist, int* counter) {
     HIP_CHECK(hipGetLastError());
 }
 
-// AMG_TPL_MARCH_WIDE=1: z-marching also for windows of more than 8 slots per lane (A/B)
-static bool tpl_march_wide() {
-    static const bool on = [] {
-        const char* e = std::getenv("AMG_TPL_MARCH_WIDE");
-        return e && std::atoi(e) != 0;
-    }();
-    return on;
-}
-
 int kernel_variant(const DevMatrix& A) {
     // variant bits: 2 = XCD-ordered blocks, 4 = gather path (no x tile), 8 = value-indexed
     // blocks (when any block qualifies), 32 = row templates (when built), 128 = z-marching
@@ -2059,7 +2050,7 @@ int kernel_variant(const DevMatrix& A) {
     // scripts/spmv_variants.py; results are identical).
     const char* ev = getenv("AMG_KERNEL_VARIANT");
     int var = ev ? atoi(ev) : (A.default_variant | (A.n_vi_blocks > 0 ? 8 : 0) | (A.n_tpl > 0 ? 32 : 0) |
-                                (A.tpl_march_s > 0 && (A.tpl_win <= 8 * kTPB || tpl_march_wide()) ? 128 : 0));
+                                (A.tpl_march_s > 0 && A.tpl_win <= 8 * kTPB ? 128 : 0));
     if (A.n_vi_blocks == 0) var &= ~8;
     if (A.n_tpl == 0) var &= ~32;
     // AMG_FORMAT_BLOCKS: the CSR block kernel on every row (no templates)
@@ -2091,20 +2082,12 @@ int DevMatrix::norm_parts() const {
 
 // window path: the persistent kernel with a grid of exactly the resident workgroups (its
 // blocks are split statically, so a workgroup that waited for a slot would double the tail),
-// or one workgroup per block when that is no more (AMG_TPL_PERSIST=0: always one per block)
+// or one workgroup per block when that is no more
 template <int M, bool N, int P, int K>
 static void launch_tpl_window(hipStream_t s, const TplArgs& a, int g, size_t lds) {
-    static const bool allow_persist = [] {
-        const char* e = std::getenv("AMG_TPL_PERSIST");
-        return !(e && std::atoi(e) == 0);
-    }();
     // larger windows: the one-block kernel (27-pt SpMV 146 us; the persistent form 164,
-    // marching 153: profiles/r2w_wide_forms.txt); AMG_TPL_WIDE_PERSIST=1: persistent (A/B)
-    static const bool wide_persist = [] {
-        const char* e = std::getenv("AMG_TPL_WIDE_PERSIST");
-        return e && std::atoi(e) != 0;
-    }();
-    if (P > 8 && !wide_persist) {
+    // marching 153: profiles/r2w_wide_forms.txt)
+    if (P > 8) {
         hipLaunchKernelGGL((tpl_kernel<M, N, P, K>), dim3(g), dim3(kTPB), lds, s, a);
         return;
     }
@@ -2120,7 +2103,7 @@ static void launch_tpl_window(hipStream_t s, const TplArgs& a, int g, size_t lds
         occ_lds = lds;
     }
     const int gp = std::min(g, cus * occ) / 8 * 8;
-    if (allow_persist && gp >= 8 && g > gp)
+    if (gp >= 8 && g > gp)
         hipLaunchKernelGGL((tpl_persist_kernel<M, N, P, K>), dim3(gp), dim3(kTPB), lds, s, a, g);
     else
         hipLaunchKernelGGL((tpl_kernel<M, N, P, K>), dim3(g), dim3(kTPB), lds, s, a);
@@ -2163,12 +2146,7 @@ void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const do
     const int g = A.tpl_blocks();
     if (g <= 0) return;
     AMG_ASSERT(A.square && A.n_tpl > 0 && A.n_tpl <= kTplMax && A.n_tpl_ent <= kTplEntries);
-    // AMG_TPL_WINDOW=0: global x loads even where the window fits (experiments)
-    static const bool allow_win = [] {
-        const char* e = std::getenv("AMG_TPL_WINDOW");
-        return !(e && std::atoi(e) == 0);
-    }();
-    const bool win = allow_win && A.tpl_win > 0;
+    const bool win = A.tpl_win > 0;
     TplArgs a{};
     a.id = A.tpl_id.p;
     a.hdr = A.tpl_hdr.p;
@@ -2504,11 +2482,7 @@ void launch_hybrid_gs(hipStream_t s, const DevMatrix& A, const double* x, const 
     GsArgs a{A.gs_slabs.p, A.gs_col.p, A.gs_val.p, x, A.halo.p, (int)A.n_cols_local, b,
              A.gs_dinv.p, y, (long long)A.first_row, (long long)A.gs_block, (int)A.n_rows,
              s1, partial, A.gs_vid.p, A.gs_vtab.p, A.gs_ndict, s0};
-    static const int forced = [] {
-        const char* e = std::getenv("AMG_GS_VARIANT");  // 0 narrow, 1 wide (experiments)
-        return e ? std::atoi(e) : -1;
-    }();
-    const bool wide = forced >= 0 ? forced == 1 : A.gs_wide;
+    const bool wide = A.gs_wide;
     const int ns = s1 - s0;
     const dim3 grid(wide ? ns : (ns + 3) / 4), block(wide ? 64 : 256);
 #define AMG_GS(BK, WD, NM)                                                                          \

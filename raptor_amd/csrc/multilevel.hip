@@ -16,14 +16,6 @@ namespace amg {
 
 namespace {
 
-// AMG_SETUP_OVERLAP=0: build the device formats after the whole hierarchy (A/B)
-bool setup_overlap() {
-    static const bool on = [] {
-        const char* e = std::getenv("AMG_SETUP_OVERLAP");
-        return !(e && *e && std::atoi(e) == 0);
-    }();
-    return on;
-}
 
 // One worker thread that builds device formats (DevMatrix::build_view: host C++ format
 // builds + uploads) in FIFO order while the setup thread coarsens the next level: level l's
@@ -258,7 +250,7 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
     }
     PhaseTimer tm(comm);
     // device formats of finished levels, built on a worker thread during the hierarchy
-    const bool overlap = comm.nranks == 1 && setup_overlap();
+    const bool overlap = comm.nranks == 1;
     const size_t maxl = (size_t)std::max(opt.max_levels, 1) + 1;
     std::vector<std::unique_ptr<DevMatrix>> preA(maxl), preP(maxl), preR(maxl), preAc(maxl), prePc(maxl), preRc(maxl);
     const bool hgs = opt.smoother == AMG_SMOOTH_HYBRID_GS;
@@ -527,16 +519,31 @@ void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_
     mark(l, post ? "post-smooth" : with_norm ? "pre-smooth + norm" : x_zero ? "pre-smooth from 0" : "pre-smooth");
 }
 
+// Timeline marks.  Eager: a timing event after the operation.  Under the timeline's capture:
+// the capture is closed there (the segment since the previous mark becomes its own graph) and
+// reopened -- HIP captures a plain event record only as a dependency marker, and an External
+// record inside a capture is refused by the runtime torch bundles, so the replay launches the
+// segments' graphs back to back with timing events recorded between them.
 void Solver::mark(size_t l, const char* what) {
     if (!tl_on) return;
+    hipStream_t s = ctx->stream;
+    const std::string label = "L" + std::to_string(l) + " " + what;
+    if (ctx->capturing) {
+        hipGraph_t g = nullptr;
+        HIP_CHECK(hipStreamEndCapture(s, &g));
+        tl_graphs.push_back(g);
+        tl_label.push_back(label);
+        HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        return;
+    }
     if (tl_n == tl_ev.size()) {
         hipEvent_t e;
         HIP_CHECK(hipEventCreate(&e));  // timing enabled
         tl_ev.push_back(e);
-        tl_label.emplace_back();
     }
-    tl_label[tl_n] = "L" + std::to_string(l) + " " + what;
-    HIP_CHECK(hipEventRecord(tl_ev[tl_n], ctx->stream));
+    if (tl_label.size() <= tl_n) tl_label.resize(tl_n + 1);
+    tl_label[tl_n] = label;
+    HIP_CHECK(hipEventRecord(tl_ev[tl_n], s));
     ++tl_n;
 }
 
@@ -545,71 +552,93 @@ bool Solver::cycle_timeline(double* x, const double* b, int reps, std::vector<st
     AMG_CHECK(ctx->host.nranks == 1, "cycle timeline: one rank");
     AMG_CHECK(reps >= 1, "cycle timeline: reps must be >= 1");
     hipStream_t s = ctx->stream;
-    hipGraphExec_t exec = nullptr;
-    auto record = [&] {
-        tl_on = true;
-        tl_n = 0;
-        try {
-            mark(0, "begin");
-            cycle_rec(0, x, b, false, false);
-        } catch (...) {
-            tl_on = false;
-            throw;
+    auto ensure_events = [&](size_t n) {
+        while (tl_ev.size() < n) {
+            hipEvent_t e;
+            HIP_CHECK(hipEventCreate(&e));
+            tl_ev.push_back(e);
         }
-        tl_on = false;
     };
-    if (use_graph) {
-        hipGraph_t g = nullptr;
+    // graphs: one captured segment per operation
+    std::vector<hipGraphExec_t> execs;
+    std::vector<std::string> seg_label;
+    bool graphs_ok = use_graph;
+    if (graphs_ok) {
+        tl_graphs.clear();
+        tl_label.clear();
+        tl_on = true;
         HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         ctx->capturing = true;
         std::string err;
         try {
-            record();
+            cycle_rec(0, x, b, false, false);
         } catch (const std::exception& e) {
             err = e.what();
         }
         ctx->capturing = false;
-        const hipError_t ce = hipStreamEndCapture(s, &g);
+        tl_on = false;
+        hipGraph_t last = nullptr;
+        const hipError_t ce = hipStreamEndCapture(s, &last);
+        if (last) (void)hipGraphDestroy(last);  // after the last mark: nothing
+        for (size_t k = 0; k < tl_graphs.size(); ++k) {
+            hipGraphExec_t e = nullptr;
+            if (err.empty() && ce == hipSuccess && hipGraphInstantiate(&e, tl_graphs[k], nullptr, nullptr, 0) == hipSuccess) {
+                execs.push_back(e);
+                seg_label.push_back(tl_label[k]);
+            } else {
+                (void)hipGetLastError();
+                graphs_ok = false;
+            }
+            (void)hipGraphDestroy(tl_graphs[k]);
+        }
+        tl_graphs.clear();
         AMG_CHECK(err.empty(), "cycle timeline capture: " + err);
-        HIP_CHECK(ce);
-        const hipError_t ie = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        if (ie != hipSuccess) {
-            (void)hipGetLastError();
-            exec = nullptr;
+        if (!graphs_ok) {
+            for (hipGraphExec_t e : execs) (void)hipGraphExecDestroy(e);
+            execs.clear();
         }
     }
-    const size_t n = tl_n;
-    std::vector<std::vector<float>> t(n > 0 ? n - 1 : 0);
+    std::vector<std::vector<float>> t;
     for (int r = 0; r < reps; ++r) {
-        if (exec) HIP_CHECK(hipGraphLaunch(exec, s));
-        else record();
+        size_t n = 0;
+        if (graphs_ok) {
+            ensure_events(execs.size() + 1);
+            HIP_CHECK(hipEventRecord(tl_ev[0], s));
+            for (size_t k = 0; k < execs.size(); ++k) {
+                HIP_CHECK(hipGraphLaunch(execs[k], s));
+                HIP_CHECK(hipEventRecord(tl_ev[k + 1], s));
+            }
+            n = execs.size() + 1;
+        } else {
+            tl_on = true;
+            tl_n = 0;
+            try {
+                mark(0, "begin");
+                cycle_rec(0, x, b, false, false);
+            } catch (...) {
+                tl_on = false;
+                throw;
+            }
+            tl_on = false;
+            n = tl_n;
+            seg_label.assign(tl_label.begin() + 1, tl_label.begin() + (n > 0 ? n : 1));
+        }
         HIP_CHECK(hipStreamSynchronize(s));
+        t.resize(n > 0 ? n - 1 : 0);
         for (size_t k = 1; k < n; ++k) {
             float ms = 0.f;
             HIP_CHECK(hipEventElapsedTime(&ms, tl_ev[k - 1], tl_ev[k]));
             t[k - 1].push_back(ms);
         }
     }
-    if (exec) {
-        HIP_CHECK(hipGraphExecDestroy(exec));
-    }
-    labels.assign(tl_label.begin() + 1, tl_label.begin() + (n > 0 ? n : 1));
+    for (hipGraphExec_t e : execs) HIP_CHECK(hipGraphExecDestroy(e));
+    labels = seg_label;
     us.clear();
     for (auto& v : t) {
         std::sort(v.begin(), v.end());
         us.push_back(1e3 * (double)v[v.size() / 2]);
     }
-    return exec != nullptr;
-}
-
-// AMG_FUSE_RESTRICT_J0=0: separate jacobi_zero launches (A/B)
-static bool fuse_restrict_j0() {
-    static const bool on = [] {
-        const char* e = std::getenv("AMG_FUSE_RESTRICT_J0");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return on;
+    return graphs_ok;
 }
 
 void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool with_norm, bool x0_in_t) {
@@ -672,7 +701,6 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
         // Jacobi: the coarse level's first sweep from x = 0 (omega dinv b) rides along with
         // the restriction that produces b (one pass over b and a launch fewer per level)
         const bool j0 = opt.smoother == AMG_SMOOTH_JACOBI && opt.pre_sweeps >= 1 && l + 2 < levels.size() &&
-                        fuse_restrict_j0() &&
                         par_restrict_j0(CR(l), L.r.p, C.b.p, C.t.p, CA(l + 1).dinv.p, opt.jacobi_omega);
         if (!j0) par_apply(CR(l), KM_SPMV, L.r.p, nullptr, C.b.p, 0.0, nullptr);
         mark(l, j0 ? "restrict + next pre-smooth from 0" : "restrict");
@@ -1046,7 +1074,7 @@ int64_t Solver::stored_bytes_per_cycle(size_t l) const {
     int64_t sweeps = 0;
     // the sweep from zero fused into the restriction above (cycle_rec): dinv read + x write
     const DevMatrix* Rup = l > 0 ? &me.CR(l - 1) : nullptr;
-    const bool j0 = !gs && Rup && (int)l != rep_level && fuse_restrict_j0() && Rup->format != AMG_FORMAT_CSR &&
+    const bool j0 = !gs && Rup && (int)l != rep_level && Rup->format != AMG_FORMAT_CSR &&
                     !Rup->tpl_on();
     // a split GS sweep from zero is its chain walk alone (par_hybrid_gs_from_zero)
     const int64_t sweep0 = gs && A.gs_split ? sweep - A.gs_old[1]->mode_bytes(KM_RESID) - 8 * n : sweep;

@@ -43,14 +43,6 @@ namespace {
 
 constexpr size_t kStageChunk = size_t(32) << 20;
 
-bool staged_copies() {
-    static const bool on = [] {
-        const char* e = std::getenv("AMG_STAGED_COPY");
-        return !(e && *e && std::atoi(e) == 0);
-    }();
-    return on;
-}
-
 // two pinned chunks + a copy stream per (device, user); kept for the process lifetime
 struct Stage {
     int device = -1;
@@ -107,7 +99,7 @@ void par_memcpy(void* dst, const void* src, size_t bytes) {
 }  // namespace
 
 void copy_to_device(void* dst, const void* src, size_t bytes) {
-    if (bytes < (size_t(4) << 20) || !staged_copies()) {
+    if (bytes < (size_t(4) << 20)) {
         if (bytes) HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
         return;
     }
@@ -127,7 +119,7 @@ void copy_to_device(void* dst, const void* src, size_t bytes) {
 
 void copy_to_host(void* dst, const void* src, size_t bytes, hipStream_t after) {
     if (after) HIP_CHECK(hipStreamSynchronize(after));
-    if (bytes < (size_t(4) << 20) || !staged_copies()) {
+    if (bytes < (size_t(4) << 20)) {
         if (bytes) HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
         return;
     }
@@ -803,9 +795,8 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
         // The gather kernel reads x from global memory: its blocks need only the kCAP-entry and
         // row caps, not the 256-line tile cap.  sa27's R1 (270 entries per row over ~200 lines
         // each) was cut into blocks of ~1 row by that cap: one lane summing while 255 idled.
-        // AMG_GATHER_LINECAP=1 keeps the cap (A/B)
         int lw = 8;
-        bool line_cap = true;
+        const bool line_cap = tiled;
         if (tiled && !s8.blocks.empty()) {
             const char* e = std::getenv("AMG_TILE_LINE");
             const int force = e ? std::atoi(e) : 0;
@@ -821,10 +812,6 @@ void DevMatrix::build_view(Context* c, const HostCSR& host, bool replicated_view
                 }
                 if (take) lw = 4;
             }
-        }
-        if (!tiled) {
-            const char* e = std::getenv("AMG_GATHER_LINECAP");
-            line_cap = e && std::atoi(e) != 0;
         }
         tm.lap("    build: row blocks, sampled cuts");
         BlockBuild bb = build_row_blocks(hrp, hcol, cls, n_cols_local, plan.n_halo(),

@@ -1668,11 +1668,7 @@ bool transpose_device_dist(Context& ctx, const HostComm& comm, const HostCSR& P,
 // R = P^T on the device for one rank: stable radix sort of the entries by column keeps each
 // R row in ascending fine-row order, like transpose().
 bool transpose_device(Context& ctx, const HostComm& comm, const HostCSR& P, HostCSR& R, SetupImages* imgs) {
-    if (comm.nranks != 1) {
-        const char* e = std::getenv("AMG_TRANSPOSE_DIST");  // 0: the host transpose (A/B, tests)
-        if (e && *e && std::atoi(e) == 0) return false;
-        return transpose_device_dist(ctx, comm, P, R, imgs);
-    }
+    if (comm.nranks != 1) return transpose_device_dist(ctx, comm, P, R, imgs);
     hipStream_t s = ctx.stream;
     const int64_t n = P.nrows(), nnz = P.nnz(), nc = P.n_global_cols;
     if (nnz == 0 || n >= INT_MAX || nnz >= INT_MAX || nc >= INT_MAX) return false;

@@ -686,15 +686,10 @@ HostCSR galerkin_device_dist(Context& ctx, const HostComm& comm, const HostCSR& 
 
 // R (A P) with A P kept on the device between the two products (one rank: no ghost rows, so
 // A P's rows are the B image of the second product as they stand; several ranks:
-// galerkin_device_dist, the ghost rows of A P gathered on the device).  AMG_GALERKIN_DIST=0:
-// several ranks run the two spgemm_device calls (A P through the host), the round-3 form.
+// galerkin_device_dist, the ghost rows of A P gathered on the device).
 HostCSR galerkin_device(Context& ctx, const HostComm& comm, const HostCSR& R, const HostCSR& A,
                         const HostCSR& P, SetupImages* imgs) {
-    if (comm.nranks > 1) {
-        const char* e = std::getenv("AMG_GALERKIN_DIST");
-        if (e && *e && std::atoi(e) == 0) return spgemm_device(ctx, comm, R, spgemm_device(ctx, comm, A, P));
-        return galerkin_device_dist(ctx, comm, R, A, P, imgs);
-    }
+    if (comm.nranks > 1) return galerkin_device_dist(ctx, comm, R, A, P, imgs);
     AMG_CHECK(A.col_starts == P.row_starts && R.col_starts == A.row_starts, "galerkin: partitions differ");
     PhaseTimer tm(comm);
     // one rank: A's (global = local) columns are P's rows, R's are A P's rows; all three

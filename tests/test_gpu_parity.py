@@ -403,7 +403,7 @@ def test_vcycle_bit_exact(ctx, oracle, kind, dims, coarsen, smoother):
             # P and R run the x-tile kernel (variant bit 4 clear: blocks that reuse x lines)
             # or the gather kernel with 16-bit column codes (bit 256): every block's columns
             # fit in <= 4 bands of 16384 at these sizes
-            for w in "PR":
+            for w in ("P_cycle", "R_cycle"):  # the operators the cycle runs
                 v = ml.level_matrix(l, w).info["kernel_variant"]
                 assert (v & 256) or not (v & 4), (l, w, v)
     n = Ao.shape[0]
