@@ -67,6 +67,9 @@ def main():
     ap.add_argument("--quick", action="store_true",
                     help="the timed solve only (no mode comparison, time to tolerance, kernel "
                          "table or CPU baseline): rehearsals and attribution runs")
+    ap.add_argument("--interp", choices=["classical", "ext+i"], default="classical",
+                    help="7pt: interpolation of the PMIS hierarchy (ext+i: distance two, P_max 4, one "
+                         "rank; DESIGN.md 3) -- the default stays classical (time to 1e-8, DESIGN.md 6)")
     ap.add_argument("--config", choices=["7pt", "sa27", "g3sub"], default="7pt",
                     help="7pt: the metric workload (default); sa27: BASELINE.json configs[2], "
                          "27-pt anisotropic Q1 diffusion, smoothed aggregation + hybrid GS; "
@@ -155,7 +158,7 @@ def main():
     if sa27 or g3:  # BASELINE.json configs[2]/[4]: smoothed aggregation + hybrid Gauss-Seidel
         ml = ra.ParSmoothedAggregationSolver(use_graph=graph).setup(A)
     else:     # BASELINE.json configs[1]/[3]: PMIS + classical interpolation, Jacobi
-        ml = ra.ParRugeStubenSolver(coarsen="pmis", use_graph=graph).setup(A)
+        ml = ra.ParRugeStubenSolver(coarsen="pmis", use_graph=graph, interp=args.interp).setup(A)
     setup_s = time.perf_counter() - t1
     nlev = ml.num_levels
     infos = [ml.level_info(l) for l in range(nlev)]
@@ -293,7 +296,9 @@ def main():
         # above 1.1 is wasted traffic (re-reads), below 1 means cache hits served part of the model
         pmc_path = os.path.join(ROOT, "profiles", "pmc_vcycle_kernels.json" if args.config == "7pt"
                                 else f"pmc_vcycle_kernels_{args.config}.json")
-        if args.config in ("7pt", "sa27") and grid == (256, 256, 256) and world == 1 and os.path.exists(pmc_path):
+        if ((args.config in ("7pt", "sa27") and grid == (256, 256, 256)) or (g3 and args.lattice == 1225 and
+                                                                           not args.no_reorder)) \
+                and world == 1 and os.path.exists(pmc_path):
             try:
                 pm = {(o["level"], o["op"]): o for o in json.load(open(pmc_path))["ops"]}
                 for row in table:
@@ -316,14 +321,16 @@ def main():
         # sweep rides with the restriction above: those rows keep their eager time only)
         timeline = None
         if world == 1 and ml.graph_enabled:
-            ops, in_graph = ml.cycle_timeline(x, b, reps=max(5, args.steps))
-            timeline = {"in_graph": in_graph, "reps": max(5, args.steps),
+            ops, tl_mode = ml.cycle_timeline(x, b, reps=max(5, args.steps))
+            in_graph = tl_mode > 0
+            timeline = {"in_graph": in_graph, "mode": {2: "event-record nodes inside one captured cycle",
+                                                       1: "one captured graph per operation",
+                                                       0: "eager"}[tl_mode],
+                        "reps": max(5, args.steps),
                         "ops": [{"op": lab, "us": round(us, 1)} for lab, us in ops],
                         "sum_us": round(sum(us for _, us in ops), 1),
-                        "what": "median event-to-event time of each operation of one V-cycle: the "
-                                "cycle captured as one graph per operation, replayed back to back "
-                                "with timing events between them (each time includes the "
-                                "graph-launch gap before the operation)"}
+                        "what": "median event-to-event time of each operation of one V-cycle, "
+                                "timing events after every operation (mode above)"}
             tl = {lab: us for lab, us in ops} if in_graph else {}
             for row in table:
                 lab = {"residual": "residual", "interp x += P e": "interp", "restrict R r": "restrict",
@@ -531,7 +538,8 @@ def main():
                 (f"3D 27-pt Q1 anisotropic diffusion (1,1,1e-3) {grid[0]}x{grid[1]}x{grid[2]}, "
                              f"smoothed aggregation (MIS(2)), hybrid GS(64) 1+1 V-cycle, {part_label}")
                 if sa27 else
-                (f"3D 7-pt Poisson {grid[0]}x{grid[1]}x{grid[2]}, PMIS + classical interp, "
+                (f"3D 7-pt Poisson {grid[0]}x{grid[1]}x{grid[2]}, PMIS + "
+                 f"{'classical' if args.interp == 'classical' else 'extended+i (P_max 4)'} interp, "
                  f"Jacobi(2/3) 1+1 V-cycle, {part_label}"),
                 "grid": list(grid),
                 "global_rows": n_global,
@@ -568,8 +576,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(dominant["stored_bytes"] / (launch_us(dominant) * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                "timing": ("in-graph: median over replays of the cycle captured one graph per "
-                           "operation, timing events between them (amg_solver_cycle_timeline)" if "in_graph_us" in dominant
+                "timing": (f"in-graph: median over replays, {timeline['mode']} "
+                           "(amg_solver_cycle_timeline)" if "in_graph_us" in dominant
                            else "eager back-to-back launches, HIP events"),
                 "eager": {"avg_launch_ms": round(dominant["us"] * 1e-3, 5), "achieved": dominant["GBps"],
                           "frac": dominant["frac"]},

@@ -205,11 +205,14 @@ int amg_par_csr_destroy(amg_matrix A);
 #define AMG_COARSEN_SA 2     /* smoothed aggregation over MIS(2) aggregates              */
 #define AMG_SMOOTH_JACOBI 0
 #define AMG_SMOOTH_HYBRID_GS 1
+#define AMG_INTERP_CLASSICAL 0  /* RS / PMIS: distance-one classical (modified) interpolation  */
+#define AMG_INTERP_EXT_I 1      /* RS / PMIS: distance-two extended+i with P_max truncation    *
+                                 * (one rank)                                    */
 
 typedef struct amg_options {
     int32_t coarsen;
     int32_t smoother;
-    double strong_threshold;  /* 0.25 classical, 0.08 SA (halved per level)              */
+    double strong_threshold;  /* 0.25 classical, 0.08 SA (x 0.75 per level)               */
     double jacobi_omega;      /* 2/3                                                     */
     int32_t pre_sweeps, post_sweeps;
     int32_t max_levels;
@@ -223,6 +226,9 @@ typedef struct amg_options {
     int64_t replicate_below;  /* multi-rank: levels with <= this many global rows are held
                                  whole by every rank and cycled without communication (one
                                  allgather of b per cycle); 0 = never.  Default 65536.      */
+    int32_t interp;           /* RS / PMIS: AMG_INTERP_CLASSICAL (default) or AMG_INTERP_EXT_I */
+    int32_t p_max;            /* AMG_INTERP_EXT_I: interpolation entries kept per row (the
+                                 largest |w|, rescaled to the row sum); 0 = all.  Default 4  */
 } amg_options;
 
 #define AMG_PRESET_PMIS_JACOBI 0  /* config 2/4: 7-pt Poisson, Jacobi V-cycle            */
@@ -274,14 +280,14 @@ int amg_solver_set_graph(amg_solver S, int32_t enable);
  * instantiate a multi-rank graph and the solver fell back to eager launches). */
 int amg_solver_get_graph(amg_solver S, int32_t* enabled);
 /* In-graph time of every operation of one V-cycle (one rank; measurement, no reference
- * counterpart): the cycle is captured as one graph per operation (smoothing sweep, residual,
- * restriction, coarse solve, interpolation), the graphs are replayed back to back `reps`
- * times with a timing event between consecutive ones; us[k] is the median event-to-event
- * time of operation k in microseconds (its kernels plus the graph-launch gap before them),
- * labels + k * label_bytes its NUL-terminated name "L<level> <op>".
- * *n_ops receives the operation count (only the first n_max are written); *in_graph is 1 when
- * the cycles replayed a captured graph, 0 when they ran eagerly (graphs off).  x is updated
- * by the reps cycles like amg_solver_cycle. */
+ * counterpart): the cycle is captured into one graph with an event-record node after every
+ * operation (smoothing sweep, residual, restriction, coarse solve, interpolation) and replayed
+ * `reps` times; us[k] is the median event-to-event time of operation k in microseconds,
+ * labels + k * label_bytes its NUL-terminated name "L<level> <op>".  *in_graph: 2 = that
+ * graph; 1 = a runtime that does not time event nodes: one graph per operation, replayed back
+ * to back with timing events between them (each time then includes a graph launch); 0 = eager
+ * cycles (graphs off).  *n_ops receives the operation count (only the first n_max are
+ * written).  x is updated by the reps cycles like amg_solver_cycle. */
 int amg_solver_cycle_timeline(amg_solver S, double* x, const double* b, int32_t reps, int32_t n_max,
                               double* us, char* labels, int32_t label_bytes, int32_t* n_ops,
                               int32_t* in_graph);

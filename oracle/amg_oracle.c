@@ -647,6 +647,130 @@ orc_csr* orc_interp_classical(const orc_csr* A, const orc_csr* S, const int32_t*
     return P;
 }
 
+/* Extended+i interpolation (row a8 option, r6; De Sterck, Falgout, Nolting, Yang 2008),
+ * distance two.  F row i: the interpolatory set Chat_i = strong C neighbours (S_i order),
+ * then the strong C neighbours of each strong F neighbour k (S_i order, S_k order), each once;
+ * num_j = 0.0 for j in Chat_i; d = a_ii; in row i's CSR order, a_ij goes to num_j for j in
+ * Chat_i, to d for a weak j (j not in S_i); then for each strong F neighbour k in row i's
+ * order, with abar_kl = a_kl of sign opposite to a_kk (else 0): s_k = sum of abar_kl over l
+ * in Chat_i u {i} (row k order, from 0.0); s_k = 0 adds a_ik to d, else (row k order)
+ * num_l += (a_ik abar_kl) / s_k for l in Chat_i and d += (a_ik abar_ki) / s_k for l = i;
+ * w_ij = -num_j / d, columns ascending.  P_max truncation (p_max > 0, a row of more entries):
+ * tot = sum of the row's w (column order), the p_max largest |w| kept (ties: smaller column),
+ * kept = their sum (column order), each kept w *= (tot / kept) unless kept = 0. */
+static int ext_abar(double akl, int pos) { return pos ? akl < 0.0 : akl > 0.0; }
+
+orc_csr* orc_interp_ext_i(const orc_csr* A, const orc_csr* S, const int32_t* cf, int64_t p_max) {
+    int64_t n = A->n_rows;
+    int64_t* cmap = XMALLOC(int64_t, n);
+    int64_t nc = 0;
+    for (int64_t i = 0; i < n; ++i) cmap[i] = cf[i] == ST_C ? nc++ : -1;
+    int64_t* strong = XMALLOC(int64_t, n); /* strong[j] == i <=> j in S_i     */
+    int64_t* inC = XMALLOC(int64_t, n);    /* inC[j] == i    <=> j in Chat_i  */
+    double* num = XMALLOC(double, n);
+    int64_t* list = XMALLOC(int64_t, n);
+    double* w = XMALLOC(double, n);
+    char* keep = XMALLOC(char, n);
+    for (int64_t j = 0; j < n; ++j) strong[j] = -1, inC[j] = -1;
+    int64_t cap = 64, nnz = 0;
+    int64_t* pc = XMALLOC(int64_t, cap);
+    double* pv = XMALLOC(double, cap);
+    int64_t* rp = XMALLOC(int64_t, n + 1);
+    rp[0] = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t m = 0;
+        if (cf[i] == ST_C) {
+            list[0] = i;
+            w[0] = 1.0;
+            keep[0] = 1;
+            m = 1;
+        } else {
+            for (int64_t t = S->rp[i]; t < S->rp[i + 1]; ++t) strong[S->col[t]] = i;
+            for (int64_t t = S->rp[i]; t < S->rp[i + 1]; ++t) {
+                int64_t j = S->col[t];
+                if (cf[j] == ST_C && inC[j] != i) inC[j] = i, list[m++] = j, num[j] = 0.0;
+            }
+            for (int64_t t = S->rp[i]; t < S->rp[i + 1]; ++t) {
+                int64_t k = S->col[t];
+                if (cf[k] == ST_C) continue;
+                for (int64_t u = S->rp[k]; u < S->rp[k + 1]; ++u) {
+                    int64_t j = S->col[u];
+                    if (cf[j] == ST_C && inC[j] != i) inC[j] = i, list[m++] = j, num[j] = 0.0;
+                }
+            }
+            double d = diag_of(A, i);
+            for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
+                int64_t j = A->col[k];
+                if (j == i) continue;
+                if (inC[j] == i) num[j] += A->val[k];
+                else if (strong[j] != i) d += A->val[k];
+            }
+            for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
+                int64_t kk = A->col[k];
+                if (kk == i || strong[kk] != i || cf[kk] == ST_C) continue;
+                int pos = diag_of(A, kk) > 0.0;
+                double sk = 0.0;
+                for (int64_t u = A->rp[kk]; u < A->rp[kk + 1]; ++u) {
+                    int64_t l = A->col[u];
+                    if (ext_abar(A->val[u], pos) && (inC[l] == i || l == i)) sk += A->val[u];
+                }
+                if (sk == 0.0) {
+                    d += A->val[k];
+                    continue;
+                }
+                for (int64_t u = A->rp[kk]; u < A->rp[kk + 1]; ++u) {
+                    int64_t l = A->col[u];
+                    if (!ext_abar(A->val[u], pos)) continue;
+                    if (inC[l] == i) num[l] += (A->val[k] * A->val[u]) / sk;
+                    else if (l == i) d += (A->val[k] * A->val[u]) / sk;
+                }
+            }
+            qsort(list, (size_t)m, sizeof(int64_t), cmp_i64);
+            for (int64_t t = 0; t < m; ++t) w[t] = -num[list[t]] / d, keep[t] = 1;
+            if (p_max > 0 && m > p_max) {
+                double tot = 0.0, kept = 0.0;
+                for (int64_t t = 0; t < m; ++t) tot += w[t], keep[t] = 0;
+                for (int64_t r = 0; r < p_max; ++r) {
+                    int64_t best = -1;
+                    for (int64_t t = 0; t < m; ++t)
+                        if (!keep[t] && (best < 0 || fabs(w[t]) > fabs(w[best]))) best = t;
+                    keep[best] = 1;
+                }
+                for (int64_t t = 0; t < m; ++t)
+                    if (keep[t]) kept += w[t];
+                if (kept != 0.0) {
+                    double f = tot / kept;
+                    for (int64_t t = 0; t < m; ++t)
+                        if (keep[t]) w[t] = w[t] * f;
+                }
+            }
+        }
+        if (nnz + m > cap) {
+            while (nnz + m > cap) cap *= 2;
+            pc = (int64_t*)realloc(pc, sizeof(int64_t) * (size_t)cap);
+            pv = (double*)realloc(pv, sizeof(double) * (size_t)cap);
+            if (!pc || !pv) abort();
+        }
+        for (int64_t t = 0; t < m; ++t)
+            if (keep[t]) pc[nnz] = cmap[list[t]], pv[nnz++] = w[t];
+        rp[i + 1] = nnz;
+    }
+    free(cmap);
+    free(strong);
+    free(inC);
+    free(num);
+    free(list);
+    free(w);
+    free(keep);
+    orc_csr* P = XMALLOC(orc_csr, 1);
+    P->n_rows = n;
+    P->n_cols = nc;
+    P->rp = rp;
+    P->col = pc;
+    P->val = pv;
+    return P;
+}
+
 /* ------------------------------------------------------------------------------ */
 /* MIS(2) aggregation (row a9; partition-independent).  Tuples (state, hash32, id)   */
 /* with state OUT < UNDECIDED < IN; two synchronous max-propagation hops over the  */
@@ -919,7 +1043,8 @@ orc_hier* orc_hier_setup(const orc_csr* A0, const orc_options* opt) {
             orc_csr* S = orc_strength_classical(A, opt->strong_threshold);
             if (opt->coarsen == ORC_COARSEN_RS) orc_rs_split(S, split);
             else orc_pmis_split(S, opt->seed + (uint64_t)l, split);
-            P = orc_interp_classical(A, S, split);
+            P = opt->interp == ORC_INTERP_EXT_I ? orc_interp_ext_i(A, S, split, opt->p_max)
+                                                : orc_interp_classical(A, S, split);
             orc_csr_free(S);
         }
         /* coarsening stalled: no coarse points, no reduction, or < 20% reduction on a level

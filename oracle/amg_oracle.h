@@ -71,6 +71,8 @@ orc_csr* orc_strength_symmetric(const orc_csr* A, double theta);
 void orc_rs_split(const orc_csr* S, int32_t* cf);   /* cf: 1 = C, 0 = F */
 void orc_pmis_split(const orc_csr* S, uint64_t seed, int32_t* cf);
 orc_csr* orc_interp_classical(const orc_csr* A, const orc_csr* S, const int32_t* cf);
+/* extended+i (distance two) with P_max truncation (p_max = 0: none); DESIGN.md 3 (r6) */
+orc_csr* orc_interp_ext_i(const orc_csr* A, const orc_csr* S, const int32_t* cf, int64_t p_max);
 int64_t orc_mis2_aggregate(const orc_csr* S, uint64_t seed, int32_t* agg);
 /* SA smoothing (r6): filtered operator, max-norm power-iteration rho, smoothed P */
 #define ORC_SA_RHO_ITERS 10
@@ -90,6 +92,7 @@ orc_csr* orc_permute(const orc_csr* A, const int64_t* new_to_old);  /* P A P^T *
 /* ---- hierarchy (ParMultilevel analogue) --------------------- */
 enum { ORC_COARSEN_RS = 0, ORC_COARSEN_PMIS = 1, ORC_COARSEN_SA = 2 };
 enum { ORC_SMOOTH_JACOBI = 0, ORC_SMOOTH_HYBRID_GS = 1 };
+enum { ORC_INTERP_CLASSICAL = 0, ORC_INTERP_EXT_I = 1 };
 
 typedef struct orc_options {
     int32_t coarsen;
@@ -101,6 +104,8 @@ typedef struct orc_options {
     int64_t max_coarse;
     int64_t gs_block;
     uint64_t seed;
+    int32_t interp;  /* RS / PMIS: ORC_INTERP_CLASSICAL or ORC_INTERP_EXT_I */
+    int64_t p_max;   /* ext+i truncation: entries kept per row (0: all) */
 } orc_options;
 
 typedef struct orc_hier orc_hier;

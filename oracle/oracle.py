@@ -18,6 +18,7 @@ _LIB_PATH = os.path.join(_HERE, "liboracle_amg.so")
 
 COARSEN_RS, COARSEN_PMIS, COARSEN_SA = 0, 1, 2
 SMOOTH_JACOBI, SMOOTH_HYBRID_GS = 0, 1
+INTERP_CLASSICAL, INTERP_EXT_I = 0, 1
 
 _i64p = C.POINTER(C.c_int64)
 _i32p = C.POINTER(C.c_int32)
@@ -36,6 +37,8 @@ class _Opt(C.Structure):
         ("max_coarse", C.c_int64),
         ("gs_block", C.c_int64),
         ("seed", C.c_uint64),
+        ("interp", C.c_int32),
+        ("p_max", C.c_int64),
     ]
 
 
@@ -85,6 +88,7 @@ def lib():
             "orc_rs_split": (None, [vp, _i32p]),
             "orc_pmis_split": (None, [vp, C.c_uint64, _i32p]),
             "orc_interp_classical": (vp, [vp, vp, _i32p]),
+            "orc_interp_ext_i": (vp, [vp, vp, _i32p, C.c_int64]),
             "orc_mis2_aggregate": (C.c_int64, [vp, C.c_uint64, _i32p]),
             "orc_sa_prolongator": (vp, [vp, _i32p, C.c_int64, C.c_double, C.c_uint64]),
             "orc_sa_filter": (vp, [vp, C.c_double]),
@@ -288,6 +292,12 @@ def interp_classical(A, S, cf):
     return Csr(lib().orc_interp_classical(A.h, S.h, _p(cf, _i32p)))
 
 
+def interp_ext_i(A, S, cf, p_max=4):
+    """Extended+i interpolation with P_max truncation."""
+    cf = np.ascontiguousarray(cf, np.int32)
+    return Csr(lib().orc_interp_ext_i(A.h, S.h, _p(cf, _i32p), p_max))
+
+
 def mis2_aggregate(S, seed):
     agg = np.empty(S.shape[0], np.int32)
     na = lib().orc_mis2_aggregate(S.h, seed, _p(agg, _i32p))
@@ -332,11 +342,13 @@ class Hierarchy:
 
     def __init__(self, A, coarsen=COARSEN_PMIS, smoother=SMOOTH_JACOBI, strong_threshold=0.25,
                  jacobi_omega=2.0 / 3.0, pre_sweeps=1, post_sweeps=1, max_levels=25,
-                 max_coarse=256, gs_block=64, seed=0x5EED, levels=None):
+                 max_coarse=256, gs_block=64, seed=0x5EED, levels=None, interp=INTERP_CLASSICAL,
+                 p_max=4):
         """Serial setup of A; or, with ``levels=[(A_l, P_l, R_l), ...]`` (Csr objects, P/R
-        None on the coarsest level), a hierarchy made of those operators."""
+        None on the coarsest level), a hierarchy made of those operators.  ``interp``
+        (RS / PMIS): INTERP_CLASSICAL or INTERP_EXT_I (``p_max`` entries kept per row)."""
         o = _Opt(coarsen, smoother, strong_threshold, jacobi_omega, pre_sweeps, post_sweeps,
-                 max_levels, max_coarse, gs_block, seed)
+                 max_levels, max_coarse, gs_block, seed, interp, p_max)
         self.A = A
         if levels is None:
             self.h = lib().orc_hier_setup(A.h, C.byref(o))

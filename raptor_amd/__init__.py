@@ -36,6 +36,8 @@ from ._lib import (  # noqa: F401  (re-exported constants)
     AMG_REORDER_RCM,
     AMG_COARSEN_RS,
     AMG_COARSEN_SA,
+    AMG_INTERP_CLASSICAL,
+    AMG_INTERP_EXT_I,
     AMG_SMOOTH_HYBRID_GS,
     AMG_SMOOTH_JACOBI,
     AMG_STENCIL_5PT,
@@ -583,21 +585,24 @@ class ParMultilevel:
     """AMG hierarchy + V-cycle (RAPtor ParMultilevel analogue).
 
     ``coarsen``: "rs" (serial Ruge-Stueben), "pmis", or "sa" (smoothed aggregation over MIS(2)
-    aggregates).  ``smoother``: "jacobi" or "hybrid_gs"."""
+    aggregates).  ``smoother``: "jacobi" or "hybrid_gs".  ``interp`` (RS / PMIS): "classical"
+    (distance one) or "ext+i" (distance two, ``p_max`` entries kept per row; one rank)."""
 
     _COARSEN = {"rs": AMG_COARSEN_RS, "pmis": AMG_COARSEN_PMIS, "sa": AMG_COARSEN_SA}
+    _INTERP = {"classical": AMG_INTERP_CLASSICAL, "ext+i": AMG_INTERP_EXT_I}
     _SMOOTH = {"jacobi": AMG_SMOOTH_JACOBI, "hybrid_gs": AMG_SMOOTH_HYBRID_GS}
 
     def __init__(self, coarsen="pmis", smoother="jacobi", strong_threshold=None,
                  jacobi_omega=2.0 / 3.0, pre_sweeps=1, post_sweeps=1, max_levels=25,
                  max_coarse=256, gs_block=64, seed=0x5EED, use_graph=None, setup_device=True,
-                 replicate_below=65536):
+                 replicate_below=65536, interp="classical", p_max=4):
         if strong_threshold is None:
             strong_threshold = 0.08 if coarsen == "sa" else 0.25
         self.options = Options(self._COARSEN[coarsen], self._SMOOTH[smoother],
                                float(strong_threshold), float(jacobi_omega), int(pre_sweeps),
                                int(post_sweeps), int(max_levels), int(max_coarse), int(gs_block),
-                               int(seed), int(setup_device), int(replicate_below))
+                               int(seed), int(setup_device), int(replicate_below),
+                               self._INTERP[interp], int(p_max))
         self.use_graph = use_graph
         self.h = None
         self.A = None
@@ -654,7 +659,8 @@ class ParMultilevel:
 
     def cycle_timeline(self, x, b, reps=20):
         """In-graph time of each operation of one V-cycle (one rank): ([(label, us), ...],
-        in_graph).  Runs `reps` cycles on x (amg_solver_cycle_timeline)."""
+        mode) -- mode 2: event nodes inside one captured cycle, 1: one graph per operation,
+        0: eager.  Runs `reps` cycles on x (amg_solver_cycle_timeline)."""
         nmax, lb = 256, 64
         us = np.zeros(nmax)
         buf = C.create_string_buffer(nmax * lb)
@@ -665,7 +671,7 @@ class ParMultilevel:
         raw = buf.raw
         ops = [(raw[k * lb:(k + 1) * lb].split(b"\0", 1)[0].decode(), float(us[k]))
                for k in range(min(n.value, nmax))]
-        return ops, bool(g.value)
+        return ops, int(g.value)
 
     def bytes_per_cycle(self) -> int:
         """Algorithmic HBM bytes of one V-cycle on this rank."""

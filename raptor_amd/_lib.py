@@ -14,6 +14,7 @@ AMG_OK = 0
 AMG_STENCIL_5PT, AMG_STENCIL_7PT, AMG_STENCIL_27PT = 0, 1, 2
 AMG_COARSEN_RS, AMG_COARSEN_PMIS, AMG_COARSEN_SA = 0, 1, 2
 AMG_SMOOTH_JACOBI, AMG_SMOOTH_HYBRID_GS = 0, 1
+AMG_INTERP_CLASSICAL, AMG_INTERP_EXT_I = 0, 1
 AMG_PRESET_PMIS_JACOBI, AMG_PRESET_RS_JACOBI, AMG_PRESET_SA_HYBRID_GS = 0, 1, 2
 AMG_REORDER_RCM = 1
 AMG_FORMAT_AUTO, AMG_FORMAT_CSR, AMG_FORMAT_BLOCKS = 0, 1, 2
@@ -41,6 +42,8 @@ class Options(C.Structure):
         ("seed", C.c_uint64),
         ("setup_device", C.c_int32),
         ("replicate_below", C.c_int64),
+        ("interp", C.c_int32),
+        ("p_max", C.c_int32),
     ]
 
 

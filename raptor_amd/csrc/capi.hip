@@ -546,6 +546,8 @@ int amg_options_default(int preset, amg_options* o) {
         o->seed = 0x5EED;
         o->setup_device = 1;
         o->replicate_below = 65536;
+        o->interp = AMG_INTERP_CLASSICAL;
+        o->p_max = 4;
         if (preset == AMG_PRESET_RS_JACOBI) {
             o->coarsen = AMG_COARSEN_RS;
         } else if (preset == AMG_PRESET_SA_HYBRID_GS) {
@@ -681,7 +683,7 @@ int amg_solver_cycle_timeline(amg_solver S, double* x, const double* b, int32_t 
         set_device(*S->s.ctx);
         std::vector<std::string> lab;
         std::vector<double> t;
-        *in_graph = S->s.cycle_timeline(x, b, reps, lab, t) ? 1 : 0;
+        *in_graph = S->s.cycle_timeline(x, b, reps, lab, t);
         *n_ops = (int32_t)t.size();
         for (size_t k = 0; k < t.size() && (int32_t)k < n_max; ++k) {
             us[k] = t[k];

@@ -614,15 +614,16 @@ struct Solver {
     // tl_on, cycle_rec marks the end of each operation -- a timing event when eager, the end of
     // a captured segment (one graph per operation, replayed back to back) when capturing
     bool tl_on = false;
+    int tl_mode = 0;  // 2: event-record nodes in one graph, 1: one graph per operation, 0: eager
     std::vector<hipEvent_t> tl_ev;
     std::vector<std::string> tl_label;
     std::vector<hipGraph_t> tl_graphs;  // the timeline's captured segments (one per operation)
     size_t tl_n = 0;
     void mark(size_t l, const char* what);
     // reps replays (eager cycles where graphs are off); per operation the median of the
-    // event-to-event times in microseconds; returns true if the cycles replayed a graph
-    bool cycle_timeline(double* x, const double* b, int reps, std::vector<std::string>& labels,
-                        std::vector<double>& us);
+    // event-to-event times in microseconds; returns the mode that timed them (tl_mode)
+    int cycle_timeline(double* x, const double* b, int reps, std::vector<std::string>& labels,
+                       std::vector<double>& us);
     int64_t bytes_per_cycle(size_t l) const;
     // the bytes level l's share of a cycle streams in the stored formats (<= what HBM can
     // move in the measured time)

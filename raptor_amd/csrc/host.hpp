@@ -169,6 +169,8 @@ std::vector<int32_t> rs_split(const HostComm& comm, const HostCSR& S);
 std::vector<int32_t> pmis_split(const HostComm& comm, const HostCSR& S, uint64_t seed);
 HostCSR interp_classical(const HostComm& comm, const HostCSR& A, const HostCSR& S,
                          const std::vector<int32_t>& cf);
+HostCSR interp_ext_i(const HostComm& comm, const HostCSR& A, const HostCSR& S, const std::vector<int32_t>& cf,
+                     int p_max);
 // returns global aggregate id per local row; *n_agg_global receives the count
 std::vector<int64_t> mis2_aggregate(const HostComm& comm, const HostCSR& S, uint64_t seed,
                                     int64_t* n_agg_global, std::vector<int64_t>* agg_starts);

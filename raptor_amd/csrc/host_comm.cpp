@@ -128,6 +128,8 @@ template std::vector<std::vector<int64_t>> HostComm::exchange(
     const std::vector<std::vector<int64_t>>&) const;
 template std::vector<std::vector<double>> HostComm::exchange(
     const std::vector<std::vector<double>>&) const;
+template std::vector<std::vector<int32_t>> HostComm::exchange(
+    const std::vector<std::vector<int32_t>>&) const;
 
 std::vector<int64_t> HostComm::allgather(int64_t v) const {
     std::vector<int64_t> s(nranks, v);

@@ -287,6 +287,115 @@ std::vector<int32_t> pmis_split(const HostComm& comm, const HostCSR& S, uint64_t
 // --------------------------------------------------------------------------------
 // Classical (modified) interpolation, distance 1.  See the oracle for the formula.
 // --------------------------------------------------------------------------------
+// Extended+i interpolation (r6 option; oracle orc_interp_ext_i): distance two,
+// P_max truncation.  One rank (the distance-two sets need the rows of strong F neighbours and
+// their strong C neighbours' states, which a multi-rank setup would fetch two halos deep).
+HostCSR interp_ext_i(const HostComm& comm, const HostCSR& A, const HostCSR& S, const std::vector<int32_t>& cf,
+                     int p_max) {
+    AMG_CHECK(comm.nranks == 1, "extended+i interpolation is implemented for one rank");
+    const int64_t n = A.nrows();
+    std::vector<int64_t> cmap(n);
+    int64_t nc = 0;
+    for (int64_t i = 0; i < n; ++i) cmap[i] = cf[i] == ST_C ? nc++ : -1;
+    const std::vector<double> diag = diagonal(comm, A);
+    std::vector<std::vector<int64_t>> pcol(n);
+    std::vector<std::vector<double>> pval(n);
+#pragma omp parallel
+    {
+        std::vector<int64_t> strong(n, -1), inC(n, -1), list;
+        std::vector<double> num(n), w;
+        std::vector<char> keep;
+#pragma omp for schedule(dynamic, 1024)
+        for (int64_t i = 0; i < n; ++i) {
+            if (cf[i] == ST_C) {
+                pcol[i].push_back(cmap[i]);
+                pval[i].push_back(1.0);
+                continue;
+            }
+            list.clear();
+            for (int64_t t = S.rp[i]; t < S.rp[i + 1]; ++t) strong[S.col[t]] = i;
+            for (int64_t t = S.rp[i]; t < S.rp[i + 1]; ++t) {
+                const int64_t j = S.col[t];
+                if (cf[j] == ST_C && inC[j] != i) inC[j] = i, list.push_back(j), num[j] = 0.0;
+            }
+            for (int64_t t = S.rp[i]; t < S.rp[i + 1]; ++t) {
+                const int64_t k = S.col[t];
+                if (cf[k] == ST_C) continue;
+                for (int64_t u = S.rp[k]; u < S.rp[k + 1]; ++u) {
+                    const int64_t j = S.col[u];
+                    if (cf[j] == ST_C && inC[j] != i) inC[j] = i, list.push_back(j), num[j] = 0.0;
+                }
+            }
+            double d = diag[i];
+            for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+                const int64_t j = A.col[k];
+                if (j == i) continue;
+                if (inC[j] == i) num[j] += A.val[k];
+                else if (strong[j] != i) d += A.val[k];
+            }
+            for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+                const int64_t kk = A.col[k];
+                if (kk == i || strong[kk] != i || cf[kk] == ST_C) continue;
+                const bool pos = diag[kk] > 0.0;
+                auto abar = [pos](double v) { return pos ? v < 0.0 : v > 0.0; };
+                double sk = 0.0;
+                for (int64_t u = A.rp[kk]; u < A.rp[kk + 1]; ++u) {
+                    const int64_t l = A.col[u];
+                    if (abar(A.val[u]) && (inC[l] == i || l == i)) sk += A.val[u];
+                }
+                if (sk == 0.0) {
+                    d += A.val[k];
+                    continue;
+                }
+                for (int64_t u = A.rp[kk]; u < A.rp[kk + 1]; ++u) {
+                    const int64_t l = A.col[u];
+                    if (!abar(A.val[u])) continue;
+                    if (inC[l] == i) num[l] += (A.val[k] * A.val[u]) / sk;
+                    else if (l == i) d += (A.val[k] * A.val[u]) / sk;
+                }
+            }
+            std::sort(list.begin(), list.end());
+            const int64_t m = (int64_t)list.size();
+            w.resize(m);
+            keep.assign(m, 1);
+            for (int64_t t = 0; t < m; ++t) w[t] = -num[list[t]] / d;
+            if (p_max > 0 && m > p_max) {
+                double tot = 0.0, kept = 0.0;
+                for (int64_t t = 0; t < m; ++t) tot += w[t], keep[t] = 0;
+                for (int r = 0; r < p_max; ++r) {
+                    int64_t best = -1;
+                    for (int64_t t = 0; t < m; ++t)
+                        if (!keep[t] && (best < 0 || std::fabs(w[t]) > std::fabs(w[best]))) best = t;
+                    keep[best] = 1;
+                }
+                for (int64_t t = 0; t < m; ++t)
+                    if (keep[t]) kept += w[t];
+                if (kept != 0.0) {
+                    const double f = tot / kept;
+                    for (int64_t t = 0; t < m; ++t)
+                        if (keep[t]) w[t] = w[t] * f;
+                }
+            }
+            for (int64_t t = 0; t < m; ++t)
+                if (keep[t]) pcol[i].push_back(cmap[list[t]]), pval[i].push_back(w[t]);
+        }
+    }
+    HostCSR P;
+    P.n_global_rows = n;
+    P.n_global_cols = nc;
+    P.row_starts = A.row_starts;
+    P.col_starts = {0, nc};
+    P.rp.assign(n + 1, 0);
+    for (int64_t i = 0; i < n; ++i) P.rp[i + 1] = P.rp[i] + (int64_t)pcol[i].size();
+    P.col.resize(P.rp[n]);
+    P.val.resize(P.rp[n]);
+    for (int64_t i = 0; i < n; ++i) {
+        std::copy(pcol[i].begin(), pcol[i].end(), P.col.begin() + P.rp[i]);
+        std::copy(pval[i].begin(), pval[i].end(), P.val.begin() + P.rp[i]);
+    }
+    return P;
+}
+
 HostCSR interp_classical(const HostComm& comm, const HostCSR& A, const HostCSR& S,
                          const std::vector<int32_t>& cf) {
     int64_t n = A.nrows(), lo = A.row_starts[comm.rank], hi = A.row_starts[comm.rank + 1];
@@ -693,7 +802,8 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
             split = opt.coarsen == AMG_COARSEN_RS ? rs_split(comm, S)
                                                   : pmis_split(comm, S, opt.seed + (uint64_t)l);
             tm.lap(L + "split");
-            P = interp_classical(comm, A, S, split);
+            P = opt.interp == AMG_INTERP_EXT_I ? interp_ext_i(comm, A, S, split, opt.p_max)
+                                               : interp_classical(comm, A, S, split);
             tm.lap(L + "interpolation");
         } else {
             throw Error(AMG_ERR_INVALID, "unknown coarsening");

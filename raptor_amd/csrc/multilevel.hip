@@ -374,6 +374,12 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
         if (!overlap) tm.lap("L" + std::to_string(l) + " device A build");
         if (l + 1 < H.levels.size()) {
             levels[l].split = std::move(hl.split);
+            if (rep) {  // a replicated level is whole on every rank: so is its splitting
+                const std::vector<std::vector<int32_t>> all =
+                    comm.exchange(std::vector<std::vector<int32_t>>(comm.nranks, levels[l].split));
+                levels[l].split.clear();
+                for (const auto& v : all) levels[l].split.insert(levels[l].split.end(), v.begin(), v.end());
+            }
             levels[l].P = make(hl.P, preP[l], pr);
             levels[l].R = make(hl.R, preR[l], pr);
             if (!overlap) tm.lap("L" + std::to_string(l) + " device P/R build");
@@ -519,16 +525,17 @@ void Solver::smooth(size_t l, double*& x, const double* b, double*& tmp, bool x_
     mark(l, post ? "post-smooth" : with_norm ? "pre-smooth + norm" : x_zero ? "pre-smooth from 0" : "pre-smooth");
 }
 
-// Timeline marks.  Eager: a timing event after the operation.  Under the timeline's capture:
-// the capture is closed there (the segment since the previous mark becomes its own graph) and
-// reopened -- HIP captures a plain event record only as a dependency marker, and an External
-// record inside a capture is refused by the runtime torch bundles, so the replay launches the
-// segments' graphs back to back with timing events recorded between them.
+// Timeline marks (amg_solver_cycle_timeline).  tl_mode 2, inside the timeline's capture: an
+// event-record node is added behind the capture's current tail and becomes the new tail, so one
+// graph of the whole cycle timestamps every operation as it replays (HIP captures a plain
+// event record only as a dependency marker).  tl_mode 1, inside the capture: the capture is
+// closed there and reopened (one graph per operation, replayed back to back with timing events
+// between them; each time then includes a graph launch).  Eager: a timing event.
 void Solver::mark(size_t l, const char* what) {
     if (!tl_on) return;
     hipStream_t s = ctx->stream;
     const std::string label = "L" + std::to_string(l) + " " + what;
-    if (ctx->capturing) {
+    if (ctx->capturing && tl_mode == 1) {
         hipGraph_t g = nullptr;
         HIP_CHECK(hipStreamEndCapture(s, &g));
         tl_graphs.push_back(g);
@@ -543,12 +550,23 @@ void Solver::mark(size_t l, const char* what) {
     }
     if (tl_label.size() <= tl_n) tl_label.resize(tl_n + 1);
     tl_label[tl_n] = label;
-    HIP_CHECK(hipEventRecord(tl_ev[tl_n], s));
+    if (ctx->capturing) {  // tl_mode 2
+        hipStreamCaptureStatus st;
+        hipGraph_t g = nullptr;
+        const hipGraphNode_t* deps = nullptr;
+        size_t nd = 0;
+        HIP_CHECK(hipStreamGetCaptureInfo_v2(s, &st, nullptr, &g, &deps, &nd));
+        hipGraphNode_t en;
+        HIP_CHECK(hipGraphAddEventRecordNode(&en, g, deps, nd, tl_ev[tl_n]));
+        HIP_CHECK(hipStreamUpdateCaptureDependencies(s, &en, 1, hipStreamSetCaptureDependencies));
+    } else {
+        HIP_CHECK(hipEventRecord(tl_ev[tl_n], s));
+    }
     ++tl_n;
 }
 
-bool Solver::cycle_timeline(double* x, const double* b, int reps, std::vector<std::string>& labels,
-                            std::vector<double>& us) {
+int Solver::cycle_timeline(double* x, const double* b, int reps, std::vector<std::string>& labels,
+                           std::vector<double>& us) {
     AMG_CHECK(ctx->host.nranks == 1, "cycle timeline: one rank");
     AMG_CHECK(reps >= 1, "cycle timeline: reps must be >= 1");
     hipStream_t s = ctx->stream;
@@ -559,18 +577,21 @@ bool Solver::cycle_timeline(double* x, const double* b, int reps, std::vector<st
             tl_ev.push_back(e);
         }
     };
-    // graphs: one captured segment per operation
+    // capture the cycle with marks in mode m; the instantiated graphs (one, or one per
+    // operation) and their labels; false where the runtime refuses
     std::vector<hipGraphExec_t> execs;
     std::vector<std::string> seg_label;
-    bool graphs_ok = use_graph;
-    if (graphs_ok) {
+    auto capture = [&](int m) {
+        tl_mode = m;
         tl_graphs.clear();
         tl_label.clear();
+        tl_n = 0;
         tl_on = true;
         HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         ctx->capturing = true;
         std::string err;
         try {
+            if (m == 2) mark(0, "begin");
             cycle_rec(0, x, b, false, false);
         } catch (const std::exception& e) {
             err = e.what();
@@ -579,29 +600,37 @@ bool Solver::cycle_timeline(double* x, const double* b, int reps, std::vector<st
         tl_on = false;
         hipGraph_t last = nullptr;
         const hipError_t ce = hipStreamEndCapture(s, &last);
-        if (last) (void)hipGraphDestroy(last);  // after the last mark: nothing
-        for (size_t k = 0; k < tl_graphs.size(); ++k) {
+        (void)hipGetLastError();
+        bool ok = err.empty() && ce == hipSuccess;
+        if (m == 2) {
+            if (last) tl_graphs.push_back(last);
+            seg_label.assign(tl_label.begin() + (tl_n > 0 ? 1 : 0), tl_label.begin() + tl_n);
+        } else {
+            if (last) (void)hipGraphDestroy(last);  // after the last mark: nothing
+            seg_label = tl_label;
+        }
+        for (hipGraph_t g : tl_graphs) {
             hipGraphExec_t e = nullptr;
-            if (err.empty() && ce == hipSuccess && hipGraphInstantiate(&e, tl_graphs[k], nullptr, nullptr, 0) == hipSuccess) {
-                execs.push_back(e);
-                seg_label.push_back(tl_label[k]);
-            } else {
-                (void)hipGetLastError();
-                graphs_ok = false;
-            }
-            (void)hipGraphDestroy(tl_graphs[k]);
+            if (ok && hipGraphInstantiate(&e, g, nullptr, nullptr, 0) == hipSuccess) execs.push_back(e);
+            else ok = false;
+            (void)hipGraphDestroy(g);
         }
         tl_graphs.clear();
-        AMG_CHECK(err.empty(), "cycle timeline capture: " + err);
-        if (!graphs_ok) {
+        (void)hipGetLastError();
+        if (!ok) {
             for (hipGraphExec_t e : execs) (void)hipGraphExecDestroy(e);
             execs.clear();
         }
-    }
-    std::vector<std::vector<float>> t;
-    for (int r = 0; r < reps; ++r) {
+        return ok;
+    };
+    // one replay: a vector of event-to-event times (ms), empty where the runtime did not time them
+    auto replay = [&](int m) {
+        std::vector<float> t;
         size_t n = 0;
-        if (graphs_ok) {
+        if (m == 2) {
+            HIP_CHECK(hipGraphLaunch(execs[0], s));
+            n = tl_n;
+        } else if (m == 1) {
             ensure_events(execs.size() + 1);
             HIP_CHECK(hipEventRecord(tl_ev[0], s));
             for (size_t k = 0; k < execs.size(); ++k) {
@@ -610,6 +639,7 @@ bool Solver::cycle_timeline(double* x, const double* b, int reps, std::vector<st
             }
             n = execs.size() + 1;
         } else {
+            tl_mode = 0;
             tl_on = true;
             tl_n = 0;
             try {
@@ -624,21 +654,44 @@ bool Solver::cycle_timeline(double* x, const double* b, int reps, std::vector<st
             seg_label.assign(tl_label.begin() + 1, tl_label.begin() + (n > 0 ? n : 1));
         }
         HIP_CHECK(hipStreamSynchronize(s));
-        t.resize(n > 0 ? n - 1 : 0);
         for (size_t k = 1; k < n; ++k) {
             float ms = 0.f;
-            HIP_CHECK(hipEventElapsedTime(&ms, tl_ev[k - 1], tl_ev[k]));
-            t[k - 1].push_back(ms);
+            if (hipEventElapsedTime(&ms, tl_ev[k - 1], tl_ev[k]) != hipSuccess) {
+                (void)hipGetLastError();
+                return std::vector<float>();
+            }
+            t.push_back(ms);
+        }
+        return t;
+    };
+    int mode = 0;
+    std::vector<std::vector<float>> t;
+    for (int m = use_graph ? 2 : 0; m >= 0 && mode == 0; --m) {
+        if (m > 0 && !capture(m)) continue;
+        std::vector<float> first = replay(m);
+        if (first.empty() && m > 0) {  // not timed: the next mode
+            for (hipGraphExec_t e : execs) (void)hipGraphExecDestroy(e);
+            execs.clear();
+            continue;
+        }
+        mode = m > 0 ? m : -1;
+        t.assign(first.size(), {});
+        for (size_t k = 0; k < first.size(); ++k) t[k].push_back(first[k]);
+        for (int r = 1; r < reps; ++r) {
+            const std::vector<float> v = replay(m);
+            for (size_t k = 0; k < v.size() && k < t.size(); ++k) t[k].push_back(v[k]);
         }
     }
     for (hipGraphExec_t e : execs) HIP_CHECK(hipGraphExecDestroy(e));
+    tl_mode = 0;
     labels = seg_label;
+    labels.resize(t.size());
     us.clear();
     for (auto& v : t) {
         std::sort(v.begin(), v.end());
         us.push_back(1e3 * (double)v[v.size() / 2]);
     }
-    return graphs_ok;
+    return mode > 0 ? mode : 0;
 }
 
 void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool with_norm, bool x0_in_t) {

@@ -1060,7 +1060,9 @@ struct DevHalo {
 // Ruge-Stueben (the serial first pass stays on the host).
 bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, const amg_options& opt,
                         int level, HostCSR& P, std::vector<int32_t>& split, SetupImages* imgs) {
+    // Ruge-Stueben (serial first pass) and extended+i (one rank, host): the host path
     if (opt.coarsen == AMG_COARSEN_RS) return false;
+    if (opt.coarsen == AMG_COARSEN_PMIS && opt.interp == AMG_INTERP_EXT_I) return false;
     hipStream_t s = ctx.stream;
     const int n = (int)A.nrows();
     if (comm.nranks == 1 && n == 0) return false;

@@ -338,6 +338,93 @@ def interp_classical(A, S, cf):
                          shape=(n, int((cf == 1).sum())))
 
 
+def interp_ext_i(A, S, cf, p_max):
+    """Extended+i (distance two, r6 option).  F row i: Chat_i = strong C
+    neighbours, then the strong C neighbours of each strong F neighbour; num_j from 0.0;
+    d = a_ii; row i in order: a_ij to num_j (j in Chat_i) or to d (weak j); each strong F
+    neighbour k (row i order): abar = a_kl of sign opposite to a_kk, s_k = sum of abar over
+    Chat_i u {i} (row k order) -- 0 adds a_ik to d, else num_l += (a_ik abar_kl) / s_k (l in
+    Chat_i), d += (a_ik abar_ki) / s_k; w = -num / d by ascending column; more than p_max
+    entries: keep the p_max largest |w| (ties: smaller column), scale them by
+    (sum of all w) / (sum of kept w), sums in column order."""
+    R = rows(A)
+    n = len(R)
+    cidx = np.cumsum(cf == 1) - 1
+    diag = {i: dict(zip(*R[i])).get(i, 0.0) for i in range(n)}
+    indptr, indices, data = [0], [], []
+    for i in range(n):
+        if cf[i] == 1:
+            indices.append(int(cidx[i]))
+            data.append(1.0)
+            indptr.append(len(indices))
+            continue
+        Si = S[i]
+        sset = set(Si)
+        ch = []
+        for j in Si:
+            if cf[j] == 1 and j not in ch:
+                ch.append(j)
+        for k in Si:
+            if cf[k] != 1:
+                for j in S[k]:
+                    if cf[j] == 1 and j not in ch:
+                        ch.append(j)
+        chs = set(ch)
+        num = {j: 0.0 for j in ch}
+        d = diag[i]
+        cols, vals = R[i]
+        for c, v in zip(cols, vals):
+            if c == i:
+                continue
+            if c in chs:
+                num[c] = num[c] + v
+            elif c not in sset:
+                d = d + v
+        for k, aik in zip(cols, vals):
+            if k == i or k not in sset or cf[k] == 1:
+                continue
+            kc, kv = R[k]
+            pos = diag[k] > 0.0
+            ab = [(c, v) for c, v in zip(kc, kv) if ((v < 0.0) if pos else (v > 0.0))]
+            sk = 0.0
+            for c, v in ab:
+                if c in chs or c == i:
+                    sk = sk + v
+            if sk == 0.0:
+                d = d + aik
+                continue
+            for c, v in ab:
+                if c in chs:
+                    num[c] = num[c] + (aik * v) / sk
+                elif c == i:
+                    d = d + (aik * v) / sk
+        order = sorted(ch)
+        w = [-num[j] / d for j in order]
+        keep = [True] * len(w)
+        if p_max > 0 and len(w) > p_max:
+            tot = 0.0
+            for v in w:
+                tot = tot + v
+            ranked = sorted(range(len(w)), key=lambda t: (-abs(w[t]), t))
+            keep = [False] * len(w)
+            for t in ranked[:p_max]:
+                keep[t] = True
+            kept = 0.0
+            for t, v in enumerate(w):
+                if keep[t]:
+                    kept = kept + v
+            if kept != 0.0:
+                f = tot / kept
+                w = [v * f if keep[t] else v for t, v in enumerate(w)]
+        for t, j in enumerate(order):
+            if keep[t]:
+                indices.append(int(cidx[j]))
+                data.append(w[t])
+        indptr.append(len(indices))
+    return sp.csr_matrix((np.array(data), np.array(indices, np.int64), np.array(indptr, np.int64)),
+                         shape=(n, int((cf == 1).sum())))
+
+
 def sa_filter(A, theta):
     """Filtered operator (r6): the diagonal and the strong off-diagonals in row order; the
     diagonal value f_i = a_ii + the weak off-diagonal a_ij (row order).  Explicit zeros kept."""
@@ -457,7 +544,8 @@ class PyHierarchy:
     pre-smooth (Jacobi 2/3 or forward l1 hybrid GS(64)), r = b - A x, b_c = R r, x_c = 0,
     recurse, x += P x_c, one post-smooth (Jacobi or backward GS)."""
 
-    def __init__(self, A, coarsen, smoother, theta, max_coarse=256, seed=0x5EED, max_levels=25):
+    def __init__(self, A, coarsen, smoother, theta, max_coarse=256, seed=0x5EED, max_levels=25,
+                 interp="classical", p_max=4):
         self.smoother = smoother
         self.A, self.P, self.R, self.split = [canon(A)], [], [], []
         th = theta
@@ -473,7 +561,7 @@ class PyHierarchy:
             else:
                 S = strength_classical(Al, theta)
                 cf = rs_split(S) if coarsen == "rs" else pmis_split(S, seed + l)
-                P = interp_classical(Al, S, cf)
+                P = interp_ext_i(Al, S, cf, p_max) if interp == "ext+i" else interp_classical(Al, S, cf)
                 split = cf
             nc = P.shape[1]
             if nc == 0 or nc >= n or (n <= 8192 and 5 * nc > 4 * n):
@@ -519,12 +607,17 @@ SETUP_CASES = [
     ("fe27_8x7x6_sa_gs_mc16", lambda: fe27(8, 7, 6), "sa", "hybrid_gs", 0.08, 16),
     ("p7_10x9x8_sa_gs_mc16", lambda: poisson7(10, 9, 8), "sa", "hybrid_gs", 0.08, 16),
     ("mixed_600_sa_gs_mc16", lambda: mixed_graph(600, 2, 11), "sa", "hybrid_gs", 0.08, 16),
+    # r6: extended+i interpolation (P_max 4) on the PMIS split; the mixed-sign graph exercises
+    # the sign rule and empty s_k
+    ("p7_10x9x8_pmis_exti4_jacobi_mc16", lambda: poisson7(10, 9, 8), "pmis+ext+i", "jacobi", 0.25, 16),
+    ("mixed_600_pmis_exti4_jacobi_mc16", lambda: mixed_graph(600, 2, 11), "pmis+ext+i", "jacobi", 0.25, 16),
 ]
 
 
 def gen_setup_case(name, gen, coarsen, smoother, theta, max_coarse):
     A = gen()
-    H = PyHierarchy(A, coarsen, smoother, theta, max_coarse)
+    interp = "ext+i" if coarsen.endswith("+ext+i") else "classical"
+    H = PyHierarchy(A, coarsen.split("+")[0], smoother, theta, max_coarse, interp=interp)
     n = A.shape[0]
     b = A @ uniform(n, 42)
     out = {"nlev": np.array(len(H.A), np.int64), "inv": H.inv, "b": b}

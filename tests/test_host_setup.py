@@ -43,6 +43,30 @@ def test_host_hierarchy_bit_exact(oracle, kind, dims, coarsen):
     assert np.array_equal(Hp.coarse_inverse(), O.dense_inverse(Ac))
 
 
+@pytest.mark.parametrize("kind,dims,p_max", [("7pt", (18, 17, 16), 4), ("27pt", (12, 11, 13), 4),
+                                             ("5pt", (40, 36), 0)])
+def test_host_hierarchy_ext_i_bit_exact(oracle, kind, dims, p_max):
+    """Extended+i interpolation (r6 option) on the PMIS split: the product's host
+    setup equals the oracle's level for level, P_max truncation included."""
+    from raptor_amd import host
+
+    O = oracle
+    A = gen(O, kind, dims)
+    rp, col, val = A.arrays()
+    Hp = host.HostHierarchy(A.shape[0], 0, rp, col, val,
+                            host.options(coarsen="pmis", max_coarse=64, interp="ext+i", p_max=p_max))
+    Ho = O.Hierarchy(A, **dict(O.DEFAULTS["pmis"], max_coarse=64, interp=O.INTERP_EXT_I, p_max=p_max))
+    assert Hp.num_levels == Ho.num_levels >= 3
+    for l in range(Ho.num_levels):
+        assert same_csr(Hp.to_scipy(l, "A"), Ho.matrix(l, "A")), l
+        if l + 1 < Ho.num_levels:
+            assert same_csr(Hp.to_scipy(l, "P"), Ho.matrix(l, "P")), l
+            assert np.array_equal(Hp.split(l), Ho.split(l)), l
+    if p_max:
+        for l in range(Ho.num_levels - 1):
+            assert np.diff(Ho.matrix(l, "P").indptr).max() <= p_max
+
+
 def test_unsorted_input_rows_are_sorted(oracle):
     from raptor_amd import host
 

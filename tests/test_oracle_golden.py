@@ -172,6 +172,8 @@ SETUP_CASES = {  # tests/golden/gen_golden.py SETUP_CASES: (generator, coarsen, 
     "fe27_8x7x6_sa_gs_mc16": ("fe27_8x7x6", "sa", 16),
     "p7_10x9x8_sa_gs_mc16": ("p7_10x9x8", "sa", 16),
     "mixed_600_sa_gs_mc16": ("mixed", "sa", 16),
+    "p7_10x9x8_pmis_exti4_jacobi_mc16": ("p7_10x9x8", "pmis+ext+i", 16),
+    "mixed_600_pmis_exti4_jacobi_mc16": ("mixed", "pmis+ext+i", 16),
 }
 
 
@@ -200,7 +202,9 @@ def test_fp_setup_and_cycle_match_restatement(oracle, case):
     g = load(f"setup_{case}")
     A = O.Csr.from_scipy(gold_csr(g, "Ain")) if prob == "mixed" else oracle_gen(O, prob)
     assert _same(_canon(A.to_scipy()), gold_csr(g, "Ain"))
-    H = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen], max_coarse=max_coarse))
+    ext = coarsen.endswith("+ext+i")
+    H = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen.split("+")[0]], max_coarse=max_coarse,
+                              interp=O.INTERP_EXT_I if ext else O.INTERP_CLASSICAL, p_max=4))
     nlev = int(g["nlev"])
     assert H.num_levels == nlev >= 3
     for l in range(nlev):
