@@ -328,10 +328,15 @@ def main():
                                                        0: "eager"}[tl_mode],
                         "reps": max(5, args.steps),
                         "ops": [{"op": lab, "us": round(us, 1)} for lab, us in ops],
-                        "sum_us": round(sum(us for _, us in ops), 1),
+                        "sum_us": round(sum(us for lab, us in ops if lab != "event-node gap"), 1),
                         "what": "median event-to-event time of each operation of one V-cycle, "
-                                "timing events after every operation (mode above)"}
-            tl = {lab: us for lab, us in ops} if in_graph else {}
+                                "timing events after every operation (mode above); the table's "
+                                "in_graph_us subtract event_node_gap_us"}
+            # the calibration pseudo-operation: what one event-record node adds to the operation
+            # before it; subtracted from every in-graph time (raw times stay in "ops")
+            gap = next((us for lab, us in ops if lab == "event-node gap"), 0.0)
+            timeline["event_node_gap_us"] = round(gap, 2)
+            tl = {lab: max(0.0, us - gap) for lab, us in ops} if in_graph else {}
             for row in table:
                 lab = {"residual": "residual", "interp x += P e": "interp", "restrict R r": "restrict",
                        "Jacobi": "post-smooth", "post GS (backward)": "post-smooth",

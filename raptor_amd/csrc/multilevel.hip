@@ -683,9 +683,48 @@ int Solver::cycle_timeline(double* x, const double* b, int reps, std::vector<std
         }
     }
     for (hipGraphExec_t e : execs) HIP_CHECK(hipGraphExecDestroy(e));
-    tl_mode = 0;
+    execs.clear();
     labels = seg_label;
     labels.resize(t.size());
+    if (mode == 2) {
+        // calibration: two event-record nodes with nothing between them -- the time a node adds
+        // to the operation before it (reported as a last pseudo-operation "event-node gap")
+        tl_mode = 2;
+        tl_graphs.clear();
+        tl_n = 0;
+        tl_on = true;
+        HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        ctx->capturing = true;
+        std::string err;
+        try {
+            mark(0, "gap a");
+            mark(0, "gap b");
+        } catch (const std::exception& e) {
+            err = e.what();
+        }
+        ctx->capturing = false;
+        tl_on = false;
+        hipGraph_t g = nullptr;
+        const hipError_t ce = hipStreamEndCapture(s, &g);
+        hipGraphExec_t e = nullptr;
+        if (err.empty() && ce == hipSuccess && g && hipGraphInstantiate(&e, g, nullptr, nullptr, 0) == hipSuccess) {
+            std::vector<float> gv;
+            for (int r = 0; r < reps; ++r) {
+                HIP_CHECK(hipGraphLaunch(e, s));
+                HIP_CHECK(hipStreamSynchronize(s));
+                float ms = 0.f;
+                if (hipEventElapsedTime(&ms, tl_ev[0], tl_ev[1]) == hipSuccess) gv.push_back(ms);
+            }
+            if (!gv.empty()) {
+                labels.push_back("event-node gap");
+                t.push_back(gv);
+            }
+            HIP_CHECK(hipGraphExecDestroy(e));
+        }
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+    }
+    tl_mode = 0;
     us.clear();
     for (auto& v : t) {
         std::sort(v.begin(), v.end());

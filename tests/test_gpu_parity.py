@@ -340,6 +340,35 @@ def test_setup_failure_with_overlapped_gs_builds_is_an_error(ctx):
     assert hist[-1] < hist[0]
 
 
+@pytest.mark.parametrize("kind,dims", [("7pt", (40, 36, 33)), ("27pt", (20, 18, 22))])
+def test_vcycle_ext_i_bit_exact(ctx, oracle, kind, dims):
+    """Extended+i interpolation (r6 option, P_max 4): the product's hierarchy equals the
+    oracle's on every level, and the GPU V-cycle (cycle-order copies included) is bit-identical
+    to the oracle's; an 8-cycle history within 1e-10."""
+    import raptor_amd as ra
+
+    O = oracle
+    Ao = {"7pt": O.gen_7pt, "27pt": O.gen_27pt}[kind](*dims)
+    A = ra.par_stencil_grid(ctx, kind, dims)
+    ml = ra.ParRugeStubenSolver(coarsen="pmis", interp="ext+i", p_max=4).setup(A)
+    Ho = O.Hierarchy(Ao, interp=O.INTERP_EXT_I, p_max=4)
+    assert ml.num_levels == Ho.num_levels >= 3
+    for l in range(ml.num_levels):
+        assert same_csr(ml.level_matrix(l, "A").to_scipy_local(), Ho.matrix(l, "A")), l
+        if l + 1 < ml.num_levels:
+            assert same_csr(ml.level_matrix(l, "P").to_scipy_local(), Ho.matrix(l, "P")), l
+    n = Ao.shape[0]
+    b = Ao.spmv(O.vec_uniform(n, 42))
+    db, dx, xo = to_dev(ctx, b), ctx.zeros(n), np.zeros(n)
+    for _ in range(3):
+        ml.cycle(dx, db)
+        xo = Ho.cycle(xo, b)
+        assert np.array_equal(to_host(ctx, dx), xo)
+    _, hist = ml.solve(ctx.zeros(n), db, max_iter=8)
+    _, hist_o = Ho.solve(np.zeros(n), b, max_iter=8)
+    assert np.all(np.abs(hist - hist_o) <= 1e-10 * hist_o)
+
+
 @pytest.mark.parametrize("coarsen,smoother", [("pmis", "jacobi"), ("sa", "hybrid_gs")])
 def test_cycle_timeline(ctx, oracle, coarsen, smoother):
     """amg_solver_cycle_timeline (the bench's in-graph durations): one labelled, positive time
@@ -362,7 +391,9 @@ def test_cycle_timeline(ctx, oracle, coarsen, smoother):
         for op in ("residual", "interp", "post-smooth"):
             assert f"L{l} {op}" in labels, (l, op, labels)
     assert "L0 pre-smooth" in labels and f"L{L - 1} coarse solve" in labels
-    assert all(us > 0.0 for _, us in ops)
+    assert all(us > 0.0 for lab, us in ops if lab != "event-node gap")
+    if mode == 2:  # the calibration entry: what one event-record node adds
+        assert labels[-1] == "event-node gap" and 0.0 <= ops[-1][1] < 50.0
     x2 = ctx.zeros(n)
     for _ in range(5):
         ml.cycle(x2, b)
