@@ -225,7 +225,7 @@ typedef struct amg_options {
                                  Results are identical in every mode.                     */
     int64_t replicate_below;  /* multi-rank: levels with <= this many global rows are held
                                  whole by every rank and cycled without communication (one
-                                 allgather of b per cycle); 0 = never.  Default 65536.      */
+                                 allgather of b per cycle); 0 = never.  Default 262144.     */
     int32_t interp;           /* RS / PMIS: AMG_INTERP_CLASSICAL (default) or AMG_INTERP_EXT_I */
     int32_t p_max;            /* AMG_INTERP_EXT_I: interpolation entries kept per row (the
                                  largest |w|, rescaled to the row sum); 0 = all.  Default 4  */

@@ -595,7 +595,7 @@ class ParMultilevel:
     def __init__(self, coarsen="pmis", smoother="jacobi", strong_threshold=None,
                  jacobi_omega=2.0 / 3.0, pre_sweeps=1, post_sweeps=1, max_levels=25,
                  max_coarse=256, gs_block=64, seed=0x5EED, use_graph=None, setup_device=True,
-                 replicate_below=65536, interp="classical", p_max=4):
+                 replicate_below=262144, interp="classical", p_max=4):
         if strong_threshold is None:
             strong_threshold = 0.08 if coarsen == "sa" else 0.25
         self.options = Options(self._COARSEN[coarsen], self._SMOOTH[smoother],

@@ -545,7 +545,7 @@ int amg_options_default(int preset, amg_options* o) {
         o->gs_block = 64;
         o->seed = 0x5EED;
         o->setup_device = 1;
-        o->replicate_below = 65536;
+        o->replicate_below = 262144;  // modelled N = 8 cycle
         o->interp = AMG_INTERP_CLASSICAL;
         o->p_max = 4;
         if (preset == AMG_PRESET_RS_JACOBI) {

@@ -13,13 +13,17 @@ Model per level and cycle (distributed): t = compute_l + e_l * (alpha + bytes_l 
 exchanges that cannot hide (coarse levels: the interior rows finish before the halo arrives);
 levels 0-2 overlap the exchange with the interior rows, so only max(0, exchange
 - interior) is added there.  A replicated level costs the whole level's compute on every rank:
-8 x the 1-GPU level time (the 512^3 level has 8 x the rows), no exchange, plus one allgather of
-the level's right-hand side at the transition.  alpha = latency of one grouped RCCL send/recv
-round over xGMI (10 and 20 us bracket it), beta = 50 GB/s per peer (a third of one xGMI link).
+the 1-GPU time of the 256^3 level of the same row count (coarse levels are launch-latency
+bound), no exchange, plus one allgather of the level's right-hand side at the transition.
+Every policy adds the coarse allgather and the norm allreduce (2 alpha).  alpha = latency of
+one grouped RCCL send/recv round over xGMI (10 and 20 us bracket it), beta = 50 GB/s per peer
+(a third of one xGMI link).  Levels the measured plan replicated get, distributed, the four
+exchanges of the level above with few-KB messages.
 
 usage: python scripts/r6/comm_model.py PLAN.json BENCH_7PT.json
 """
 import json
+import math
 import re
 import sys
 
@@ -35,21 +39,34 @@ def level_compute(bench):
     return t
 
 
-def model(plan, comp, rep_level, alpha, overlap_levels=3, ranks=8):
-    total = 0.0
+def matched(comp, rows1, n):
+    """1-GPU time of the 256^3 level whose row count is nearest n (log scale): a replicated
+    512^3 level is the whole level on one GPU, and the coarse levels are launch-latency
+    bound, so its cost follows the level of the same size, not 8 x the same index."""
+    k = min(rows1, key=lambda q: abs(math.log(max(1, rows1[q]) / max(1, n))))
+    return comp.get(k, 0.0)
+
+
+def model(plan, comp, rep_level, alpha, rows1, overlap_levels=3):
+    # every policy: the coarsest level's allgather of b and the norm's allreduce
+    total = 2 * alpha
     rows = []
     for L in plan["levels"]:
         l = L["level"]
         c1 = comp.get(l, 0.0)
         if rep_level is not None and l >= rep_level:
-            t = ranks * c1
+            t = matched(comp, rows1, L["n_global"])
             ex = 0.0
             if l == rep_level:  # the transition's allgather of b_l (padded slots)
-                ex = alpha + 8.0 * L["n_global"] / ranks / BETA
+                ex = alpha + 8.0 * L["n_global"] / 8 / BETA
             rows.append((l, L["n_global"], "replicated", round(t, 1), round(ex, 1)))
             total += t + ex
             continue
         ex = 0.0
+        if L.get("replicated"):
+            # replicated in the measured plan: distributed, it would post the exchanges of the
+            # level above (2 for A, 1 for P, 1 for R) with messages of a few KB
+            ex = 4 * (alpha + 4096 / BETA)
         for w in "APR":
             e = L.get(w)
             if not e or not e["per_cycle"]:
@@ -67,6 +84,7 @@ def main(plan_path, bench_path):
     plan = json.load(open(plan_path))
     bench = json.load(open(bench_path))
     comp = level_compute(bench)
+    rows1 = dict(enumerate(bench["config"]["level_rows"]))
     t1 = bench["cycle_timeline"]["sum_us"]
     levels = {L["level"]: L["n_global"] for L in plan["levels"]}
     print(f"1-GPU 256^3 cycle (in-graph timeline): {t1:.0f} us")
@@ -78,9 +96,9 @@ def main(plan_path, bench_path):
         if thr:
             rep = min((l for l, n in levels.items() if l > 0 and n <= thr), default=None)
         for alpha in (10.0, 20.0):
-            t, _ = model(plan, comp, rep, alpha)
+            t, _ = model(plan, comp, rep, alpha, rows1)
             print(f"| {name} | {'level ' + str(rep) if rep is not None else '-'} | {alpha:.0f} | {t:.0f} | {t1 / t:.2f} |")
-    t, rows = model(plan, comp, min(l for l, n in levels.items() if l > 0 and n <= 65536), 15.0)
+    t, rows = model(plan, comp, min(l for l, n in levels.items() if l > 0 and n <= 65536), 15.0, rows1)
     print("\nper level at alpha = 15 us, default policy (level, rows, kind, compute us, exposed exchange us):")
     for r in rows:
         print(" ", r)

@@ -97,7 +97,7 @@ def test_cycle_order_multirank(ctx, nranks, boxes):
     from tests.test_gpu_multirank import run_ranks
     from tests.util import loopback_ctx
 
-    dims = (96, 80, 64)  # level 1 above the default replicate_below (65,536 rows)
+    dims = (96, 80, 64)  # level 1 (~151 k rows) above replicate_below = 65,536: distributed
     A = ra.par_stencil_grid(ctx, "7pt", dims, boxes=boxes)
     n = A.local_rows
     ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
@@ -109,7 +109,7 @@ def test_cycle_order_multirank(ctx, nranks, boxes):
         c = loopback_ctx(r, nr, world)
         Ar = ra.par_stencil_grid(c, "7pt", dims, boxes=boxes)
         f, m = Ar.first_row, Ar.local_rows
-        mr = ra.ParRugeStubenSolver(coarsen="pmis").setup(Ar)
+        mr = ra.ParRugeStubenSolver(coarsen="pmis", replicate_below=65536).setup(Ar)
         permuted = not np.array_equal(mr.level_matrix(1, "A_cycle").export()[1],
                                       mr.level_matrix(1, "A").export()[1])
         xs = _cycles(c, mr, to_dev(c, b[f:f + m]), m, 3)
