@@ -78,6 +78,9 @@ def main():
     ap.add_argument("--lattice", type=int, default=1225,
                     help="g3sub: lattice side (1225^2 = 1.5M rows, G3_circuit size)")
     ap.add_argument("--no-reorder", action="store_true", help="g3sub: keep the random numbering")
+    ap.add_argument("--drop-tol", type=float, default=None,
+                    help="coarse-operator drop tolerance (non-Galerkin lumping, DESIGN.md 3); default "
+                         "0.005 for g3sub (VERDICT r5 item 8: complexity), 0 (Galerkin) otherwise")
     ap.add_argument("--partition", choices=["boxes", "slabs"], default="boxes",
                     help="7pt/sa27 over N ranks: boxes (default; 2 x 2 x 2 cubes of 256^3 at N = 8, "
                          "the grid numbered box by box) or z-slabs of the natural numbering")
@@ -155,10 +158,12 @@ def main():
     log(rank, f"matrix {grid} built in {time.perf_counter() - t0:.1f}s; local rows {A.local_rows}")
     t1 = time.perf_counter()
     graph = False if args.no_graph else None
+    drop_tol = args.drop_tol if args.drop_tol is not None else (0.005 if g3 else 0.0)
     if sa27 or g3:  # BASELINE.json configs[2]/[4]: smoothed aggregation + hybrid Gauss-Seidel
-        ml = ra.ParSmoothedAggregationSolver(use_graph=graph).setup(A)
+        ml = ra.ParSmoothedAggregationSolver(use_graph=graph, drop_tol=drop_tol).setup(A)
     else:     # BASELINE.json configs[1]/[3]: PMIS + classical interpolation, Jacobi
-        ml = ra.ParRugeStubenSolver(coarsen="pmis", use_graph=graph, interp=args.interp).setup(A)
+        ml = ra.ParRugeStubenSolver(coarsen="pmis", use_graph=graph, interp=args.interp,
+                                    drop_tol=drop_tol).setup(A)
     setup_s = time.perf_counter() - t1
     nlev = ml.num_levels
     infos = [ml.level_info(l) for l in range(nlev)]
@@ -538,7 +543,8 @@ def main():
                 "workload": (f"G3_circuit substitute: graph Laplacian on a {grid[0]}x{grid[1]} lattice "
                              f"({n_global} rows, {infos[0]['nnz_global']} nnz, seed 1), "
                              f"{'random numbering' if args.no_reorder else 'RCM-reordered'}, smoothed "
-                             f"aggregation (MIS(2)), hybrid GS(64) 1+1 V-cycle, {part_label}")
+                             f"aggregation (MIS(2)), hybrid GS(64) 1+1 V-cycle, {part_label}" +
+                             (f", coarse drop tolerance {drop_tol:g}" if drop_tol else ""))
                 if g3 else
                 (f"3D 27-pt Q1 anisotropic diffusion (1,1,1e-3) {grid[0]}x{grid[1]}x{grid[2]}, "
                              f"smoothed aggregation (MIS(2)), hybrid GS(64) 1+1 V-cycle, {part_label}")
@@ -552,6 +558,10 @@ def main():
                 "level_rows": [i["n_global"] for i in infos],
                 "level_nnz": [i["nnz_global"] for i in infos],
                 "operator_complexity": round(sum(i["nnz_global"] for i in infos) / infos[0]["nnz_global"], 3),
+                # the densest coarse level's mean nonzeros per row
+                "coarse_nnz_per_row_max": max((round(i["nnz_global"] / max(1, i["n_global"]), 1)
+                                               for i in infos[1:]), default=None),
+                "drop_tol": drop_tol,
                 "parallelism": f"row-partition x{world}, RCCL halo",
                 "partition": part_label,
                 "setup_s": round(setup_s, 2),

@@ -229,6 +229,10 @@ typedef struct amg_options {
     int32_t interp;           /* RS / PMIS: AMG_INTERP_CLASSICAL (default) or AMG_INTERP_EXT_I */
     int32_t p_max;            /* AMG_INTERP_EXT_I: interpolation entries kept per row (the
                                  largest |w|, rescaled to the row sum); 0 = all.  Default 4  */
+    double drop_tol;          /* coarse-operator drop tolerance (non-Galerkin): off-diagonals of
+                                 A_{l+1} = R A_l P with |a_ij| < drop_tol sqrt(|a_ii a_jj|) are
+                                 added to the diagonal (row order; row sums kept).  0 = the
+                                 Galerkin operator (default).  DESIGN.md 3                  */
 } amg_options;
 
 #define AMG_PRESET_PMIS_JACOBI 0  /* config 2/4: 7-pt Poisson, Jacobi V-cycle            */

@@ -849,6 +849,49 @@ int64_t orc_mis2_aggregate(const orc_csr* S, uint64_t seed, int32_t* agg) {
 
 double orc_sa_theta_next(double theta) { return theta * 0.75; }
 
+/* Coarse-operator drop tolerance (r6 option, non-Galerkin): off-diagonal a_ij of A_c with
+ * |a_ij| < tau * sqrt(|a_ii a_jj|) (a_ii, a_jj the stored diagonals) are removed and added to
+ * the diagonal, in row order from a_ii; kept entries stay in row order.  Row sums are kept.
+ * A row without a stored diagonal is left as it is. */
+orc_csr* orc_sparsify(const orc_csr* A, double tau) {
+    int64_t n = A->n_rows, nnz = 0;
+    double* d = XMALLOC(double, n);
+    char* has = XMALLOC(char, n);
+    for (int64_t i = 0; i < n; ++i) {
+        has[i] = 0;
+        d[i] = 0.0;
+        for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k)
+            if (A->col[k] == i) { d[i] = A->val[k]; has[i] = 1; break; }
+    }
+    orc_csr* B = csr_alloc(n, A->n_cols, orc_csr_nnz(A));
+    B->rp[0] = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        double f = d[i];
+        if (has[i])
+            for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
+                int64_t j = A->col[k];
+                if (j != i && fabs(A->val[k]) < tau * sqrt(fabs(d[i] * d[j]))) f += A->val[k];
+            }
+        for (int64_t k = A->rp[i]; k < A->rp[i + 1]; ++k) {
+            int64_t j = A->col[k];
+            if (!has[i]) {
+                B->col[nnz] = j;
+                B->val[nnz++] = A->val[k];
+            } else if (j == i) {
+                B->col[nnz] = j;
+                B->val[nnz++] = f;
+            } else if (!(fabs(A->val[k]) < tau * sqrt(fabs(d[i] * d[j])))) {
+                B->col[nnz] = j;
+                B->val[nnz++] = A->val[k];
+            }
+        }
+        B->rp[i + 1] = nnz;
+    }
+    free(d);
+    free(has);
+    return B;
+}
+
 /* Filtered operator of SA smoothing (row a9, r6): the diagonal and the strong off-diagonals
  * (sa_strong, the strength test above) in CSR order; the diagonal value becomes
  * f_i = a_ii + the weak off-diagonal a_ij, added in row order.  Row sums are kept. */
@@ -1058,6 +1101,11 @@ orc_hier* orc_hier_setup(const orc_csr* A0, const orc_options* opt) {
         orc_csr* AP = orc_spgemm(A, P);
         H->A[l + 1] = orc_spgemm(R, AP);
         orc_csr_free(AP);
+        if (opt->drop_tol > 0.0) {
+            orc_csr* B = orc_sparsify(H->A[l + 1], opt->drop_tol);
+            orc_csr_free(H->A[l + 1]);
+            H->A[l + 1] = B;
+        }
         H->P[l] = P;
         H->R[l] = R;
         H->split[l] = split;

@@ -80,6 +80,8 @@ orc_csr* orc_sa_filter(const orc_csr* A, double theta);
 double orc_sa_rho(const orc_csr* F, const double* d, uint64_t seed);
 orc_csr* orc_sa_prolongator(const orc_csr* A, const int32_t* agg, int64_t n_agg, double theta,
                             uint64_t seed);
+/* coarse-operator drop tolerance: small off-diagonals lumped onto the diagonal (r6) */
+orc_csr* orc_sparsify(const orc_csr* A, double tau);
 /* SA strength threshold of the next level: theta * 0.75 */
 double orc_sa_theta_next(double theta);
 void orc_dense_inverse(int64_t n, const orc_csr* A, double* inv); /* row-major n*n */
@@ -106,6 +108,7 @@ typedef struct orc_options {
     uint64_t seed;
     int32_t interp;  /* RS / PMIS: ORC_INTERP_CLASSICAL or ORC_INTERP_EXT_I */
     int64_t p_max;   /* ext+i truncation: entries kept per row (0: all) */
+    double drop_tol; /* coarse-operator drop tolerance (0: Galerkin) */
 } orc_options;
 
 typedef struct orc_hier orc_hier;

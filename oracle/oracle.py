@@ -39,6 +39,7 @@ class _Opt(C.Structure):
         ("seed", C.c_uint64),
         ("interp", C.c_int32),
         ("p_max", C.c_int64),
+        ("drop_tol", C.c_double),
     ]
 
 
@@ -94,6 +95,7 @@ def lib():
             "orc_sa_filter": (vp, [vp, C.c_double]),
             "orc_sa_rho": (C.c_double, [vp, _f64p, C.c_uint64]),
             "orc_sa_theta_next": (C.c_double, [C.c_double]),
+            "orc_sparsify": (vp, [vp, C.c_double]),
             "orc_dense_inverse": (None, [C.c_int64, vp, _f64p]),
             "orc_hier_setup": (vp, [vp, C.POINTER(_Opt)]),
             "orc_hier_free": (None, [vp]),
@@ -319,6 +321,11 @@ def sa_rho(F, d, seed):
     return lib().orc_sa_rho(F.h, _p(d, _f64p), seed)
 
 
+def sparsify(A, tau):
+    """Coarse-operator drop tolerance."""
+    return Csr(lib().orc_sparsify(A.h, tau))
+
+
 def sa_theta_next(theta):
     return lib().orc_sa_theta_next(theta)
 
@@ -343,12 +350,12 @@ class Hierarchy:
     def __init__(self, A, coarsen=COARSEN_PMIS, smoother=SMOOTH_JACOBI, strong_threshold=0.25,
                  jacobi_omega=2.0 / 3.0, pre_sweeps=1, post_sweeps=1, max_levels=25,
                  max_coarse=256, gs_block=64, seed=0x5EED, levels=None, interp=INTERP_CLASSICAL,
-                 p_max=4):
+                 p_max=4, drop_tol=0.0):
         """Serial setup of A; or, with ``levels=[(A_l, P_l, R_l), ...]`` (Csr objects, P/R
         None on the coarsest level), a hierarchy made of those operators.  ``interp``
         (RS / PMIS): INTERP_CLASSICAL or INTERP_EXT_I (``p_max`` entries kept per row)."""
         o = _Opt(coarsen, smoother, strong_threshold, jacobi_omega, pre_sweeps, post_sweeps,
-                 max_levels, max_coarse, gs_block, seed, interp, p_max)
+                 max_levels, max_coarse, gs_block, seed, interp, p_max, drop_tol)
         self.A = A
         if levels is None:
             self.h = lib().orc_hier_setup(A.h, C.byref(o))

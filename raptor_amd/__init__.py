@@ -586,7 +586,9 @@ class ParMultilevel:
 
     ``coarsen``: "rs" (serial Ruge-Stueben), "pmis", or "sa" (smoothed aggregation over MIS(2)
     aggregates).  ``smoother``: "jacobi" or "hybrid_gs".  ``interp`` (RS / PMIS): "classical"
-    (distance one) or "ext+i" (distance two, ``p_max`` entries kept per row; one rank)."""
+    (distance one) or "ext+i" (distance two, ``p_max`` entries kept per row; one rank).
+    ``drop_tol`` > 0: coarse operators lose their off-diagonals below drop_tol sqrt(|a_ii a_jj|),
+    lumped onto the diagonal (non-Galerkin)."""
 
     _COARSEN = {"rs": AMG_COARSEN_RS, "pmis": AMG_COARSEN_PMIS, "sa": AMG_COARSEN_SA}
     _INTERP = {"classical": AMG_INTERP_CLASSICAL, "ext+i": AMG_INTERP_EXT_I}
@@ -595,14 +597,14 @@ class ParMultilevel:
     def __init__(self, coarsen="pmis", smoother="jacobi", strong_threshold=None,
                  jacobi_omega=2.0 / 3.0, pre_sweeps=1, post_sweeps=1, max_levels=25,
                  max_coarse=256, gs_block=64, seed=0x5EED, use_graph=None, setup_device=True,
-                 replicate_below=262144, interp="classical", p_max=4):
+                 replicate_below=262144, interp="classical", p_max=4, drop_tol=0.0):
         if strong_threshold is None:
             strong_threshold = 0.08 if coarsen == "sa" else 0.25
         self.options = Options(self._COARSEN[coarsen], self._SMOOTH[smoother],
                                float(strong_threshold), float(jacobi_omega), int(pre_sweeps),
                                int(post_sweeps), int(max_levels), int(max_coarse), int(gs_block),
                                int(seed), int(setup_device), int(replicate_below),
-                               self._INTERP[interp], int(p_max))
+                               self._INTERP[interp], int(p_max), float(drop_tol))
         self.use_graph = use_graph
         self.h = None
         self.A = None
@@ -721,8 +723,9 @@ class ParRugeStubenSolver(ParMultilevel):
 
 
 class ParSmoothedAggregationSolver(ParMultilevel):
-    """Smoothed aggregation: symmetric strength 0.08 (halved per level), MIS(2) aggregates,
-    Jacobi-smoothed prolongator, hybrid Gauss-Seidel smoothing."""
+    """Smoothed aggregation: signed strength 0.08 (x 0.75 per level), MIS(2) aggregates,
+    prolongator smoothed with the filtered operator (omega = 4 / (3 rho)), hybrid Gauss-Seidel
+    smoothing."""
 
     def __init__(self, smoother="hybrid_gs", **kw):
         super().__init__(coarsen="sa", smoother=smoother, **kw)

@@ -44,6 +44,7 @@ class Options(C.Structure):
         ("replicate_below", C.c_int64),
         ("interp", C.c_int32),
         ("p_max", C.c_int32),
+        ("drop_tol", C.c_double),
     ]
 
 

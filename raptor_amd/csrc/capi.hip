@@ -548,6 +548,7 @@ int amg_options_default(int preset, amg_options* o) {
         o->replicate_below = 262144;  // modelled N = 8 cycle
         o->interp = AMG_INTERP_CLASSICAL;
         o->p_max = 4;
+        o->drop_tol = 0.0;
         if (preset == AMG_PRESET_RS_JACOBI) {
             o->coarsen = AMG_COARSEN_RS;
         } else if (preset == AMG_PRESET_SA_HYBRID_GS) {

@@ -163,6 +163,9 @@ GhostRows fetch_rows(const HostComm& comm, const HaloPlan& plan, const HostCSR& 
 HostCSR transpose(const HostComm& comm, const HostCSR& P);
 HostCSR spgemm(const HostComm& comm, const HostCSR& A, const HostCSR& B);
 std::vector<double> diagonal(const HostComm& comm, const HostCSR& A);  // local rows
+// coarse-operator drop tolerance (oracle orc_sparsify): off-diagonals below
+// tau sqrt(|a_ii a_jj|) are added to the diagonal in row order
+HostCSR sparsify(const HostComm& comm, const HostCSR& A, double tau);
 HostCSR strength_classical(const HostComm& comm, const HostCSR& A, double theta);
 HostCSR strength_symmetric(const HostComm& comm, const HostCSR& A, double theta);
 std::vector<int32_t> rs_split(const HostComm& comm, const HostCSR& S);
@@ -230,7 +233,8 @@ using TransposeFn = std::function<bool(const HostCSR& P, HostCSR& R)>;
 // is written again by build_hierarchy
 using LevelDoneFn = std::function<void(int level)>;
 // the whole Galerkin product R (A P) in one hook (the device keeps A P between the two
-// products); when absent, two SpgemmFn / spgemm() calls
+// products); when absent, two SpgemmFn / spgemm() calls.  It returns the level's coarse
+// operator with opt.drop_tol already applied (sparsify)
 using RapFn = std::function<HostCSR(const HostCSR& R, const HostCSR& A, const HostCSR& P)>;
 void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options& opt,
                      HostHierarchy& H, const SpgemmFn& galerkin = nullptr,

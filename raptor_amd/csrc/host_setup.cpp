@@ -127,6 +127,34 @@ HostCSR sa_filter(const HostComm& comm, const HostCSR& A, double theta) {
     return F;
 }
 
+// coarse-operator drop tolerance (r6 option; oracle orc_sparsify): the same loop as sa_filter
+// with |a_ij| < tau sqrt(|a_ii a_jj|) for "dropped".  A row without a stored diagonal has
+// d_i = 0, so nothing of it is dropped (the oracle leaves such rows as they are).
+HostCSR sparsify(const HostComm& comm, const HostCSR& A, double tau) {
+    int64_t lo = A.row_starts[comm.rank], hi = A.row_starts[comm.rank + 1];
+    std::vector<double> d = diagonal(comm, A);
+    HaloPlan plan = halo_plan_for_cols(comm, A);
+    std::vector<double> hd(plan.n_halo());
+    plan.forward(comm, d.data(), hd.data());
+    auto dropped = [&](int64_t i, int64_t k) {
+        int64_t j = A.col[k];
+        if (j == lo + i) return false;
+        double dj = (j >= lo && j < hi) ? d[j - lo] : hd[plan.find(j)];
+        return std::fabs(A.val[k]) < tau * std::sqrt(std::fabs(d[i] * dj));
+    };
+    HostCSR B = filter_rows(A, [&](int64_t i, int64_t k) { return !dropped(i, k); });
+    const int64_t n = A.nrows();
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        double f = d[i];
+        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k)
+            if (dropped(i, k)) f += A.val[k];
+        for (int64_t k = B.rp[i]; k < B.rp[i + 1]; ++k)
+            if (B.col[k] == lo + i) B.val[k] = f;
+    }
+    return B;
+}
+
 // local transpose pattern of the local-local part of S (row i -> local j with i in S_j)
 static void local_transpose(const HostCSR& S, int64_t lo, int64_t hi, std::vector<int64_t>& tp,
                             std::vector<int64_t>& tc) {
@@ -817,13 +845,17 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
         tm.lap(L + "transpose");
         HostCSR Ac;
         if (rap_fn) {
-            Ac = rap_fn(R, A, P);
+            Ac = rap_fn(R, A, P);  // the drop tolerance applied (RapFn)
             tm.lap(L + "R*(AP)");
         } else {
             HostCSR AP = mm(A, P);
             tm.lap(L + "A*P");
             Ac = mm(R, AP);
             tm.lap(L + "R*(AP)");
+            if (opt.drop_tol > 0.0) {
+                Ac = sparsify(comm, Ac, opt.drop_tol);
+                tm.lap(L + "drop tolerance");
+            }
         }
         H.levels[l].split = std::move(split);
         H.levels[l].P = std::move(P);

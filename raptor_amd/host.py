@@ -192,9 +192,9 @@ class HostCSR:
 
 def options(coarsen="pmis", smoother="jacobi", strong_threshold=None, jacobi_omega=2.0 / 3.0,
             pre_sweeps=1, post_sweeps=1, max_levels=25, max_coarse=256, gs_block=64, seed=0x5EED,
-            interp="classical", p_max=4):
+            interp="classical", p_max=4, drop_tol=0.0):
     from . import ParMultilevel
 
     return ParMultilevel(coarsen, smoother, strong_threshold, jacobi_omega, pre_sweeps,
                          post_sweeps, max_levels, max_coarse, gs_block, seed, interp=interp,
-                         p_max=p_max).options
+                         p_max=p_max, drop_tol=drop_tol).options

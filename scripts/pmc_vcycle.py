@@ -22,7 +22,7 @@ if CFG == "sa27":
     ml = ra.ParSmoothedAggregationSolver().setup(A)
 elif CFG == "g3sub":  # configs[4]'s substitute, as bench.py --config g3sub builds it (N unused)
     A, _ = ra.par_graph_laplacian(ctx, 1225, 1225, seed=1).reorder("rcm")
-    ml = ra.ParSmoothedAggregationSolver().setup(A)
+    ml = ra.ParSmoothedAggregationSolver(drop_tol=0.005).setup(A)
 else:
     A = ra.par_stencil_grid(ctx, "7pt", (N, N, N))
     ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)

@@ -19,6 +19,7 @@ Run: python tests/golden/gen_golden.py   (writes the .npz files next to this scr
 from __future__ import annotations
 
 import heapq
+import math
 import os
 
 import numpy as np
@@ -529,6 +530,45 @@ def norm2(v):
     return float(np.sqrt(s))
 
 
+def sparsify(A, tau):
+    """Coarse-operator drop tolerance (r6 option): off-diagonal a_ij with |a_ij| <
+    tau sqrt(|a_ii a_jj|) move onto the diagonal, summed in row order from a_ii; rows without a
+    stored diagonal stay as they are.  Loops over the CSR arrays, written from the definition
+    in DESIGN.md 3 (not from the C)."""
+    A = sp.csr_matrix(A)
+    n = A.shape[0]
+    d = np.zeros(n)
+    has = np.zeros(n, bool)
+    for i in range(n):
+        for k in range(A.indptr[i], A.indptr[i + 1]):
+            if A.indices[k] == i:
+                d[i], has[i] = A.data[k], True
+                break
+    rp, ci, va = [0], [], []
+    for i in range(n):
+        cols = A.indices[A.indptr[i]:A.indptr[i + 1]]
+        vals = A.data[A.indptr[i]:A.indptr[i + 1]]
+        if not has[i]:
+            ci.extend(cols)
+            va.extend(vals)
+            rp.append(len(ci))
+            continue
+        drop = [j != i and abs(v) < tau * math.sqrt(abs(d[i] * d[j])) for j, v in zip(cols, vals)]
+        f = d[i]
+        for v, dr in zip(vals, drop):
+            if dr:
+                f += v
+        for j, v, dr in zip(cols, vals, drop):
+            if j == i:
+                ci.append(j)
+                va.append(f)
+            elif not dr:
+                ci.append(j)
+                va.append(v)
+        rp.append(len(ci))
+    return sp.csr_matrix((np.array(va, float), np.array(ci, np.int64), np.array(rp, np.int64)), shape=A.shape)
+
+
 def canon(M):
     M = sp.csr_matrix(M)
     M.eliminate_zeros()
@@ -545,7 +585,7 @@ class PyHierarchy:
     recurse, x += P x_c, one post-smooth (Jacobi or backward GS)."""
 
     def __init__(self, A, coarsen, smoother, theta, max_coarse=256, seed=0x5EED, max_levels=25,
-                 interp="classical", p_max=4):
+                 interp="classical", p_max=4, drop_tol=0.0):
         self.smoother = smoother
         self.A, self.P, self.R, self.split = [canon(A)], [], [], []
         th = theta
@@ -571,7 +611,8 @@ class PyHierarchy:
             self.P.append(P)
             self.R.append(R)
             self.split.append(np.asarray(split, np.int32))
-            self.A.append(canon(R @ (Al @ P)))
+            Ac = canon(R @ (Al @ P))
+            self.A.append(canon(sparsify(Ac, drop_tol)) if drop_tol > 0 else Ac)
             th = th * 0.75  # SA: theta_{l+1} = theta_l * 3/4 (r6)
         self.inv = gauss_jordan_inverse(self.A[-1].toarray())
 
@@ -611,13 +652,16 @@ SETUP_CASES = [
     # the sign rule and empty s_k
     ("p7_10x9x8_pmis_exti4_jacobi_mc16", lambda: poisson7(10, 9, 8), "pmis+ext+i", "jacobi", 0.25, 16),
     ("mixed_600_pmis_exti4_jacobi_mc16", lambda: mixed_graph(600, 2, 11), "pmis+ext+i", "jacobi", 0.25, 16),
+    # r6: coarse-operator drop tolerance 0.01 (non-Galerkin lumping) on SA
+    ("mixed_600_sa_gs_drop01_mc16", lambda: mixed_graph(600, 2, 11), "sa", "hybrid_gs", 0.08, 16, 0.01),
+    ("fe27_8x7x6_sa_gs_drop01_mc16", lambda: fe27(8, 7, 6), "sa", "hybrid_gs", 0.08, 16, 0.01),
 ]
 
 
-def gen_setup_case(name, gen, coarsen, smoother, theta, max_coarse):
+def gen_setup_case(name, gen, coarsen, smoother, theta, max_coarse, drop_tol=0.0):
     A = gen()
     interp = "ext+i" if coarsen.endswith("+ext+i") else "classical"
-    H = PyHierarchy(A, coarsen.split("+")[0], smoother, theta, max_coarse, interp=interp)
+    H = PyHierarchy(A, coarsen.split("+")[0], smoother, theta, max_coarse, interp=interp, drop_tol=drop_tol)
     n = A.shape[0]
     b = A @ uniform(n, 42)
     out = {"nlev": np.array(len(H.A), np.int64), "inv": H.inv, "b": b}

@@ -32,9 +32,11 @@ def _worker(rank, ws, port, q):
         from raptor_amd import host
 
         fails = []
-        cases = [("7pt", O.gen_7pt(14, 13, 12), "pmis"), ("5pt", O.gen_5pt(40, 37), "pmis"),
-                 ("27pt", O.gen_27pt(11, 10, 12), "sa"), ("7pt", O.gen_7pt(16, 12, 14), "sa")]
-        for name, A, coarsen in cases:
+        cases = [("7pt", O.gen_7pt(14, 13, 12), "pmis", 0.0), ("5pt", O.gen_5pt(40, 37), "pmis", 0.0),
+                 ("27pt", O.gen_27pt(11, 10, 12), "sa", 0.0), ("7pt", O.gen_7pt(16, 12, 14), "sa", 0.0),
+                 # r6: coarse-operator drop tolerance (off-rank diagonals through the halo)
+                 ("27pt drop", O.gen_27pt(11, 10, 12), "sa", 0.02), ("7pt drop", O.gen_7pt(14, 13, 12), "pmis", 0.05)]
+        for name, A, coarsen, tol in cases:
             M = A.to_scipy()
             n = M.shape[0]
             # uneven contiguous partition (not plane aligned)
@@ -43,9 +45,9 @@ def _worker(rank, ws, port, q):
             lo, hi = cuts[rank], cuts[rank + 1]
             Ml = M[lo:hi]
             Hp = host.HostHierarchy(n, lo, Ml.indptr, Ml.indices, Ml.data,
-                                    host.options(coarsen=coarsen, max_coarse=32),
+                                    host.options(coarsen=coarsen, max_coarse=32, drop_tol=tol),
                                     rank=rank, nranks=ws, group=dist.group.WORLD)
-            Ho = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen], max_coarse=32))
+            Ho = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen], max_coarse=32, drop_tol=tol))
             if Hp.num_levels != Ho.num_levels:
                 fails.append((name, "levels", Hp.num_levels, Ho.num_levels))
                 continue

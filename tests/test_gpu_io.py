@@ -44,9 +44,11 @@ def test_graph_laplacian_and_rcm_on_device(ctx, oracle, tmp_path):
     assert same_csr(D.to_scipy_local(), Bo.to_scipy())
 
 
-@pytest.mark.parametrize("coarsen,smoother,reorder", [("sa", "hybrid_gs", False), ("sa", "hybrid_gs", True),
-                                                      ("sa", "jacobi", True), ("pmis", "jacobi", False)])
-def test_vcycle_on_graph_laplacian(ctx, oracle, coarsen, smoother, reorder):
+@pytest.mark.parametrize("coarsen,smoother,reorder,tol", [("sa", "hybrid_gs", False, 0.0), ("sa", "hybrid_gs", True, 0.0),
+                                                          ("sa", "jacobi", True, 0.0), ("pmis", "jacobi", False, 0.0),
+                                                          # r6: coarse-operator drop tolerance
+                                                          ("sa", "hybrid_gs", True, 0.01)])
+def test_vcycle_on_graph_laplacian(ctx, oracle, coarsen, smoother, reorder, tol):
     import raptor_amd as ra
 
     O = oracle
@@ -55,9 +57,9 @@ def test_vcycle_on_graph_laplacian(ctx, oracle, coarsen, smoother, reorder):
     if reorder:
         A, perm = A.reorder("rcm")
         Ao = O.permute(Ao, perm)
-    ml = ra.ParMultilevel(coarsen=coarsen, smoother=smoother).setup(A)
+    ml = ra.ParMultilevel(coarsen=coarsen, smoother=smoother, drop_tol=tol).setup(A)
     Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS[coarsen], smoother=O.SMOOTH_JACOBI if smoother == "jacobi"
-                                else O.SMOOTH_HYBRID_GS))
+                                else O.SMOOTH_HYBRID_GS, drop_tol=tol))
     assert ml.num_levels == Ho.num_levels
     for l in range(ml.num_levels):
         assert same_csr(ml.level_matrix(l, "A").to_scipy_local(), Ho.matrix(l, "A"))
@@ -75,15 +77,15 @@ def test_vcycle_on_graph_laplacian(ctx, oracle, coarsen, smoother, reorder):
     assert np.all(np.abs(hist - hist_o) <= 1e-9 * hist_o[0])
 
 
-@pytest.mark.parametrize("nranks", [2, 3])
-def test_multirank_graph_laplacian(oracle, nranks):
+@pytest.mark.parametrize("nranks,tol", [(2, 0.0), (3, 0.0), (2, 0.01)])
+def test_multirank_graph_laplacian(oracle, nranks, tol):
     import raptor_amd as ra
 
     O = oracle
     Ao = O.gen_graph_laplacian(70, 66, 5)
     p = O.rcm(Ao)
     Bo = O.permute(Ao, p)
-    Ho = O.Hierarchy(Bo, **O.DEFAULTS["sa"])
+    Ho = O.Hierarchy(Bo, **dict(O.DEFAULTS["sa"], drop_tol=tol))
     n = Bo.shape[0]
     b = O.vec_uniform(n, 8)
 
@@ -91,7 +93,7 @@ def test_multirank_graph_laplacian(oracle, nranks):
         ctx = loopback_ctx(r, nr, world)
         A = ra.par_graph_laplacian(ctx, 70, 66, seed=5)
         B, perm = A.reorder("rcm")
-        ml = ra.ParSmoothedAggregationSolver(replicate_below=400).setup(B)
+        ml = ra.ParSmoothedAggregationSolver(replicate_below=400, drop_tol=tol).setup(B)
         f, m = B.first_row, B.local_rows
         dx = ctx.zeros(m)
         db = to_dev(ctx, b[f:f + m])

@@ -369,6 +369,33 @@ def test_vcycle_ext_i_bit_exact(ctx, oracle, kind, dims):
     assert np.all(np.abs(hist - hist_o) <= 1e-10 * hist_o)
 
 
+@pytest.mark.parametrize("kind,dims,coarsen,smoother,tol", [("27pt", (30, 28, 26), "sa", "hybrid_gs", 0.02),
+                                                           ("7pt", (40, 36, 33), "pmis", "jacobi", 0.05)])
+def test_vcycle_drop_tol_bit_exact(ctx, oracle, kind, dims, coarsen, smoother, tol):
+    """Coarse-operator drop tolerance (r6 option): the device setup (Galerkin product on the GPU,
+    then the drop) equals the oracle on every level; the V-cycle is bit-identical."""
+    import raptor_amd as ra
+
+    O = oracle
+    Ao = {"7pt": O.gen_7pt, "27pt": O.gen_27pt}[kind](*dims)
+    A = ra.par_stencil_grid(ctx, kind, dims)
+    ml = ra.ParMultilevel(coarsen=coarsen, smoother=smoother, drop_tol=tol).setup(A)
+    Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS[coarsen], smoother=O.SMOOTH_JACOBI if smoother == "jacobi"
+                                else O.SMOOTH_HYBRID_GS, drop_tol=tol))
+    assert ml.num_levels == Ho.num_levels >= 3
+    for l in range(ml.num_levels):
+        assert same_csr(ml.level_matrix(l, "A").to_scipy_local(), Ho.matrix(l, "A")), l
+        if l + 1 < ml.num_levels:
+            assert same_csr(ml.level_matrix(l, "P").to_scipy_local(), Ho.matrix(l, "P")), l
+    n = Ao.shape[0]
+    b = Ao.spmv(O.vec_uniform(n, 42))
+    db, dx, xo = to_dev(ctx, b), ctx.zeros(n), np.zeros(n)
+    for _ in range(3):
+        ml.cycle(dx, db)
+        xo = Ho.cycle(xo, b)
+        assert np.array_equal(to_host(ctx, dx), xo)
+
+
 @pytest.mark.parametrize("coarsen,smoother", [("pmis", "jacobi"), ("sa", "hybrid_gs")])
 def test_cycle_timeline(ctx, oracle, coarsen, smoother):
     """amg_solver_cycle_timeline (the bench's in-graph durations): one labelled, positive time

@@ -67,6 +67,40 @@ def test_host_hierarchy_ext_i_bit_exact(oracle, kind, dims, p_max):
             assert np.diff(Ho.matrix(l, "P").indptr).max() <= p_max
 
 
+@pytest.mark.parametrize("kind,dims,coarsen,tol", [("27pt", (13, 12, 11), "sa", 0.02), ("7pt", (20, 20, 20), "pmis", 0.05),
+                                                  ("graph", (60, 50), "sa", 0.01)])
+def test_host_hierarchy_drop_tol_bit_exact(oracle, kind, dims, coarsen, tol):
+    """Coarse-operator drop tolerance (r6 option): the product's host setup equals
+    the oracle's level for level; every coarse operator keeps its Galerkin row sums (up to
+    rounding) and loses entries."""
+    from raptor_amd import host
+
+    O = oracle
+    if kind == "graph":
+        G = O.gen_graph_laplacian(*dims, 1)
+        A = O.permute(G, O.rcm(G))
+    else:
+        A = gen(O, kind, dims)
+    rp, col, val = A.arrays()
+    Hp = host.HostHierarchy(A.shape[0], 0, rp, col, val,
+                            host.options(coarsen=coarsen, max_coarse=64, drop_tol=tol))
+    Ho = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen], max_coarse=64, drop_tol=tol))
+    Hg = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen], max_coarse=64))
+    assert Hp.num_levels == Ho.num_levels >= 3
+    for l in range(Ho.num_levels):
+        assert same_csr(Hp.to_scipy(l, "A"), Ho.matrix(l, "A")), l
+        if l + 1 < Ho.num_levels:
+            assert same_csr(Hp.to_scipy(l, "P"), Ho.matrix(l, "P")), l
+            assert np.array_equal(Hp.split(l), Ho.split(l)), l
+    assert np.array_equal(Hp.coarse_inverse(), O.dense_inverse(O.Csr.from_scipy(Ho.matrix(Ho.num_levels - 1, "A"))))
+    # level 1 from the same P: the Galerkin product less the dropped entries, row sums kept
+    A1, G1 = Ho.matrix(1, "A"), Hg.matrix(1, "A")
+    assert A1.nnz < G1.nnz
+    assert np.allclose(np.asarray(A1.sum(axis=1)).ravel(), np.asarray(G1.sum(axis=1)).ravel(),
+                       rtol=0, atol=1e-12 * abs(G1).max())
+    assert np.array_equal(O.sparsify(O.Csr.from_scipy(G1), tol).to_scipy().toarray(), A1.toarray())
+
+
 def test_unsorted_input_rows_are_sorted(oracle):
     from raptor_amd import host
 

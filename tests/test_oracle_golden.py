@@ -174,6 +174,8 @@ SETUP_CASES = {  # tests/golden/gen_golden.py SETUP_CASES: (generator, coarsen, 
     "mixed_600_sa_gs_mc16": ("mixed", "sa", 16),
     "p7_10x9x8_pmis_exti4_jacobi_mc16": ("p7_10x9x8", "pmis+ext+i", 16),
     "mixed_600_pmis_exti4_jacobi_mc16": ("mixed", "pmis+ext+i", 16),
+    "mixed_600_sa_gs_drop01_mc16": ("mixed", "sa", 16, 0.01),
+    "fe27_8x7x6_sa_gs_drop01_mc16": ("fe27_8x7x6", "sa", 16, 0.01),
 }
 
 
@@ -198,13 +200,14 @@ def test_fp_setup_and_cycle_match_restatement(oracle, case):
     inverse bit for bit, three V-cycle iterates (butterfly coarse solve, Jacobi / l1 hybrid GS)
     bit for bit, and an 8-cycle solve history (sequential norm) bit for bit."""
     O = oracle
-    prob, coarsen, max_coarse = SETUP_CASES[case]
+    prob, coarsen, max_coarse, *drop = SETUP_CASES[case]
     g = load(f"setup_{case}")
     A = O.Csr.from_scipy(gold_csr(g, "Ain")) if prob == "mixed" else oracle_gen(O, prob)
     assert _same(_canon(A.to_scipy()), gold_csr(g, "Ain"))
     ext = coarsen.endswith("+ext+i")
     H = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen.split("+")[0]], max_coarse=max_coarse,
-                              interp=O.INTERP_EXT_I if ext else O.INTERP_CLASSICAL, p_max=4))
+                              interp=O.INTERP_EXT_I if ext else O.INTERP_CLASSICAL, p_max=4,
+                              drop_tol=drop[0] if drop else 0.0))
     nlev = int(g["nlev"])
     assert H.num_levels == nlev >= 3
     for l in range(nlev):
