@@ -191,7 +191,7 @@ def test_512cubed_rccl_eight_processes_vs_one_rank(tmp_path, capfd):
     ctx = ra.Context.native(0)
     A = ra.par_stencil_grid(ctx, "7pt", DIMS, boxes=(2, 2, 2))
     t = time.perf_counter()
-    ml = ra.ParMultilevel(coarsen="pmis", smoother="jacobi", replicate_below=65536, use_graph=True).setup(A)
+    ml = ra.ParMultilevel(coarsen="pmis", smoother="jacobi", replicate_below=262144, use_graph=True).setup(A)
     report["setup_1rank_s"] = time.perf_counter() - t
     sizes1 = [[ml.level_info(l)["n_global"], ml.level_info(l)["nnz_global"]] for l in range(ml.num_levels)]
     xs = ra.vector_uniform(ctx, n, 0, 42)
@@ -207,7 +207,7 @@ def test_512cubed_rccl_eight_processes_vs_one_rank(tmp_path, capfd):
     ctx.synchronize()
     del ctx
 
-    spec = dict(kind="7pt", dims=list(DIMS), boxes=[2, 2, 2], coarsen="pmis", smoother="jacobi", rep=65536,
+    spec = dict(kind="7pt", dims=list(DIMS), boxes=[2, 2, 2], coarsen="pmis", smoother="jacobi", rep=262144,
                 native=True, graph=True, big=True)
     res = run_rccl(NRANKS, spec, tmp_path, timeout=900)
     say(f"{NRANKS} RCCL processes: setup {max(float(r['setup_s']) for r in res):.1f}s, "
