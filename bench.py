@@ -547,11 +547,13 @@ def main():
                              (f", coarse drop tolerance {drop_tol:g}" if drop_tol else ""))
                 if g3 else
                 (f"3D 27-pt Q1 anisotropic diffusion (1,1,1e-3) {grid[0]}x{grid[1]}x{grid[2]}, "
-                             f"smoothed aggregation (MIS(2)), hybrid GS(64) 1+1 V-cycle, {part_label}")
+                             f"smoothed aggregation (MIS(2)), hybrid GS(64) 1+1 V-cycle, {part_label}" +
+                             (f", coarse drop tolerance {drop_tol:g}" if drop_tol else ""))
                 if sa27 else
                 (f"3D 7-pt Poisson {grid[0]}x{grid[1]}x{grid[2]}, PMIS + "
                  f"{'classical' if args.interp == 'classical' else 'extended+i (P_max 4)'} interp, "
-                 f"Jacobi(2/3) 1+1 V-cycle, {part_label}"),
+                 f"Jacobi(2/3) 1+1 V-cycle, {part_label}" +
+                 (f", coarse drop tolerance {drop_tol:g} (non-Galerkin)" if drop_tol else "")),
                 "grid": list(grid),
                 "global_rows": n_global,
                 "levels": nlev,
