@@ -795,6 +795,7 @@ void build_hierarchy(const HostComm& comm, const HostCSR& A0, const amg_options&
                      const TransposeFn& transpose_fn, const LevelDoneFn& level_done,
                      const RapFn& rap_fn) {
     AMG_CHECK(opt.max_levels >= 1, "max_levels must be >= 1");
+    AMG_CHECK(opt.drop_tol >= 0.0 && std::isfinite(opt.drop_tol), "drop_tol must be finite and >= 0");
     auto mm = [&](const HostCSR& X, const HostCSR& Y) {
         return galerkin ? galerkin(X, Y) : spgemm(comm, X, Y);
     };

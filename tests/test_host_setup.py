@@ -101,6 +101,17 @@ def test_host_hierarchy_drop_tol_bit_exact(oracle, kind, dims, coarsen, tol):
     assert np.array_equal(O.sparsify(O.Csr.from_scipy(G1), tol).to_scipy().toarray(), A1.toarray())
 
 
+def test_drop_tol_must_be_finite_and_nonnegative(oracle):
+    from raptor_amd import host
+    from raptor_amd._lib import AmgError
+
+    A = oracle.gen_5pt(12, 12)
+    rp, col, val = A.arrays()
+    for bad in (-0.01, float("nan"), float("inf")):
+        with pytest.raises(AmgError, match="drop_tol"):
+            host.HostHierarchy(A.shape[0], 0, rp, col, val, host.options(coarsen="pmis", drop_tol=bad))
+
+
 def test_unsorted_input_rows_are_sorted(oracle):
     from raptor_amd import host
 
