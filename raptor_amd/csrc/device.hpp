@@ -218,6 +218,9 @@ bool level_setup_device(Context& ctx, const HostComm& comm, const HostCSR& A, co
                         int level, HostCSR& P, std::vector<int32_t>& split, SetupImages* imgs = nullptr);
 bool transpose_device(Context& ctx, const HostComm& comm, const HostCSR& P, HostCSR& R,
                       SetupImages* imgs = nullptr);
+// coarse-operator drop tolerance (host_setup.cpp sparsify) on A's device image (one rank; the
+// host sparsify otherwise); the result is registered in imgs
+HostCSR sparsify_device(Context& ctx, const HostComm& comm, const HostCSR& A, double tau, SetupImages* imgs);
 // C = A B with A on the device (DevCsr: rp64, col32, val; one rank, global = local columns)
 // and B's image on the device; C left on the device (rp also on the host)
 struct DevCSR64 {

@@ -236,7 +236,7 @@ void Solver::setup(DevMatrix& A, const amg_options& o) {
             HostCSR Ac = galerkin_device(*ctx, comm, R, Am, P, im);
             // the drop tolerance before keep_only: the Galerkin product's device image goes
             // (images are keyed by the host arrays' address)
-            if (opt.drop_tol > 0.0) Ac = sparsify(comm, Ac, opt.drop_tol);
+            if (opt.drop_tol > 0.0) Ac = sparsify_device(*ctx, comm, Ac, opt.drop_tol, im);
             if (im) im->keep_only(Ac);
             return Ac;
         };

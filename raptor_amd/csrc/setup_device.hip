@@ -958,6 +958,105 @@ void SetupImages::keep_only(const HostCSR& M) {
 
 namespace {
 
+// coarse drop tolerance on the device (one rank: global column = local row).  d_i = the row's
+// stored diagonal (first match, 0.0 without one: then nothing of the row is dropped)
+__global__ void sp_diag_kernel(long long n, const long long* __restrict__ rp, const long long* __restrict__ col,
+                               const double* __restrict__ val, double* __restrict__ d) {
+    for (long long i = (long long)blockIdx.x * kT + threadIdx.x; i < n; i += (long long)gridDim.x * kT) {
+        double v = 0.0;
+        for (long long k = rp[i]; k < rp[i + 1]; ++k)
+            if (col[k] == i) {
+                v = val[k];
+                break;
+            }
+        d[i] = v;
+    }
+}
+
+__device__ __forceinline__ bool sp_dropped(long long i, long long j, double v, const double* d, double tau) {
+    return j != i && fabs(v) < tau * sqrt(fabs(d[i] * d[j]));
+}
+
+// FILL = false: kept entries per row; true: the kept entries in row order, the diagonal's value
+// a_ii + the dropped entries of the row (row order) -- host sparsify's loop
+template <bool FILL>
+__global__ void sp_rows_kernel(long long n, const long long* __restrict__ rp, const long long* __restrict__ col,
+                               const double* __restrict__ val, const double* __restrict__ d, double tau,
+                               int* __restrict__ cnt, const int* __restrict__ orp, long long* __restrict__ ocol,
+                               double* __restrict__ oval) {
+    for (long long i = (long long)blockIdx.x * kT + threadIdx.x; i < n; i += (long long)gridDim.x * kT) {
+        if (!FILL) {
+            int c = 0;
+            for (long long k = rp[i]; k < rp[i + 1]; ++k) c += sp_dropped(i, col[k], val[k], d, tau) ? 0 : 1;
+            cnt[i] = c;
+            continue;
+        }
+        double f = d[i];
+        for (long long k = rp[i]; k < rp[i + 1]; ++k)
+            if (sp_dropped(i, col[k], val[k], d, tau)) f += val[k];
+        long long o = orp[i];
+        for (long long k = rp[i]; k < rp[i + 1]; ++k) {
+            const long long j = col[k];
+            if (sp_dropped(i, j, val[k], d, tau)) continue;
+            ocol[o] = j;
+            oval[o] = j == i ? f : val[k];
+            ++o;
+        }
+    }
+}
+
+std::vector<int32_t> download_ints(hipStream_t s, const int* p, int64_t n);
+
+}  // namespace
+
+HostCSR sparsify_device(Context& ctx, const HostComm& comm, const HostCSR& A, double tau, SetupImages* imgs) {
+    DevCsr* D = imgs && comm.nranks == 1 ? imgs->find(A) : nullptr;
+    if (!D || A.nrows() >= INT_MAX) return sparsify(comm, A, tau);
+    hipStream_t s = ctx.stream;
+    D->ensure_rp64(s);
+    D->ensure_col64(s);
+    const int64_t n = A.nrows();
+    DevBuf<double> d;
+    DevBuf<int> cnt, orp;
+    DevBuf<char> tmp;
+    d.alloc((size_t)std::max<int64_t>(n, 1));
+    cnt.alloc((size_t)n + 1);
+    orp.alloc((size_t)n + 1);
+    HIP_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int) * cnt.n, s));
+    if (n) {
+        hipLaunchKernelGGL(sp_diag_kernel, dim3(grid_cap(n)), dim3(kT), 0, s, (long long)n, D->rp64.p, D->col64.p,
+                           D->val.p, d.p);
+        hipLaunchKernelGGL(sp_rows_kernel<false>, dim3(grid_cap(n)), dim3(kT), 0, s, (long long)n, D->rp64.p,
+                           D->col64.p, D->val.p, d.p, tau, cnt.p, nullptr, nullptr, nullptr);
+        HIP_CHECK(hipGetLastError());
+    }
+    const int64_t nnz = exclusive_scan(s, cnt.p, orp.p, (int)n, tmp);
+    std::unique_ptr<DevCsr> B(new DevCsr());
+    B->rp32 = std::move(orp);
+    B->col64.alloc((size_t)std::max<int64_t>(nnz, 1));
+    B->val.alloc((size_t)std::max<int64_t>(nnz, 1));
+    if (n)
+        hipLaunchKernelGGL(sp_rows_kernel<true>, dim3(grid_cap(n)), dim3(kT), 0, s, (long long)n, D->rp64.p, D->col64.p,
+                           D->val.p, d.p, tau, nullptr, B->rp32.p, B->col64.p, B->val.p);
+    HIP_CHECK(hipGetLastError());
+    HostCSR out;
+    out.n_global_rows = A.n_global_rows;
+    out.n_global_cols = A.n_global_cols;
+    out.row_starts = A.row_starts;
+    out.col_starts = A.col_starts;
+    std::vector<int> hrp = download_ints(s, B->rp32.p, n + 1);
+    out.rp.assign(hrp.begin(), hrp.end());
+    out.col.resize((size_t)nnz);
+    out.val.resize((size_t)nnz);
+    static_assert(sizeof(long long) == sizeof(int64_t), "int64 columns");
+    copy_to_host(out.col.data(), B->col64.p, sizeof(long long) * nnz, s);
+    copy_to_host(out.val.data(), B->val.p, sizeof(double) * nnz, nullptr);
+    imgs->put(out, std::move(B));
+    return out;
+}
+
+namespace {
+
 // the level operator on the device: this rank's rows, global column ids (int32)
 struct DevLevel {
     DevBuf<int> rp, col;
