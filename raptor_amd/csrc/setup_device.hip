@@ -1011,7 +1011,7 @@ std::vector<int32_t> download_ints(hipStream_t s, const int* p, int64_t n);
 
 HostCSR sparsify_device(Context& ctx, const HostComm& comm, const HostCSR& A, double tau, SetupImages* imgs) {
     DevCsr* D = imgs && comm.nranks == 1 ? imgs->find(A) : nullptr;
-    if (!D || A.nrows() >= INT_MAX) return sparsify(comm, A, tau);
+    if (!D || A.nrows() >= INT_MAX || A.nnz() >= INT_MAX) return sparsify(comm, A, tau);  // int32 scan
     hipStream_t s = ctx.stream;
     D->ensure_rp64(s);
     D->ensure_col64(s);
