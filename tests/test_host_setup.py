@@ -101,6 +101,38 @@ def test_host_hierarchy_drop_tol_bit_exact(oracle, kind, dims, coarsen, tol):
     assert np.array_equal(O.sparsify(O.Csr.from_scipy(G1), tol).to_scipy().toarray(), A1.toarray())
 
 
+def test_drop_tol_edge_cases(oracle):
+    """sparsify: a row without a stored diagonal keeps every entry (d_i = 0 drops
+    nothing, and no column can be lumped onto it); a huge tolerance leaves a diagonal operator,
+    after which coarsening stops -- host setup and oracle agree level for level."""
+    import scipy.sparse as sp
+
+    from raptor_amd import host
+
+    O = oracle
+    M = sp.csr_matrix(np.array([[4.0, -0.001, -1.0, 0.0],
+                                [-0.001, 0.0, -0.5, 0.2],   # no stored diagonal
+                                [-1.0, -0.5, 3.0, -0.002],
+                                [0.0, 0.2, -0.002, 2.0]]))
+    M.eliminate_zeros()
+    B = O.sparsify(O.Csr.from_scipy(M), 0.01).to_scipy().toarray()
+    # row 1 (no diagonal): unchanged; rows 0, 2, 3: the entries below 0.01 sqrt(|a_ii a_jj|)
+    # against a stored neighbour diagonal are lumped (a_jj = 0 for j = 1 keeps them)
+    assert np.array_equal(B[1], M.toarray()[1])
+    assert B[0, 1] == -0.001 and B[2, 1] == -0.5
+    assert B[2, 3] == 0.0 and B[2, 2] == 3.0 + -0.002 and B[3, 2] == 0.0 and B[3, 3] == 2.0 + -0.002
+    for kind, dims, coarsen in [("7pt", (16, 15, 14), "pmis"), ("27pt", (12, 11, 10), "sa")]:
+        A = gen(O, kind, dims)
+        rp, col, val = A.arrays()
+        Hp = host.HostHierarchy(A.shape[0], 0, rp, col, val,
+                                host.options(coarsen=coarsen, max_coarse=16, drop_tol=10.0))
+        Ho = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen], max_coarse=16, drop_tol=10.0))
+        assert Hp.num_levels == Ho.num_levels == 2, (kind, Ho.num_levels)
+        A1 = Ho.matrix(1, "A")
+        assert same_csr(Hp.to_scipy(1, "A"), A1)
+        assert (sp.csr_matrix(A1) - sp.diags(A1.diagonal())).count_nonzero() == 0  # diagonal only
+
+
 def test_drop_tol_must_be_finite_and_nonnegative(oracle):
     from raptor_amd import host
     from raptor_amd._lib import AmgError
