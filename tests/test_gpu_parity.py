@@ -370,9 +370,7 @@ def test_vcycle_ext_i_bit_exact(ctx, oracle, kind, dims):
 
 
 @pytest.mark.parametrize("kind,dims,coarsen,smoother,tol", [("27pt", (30, 28, 26), "sa", "hybrid_gs", 0.02),
-                                                           ("7pt", (40, 36, 33), "pmis", "jacobi", 0.05),
-                                                           # everything off-diagonal dropped: 2 levels
-                                                           ("7pt", (20, 18, 16), "pmis", "jacobi", 10.0)])
+                                                           ("7pt", (40, 36, 33), "pmis", "jacobi", 0.05)])
 def test_vcycle_drop_tol_bit_exact(ctx, oracle, kind, dims, coarsen, smoother, tol):
     """Coarse-operator drop tolerance (r6 option): the device setup (Galerkin product on the GPU,
     then the drop) equals the oracle on every level; the V-cycle is bit-identical."""
@@ -384,7 +382,7 @@ def test_vcycle_drop_tol_bit_exact(ctx, oracle, kind, dims, coarsen, smoother, t
     ml = ra.ParMultilevel(coarsen=coarsen, smoother=smoother, drop_tol=tol).setup(A)
     Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS[coarsen], smoother=O.SMOOTH_JACOBI if smoother == "jacobi"
                                 else O.SMOOTH_HYBRID_GS, drop_tol=tol))
-    assert ml.num_levels == Ho.num_levels >= (2 if tol > 1 else 3)
+    assert ml.num_levels == Ho.num_levels >= 3
     for l in range(ml.num_levels):
         assert same_csr(ml.level_matrix(l, "A").to_scipy_local(), Ho.matrix(l, "A")), l
         if l + 1 < ml.num_levels:

@@ -104,7 +104,9 @@ def test_host_hierarchy_drop_tol_bit_exact(oracle, kind, dims, coarsen, tol):
 def test_drop_tol_edge_cases(oracle):
     """sparsify: a row without a stored diagonal keeps every entry (d_i = 0 drops
     nothing, and no column can be lumped onto it); a huge tolerance leaves a diagonal operator,
-    after which coarsening stops -- host setup and oracle agree level for level."""
+    after which coarsening stops -- host setup and oracle agree level for level.  (Setup only:
+    the lumped diagonal is the Galerkin row sum, ~0 for a Laplacian's interior rows, so that
+    coarse operator is near-singular and no cycle is run on it.)"""
     import scipy.sparse as sp
 
     from raptor_amd import host
