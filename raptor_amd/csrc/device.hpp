@@ -385,7 +385,6 @@ struct DevMatrix {
     // tpl_mne = 0: not uniform.  tpl_mem / tpl_mep: master index of offset -1 / +1 (-1: none)
     int tpl_mne = 0, tpl_mdiag = -1, tpl_mem = -1, tpl_mep = -1;
     std::vector<int> tpl_mslot;
-    std::vector<int> tpl_moff;  // the master's (column - row) offsets (tpl_jacres_kernel)
     std::vector<double> tpl_mval;
     double tpl_mpd = 0.0;
     DevBuf<unsigned> tpl_mmask, gs_tmask;
@@ -455,12 +454,6 @@ enum KernelMode { KM_SPMV = 0, KM_SPMV_ADD = 1, KM_RESID = 2, KM_JACOBI = 3, KM_
 // csr-stream variant bits in effect for A (DevMatrix::default_variant, VI and template bits,
 // or AMG_KERNEL_VARIANT): 2 XCD order, 4 gather, 8 value-indexed, 32 row templates
 int kernel_variant(const DevMatrix& A);
-// level-0 pre-smoothing Jacobi + the residual of its result in one z-march (kernels.hip,
-// tpl_jacres_kernel): x1 = x0 + omega D^-1 (b - A x0), r = b - A x1, partial (non-null): the
-// Jacobi launch's norm partials of b - A x0.  tpl_jacres_ok: where it applies
-bool tpl_jacres_ok(const DevMatrix& A, const double* x);
-void launch_tpl_jacres(hipStream_t s, const DevMatrix& A, const double* x0, const double* b, double* x1,
-                       double* r, double omega, double* partial);
 // partial slot of block bid's wave w: part_off + bid * kNormParts + w
 void launch_csr_stream(hipStream_t s, int mode, bool norm, const DevMatrix& A, int first_block,
                        int n_blocks, const double* x, const double* b, double* y, double omega,
@@ -614,8 +607,6 @@ struct Solver {
                 bool post = false);
     void ensure_hist(int32_t n);
     bool can_fuse_norm() const;
-    // level 0 runs its one Jacobi pre-sweep and the residual as one march (tpl_jacres_kernel)
-    bool jacres_level0(size_t l, bool x_zero, bool x0_in_t, const double* x);
     // ParMultilevel::solve; hist_host gets it+1 norms
     int32_t solve(double* x, const double* b, int32_t max_iter, double tol, double* hist_host);
     // AMG-preconditioned conjugate gradients (one V-cycle per iteration as M^-1)

@@ -1364,186 +1364,6 @@ __global__ __launch_bounds__(kTPB, tpl_march_waves(NPL, NORM)) void tpl_march_ke
     }
 }
 
-// Level-0 pre-smoothing Jacobi and the residual of its result in one z-march (r6; DESIGN.md
-// 4.0).  7-pt uniform stencil, master offsets {-P, -H, -1, 0, 1, H, P} (P = S blocks of
-// kTplRows rows, H <= 256), one rank, every row templated.  A chain walks planes u of one column
-// of blocks: step u computes x1 = x0 + omega (1/a_ii) (b - A x0) on the block's rows and H rows
-// either side (the extended rows E_u, the in-plane halo the residual needs from the neighbouring
-// columns, recomputed here instead of exchanged), and r = b - A x1 on the rows of plane u - 1
-// (its -P / +P neighbours are planes u - 2 and u, all in the ring).  LDS: a ring of 3 x0 plane
-// slabs [r0 - 2H, r0 + B + 2H) (one loaded per step, prefetched into registers the step
-// before) and a ring of 3 x1 slabs over E.  Each row's sums are the template kernel's -- the
-// master's products in order from 0.0, selected addends for the entries a row lacks -- so x1,
-// r and the norm partials are bit-identical to the two launches it replaces (the partials
-// recomputed in the Jacobi kernel's lane layout: tpl_lrow<true>, two rows per lane).
-struct JrArgs {
-    const uint8_t* id;
-    const unsigned* mask;  // per template: master-entry bits
-    int ntpl, n, P, H, S, K, nchunk;
-    double mval[7];
-    double mpd, omega;
-    const double* x0;
-    const double* b;
-    double* x1;
-    double* r;
-    double* partial;  // NORM: the Jacobi launch's per-block partials of (b - A x0)^2
-};
-constexpr int kJrT = 512;  // threads: up to 2 extended rows and 1 own row per lane
-
-__device__ __forceinline__ int jr_ring(int p) { return ((p % 3) + 3) % 3; }
-
-// sum_e [bit e] v_e x_e in master order from 0.0 (tpl_rows_master's selected addends)
-__device__ __forceinline__ double jr_rowsum(const JrArgs& a, unsigned m, const double (&xs)[7]) {
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-        const double p = a.mval[k] * xs[k];
-        s = s + (((m >> k) & 1u) ? p : 0.0);
-    }
-    return s;
-}
-
-template <bool NORM>
-__global__ __launch_bounds__(kJrT, 4) void tpl_jacres_kernel(JrArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double jr_lds[];
-    constexpr int B = kTplRows;
-    const int H = a.H, EL = B + 2 * H, SL = B + 4 * H, P = a.P, S = a.S, K = a.K;
-    double* slab = jr_lds;         // 3 x SL: x0[r0(p) - 2H + i]
-    double* xr = slab + 3 * SL;    // 3 x EL: x1[r0(p) - H + e]
-    unsigned* msk = (unsigned*)(xr + 3 * EL);
-    const int tid = threadIdx.x;
-    for (int k = tid; k < a.ntpl; k += kJrT) msk[k] = a.mask[k];
-    const __amdgpu_buffer_rsrc_t xrs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)a.x0, (short)0, (int)((unsigned)a.n * 8u), 0x00020000);
-    const int npair = SL / 2;  // SL even (B, H even)
-    auto slab_load = [&](int col, int p, v2d_t (&v)[2]) {
-        const int base = col * B + p * P - 2 * H;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int q = tid + kJrT * j, i = base + 2 * q;
-            const int vo = (q < npair && i >= 0 && i < a.n) ? i * 8 : -16;  // outside x: 0
-            v[j] = __builtin_bit_cast(v2d_t, __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, 0, 0));
-        }
-    };
-    auto slab_store = [&](int p, const v2d_t (&v)[2]) {
-        double* d = slab + jr_ring(p) * SL;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int q = tid + kJrT * j;
-            if (q < npair) *(v2d_t*)(d + 2 * q) = v[j];
-        }
-    };
-    // the lane's extended rows e = tid + kJrT j of plane p: template ids and b (clamped loads;
-    // rows outside the matrix are never used)
-    auto rows_load = [&](int col, int p, int (&id)[2], double (&bv)[2]) {
-        const int r0p = col * B + p * P;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int e = tid + kJrT * j, g = r0p - H + e;
-            const int gg = (e < EL && g >= 0 && g < a.n) ? g : 0;
-            id[j] = a.id[gg];
-            bv[j] = a.b[gg];
-        }
-    };
-    // the lane's own row (one per lane): extended row eo = tid (lanes >= H) or tid + kJrT
-    const int jo = tid >= H ? 0 : 1, Lo = tid + kJrT * jo - H;
-    const int per = (K + a.nchunk - 1) / a.nchunk;  // planes per chain
-    // chains ordered (chunk, column); XCD x = blockIdx % 8 takes a contiguous 1/8 of them
-    const int C = S * a.nchunk, x = blockIdx.x & 7, lw = blockIdx.x >> 3, nw = gridDim.x >> 3;
-    const int c0 = x * (C >> 3) + min(x, C & 7), c1 = c0 + (C >> 3) + (x < (C & 7) ? 1 : 0);
-    for (int ch = c0 + lw; ch < c1; ch += nw) {
-        const int col = ch % S, t0 = (ch / S) * per, t1 = min(K, t0 + per);
-        if (t0 >= t1) continue;  // workgroup-uniform
-        v2d_t v[2], pf[2];
-        int nid[2];
-        double nb[2];
-        __syncthreads();  // the previous chain's readers of both rings are done
-        for (int p = t0 - 2; p <= t0; ++p) {
-            slab_load(col, p, v);
-            slab_store(p, v);
-        }
-        slab_load(col, t0 + 1, pf);
-        rows_load(col, t0 - 1, nid, nb);
-        double ob = 0.0;  // the own row of the previous plane: b and mask (its residual)
-        unsigned om = 0u;
-        for (int u = t0 - 1; u <= t1; ++u) {
-            if (u >= t0) {
-                __syncthreads();  // every wave is done with step u - 1 (slab u - 2's ring slot)
-                slab_store(u + 1, pf);
-            }
-            const int cid[2] = {nid[0], nid[1]};
-            const double cb[2] = {nb[0], nb[1]};
-            if (u + 1 <= t1) {  // in flight during this step
-                if (u >= t0) slab_load(col, u + 2, pf);
-                rows_load(col, u + 1, nid, nb);
-            }
-            __syncthreads();  // slabs u - 1 .. u + 1 (and the masks) visible
-            const int r0u = col * B + u * P;
-            const double* sm = slab + jr_ring(u - 1) * SL;
-            const double* sc = slab + jr_ring(u) * SL;
-            const double* sp = slab + jr_ring(u + 1) * SL;
-            double* xo = xr + jr_ring(u) * EL;
-            const bool own_plane = u >= t0 && u < t1;  // uniform
-            double t_own = 0.0;
-            unsigned m_own = 0u;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int e = tid + kJrT * j;
-                if (e < EL) {
-                    const int g = r0u - H + e;
-                    const unsigned m = msk[cid[j]];
-                    double xv = 0.0;
-                    if (g >= 0 && g < a.n) {
-                        const double xs[7] = {sm[e + H], sc[e], sc[e + H - 1], sc[e + H], sc[e + H + 1],
-                                              sc[e + 2 * H], sp[e + H]};
-                        const double t = cb[j] - jr_rowsum(a, m, xs);
-                        xv = xs[3] + a.omega * (a.mpd * t);
-                        if (j == jo) {
-                            t_own = t;
-                            if (own_plane) a.x1[g] = xv;
-                        }
-                    }
-                    if (j == jo) m_own = m;
-                    xo[e] = xv;
-                }
-            }
-            __syncthreads();  // x1 of plane u visible; slab u - 1 is free
-            if (NORM && own_plane) {
-                // the Jacobi launch's partial sums of this block, in its lane layout
-                // (tpl_lrow<true>): the own rows' b - A x0 through slab u - 1's slot
-                double* tq = slab + jr_ring(u - 1) * SL;
-                tq[Lo] = t_own;
-                __syncthreads();
-                if (tid < kTPB) {
-                    double sq = 0.0;
-#pragma unroll
-                    for (int j = 0; j < kTplRPL; ++j) {
-                        const int L = kTPB * j + ((tid + 1) & (kTPB - 1));
-                        const double t = tq[L];
-                        sq += r0u + L < a.n ? t * t : 0.0;
-                    }
-                    sq = wave_sum(sq);
-                    if ((tid & 63) == 0) a.partial[(r0u / B) * kNormParts + (tid >> 6)] = sq;
-                }
-            }
-            const int vq = u - 1;
-            if (vq >= t0 && vq < t1) {  // the residual of plane u - 1 (the lane's own row), from the x1 ring
-                const int g = r0u - P + Lo;
-                if (g < a.n) {
-                    const double* xm = xr + jr_ring(vq - 1) * EL;
-                    const double* xc = xr + jr_ring(vq) * EL;
-                    const double* xp = xr + jr_ring(vq + 1) * EL;
-                    const double xs[7] = {xm[Lo + H], xc[Lo], xc[Lo + H - 1], xc[Lo + H], xc[Lo + H + 1],
-                                          xc[Lo + 2 * H], xp[Lo + H]};
-                    a.r[g] = ob - jr_rowsum(a, om, xs);
-                }
-            }
-            ob = cb[jo];
-            om = m_own;
-        }
-    }
-}
-
 // l1 hybrid Gauss-Seidel (row a5; definition DESIGN.md 3).  One wavefront per slab of <= 64
 // rows (whole GS chunks), lane = row.
 //  phase 1: the lane walks its row in the slab's sliced-ELL layout (entry k of all lanes is
@@ -2319,71 +2139,6 @@ static void launch_tpl_march(hipStream_t s, const TplArgs& a, int g, size_t lds,
         const int gp = std::max(8, std::min(res, (S * nchunk + 7) / 8 * 8));
         hipLaunchKernelGGL((tpl_march_kernel<M, N, P, K>), dim3(gp), dim3(kTPB), lds, s, a, g, S, nchunk);
     }
-}
-
-// the fused level-0 Jacobi + residual (tpl_jacres_kernel) applies: one rank, every row on the
-// uniform 7-pt templates, the plane a whole number of blocks, x 16-byte aligned
-bool tpl_jacres_ok(const DevMatrix& A, const double* x) {
-    const char* env = std::getenv("AMG_JACRES");  // read per call: tests compare both in one process
-    const bool off = env && *env && std::atoi(env) == 0;
-    if (off || !A.square || A.ctx->host.nranks != 1 || A.replicated || A.plan.n_halo() != 0) return false;
-    if (!A.tpl_on() || A.format != AMG_FORMAT_AUTO || !(kernel_variant(A) & 512) || A.tpl_mne != 7) return false;
-    if (A.tpl_rows != A.n_rows || A.nb_int + A.nb_bnd - A.nb_skip != 0 || A.n_tpl > 256) return false;
-    if ((int)A.tpl_moff.size() != 7 || A.tpl_mdiag != 3 || ((uintptr_t)x & 15) != 0) return false;
-    const int64_t P = -(int64_t)A.tpl_moff[0], H = -(int64_t)A.tpl_moff[1], n = A.n_rows;
-    const int m[7] = {(int)-P, (int)-H, -1, 0, 1, (int)H, (int)P};
-    for (int e = 0; e < 7; ++e)
-        if (A.tpl_moff[e] != m[e]) return false;
-    return H >= 2 && H <= 256 && H % 2 == 0 && P > 2 * H && P % kTplRows == 0 && n % P == 0 && n / P >= 1 &&
-           n < (int64_t(1) << 28);
-}
-
-size_t tpl_jacres_lds(int H) {
-    return 8 * (size_t)(3 * (kTplRows + 4 * H) + 3 * (kTplRows + 2 * H)) + 4 * 256;
-}
-
-void launch_tpl_jacres(hipStream_t s, const DevMatrix& A, const double* x0, const double* b, double* x1,
-                       double* r, double omega, double* partial) {
-    JrArgs a{};
-    a.id = A.tpl_id.p;
-    a.mask = A.tpl_mmask.p;
-    a.ntpl = A.n_tpl;
-    a.n = (int)A.n_rows;
-    a.P = -A.tpl_moff[0];
-    a.H = -A.tpl_moff[1];
-    a.S = a.P / kTplRows;
-    a.K = a.n / a.P;
-    for (int e = 0; e < 7; ++e) a.mval[e] = A.tpl_mval[e];
-    a.mpd = A.tpl_mpd;
-    a.omega = omega;
-    a.x0 = x0;
-    a.b = b;
-    a.x1 = x1;
-    a.r = r;
-    a.partial = partial;
-    const size_t lds = tpl_jacres_lds(a.H);
-    thread_local int ncu = 0, occ[2] = {0, 0};
-    thread_local size_t occ_lds[2] = {0, 0};
-    const int k = partial ? 1 : 0;
-    if (ncu == 0) {
-        int dev = 0;
-        HIP_CHECK(hipGetDevice(&dev));
-        HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    if (occ_lds[k] != lds) {
-        if (partial) HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[k], tpl_jacres_kernel<true>, kJrT, lds));
-        else HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[k], tpl_jacres_kernel<false>, kJrT, lds));
-        occ_lds[k] = lds;
-    }
-    const int res = std::max(8, std::max(1, occ[k]) * ncu / 8 * 8);  // resident workgroups
-    a.nchunk = std::max(1, res / a.S);                               // chains per column
-    const int cap = tpl_march_chunk_cap();
-    if (cap > 0) a.nchunk = std::min(a.nchunk, cap);
-    a.nchunk = std::min(a.nchunk, a.K);
-    const int gp = std::max(8, std::min(res, (a.S * a.nchunk + 7) / 8 * 8));
-    if (partial) hipLaunchKernelGGL(tpl_jacres_kernel<true>, dim3(gp), dim3(kJrT), lds, s, a);
-    else hipLaunchKernelGGL(tpl_jacres_kernel<false>, dim3(gp), dim3(kJrT), lds, s, a);
-    HIP_CHECK(hipGetLastError());
 }
 
 void launch_tpl(hipStream_t s, int mode, bool norm, const DevMatrix& A, const double* x,

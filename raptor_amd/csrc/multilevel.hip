@@ -766,23 +766,14 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
     double* cur = x;
     double* tmp = L.t.p;
     bool zero = x_zero;
-    if (jacres_level0(l, x_zero, x0_in_t, cur)) {
-        // level 0, one Jacobi pre-sweep: the sweep and the residual of its result in one z-march
-        // (tpl_jacres_kernel; the same x1, r and norm partials as the two launches below)
-        launch_tpl_jacres(s, A, cur, b, tmp, L.r.p, opt.jacobi_omega, with_norm ? sink.partial : nullptr);
-        if (with_norm) norm_finish(A, sink);
-        std::swap(cur, tmp);
-        mark(l, "pre-smooth + residual (one march)");
-    } else {
-        for (int k = 0; k < opt.pre_sweeps; ++k) {
-            if (k == 0 && x0_in_t) std::swap(cur, tmp);  // the sweep from zero is in tmp already
-            else smooth(l, cur, b, tmp, zero, with_norm && k == 0);
-            zero = false;
-        }
-        if (zero) launch_zero(s, A.n_rows, cur);
-        par_apply(A, KM_RESID, cur, b, L.r.p, 0.0, nullptr);
-        mark(l, "residual");
+    for (int k = 0; k < opt.pre_sweeps; ++k) {
+        if (k == 0 && x0_in_t) std::swap(cur, tmp);  // the sweep from zero is in tmp already
+        else smooth(l, cur, b, tmp, zero, with_norm && k == 0);
+        zero = false;
     }
+    if (zero) launch_zero(s, A.n_rows, cur);
+    par_apply(A, KM_RESID, cur, b, L.r.p, 0.0, nullptr);
+    mark(l, "residual");
     Level& C = levels[l + 1];
     if ((int)l + 1 == rep_level) {
         // distributed R output -> whole b_{l+1} on every rank (padded allgather + unpad)
@@ -817,11 +808,6 @@ void Solver::cycle_rec(size_t l, double* x, const double* b, bool x_zero, bool w
         HIP_CHECK(hipMemcpyAsync(x, cur, A.n_rows * sizeof(double), hipMemcpyDeviceToDevice, s));
         mark(l, "copy");
     }
-}
-
-bool Solver::jacres_level0(size_t l, bool x_zero, bool x0_in_t, const double* x) {
-    return l == 0 && !x_zero && !x0_in_t && opt.pre_sweeps == 1 && opt.smoother == AMG_SMOOTH_JACOBI &&
-           levels.size() >= 2 && tpl_jacres_ok(CA(0), x);
 }
 
 bool Solver::can_fuse_norm() const {
@@ -1194,9 +1180,6 @@ int64_t Solver::stored_bytes_per_cycle(size_t l) const {
     }
     if (zero) b += 8 * n;
     b += A.mode_bytes(KM_RESID);
-    // level 0 with the fused sweep + residual (cycle_rec, jacres_level0): the residual reads
-    // neither x1 nor b nor the row ids again
-    if (l == 0 && opt.pre_sweeps == 1 && !gs && tpl_jacres_ok(A, A.dinv.p)) b -= 17 * n;
     b += me.CR(l).mode_bytes(KM_SPMV);
     b += me.CP(l).mode_bytes(KM_SPMV_ADD);
     b += opt.post_sweeps * sweep;

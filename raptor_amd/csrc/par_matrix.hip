@@ -597,7 +597,6 @@ static void find_master_template(DevMatrix& D, const TplBuild& tb, const std::ve
     D.tpl_mne = 0;
     D.tpl_mdiag = D.tpl_mem = D.tpl_mep = -1;
     D.tpl_mslot.clear();
-    D.tpl_moff.clear();
     D.tpl_mval.clear();
     D.tpl_mmask.reset();
     const char* env = std::getenv("AMG_TPL_MASTER");
@@ -636,7 +635,6 @@ static void find_master_template(DevMatrix& D, const TplBuild& tb, const std::ve
     D.tpl_mpd = tb.pd[M];
     for (int e = 0; e < ne; ++e) {
         D.tpl_mslot.push_back(ldo[sm + e]);
-        D.tpl_moff.push_back(tb.off[sm + e]);
         D.tpl_mval.push_back(tb.val[sm + e]);
         if (tb.off[sm + e] == -1) D.tpl_mem = e;
         if (tb.off[sm + e] == 1) D.tpl_mep = e;

@@ -648,41 +648,3 @@ def test_pcg_matches_oracle(ctx, oracle, coarsen, smoother):
     assert hist[-1] < hv[-1]  # CG accelerates the plain V-cycle iteration
     _, ht = ml.pcg(ctx.zeros(n), to_dev(ctx, b), max_iter=100, tol=1e-10)
     assert ht[-1] / ht[0] < 1e-10 and len(ht) < 101
-
-
-@pytest.mark.parametrize("dims,chunks", [((32, 16, 24), 0), ((32, 16, 24), 1), ((64, 32, 20), 3), ((256, 4, 10), 0),
-                                         ((64, 32, 20), 0)])
-def test_level0_jacobi_residual_march_bit_exact(ctx, oracle, monkeypatch, dims, chunks):
-    """Level 0's pre-smoothing Jacobi and the residual of its result in one z-march
-    (tpl_jacres_kernel, r6; 7-pt planes of whole 512-row blocks): the cycle runs it (timeline
-    label), three V-cycle iterates equal the oracle's bit for bit, and a solve's fused-norm
-    history (the march's partials) is bit-identical to the two-launch path (AMG_JACRES=0).
-    AMG_TPL_MARCH_CHUNKS caps the chains per column (1: one chain over all planes; 3: uneven)."""
-    import raptor_amd as ra
-
-    O = oracle
-    if chunks:
-        monkeypatch.setenv("AMG_TPL_MARCH_CHUNKS", str(chunks))
-    Ao = O.gen_7pt(*dims)
-    A = ra.par_stencil_grid(ctx, "7pt", dims)
-    Ho = O.Hierarchy(Ao, **O.DEFAULTS["pmis"])
-    n = Ao.shape[0]
-    b = Ao.spmv(O.vec_uniform(n, 42))
-    db = to_dev(ctx, b)
-    hists = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("AMG_JACRES", mode)
-        ml = ra.ParRugeStubenSolver(coarsen="pmis").setup(A)
-        assert ml.num_levels == Ho.num_levels >= 3
-        dx, xo = ctx.zeros(n), np.zeros(n)
-        for _ in range(3):
-            ml.cycle(dx, db)
-            xo = Ho.cycle(xo, b)
-            assert np.array_equal(to_host(ctx, dx), xo), mode
-        ops, _ = ml.cycle_timeline(ctx.zeros(n), db, reps=1)
-        fused = any("one march" in o[0] for o in ops)
-        assert fused == (mode == "1"), [o[0] for o in ops][:4]
-        x, hist = ml.solve(ctx.zeros(n), db, max_iter=6)
-        hists[mode] = (to_host(ctx, x), hist)
-    assert np.array_equal(hists["1"][0], hists["0"][0])
-    assert np.array_equal(hists["1"][1], hists["0"][1])
