@@ -85,7 +85,8 @@ def main():
 
         t = time.perf_counter()
         ml = ra.ParMultilevel(coarsen=spec["coarsen"], smoother=spec["smoother"],
-                              replicate_below=spec["rep"], use_graph=spec["graph"]).setup(A)
+                              replicate_below=spec["rep"], use_graph=spec["graph"],
+                              drop_tol=spec.get("drop", 0.0)).setup(A)
         barrier()
         res["setup_s"] = time.perf_counter() - t
         res["levels"] = np.array([[ml.level_info(l)["n_global"], ml.level_info(l)["nnz_global"]]
@@ -124,7 +125,8 @@ def main():
     res.update(ra.runtime_versions())
     try:
         ml = ra.ParMultilevel(coarsen=spec["coarsen"], smoother=spec["smoother"],
-                              replicate_below=spec["rep"], use_graph=spec["graph"]).setup(A)
+                              replicate_below=spec["rep"], use_graph=spec["graph"],
+                              drop_tol=spec.get("drop", 0.0)).setup(A)
     except ra.AmgError as e:
         # graph=True on a runtime whole-cycle capture is not validated on: the gate's error
         # is the result (tests/test_gpu_rccl.py checks it)

@@ -69,6 +69,8 @@ CASES = [
     (3, dict(kind="27pt", dims=[10, 11, 16], coarsen="sa", smoother="hybrid_gs", rep=0)),
     (8, dict(kind="7pt", dims=[24, 24, 64], coarsen="pmis", smoother="jacobi", rep=0)),
     (8, dict(kind="7pt", dims=[24, 24, 64], coarsen="sa", smoother="hybrid_gs", rep=65536)),
+    # r6: coarse drop tolerance on N ranks (host sparsify, off-rank diagonals through the halo)
+    (3, dict(kind="27pt", dims=[10, 11, 16], coarsen="sa", smoother="hybrid_gs", rep=0, drop=0.02)),
 ]
 
 
@@ -87,7 +89,8 @@ MODES = {"torch-eager": dict(native=False, graph=False), "native-graph": dict(na
 
 @pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("nranks,spec", CASES,
-                         ids=[f"{n}r-{s['kind']}-{s['coarsen']}-rep{s['rep']}" for n, s in CASES])
+                         ids=[f"{n}r-{s['kind']}-{s['coarsen']}-rep{s['rep']}" + (f"-drop{s['drop']}" if "drop" in s else "")
+                              for n, s in CASES])
 def test_rccl_vcycle_bit_exact(oracle, tmp_path, nranks, spec, mode):
     _check_vs_oracle(oracle, tmp_path, nranks, dict(spec, **MODES[mode]))
 
@@ -119,7 +122,7 @@ def _check_vs_oracle(oracle, tmp_path, nranks, spec):
             assert np.array_equal(r[k], ref[k][f:f + m]), k
         assert abs(float(r["rn"]) - rn) <= 1e-12 * rn
     smoother = O.SMOOTH_JACOBI if spec["smoother"] == "jacobi" else O.SMOOTH_HYBRID_GS
-    Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS[spec["coarsen"]], smoother=smoother))
+    Ho = O.Hierarchy(Ao, **dict(O.DEFAULTS[spec["coarsen"]], smoother=smoother, drop_tol=spec.get("drop", 0.0)))
     assert all(int(r["levels"]) == Ho.num_levels for r in res)
     for l in range(Ho.num_levels):
         Ho.set_cuts(l, sorted({int(r["starts"][l]) for r in res}))
