@@ -77,8 +77,9 @@ int amg_context_destroy(amg_context ctx);
  * sorted by the call), val[nnz].  Collective over the ranks of the context.
  * Memory: on one rank a square matrix also keeps its uploaded CSR on the device (int32
  * row_ptr / col + fp64 val, 4 (n+1) + 12 nnz bytes: ~5 GB for a 256^3 27-point operator) as
- * the level-0 image of a later amg_solver_setup, which takes it over; a matrix that is never
- * set up holds it until amg_par_csr_destroy.                                               */
+ * the level-0 image of a later amg_solver_setup, which takes it over; the first computation
+ * on the matrix (amg_par_csr_mult, _residual, ...) frees it instead (a setup after that
+ * uploads the operator again).                                                             */
 int amg_par_csr_create(amg_context ctx, int64_t n_global, int64_t first_row, int64_t n_local,
                        const int64_t* row_ptr, const int64_t* col_global, const double* val,
                        amg_matrix* out);

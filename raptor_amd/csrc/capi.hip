@@ -439,12 +439,20 @@ int amg_par_csr_export(amg_matrix A, int64_t* rp, int64_t* col, double* val) {
     });
 }
 
+// an operator's setup image (DevMatrix::setup_csr, 12 B per nonzero) is held only
+// until the matrix is set up as a solver's level 0 or used for a computation, whichever comes
+// first (a later setup uploads the operator again)
+static void release_setup_image(DevMatrix& M) {
+    if (M.setup_csr) M.setup_csr.reset();
+}
+
 static int apply(amg_matrix A, int mode, const double* x, const double* b, double* y, double w) {
     return guard([&] {
         AMG_CHECK(A, "null matrix");
         AMG_CHECK((x || A->m->n_cols_local == 0) && (y || A->m->n_rows == 0), "null vector");
         set_device(*A->m->ctx);
         A->m->ensure_built();
+        release_setup_image(*A->m);
         par_apply(*A->m, mode, x, b, y, w, nullptr);
     });
 }
@@ -466,6 +474,7 @@ int amg_par_csr_hybrid_gs(amg_matrix A, const double* x, const double* b, double
         AMG_CHECK(x != xo, "hybrid GS is out of place: x and x_out must differ");
         set_device(*A->m->ctx);
         A->m->ensure_built();
+        release_setup_image(*A->m);
         par_hybrid_gs(*A->m, x, b, xo, block);
     });
 }
@@ -477,6 +486,7 @@ int amg_par_csr_hybrid_gs_backward(amg_matrix A, const double* x, const double* 
         AMG_CHECK(x != xo, "hybrid GS is out of place: x and x_out must differ");
         set_device(*A->m->ctx);
         A->m->ensure_built();
+        release_setup_image(*A->m);
         par_hybrid_gs(*A->m, x, b, xo, block, true);
     });
 }
@@ -502,6 +512,7 @@ int amg_par_csr_residual_norm(amg_matrix A, const double* x, const double* b, do
         Context& c = *A->m->ctx;
         set_device(c);
         A->m->ensure_built();
+        release_setup_image(*A->m);
         const size_t nb = (size_t)A->m->norm_parts_max(), tmpn = nb / 4096 + 64;
         DevBuf<double> r, buf;
         DevBuf<int> cnt;

@@ -345,7 +345,8 @@ struct DevMatrix {
     // r5: an operator the caller created (C-ABI constructors) keeps, on one rank, the CSR the
     // device format build uploaded (row pointers, columns, values in row order) until a solver
     // setup takes it as its level-0 image (SetupImages) instead of uploading the operator
-    // again; 12 B per nonzero while it is held
+    // again; 12 B per nonzero while it is held (r6: the first C-ABI computation on the matrix
+    // frees it too, capi.hip release_setup_image)
     bool keep_setup_csr = false;
     std::unique_ptr<DevCsr> setup_csr;
     DevBuf<int4> gs_cslabs[2];
