@@ -3,7 +3,8 @@
 // with -fsanitize=address,undefined (no HIP: the host setup is plain C++ + OpenMP); exercises
 // the setup paths the GPU solver runs before uploading: stencil slabs, strength, RS / PMIS
 // splits + classical interpolation, MIS(2) aggregation + smoothed prolongator, transposes,
-// Galerkin SpGEMM, the coarse dense inverse, the graph-Laplacian generator, RCM reordering
+// Galerkin SpGEMM, extended+i and the coarse drop tolerance (r6), the coarse dense inverse,
+// the graph-Laplacian generator, RCM reordering
 // and the Matrix Market / binary CSR readers and writer.
 #include <cstdio>
 #include <cstdlib>
@@ -39,13 +40,21 @@ int main(int argc, char** argv) {
         int64_t nx, ny, nz;
         int coarsen, smoother;
         double theta;
-    } cases[] = {{AMG_STENCIL_7PT, 14, 13, 12, AMG_COARSEN_PMIS, AMG_SMOOTH_JACOBI, 0.25},
-                 {AMG_STENCIL_5PT, 40, 33, 1, AMG_COARSEN_RS, AMG_SMOOTH_JACOBI, 0.25},
-                 {AMG_STENCIL_27PT, 11, 10, 9, AMG_COARSEN_SA, AMG_SMOOTH_HYBRID_GS, 0.08}};
+        int interp;       // r6 options: extended+i interpolation (P_max 4)
+        double drop_tol;  // and the coarse drop tolerance
+    } cases[] = {{AMG_STENCIL_7PT, 14, 13, 12, AMG_COARSEN_PMIS, AMG_SMOOTH_JACOBI, 0.25, AMG_INTERP_CLASSICAL, 0.0},
+                 {AMG_STENCIL_5PT, 40, 33, 1, AMG_COARSEN_RS, AMG_SMOOTH_JACOBI, 0.25, AMG_INTERP_CLASSICAL, 0.0},
+                 {AMG_STENCIL_27PT, 11, 10, 9, AMG_COARSEN_SA, AMG_SMOOTH_HYBRID_GS, 0.08, AMG_INTERP_CLASSICAL, 0.0},
+                 {AMG_STENCIL_7PT, 14, 13, 12, AMG_COARSEN_PMIS, AMG_SMOOTH_JACOBI, 0.25, AMG_INTERP_EXT_I, 0.05},
+                 {AMG_STENCIL_27PT, 11, 10, 9, AMG_COARSEN_SA, AMG_SMOOTH_HYBRID_GS, 0.08, AMG_INTERP_CLASSICAL, 0.02}};
     for (const Case& c : cases) {
         HostCSR A = stencil_slab(serial, c.kind, c.nx, c.ny, c.nz, eps);
         HostHierarchy H;
-        build_hierarchy(serial, A, opts(c.coarsen, c.smoother, c.theta), H);
+        amg_options o = opts(c.coarsen, c.smoother, c.theta);
+        o.interp = c.interp;
+        o.p_max = 4;
+        o.drop_tol = c.drop_tol;
+        build_hierarchy(serial, A, o, H);
         levels += (int)H.levels.size();
         if (H.levels.size() < 2 || H.coarse_inv.empty()) {
             std::fprintf(stderr, "hierarchy too shallow\n");

@@ -6,8 +6,15 @@
 
 #include "../../oracle/amg_oracle.h"
 
+static int run_opt(orc_csr* A, int coarsen, int smoother, double theta, int interp, double drop_tol);
 static int run(orc_csr* A, int coarsen, int smoother, double theta) {
+    return run_opt(A, coarsen, smoother, theta, ORC_INTERP_CLASSICAL, 0.0);
+}
+static int run_opt(orc_csr* A, int coarsen, int smoother, double theta, int interp, double drop_tol) {
     orc_options o = {coarsen, smoother, theta, 2.0 / 3.0, 1, 1, 25, 64, 64, 0x5EED};
+    o.interp = interp;  /* r6 options: extended+i (P_max 4) and the coarse drop tolerance */
+    o.p_max = 4;
+    o.drop_tol = drop_tol;
     int64_t n = orc_csr_rows(A);
     double* b = malloc(sizeof(double) * n);
     double* x = calloc(n, sizeof(double));
@@ -34,6 +41,8 @@ int main(void) {
     int lv = 0;
     orc_csr* A = orc_gen_7pt(14, 13, 12);
     lv += run(A, ORC_COARSEN_PMIS, ORC_SMOOTH_JACOBI, 0.25);
+    lv += run_opt(A, ORC_COARSEN_PMIS, ORC_SMOOTH_JACOBI, 0.25, ORC_INTERP_EXT_I, 0.05);
+    lv += run_opt(A, ORC_COARSEN_SA, ORC_SMOOTH_HYBRID_GS, 0.08, ORC_INTERP_CLASSICAL, 0.02);
     orc_csr_free(A);
     A = orc_gen_5pt(40, 33);
     lv += run(A, ORC_COARSEN_RS, ORC_SMOOTH_JACOBI, 0.25);
