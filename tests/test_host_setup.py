@@ -68,7 +68,7 @@ def test_host_hierarchy_ext_i_bit_exact(oracle, kind, dims, p_max):
 
 
 @pytest.mark.parametrize("kind,dims,coarsen,tol", [("27pt", (13, 12, 11), "sa", 0.02), ("7pt", (20, 20, 20), "pmis", 0.05),
-                                                  ("graph", (60, 50), "sa", 0.01)])
+                                                  ("graph", (60, 50), "sa", 0.01), ("7pt", (18, 17, 16), "pmis+ext+i", 0.02)])
 def test_host_hierarchy_drop_tol_bit_exact(oracle, kind, dims, coarsen, tol):
     """Coarse-operator drop tolerance (r6 option): the product's host setup equals
     the oracle's level for level; every coarse operator keeps its Galerkin row sums (up to
@@ -82,10 +82,14 @@ def test_host_hierarchy_drop_tol_bit_exact(oracle, kind, dims, coarsen, tol):
     else:
         A = gen(O, kind, dims)
     rp, col, val = A.arrays()
+    ext = coarsen.endswith("+ext+i")  # with extended+i interpolation (P_max 4)
+    coarsen = coarsen.split("+")[0]
     Hp = host.HostHierarchy(A.shape[0], 0, rp, col, val,
-                            host.options(coarsen=coarsen, max_coarse=64, drop_tol=tol))
-    Ho = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen], max_coarse=64, drop_tol=tol))
-    Hg = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen], max_coarse=64))
+                            host.options(coarsen=coarsen, max_coarse=64, drop_tol=tol,
+                                         interp="ext+i" if ext else "classical"))
+    ikw = dict(interp=O.INTERP_EXT_I, p_max=4) if ext else {}
+    Ho = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen], max_coarse=64, drop_tol=tol, **ikw))
+    Hg = O.Hierarchy(A, **dict(O.DEFAULTS[coarsen], max_coarse=64, **ikw))
     assert Hp.num_levels == Ho.num_levels >= 3
     for l in range(Ho.num_levels):
         assert same_csr(Hp.to_scipy(l, "A"), Ho.matrix(l, "A")), l
